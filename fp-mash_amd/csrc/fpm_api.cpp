@@ -1,0 +1,665 @@
+// fpm_api.cpp — implementation of the C ABI declared in include/fpmash.h.
+//
+// Host-side staging (record packing, tile plan, merge schedule) and kernel
+// launches for the gfx950 kernels in sketch.hip / fingerprint.hip / dist.hip.
+// There is deliberately no CPU compute path here: without a usable device every
+// compute entry point returns FPM_ENODEV.
+#include "fpm_kernels.hpp"
+#include "../../include/fpmash.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace fpm;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(FPM_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));      \
+    } while (0)
+
+// Reference complement table for 'A'..'Z' (Sketch.cpp:1223-1250); other bytes 'N'.
+const char kComplAZ[26] = {'T', 'V', 'G', 'H', 'N', 'N', 'C', 'D', 'N', 'N', 'M', 'N', 'K',
+                           'N', 'N', 'N', 'N', 'Y', 'S', 'A', 'A', 'B', 'W', 'N', 'R', 'N'};
+
+// Tile sizing: small records are packed up to kPackKmers k-mer starts per tile,
+// long records are cut into kChunkKmers-start chunks (k-1 bytes of halo).
+constexpr uint32_t kPackKmers = 2048;
+constexpr uint32_t kChunkKmers = 4096;
+
+int tile_class(uint32_t nstarts)
+{
+    for (int c = 0; c < kTileClasses; c++)
+        if (nstarts <= kTileCap[c]) return c;
+    return -1;
+}
+
+}  // namespace
+
+struct fpm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool timing = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
+};
+
+// RAII-free event bracket: records start before and stop after a launch.
+struct TimedLaunch {
+    fpm_ctx *ctx; int kid; hipStream_t st; hipEvent_t a = nullptr, b = nullptr;
+    TimedLaunch(fpm_ctx *c, int k, hipStream_t s) : ctx(c), kid(k), st(s)
+    {
+        if (ctx->timing) {
+            (void)hipEventCreate(&a);
+            (void)hipEventCreate(&b);
+            (void)hipEventRecord(a, st);
+        }
+    }
+    void done()
+    {
+        if (ctx->timing) {
+            (void)hipEventRecord(b, st);
+            ctx->ev[kid].push_back({a, b});
+        }
+    }
+};
+
+static int set_device(fpm_ctx *ctx)
+{
+    if (!ctx) return fail(FPM_EINVAL, "null context");
+    HIP_TRY(hipSetDevice(ctx->device));
+    return FPM_OK;
+}
+
+static hipStream_t pick_stream(fpm_ctx *ctx, void *stream)
+{
+    return stream ? (hipStream_t)stream : ctx->stream;
+}
+
+extern "C" {
+
+int fpm_abi_version(void) { return FPM_ABI_VERSION; }
+
+const char *fpm_last_error(void) { return g_err.c_str(); }
+
+int fpm_device_count(int *count)
+{
+    if (!count) return fail(FPM_EINVAL, "null count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return FPM_OK;
+}
+
+int fpm_ctx_create(int device, fpm_ctx **out)
+{
+    if (!out) return fail(FPM_EINVAL, "null out");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0)
+        return fail(FPM_ENODEV, "no HIP device visible (fpmash has no CPU fallback)");
+    if (device < 0 || device >= n) return fail(FPM_EINVAL, "device index out of range");
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+        return fail(FPM_ENODEV, std::string("device is ") + prop.gcnArchName +
+                                    ", fpmash kernels are built for gfx950 only");
+    fpm_ctx *ctx = new fpm_ctx();
+    ctx->device = device;
+    hipError_t e = hipSetDevice(device);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+        delete ctx;
+        return fail(FPM_EHIP, std::string("context init: ") + hipGetErrorString(e));
+    }
+    *out = ctx;
+    return FPM_OK;
+}
+
+void fpm_ctx_destroy(fpm_ctx *ctx)
+{
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    fpm_ctx_reset_timing(ctx);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void *fpm_ctx_stream(fpm_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
+
+int fpm_ctx_synchronize(fpm_ctx *ctx)
+{
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return FPM_OK;
+}
+
+int fpm_malloc(fpm_ctx *ctx, void **dptr, size_t bytes)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!dptr) return fail(FPM_EINVAL, "null dptr");
+    hipError_t e = hipMalloc(dptr, bytes ? bytes : 1);
+    if (e != hipSuccess) return fail(FPM_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return FPM_OK;
+}
+
+int fpm_free(fpm_ctx *ctx, void *dptr)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (dptr) HIP_TRY(hipFree(dptr));
+    return FPM_OK;
+}
+
+int fpm_memcpy_h2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return FPM_OK;
+}
+
+int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return FPM_OK;
+}
+
+int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (bytes) HIP_TRY(hipMemsetAsync(dptr, value, bytes, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_ctx_set_timing(fpm_ctx *ctx, int enable)
+{
+    if (!ctx) return fail(FPM_EINVAL, "null context");
+    ctx->timing = enable != 0;
+    return FPM_OK;
+}
+
+int fpm_ctx_reset_timing(fpm_ctx *ctx)
+{
+    if (!ctx) return fail(FPM_EINVAL, "null context");
+    for (auto &v : ctx->ev) {
+        for (auto &pr : v) {
+            (void)hipEventDestroy(pr.first);
+            (void)hipEventDestroy(pr.second);
+        }
+        v.clear();
+    }
+    return FPM_OK;
+}
+
+int fpm_ctx_kernel_time(fpm_ctx *ctx, int kernel, double *total_ms, uint64_t *launches)
+{
+    if (!ctx || kernel < 0 || kernel >= FPM_K_COUNT) return fail(FPM_EINVAL, "bad kernel id");
+    if (int rc = set_device(ctx)) return rc;
+    double t = 0;
+    for (auto &pr : ctx->ev[kernel]) {
+        HIP_TRY(hipEventSynchronize(pr.second));
+        float ms = 0;
+        HIP_TRY(hipEventElapsedTime(&ms, pr.first, pr.second));
+        t += ms;
+    }
+    if (total_ms) *total_ms = t;
+    if (launches) *launches = ctx->ev[kernel].size();
+    return FPM_OK;
+}
+
+}  // extern "C"
+
+// ----------------------------------------------------------------------------
+// Sketch job: packing + tile plan + merge schedule
+// ----------------------------------------------------------------------------
+// Rows of one device matrix d_rows[n_rows][s]: rows [0, n_groups) are the final
+// sketches, rows >= n_groups hold per-tile / intermediate lists of groups whose
+// records span several tiles; those are reduced by pairwise merge rounds.
+
+struct fpm_sketch_job {
+    fpm_ctx *ctx = nullptr;
+    SketchKParams kp{};
+    uint32_t n_groups = 0;
+    uint32_t n_rows = 0;
+    uint64_t seq_bytes = 0;
+    uint64_t n_kmers = 0;
+    uint64_t n_tiles = 0;
+    uint8_t *d_seq = nullptr;
+    TileDesc *d_tiles = nullptr;
+    uint64_t *d_rows = nullptr;
+    uint32_t *d_count = nullptr;
+    MergeDesc *d_merge = nullptr;
+    uint32_t class_begin[kTileClasses + 1] = {0};
+    std::vector<uint32_t> round_begin;
+};
+
+static void job_release(fpm_sketch_job *j)
+{
+    if (!j) return;
+    (void)hipSetDevice(j->ctx->device);
+    (void)hipFree(j->d_seq); (void)hipFree(j->d_tiles); (void)hipFree(j->d_rows); (void)hipFree(j->d_count);
+    (void)hipFree(j->d_merge);
+}
+
+extern "C" {
+
+int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
+                     const uint64_t *rec_off, uint32_t n_rec, const uint32_t *group_of_rec,
+                     uint32_t n_groups, fpm_sketch_job **job_out)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!p || !job_out || (n_rec && (!seq || !rec_off))) return fail(FPM_EINVAL, "null argument");
+    if (p->kmer_size < 1 || p->kmer_size > 32) return fail(FPM_EINVAL, "kmer_size must be 1..32");
+    if (p->sketch_size < 1) return fail(FPM_EINVAL, "sketch_size must be >= 1");
+    *job_out = nullptr;
+    const uint32_t k = p->kmer_size, s = p->sketch_size;
+    if (!group_of_rec) n_groups = n_rec;
+    for (uint32_t r = 0; r < n_rec; r++)
+        if (rec_off[r + 1] < rec_off[r]) return fail(FPM_EINVAL, "record offsets must be non-decreasing");
+    if (group_of_rec)
+        for (uint32_t r = 0; r < n_rec; r++)
+            if (group_of_rec[r] >= n_groups) return fail(FPM_EINVAL, "group id out of range");
+
+    SketchKParams kp{};
+    kp.k = k; kp.s = s; kp.seed = p->seed; kp.use64 = p->use64 ? 1 : 0;
+    kp.canonical = p->noncanonical ? 0 : 1; kp.preserve_case = p->preserve_case ? 1 : 0;
+    for (int c = 0; c < 256; c++) {
+        kp.alphabet[c] = p->alphabet[c] ? 1 : 0;
+        kp.complement[c] = (c >= 'A' && c <= 'Z') ? (uint8_t)kComplAZ[c - 'A'] : (uint8_t)'N';
+    }
+    kp.alphabet[0] = 0;   // the separator byte is never a k-mer byte
+
+    // records of a group in stream order, groups ascending
+    std::vector<uint32_t> order(n_rec);
+    for (uint32_t r = 0; r < n_rec; r++) order[r] = r;
+    if (group_of_rec)
+        std::stable_sort(order.begin(), order.end(),
+                         [&](uint32_t a, uint32_t b) { return group_of_rec[a] < group_of_rec[b]; });
+
+    // pack records >= k (each followed by 0x00) and cut tiles
+    uint64_t total = 0;
+    for (uint32_t r : order) {
+        uint64_t l = rec_off[r + 1] - rec_off[r];
+        if (l >= k) total += l + 1;
+    }
+    std::vector<uint8_t> packed;
+    packed.reserve(total + 64);
+    std::vector<TileDesc> tiles;
+    std::vector<uint32_t> tile_group;
+    uint64_t n_kmers = 0;
+    uint32_t cur_group = UINT32_MAX;
+    bool open = false;
+    TileDesc cur{};
+    auto close = [&]() {
+        if (open) { tiles.push_back(cur); tile_group.push_back(cur_group); open = false; }
+    };
+    for (uint32_t r : order) {
+        const uint64_t l = rec_off[r + 1] - rec_off[r];
+        const uint32_t g = group_of_rec ? group_of_rec[r] : r;
+        if (g != cur_group) { close(); cur_group = g; }
+        if (l < k) continue;
+        const uint64_t poff = packed.size();
+        packed.insert(packed.end(), seq + rec_off[r], seq + rec_off[r] + l);
+        packed.push_back(0);
+        const uint64_t nk = l - k + 1;
+        n_kmers += nk;
+        if (nk > kPackKmers) {
+            close();
+            for (uint64_t c0 = 0; c0 < nk; c0 += kChunkKmers) {
+                uint64_t cn = std::min<uint64_t>(kChunkKmers, nk - c0);
+                tiles.push_back(TileDesc{poff + c0, (uint32_t)(cn + k - 1), 0});
+                tile_group.push_back(g);
+            }
+        } else if (open && (uint64_t)cur.n_bytes + 1 + l - k + 1 <= kPackKmers) {
+            cur.n_bytes += (uint32_t)(1 + l);   // separator + this record
+        } else {
+            close();
+            cur = TileDesc{poff, (uint32_t)l, 0};
+            open = true;
+        }
+    }
+    close();
+
+    // rows: single-tile groups write their final row, others get temp rows
+    std::vector<uint32_t> ntile_of(n_groups, 0);
+    for (uint32_t g : tile_group) ntile_of[g]++;
+    std::vector<std::vector<uint32_t>> lists(n_groups);
+    uint32_t n_rows = n_groups;
+    for (size_t t = 0; t < tiles.size(); t++) {
+        uint32_t g = tile_group[t];
+        if (ntile_of[g] == 1) tiles[t].out_row = g;
+        else { tiles[t].out_row = n_rows; lists[g].push_back(n_rows); n_rows++; }
+    }
+    struct Plan { uint32_t a, b, c; };
+    std::vector<Plan> mplan;
+    std::vector<uint32_t> rb{0};
+    for (;;) {
+        bool any = false;
+        for (uint32_t g = 0; g < n_groups; g++) {
+            auto &L = lists[g];
+            if (L.size() < 2) continue;
+            any = true;
+            std::vector<uint32_t> next;
+            for (size_t i = 0; i + 1 < L.size(); i += 2) {
+                uint32_t c = (L.size() == 2) ? g : n_rows++;
+                mplan.push_back({L[i], L[i + 1], c});
+                next.push_back(c);
+            }
+            if (L.size() % 2) next.push_back(L.back());
+            if (next.size() == 1) next.clear();   // reached the final row
+            L.swap(next);
+        }
+        if (!any) break;
+        rb.push_back((uint32_t)mplan.size());
+    }
+
+    // tiles ordered by capacity class
+    std::vector<TileDesc> by_class;
+    by_class.reserve(tiles.size());
+    uint32_t class_begin[kTileClasses + 1] = {0};
+    for (int c = 0; c < kTileClasses; c++) {
+        for (auto &t : tiles)
+            if (tile_class(t.n_bytes - k + 1) == c) by_class.push_back(t);
+        class_begin[c + 1] = (uint32_t)by_class.size();
+    }
+    if (by_class.size() != tiles.size()) return fail(FPM_EINVAL, "internal: tile exceeds capacity");
+
+    auto *job = new fpm_sketch_job();
+    job->ctx = ctx;
+    job->kp = kp;
+    job->n_groups = n_groups;
+    job->n_rows = n_rows;
+    job->seq_bytes = packed.size();
+    job->n_kmers = n_kmers;
+    job->n_tiles = tiles.size();
+    memcpy(job->class_begin, class_begin, sizeof(class_begin));
+    job->round_begin = rb;
+
+    hipError_t e = hipSuccess;
+    auto alloc = [&](void **ptr, size_t bytes) {
+        if (e == hipSuccess) e = hipMalloc(ptr, bytes ? bytes : 16);
+    };
+    alloc((void **)&job->d_seq, packed.size() + 64);
+    alloc((void **)&job->d_tiles, by_class.size() * sizeof(TileDesc));
+    alloc((void **)&job->d_rows, (size_t)n_rows * s * sizeof(uint64_t));
+    alloc((void **)&job->d_count, (size_t)n_rows * sizeof(uint32_t));
+    alloc((void **)&job->d_merge, mplan.size() * sizeof(MergeDesc));
+    if (e != hipSuccess) {
+        job_release(job);
+        delete job;
+        return fail(FPM_ENOMEM, std::string("sketch staging alloc: ") + hipGetErrorString(e));
+    }
+    std::vector<MergeDesc> md(mplan.size());
+    for (size_t i = 0; i < mplan.size(); i++) {
+        md[i].a = job->d_rows + (uint64_t)mplan[i].a * s;
+        md[i].alen = job->d_count + mplan[i].a;
+        md[i].b = job->d_rows + (uint64_t)mplan[i].b * s;
+        md[i].blen = job->d_count + mplan[i].b;
+        md[i].c = job->d_rows + (uint64_t)mplan[i].c * s;
+        md[i].clen = job->d_count + mplan[i].c;
+    }
+    if (!packed.empty()) e = hipMemcpy(job->d_seq, packed.data(), packed.size(), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !by_class.empty())
+        e = hipMemcpy(job->d_tiles, by_class.data(), by_class.size() * sizeof(TileDesc),
+                      hipMemcpyHostToDevice);
+    if (e == hipSuccess && !md.empty())
+        e = hipMemcpy(job->d_merge, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        job_release(job);
+        delete job;
+        return fail(FPM_EHIP, std::string("sketch staging copy: ") + hipGetErrorString(e));
+    }
+    *job_out = job;
+    return FPM_OK;
+}
+
+int fpm_sketch_run(fpm_sketch_job *job, void *stream)
+{
+    if (!job) return fail(FPM_EINVAL, "null job");
+    fpm_ctx *ctx = job->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t st = pick_stream(ctx, stream);
+    // groups without any k-mer keep count 0
+    HIP_TRY(hipMemsetAsync(job->d_count, 0, (size_t)job->n_groups * sizeof(uint32_t), st));
+    for (int c = 0; c < kTileClasses; c++) {
+        uint32_t b = job->class_begin[c], n = job->class_begin[c + 1] - b;
+        if (!n) continue;
+        TimedLaunch tl(ctx, FPM_K_SKETCH, st);
+        HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_tiles + b, n, job->kp, job->d_rows,
+                                    job->d_count, st));
+        tl.done();
+    }
+    for (size_t r = 0; r + 1 < job->round_begin.size(); r++) {
+        uint32_t b = job->round_begin[r], n = job->round_begin[r + 1] - b;
+        TimedLaunch tl(ctx, FPM_K_MERGE, st);
+        HIP_TRY(launch_merge(job->d_merge + b, n, job->kp.s, st));
+        tl.done();
+    }
+    return FPM_OK;
+}
+
+int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,
+                             uint32_t *n_groups, uint32_t *row_stride)
+{
+    if (!job) return fail(FPM_EINVAL, "null job");
+    if (d_hashes) *d_hashes = job->d_rows;
+    if (d_count) *d_count = job->d_count;
+    if (n_groups) *n_groups = job->n_groups;
+    if (row_stride) *row_stride = job->kp.s;
+    return FPM_OK;
+}
+
+int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_count)
+{
+    if (!job) return fail(FPM_EINVAL, "null job");
+    fpm_ctx *ctx = job->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    HIP_TRY(hipDeviceSynchronize());
+    if (out_hashes && job->n_groups)
+        HIP_TRY(hipMemcpy(out_hashes, job->d_rows, (size_t)job->n_groups * job->kp.s * sizeof(uint64_t),
+                          hipMemcpyDeviceToHost));
+    if (out_count && job->n_groups)
+        HIP_TRY(hipMemcpy(out_count, job->d_count, (size_t)job->n_groups * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost));
+    return FPM_OK;
+}
+
+int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_tiles,
+                        uint64_t *n_kmers)
+{
+    if (!job) return fail(FPM_EINVAL, "null job");
+    if (seq_bytes) *seq_bytes = job->seq_bytes;
+    if (n_tiles) *n_tiles = job->n_tiles;
+    if (n_kmers) *n_kmers = job->n_kmers;
+    return FPM_OK;
+}
+
+void fpm_sketch_job_free(fpm_sketch_job *job)
+{
+    if (!job) return;
+    job_release(job);
+    delete job;
+}
+
+int fpm_sketch_batch(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
+                     const uint64_t *rec_off, uint32_t n_rec, const uint32_t *group_of_rec,
+                     uint32_t n_groups, uint64_t *out_hashes, uint32_t *out_count)
+{
+    fpm_sketch_job *job = nullptr;
+    int rc = fpm_sketch_stage(ctx, p, seq, rec_off, n_rec, group_of_rec, n_groups, &job);
+    if (rc) return rc;
+    rc = fpm_sketch_run(job, nullptr);
+    if (!rc) rc = fpm_sketch_fetch(job, out_hashes, out_count);
+    fpm_sketch_job_free(job);
+    return rc;
+}
+
+// ----------------------------------------------------------------------------
+// -fp line hashing
+// ----------------------------------------------------------------------------
+
+int fpm_fp_hash_lines_dev(fpm_ctx *ctx, const uint64_t *d_vals, const uint64_t *d_line_off,
+                          uint64_t n_lines, uint32_t seed, uint32_t use64, void *d_out,
+                          void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t st = pick_stream(ctx, stream);
+    TimedLaunch tl(ctx, FPM_K_FPHASH, st);
+    HIP_TRY(launch_fp_hash(d_vals, d_line_off, n_lines, seed, use64, d_out, st));
+    tl.done();
+    return FPM_OK;
+}
+
+int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_off,
+                      uint64_t n_lines, uint32_t seed, uint32_t use64, void *out)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!line_off || (n_lines && !out)) return fail(FPM_EINVAL, "null argument");
+    if (n_lines == 0) return FPM_OK;
+    const uint64_t nv = line_off[n_lines];
+    const size_t ob = (use64 ? 8 : 4) * n_lines;
+    uint64_t *dv = nullptr, *doff = nullptr;
+    void *dout = nullptr;
+    hipError_t e = hipMalloc((void **)&dv, (nv ? nv : 1) * 8);
+    if (e == hipSuccess) e = hipMalloc((void **)&doff, (n_lines + 1) * 8);
+    if (e == hipSuccess) e = hipMalloc(&dout, ob);
+    if (e == hipSuccess && nv) e = hipMemcpy(dv, vals, nv * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(doff, line_off, (n_lines + 1) * 8, hipMemcpyHostToDevice);
+    int rc = FPM_OK;
+    if (e != hipSuccess) rc = fail(FPM_EHIP, std::string("fp staging: ") + hipGetErrorString(e));
+    if (!rc) rc = fpm_fp_hash_lines_dev(ctx, dv, doff, n_lines, seed, use64, dout, nullptr);
+    if (!rc) {
+        e = hipStreamSynchronize(ctx->stream);
+        if (e == hipSuccess) e = hipMemcpy(out, dout, ob, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) rc = fail(FPM_EHIP, std::string("fp fetch: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(dv); (void)hipFree(doff); (void)hipFree(dout);
+    return rc;
+}
+
+// ----------------------------------------------------------------------------
+// dist
+// ----------------------------------------------------------------------------
+
+int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
+                         uint32_t *d_denom, void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
+    hipStream_t st = pick_stream(ctx, stream);
+    TimedLaunch tl(ctx, FPM_K_COMPARE, st);
+    HIP_TRY(launch_compare_grid(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
+                                n_qry, hash_bytes, sketch_size, d_numer, d_denom, st));
+    tl.done();
+    return FPM_OK;
+}
+
+int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,
+                          const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+                          uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
+                          double kmer_space, double max_dist, double max_pvalue,
+                          double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t st = pick_stream(ctx, stream);
+    TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
+    HIP_TRY(launch_dist_finalize(d_numer, d_denom, d_ref_length, d_qry_length, n_ref, n_qry,
+                                 kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue,
+                                 d_pass, st));
+    tl.done();
+    return FPM_OK;
+}
+
+namespace {
+struct DevBuf {
+    void *p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+};
+}  // namespace
+
+int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
+             uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,
+             const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+             double max_dist, double max_pvalue, uint32_t *out_numer, uint32_t *out_denom,
+             double *out_dist, double *out_pvalue, uint8_t *out_pass)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
+    const uint64_t np = (uint64_t)n_ref * n_qry;
+    if (np == 0) return FPM_OK;
+    const bool fin = out_dist || out_pvalue || out_pass;
+    if (fin && (!ref_length || !qry_length)) return fail(FPM_EINVAL, "lengths required for distance");
+    DevBuf r, rl, rL, q, ql, qL, nu, de, di, pv, pa;
+    hipError_t e = hipSuccess;
+    auto up = [&](DevBuf &b, const void *h, size_t bytes) {
+        if (e != hipSuccess) return;
+        e = hipMalloc(&b.p, bytes ? bytes : 16);
+        if (e == hipSuccess && h && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+    };
+    up(r, ref, (size_t)n_ref * ref_stride * hash_bytes);
+    up(rl, ref_len, (size_t)n_ref * 4);
+    up(q, qry, (size_t)n_qry * qry_stride * hash_bytes);
+    up(ql, qry_len, (size_t)n_qry * 4);
+    up(nu, nullptr, np * 4);
+    up(de, nullptr, np * 4);
+    if (fin) {
+        up(rL, ref_length, (size_t)n_ref * 8);
+        up(qL, qry_length, (size_t)n_qry * 8);
+        up(di, nullptr, np * 8);
+        up(pv, nullptr, np * 8);
+        up(pa, nullptr, np);
+    }
+    if (e != hipSuccess) return fail(FPM_ENOMEM, std::string("dist staging: ") + hipGetErrorString(e));
+    int rc = fpm_compare_grid_dev(ctx, r.p, (const uint32_t *)rl.p, ref_stride, n_ref, q.p,
+                                  (const uint32_t *)ql.p, qry_stride, n_qry, hash_bytes, sketch_size,
+                                  (uint32_t *)nu.p, (uint32_t *)de.p, nullptr);
+    if (!rc && fin)
+        rc = fpm_dist_finalize_dev(ctx, (const uint32_t *)nu.p, (const uint32_t *)de.p,
+                                   (const uint64_t *)rL.p, (const uint64_t *)qL.p, n_ref, n_qry,
+                                   kmer_size, kmer_space, max_dist, max_pvalue, (double *)di.p,
+                                   (double *)pv.p, (uint8_t *)pa.p, nullptr);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    if (out_numer) HIP_TRY(hipMemcpy(out_numer, nu.p, np * 4, hipMemcpyDeviceToHost));
+    if (out_denom) HIP_TRY(hipMemcpy(out_denom, de.p, np * 4, hipMemcpyDeviceToHost));
+    if (out_dist) HIP_TRY(hipMemcpy(out_dist, di.p, np * 8, hipMemcpyDeviceToHost));
+    if (out_pvalue) HIP_TRY(hipMemcpy(out_pvalue, pv.p, np * 8, hipMemcpyDeviceToHost));
+    if (out_pass) HIP_TRY(hipMemcpy(out_pass, pa.p, np, hipMemcpyDeviceToHost));
+    return FPM_OK;
+}
+
+int fpm_compare_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                     uint64_t ref_stride, uint32_t n_ref, const void *qry,
+                     const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,
+                     uint32_t hash_bytes, uint32_t sketch_size, uint32_t *out_numer,
+                     uint32_t *out_denom)
+{
+    return fpm_dist(ctx, ref, ref_len, nullptr, ref_stride, n_ref, qry, qry_len, nullptr,
+                    qry_stride, n_qry, hash_bytes, sketch_size, 0, 0.0, -1.0, -1.0, out_numer,
+                    out_denom, nullptr, nullptr, nullptr);
+}
+
+}  // extern "C"

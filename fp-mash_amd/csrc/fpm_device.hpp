@@ -1,0 +1,85 @@
+// fpm_device.hpp — device-side building blocks shared by the gfx950 kernels.
+//
+// MurmurHash3_x64_128 (replaces MurmurHash3.cpp:255-331 as used by getHash,
+// hash.cpp:12-40): on CDNA4 there is no 64x64 multiply, so every constant
+// multiply lowers to v_mul_lo_u32/v_mul_hi_u32/v_mad_u64_u32 — the k-mer sketch
+// is integer-VALU bound, not HBM bound.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpm {
+
+constexpr uint64_t kC1 = 0x87c37b91114253d5ULL;
+constexpr uint64_t kC2 = 0x4cf5ad432745937fULL;
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+
+__device__ __forceinline__ uint64_t fmix64(uint64_t k)
+{
+    k ^= k >> 33;
+    k *= 0xff51afd7ed558ccdULL;
+    k ^= k >> 33;
+    k *= 0xc4ceb9fe1a85ec53ULL;
+    k ^= k >> 33;
+    return k;
+}
+
+__device__ __forceinline__ void mur_block(uint64_t &h1, uint64_t &h2, uint64_t k1, uint64_t k2)
+{
+    k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+    h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
+    k2 *= kC2; k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2;
+    h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
+}
+
+__device__ __forceinline__ uint64_t mur_final(uint64_t h1, uint64_t h2, uint64_t len)
+{
+    h1 ^= len; h2 ^= len;
+    h1 += h2; h2 += h1;
+    h1 = fmix64(h1); h2 = fmix64(h2);
+    return h1 + h2;   // h1 of the 128-bit result (the only half getHash reads)
+}
+
+// Murmur over `len` (<= 32) bytes held little-endian in w[0..3]; bytes past len are 0.
+// `len` is wave-uniform (the k-mer size), so the branches do not diverge.
+__device__ __forceinline__ uint64_t murmur_h1_le32(const uint64_t w[4], int len, uint32_t seed)
+{
+    uint64_t h1 = seed, h2 = seed;
+    int nb = len >> 4;
+    if (nb >= 1) mur_block(h1, h2, w[0], w[1]);
+    if (nb >= 2) mur_block(h1, h2, w[2], w[3]);
+    int rem = len & 15;
+    if (rem) {
+        uint64_t k1 = (nb == 0) ? w[0] : w[2];
+        uint64_t k2 = (nb == 0) ? w[1] : w[3];
+        if (rem > 8) { k2 *= kC2; k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2; }
+        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+    }
+    return mur_final(h1, h2, (uint64_t)len);
+}
+
+// Murmur over n little-endian u64 values (getHashFingerPrint hash.cpp:45-73,
+// length = 8*n bytes): blocks are value pairs, an odd last value is the k1 tail.
+template <typename LoadFn>
+__device__ __forceinline__ uint64_t murmur_h1_u64s(LoadFn load, uint64_t n, uint32_t seed)
+{
+    uint64_t h1 = seed, h2 = seed;
+    uint64_t i = 0;
+    for (; i + 2 <= n; i += 2) mur_block(h1, h2, load(i), load(i + 1));
+    if (i < n) {
+        uint64_t k1 = load(i);
+        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+    }
+    return mur_final(h1, h2, (uint64_t)(int64_t)(int)(n * 8));
+}
+
+// 4 bytes starting at an arbitrary byte offset of an LDS byte image (read as dwords).
+__device__ __forceinline__ uint32_t lds_u32_at(const uint32_t *img, uint32_t byte_off)
+{
+    uint32_t q = byte_off >> 2, r = byte_off & 3;
+    return __builtin_amdgcn_alignbyte(img[q + 1], img[q], r);
+}
+
+}  // namespace fpm

@@ -1,0 +1,64 @@
+// fpm_kernels.hpp — launch interface between the C-ABI (fpm_api.cpp) and the
+// gfx950 kernels (sketch.hip, dist.hip, fingerprint.hip).  Host-only types.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fpm {
+
+// One tile = a contiguous byte range of the packed, separator-delimited sequence
+// buffer, all of it from one sketch group.  Every k-mer start of the tile lies
+// in [byte_off, byte_off + n_bytes - k]; windows that cross a 0x00 separator are
+// invalid by construction (0x00 is never in an alphabet).
+struct TileDesc {
+    uint64_t byte_off;
+    uint32_t n_bytes;
+    uint32_t out_row;   // row of the output (or temp) matrix this tile writes
+};
+
+struct SketchKParams {
+    uint32_t k;
+    uint32_t s;             // sketch size (row stride of the output matrix)
+    uint32_t seed;
+    uint32_t use64;
+    uint32_t canonical;
+    uint32_t preserve_case;
+    uint8_t alphabet[256];  // 1 = valid (after uppercasing)
+    uint8_t complement[256];
+};
+
+// Pairwise merge of two ascending distinct lists into the first s distinct of
+// their union (bottom-s of a union = bottom-s of the union of bottom-s sets).
+struct MergeDesc {
+    const uint64_t *a; const uint32_t *alen;
+    const uint64_t *b; const uint32_t *blen;   // b == nullptr: copy a
+    uint64_t *c; uint32_t *clen;
+};
+
+// Tile capacity classes (k-mer starts per tile).
+constexpr int kTileClasses = 6;
+constexpr uint32_t kTileCap[kTileClasses] = {256, 512, 1024, 2048, 4096, 8192};
+
+hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
+                               uint32_t n_tiles, const SketchKParams &p, uint64_t *d_out,
+                               uint32_t *d_count, hipStream_t st);
+hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st);
+
+hipError_t launch_fp_hash(const uint64_t *d_vals, const uint64_t *d_line_off, uint64_t n_lines,
+                          uint32_t seed, uint32_t use64, void *d_out, hipStream_t st);
+
+hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                               uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
+                               uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
+                               uint32_t sketch_size, uint32_t *d_numer, uint32_t *d_denom,
+                               hipStream_t st);
+
+hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
+                                const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+                                uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
+                                double kmer_space, double max_dist, double max_pvalue,
+                                double *d_dist, double *d_pvalue, uint8_t *d_pass,
+                                hipStream_t st);
+
+}  // namespace fpm

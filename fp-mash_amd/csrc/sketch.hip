@@ -1,0 +1,275 @@
+// sketch.hip — DNA/alphabet k-mer sketching for gfx950.
+//
+// Replaces the per-k-mer loop of addMinHashes (Sketch.cpp:664-735) feeding
+// MinHashHeap::tryInsert (MinHashHeap.cpp:68-146) and the final
+// HashSet::toHashList sort (HashSet.cpp:78-118): instead of a heap walked one
+// k-mer at a time, one workgroup owns a tile of up to P k-mer starts, stages the
+// tile's bytes (and their reverse complement) in LDS, hashes every window in
+// parallel, bitonic-sorts the P keys in LDS and keeps the first s distinct.
+// Result: the s smallest distinct hashes, ascending — exactly the set the
+// reference heap holds at the end of the stream.
+#include "fpm_device.hpp"
+#include "fpm_kernels.hpp"
+
+namespace fpm {
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+// Block-wide exclusive scan of one u32 per thread; returns the exclusive prefix
+// and writes the block total to *total.  `tmp` holds kWaves+1 dwords of LDS.
+__device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *tmp, uint32_t *total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) tmp[wave] = x;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int w = 0; w < kWaves; w++) { uint32_t t = tmp[w]; tmp[w] = acc; acc += t; }
+        tmp[kWaves] = acc;
+    }
+    __syncthreads();
+    uint32_t ex = tmp[wave] + x - v;
+    *total = tmp[kWaves];
+    __syncthreads();
+    return ex;
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
+    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
+    uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+{
+    // byte images padded so that 9-dword window reads past the end stay in bounds
+    constexpr int kImgWords = (P + 32 + 64) / 4;
+    __shared__ uint32_t fwd_img[kImgWords];
+    __shared__ uint32_t rc_img[kImgWords];
+    __shared__ uint32_t badmask[(P + 32 + 64) / 32];
+    __shared__ uint64_t keys[P];
+    __shared__ uint8_t alpha[256];
+    __shared__ uint8_t compl_tab[256];
+    __shared__ uint32_t scan_tmp[kWaves + 1];
+
+    const TileDesc td = tiles[blockIdx.x];
+    const uint32_t n = td.n_bytes;
+    const uint32_t k = p.k;
+    const int tid = threadIdx.x;
+
+    alpha[tid] = p.alphabet[tid];
+    compl_tab[tid] = p.complement[tid];
+    __syncthreads();
+
+    // ---- stage bytes: uppercase (Sketch.cpp:676-682), validity bitmask, rc image
+    uint8_t *fb = reinterpret_cast<uint8_t *>(fwd_img);
+    uint8_t *rb = reinterpret_cast<uint8_t *>(rc_img);
+    constexpr int kImgBytes = kImgWords * 4;
+    for (int b = tid; b < kImgBytes; b += kBlock) {
+        uint8_t c = 0;
+        if ((uint32_t)b < n) {
+            c = seq[td.byte_off + b];
+            if (!p.preserve_case && c > 96 && c < 123) c -= 32;
+        }
+        fb[b] = c;
+        bool bad = (uint32_t)b >= n || !alpha[c];
+        unsigned long long m = __ballot(bad);
+        if ((tid & 63) == 0 && b / 32 + 1 < (P + 32 + 64) / 32) {
+            badmask[b / 32] = (uint32_t)m;
+            badmask[b / 32 + 1] = (uint32_t)(m >> 32);
+        }
+        if ((uint32_t)b < n) rb[n - 1 - b] = compl_tab[c];   // reverseComplement Sketch.cpp:1252-1258
+        else rb[b] = 0;
+    }
+    __syncthreads();
+
+    // ---- hash every window (one k-mer start per thread per pass)
+    const uint32_t nk = n >= k ? n - k + 1 : 0;
+    const int nw = (k + 3) >> 2;                           // dwords per k-mer
+    const uint32_t tail_mask = (k & 3) ? ((1u << (8 * (k & 3))) - 1u) : 0xffffffffu;
+    const uint32_t kmask = (k == 32) ? 0xffffffffu : ((1u << k) - 1u);
+    uint32_t nvalid_local = 0;
+    for (int i = tid; i < P; i += kBlock) {
+        uint64_t key = ~0ULL;
+        if ((uint32_t)i < nk) {
+            // window [i, i+k) must hold alphabet bytes only (Sketch.cpp:696-713)
+            uint32_t w = i >> 5, sh = i & 31;
+            uint64_t bits = ((uint64_t)badmask[w] | ((uint64_t)badmask[w + 1] << 32)) >> sh;
+            if (((uint32_t)bits & kmask) == 0) {
+                uint32_t d[8];
+#pragma unroll
+                for (int m = 0; m < 8; m++)
+                    d[m] = (m < nw) ? lds_u32_at(fwd_img, i + 4 * m) : 0u;
+                d[nw - 1] &= tail_mask;
+                if (p.canonical) {
+                    // canonical = memcmp(fwd, rev) <= 0 ? fwd : rev (Sketch.cpp:719-723)
+                    const uint32_t ro = n - i - k;
+                    uint32_t r[8];
+#pragma unroll
+                    for (int m = 0; m < 8; m++)
+                        r[m] = (m < nw) ? lds_u32_at(rc_img, ro + 4 * m) : 0u;
+                    r[nw - 1] &= tail_mask;
+                    int cmp = 0;
+#pragma unroll
+                    for (int m = 0; m < 8; m++) {
+                        uint32_t fbe = __builtin_bswap32(d[m]), rbe = __builtin_bswap32(r[m]);
+                        if (cmp == 0 && m < nw) cmp = (fbe > rbe) - (fbe < rbe);
+                    }
+                    if (cmp > 0) {
+#pragma unroll
+                        for (int m = 0; m < 8; m++) d[m] = r[m];
+                    }
+                }
+                uint64_t wd[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) wd[j] = (uint64_t)d[2 * j] | ((uint64_t)d[2 * j + 1] << 32);
+                uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
+                key = p.use64 ? h : (h & 0xffffffffULL);   // getHash hash.cpp:30-37
+                nvalid_local++;
+            }
+        }
+        keys[i] = key;
+    }
+    uint32_t nvalid;
+    block_exscan(nvalid_local, scan_tmp, &nvalid);   // also a barrier over keys[]
+
+    // ---- bitonic sort of P keys, ascending
+    for (int ks = 2; ks <= P; ks <<= 1) {
+        for (int j = ks >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < P / 2; t += kBlock) {
+                int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                int l = i + j;
+                bool up = (i & ks) == 0;
+                uint64_t a = keys[i], b = keys[l];
+                if ((a > b) == up) { keys[i] = b; keys[l] = a; }
+            }
+            __syncthreads();
+        }
+    }
+
+    // ---- first s distinct (ties removed: the heap is a set, MinHashHeap.cpp:74)
+    constexpr int E = P / kBlock > 0 ? P / kBlock : 1;
+    const int base = tid * E;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        int idx = base + e;
+        if (idx < P && (uint32_t)idx < nvalid && (idx == 0 || keys[idx] != keys[idx - 1])) cnt++;
+    }
+    uint32_t total;
+    uint32_t rank = block_exscan(cnt, scan_tmp, &total);
+    uint64_t *row = out + (uint64_t)td.out_row * p.s;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        int idx = base + e;
+        if (idx < P && (uint32_t)idx < nvalid && (idx == 0 || keys[idx] != keys[idx - 1])) {
+            if (rank < p.s) row[rank] = keys[idx];
+            rank++;
+        }
+    }
+    if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;
+}
+
+// Merge of two ascending distinct lists, keeping the first s distinct of the union.
+// A[i] lands at i + lower_bound(B, A[i]) - #dups among A[0..i); B[j] that equals an
+// A element is dropped, the others land at j + upper_bound(A, B[j]) - #dups among B[0..j).
+__device__ __forceinline__ uint32_t lower_bound_u64(const uint64_t *v, uint32_t n, uint64_t x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (v[m] < x) lo = m + 1; else hi = m; }
+    return lo;
+}
+__device__ __forceinline__ uint32_t upper_bound_u64(const uint64_t *v, uint32_t n, uint64_t x)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (v[m] <= x) lo = m + 1; else hi = m; }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void merge_kernel(const MergeDesc *__restrict__ descs, uint32_t s)
+{
+    __shared__ uint32_t scan_tmp[kWaves + 1];
+    const MergeDesc md = descs[blockIdx.x];
+    const uint32_t la = *md.alen, lb = md.b ? *md.blen : 0;
+    uint32_t dups_total = 0;
+    // A side
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < la; c0 += kBlock) {
+        uint32_t i = c0 + threadIdx.x;
+        uint64_t a = 0; uint32_t pos = 0; uint32_t dup = 0;
+        if (i < la) {
+            a = md.a[i];
+            pos = lb ? lower_bound_u64(md.b, lb, a) : 0;
+            dup = (pos < lb && md.b[pos] == a) ? 1u : 0u;
+        }
+        uint32_t tot;
+        uint32_t ex = block_exscan(dup, scan_tmp, &tot);
+        if (i < la) {
+            uint32_t f = i + pos - (carry + ex);
+            if (f < s) md.c[f] = a;
+        }
+        carry += tot;
+    }
+    dups_total = carry;
+    // B side
+    carry = 0;
+    for (uint32_t c0 = 0; c0 < lb; c0 += kBlock) {
+        uint32_t j = c0 + threadIdx.x;
+        uint64_t b = 0; uint32_t pos = 0; uint32_t dup = 0;
+        if (j < lb) {
+            b = md.b[j];
+            pos = upper_bound_u64(md.a, la, b);
+            dup = (pos > 0 && md.a[pos - 1] == b) ? 1u : 0u;
+        }
+        uint32_t tot;
+        uint32_t ex = block_exscan(dup, scan_tmp, &tot);
+        if (j < lb && !dup) {
+            uint32_t f = j + pos - (carry + ex);
+            if (f < s) md.c[f] = b;
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        uint32_t u = la + lb - dups_total;
+        *md.clen = u < s ? u : s;
+    }
+}
+
+template <int P>
+static hipError_t launch_p(const uint8_t *d_seq, const TileDesc *d_tiles, uint32_t n_tiles,
+                           const SketchKParams &p, uint64_t *d_out, uint32_t *d_count,
+                           hipStream_t st)
+{
+    if (n_tiles == 0) return hipSuccess;
+    hipLaunchKernelGGL(sketch_tiles_kernel<P>, dim3(n_tiles), dim3(kBlock), 0, st, d_seq, d_tiles,
+                       p, d_out, d_count);
+    return hipGetLastError();
+}
+
+hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
+                               uint32_t n_tiles, const SketchKParams &p, uint64_t *d_out,
+                               uint32_t *d_count, hipStream_t st)
+{
+    switch (cls) {
+    case 0: return launch_p<256>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 1: return launch_p<512>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 2: return launch_p<1024>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 3: return launch_p<2048>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 4: return launch_p<4096>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 5: return launch_p<8192>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(merge_kernel, dim3(n), dim3(kBlock), 0, st, d_desc, s);
+    return hipGetLastError();
+}
+
+}  // namespace fpm

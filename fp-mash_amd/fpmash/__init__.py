@@ -1,0 +1,356 @@
+"""fpmash — Python binding of the gfx950 sketch + dist C ABI (include/fpmash.h).
+
+A ctypes mirror of the reference's engine calls for this path:
+  Sketch sketching (addMinHashes/MinHashHeap, Sketch.cpp:664-735, 1490-1517) -> Context.sketch
+  -fp line hashing (getHashFingerPrint, hash.cpp:45-73)                    -> Context.fp_hash_lines
+  compare/compareSketches/pValue (CommandDistance.cpp:335-450)             -> Context.dist
+The shared library is built in-tree (fp-mash_amd/lib/libfpmash.so).  There is no
+CPU fallback: if the library is missing this import fails, and without a gfx950
+device Context() raises FpmError(FPM_ENODEV).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfpmash.so")
+BIN_PATH = os.path.join(PKG_ROOT, "bin", "fpmash")
+
+FPM_OK, FPM_EINVAL, FPM_ENODEV, FPM_EHIP, FPM_ENOMEM = 0, -1, -2, -3, -4
+K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE = range(5)
+KERNEL_NAMES = {K_SKETCH: "sketch_tiles_kernel", K_MERGE: "merge_kernel",
+                K_FPHASH: "fp_hash_kernel", K_COMPARE: "compare_grid_kernel",
+                K_FINALIZE: "dist_finalize_kernel"}
+
+ALPHABET_NUCLEOTIDE = "ACGT"                     # Sketch.h alphabetNucleotide
+ALPHABET_PROTEIN = "ACDEFGHIKLMNPQRSTVWY"         # Sketch.h alphabetProtein
+
+u64p = C.POINTER(C.c_uint64)
+u32p = C.POINTER(C.c_uint32)
+f64p = C.POINTER(C.c_double)
+u8p = C.POINTER(C.c_uint8)
+vp = C.c_void_p
+
+# every symbol include/fpmash.h declares: (name, restype, argtypes)
+SYMBOLS = [
+    ("fpm_abi_version", C.c_int, []),
+    ("fpm_last_error", C.c_char_p, []),
+    ("fpm_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("fpm_ctx_create", C.c_int, [C.c_int, C.POINTER(vp)]),
+    ("fpm_ctx_destroy", None, [vp]),
+    ("fpm_ctx_stream", vp, [vp]),
+    ("fpm_ctx_synchronize", C.c_int, [vp]),
+    ("fpm_malloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
+    ("fpm_free", C.c_int, [vp, vp]),
+    ("fpm_memcpy_h2d", C.c_int, [vp, vp, vp, C.c_size_t]),
+    ("fpm_memcpy_d2h", C.c_int, [vp, vp, vp, C.c_size_t]),
+    ("fpm_memset", C.c_int, [vp, vp, C.c_int, C.c_size_t]),
+    ("fpm_ctx_set_timing", C.c_int, [vp, C.c_int]),
+    ("fpm_ctx_reset_timing", C.c_int, [vp]),
+    ("fpm_ctx_kernel_time", C.c_int, [vp, C.c_int, f64p, u64p]),
+    ("fpm_sketch_batch", C.c_int, [vp, vp, C.c_char_p, u64p, C.c_uint32, u32p, C.c_uint32,
+                                   u64p, u32p]),
+    ("fpm_sketch_stage", C.c_int, [vp, vp, C.c_char_p, u64p, C.c_uint32, u32p, C.c_uint32,
+                                   C.POINTER(vp)]),
+    ("fpm_sketch_run", C.c_int, [vp, vp]),
+    ("fpm_sketch_device_output", C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), u32p, u32p]),
+    ("fpm_sketch_fetch", C.c_int, [vp, u64p, u32p]),
+    ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
+    ("fpm_sketch_job_free", None, [vp]),
+    ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
+    ("fpm_fp_hash_lines_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32, vp,
+                                        vp]),
+    ("fpm_compare_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p, C.c_uint64,
+                                   C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p]),
+    ("fpm_compare_grid_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, C.c_uint64,
+                                       C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
+    ("fpm_dist_finalize_dev", C.c_int, [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32,
+                                        C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
+    ("fpm_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, vp, u32p, u64p,
+                           C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                           C.c_double, C.c_double, C.c_double, u32p, u32p, f64p, f64p, u8p]),
+]
+
+
+class FpmError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"fpmash error {code}: {msg}")
+        self.code = code
+
+
+class SketchParams(C.Structure):
+    """fpm_sketch_params == Sketch::Parameters subset (Sketch.h:40-113)."""
+    _fields_ = [
+        ("kmer_size", C.c_uint32),
+        ("sketch_size", C.c_uint32),
+        ("seed", C.c_uint32),
+        ("use64", C.c_uint32),
+        ("noncanonical", C.c_uint32),
+        ("preserve_case", C.c_uint32),
+        ("alphabet", C.c_uint8 * 256),
+    ]
+
+
+def make_params(k=21, s=1000, seed=42, alphabet=ALPHABET_NUCLEOTIDE, noncanonical=False,
+                preserve_case=False, fingerprint=False, protein=False):
+    """sketchParameterSetup (sketchParameterSetup.cpp:9-126) + setAlphabetFromString
+    (Sketch.cpp:1260-1289)."""
+    if fingerprint:                      # -fp: k=1, noncanonical, "0123456789"
+        k, noncanonical, alphabet = 1, True, "0123456789"
+    elif protein:
+        noncanonical, alphabet = True, ALPHABET_PROTEIN
+    P = SketchParams()
+    P.kmer_size, P.sketch_size, P.seed = k, s, seed
+    P.noncanonical, P.preserve_case = int(noncanonical), int(preserve_case)
+    n = 0
+    for ch in alphabet.encode():
+        if not preserve_case and 96 < ch < 123:
+            ch -= 32
+        if not P.alphabet[ch]:
+            n += 1
+        P.alphabet[ch] = 1
+    P.use64 = int(float(n) ** k > 2.0 ** 32)
+    return P
+
+
+_LIB = None
+
+
+def lib():
+    """Load libfpmash.so (raises if the HIP build is absent: no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built (run `make -C fp-mash_amd`); "
+                              "fpmash has no CPU fallback")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SYMBOLS:
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def _check(rc):
+    if rc != FPM_OK:
+        raise FpmError(rc, lib().fpm_last_error().decode(errors="replace"))
+
+
+def device_count():
+    n = C.c_int(0)
+    _check(lib().fpm_device_count(C.byref(n)))
+    return n.value
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(t)
+
+
+def pack_records(seqs):
+    off = np.zeros(len(seqs) + 1, dtype=np.uint64)
+    if seqs:
+        off[1:] = np.cumsum([len(s) for s in seqs])
+    return b"".join(seqs), off
+
+
+class DeviceBuffer:
+    def __init__(self, ctx, nbytes):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = vp()
+        _check(lib().fpm_malloc(ctx.h, C.byref(p), self.nbytes))
+        self.ptr = p.value
+
+    @classmethod
+    def from_array(cls, ctx, arr):
+        arr = np.ascontiguousarray(arr)
+        b = cls(ctx, arr.nbytes)
+        _check(lib().fpm_memcpy_h2d(ctx.h, b.ptr, arr.ctypes.data, arr.nbytes))
+        return b
+
+    def to_array(self, dtype, count):
+        out = np.empty(count, dtype=dtype)
+        _check(lib().fpm_memcpy_d2h(self.ctx.h, out.ctypes.data, self.ptr, out.nbytes))
+        return out
+
+    def free(self):
+        if self.ptr:
+            lib().fpm_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class SketchJob:
+    """fpm_sketch_stage/run/fetch: inputs staged once in HBM, kernels re-runnable."""
+
+    def __init__(self, ctx, params, seqs, groups=None, n_groups=None):
+        self.ctx, self.params = ctx, params
+        data, off = pack_records(seqs)
+        self._keep = (data, off)
+        n_rec = len(seqs)
+        if groups is not None:
+            g = np.ascontiguousarray(groups, dtype=np.uint32)
+            self.n_groups = int(n_groups if n_groups is not None else (int(g.max()) + 1 if n_rec else 0))
+            gp = _p(g, u32p)
+        else:
+            self.n_groups, gp = n_rec, None
+        h = vp()
+        _check(lib().fpm_sketch_stage(ctx.h, C.byref(params), data, _p(off, u64p), n_rec, gp,
+                                      self.n_groups, C.byref(h)))
+        self.h = h.value
+
+    def run(self, stream=None):
+        _check(lib().fpm_sketch_run(self.h, stream))
+
+    def info(self):
+        a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        _check(lib().fpm_sketch_job_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
+        return {"seq_bytes": a.value, "n_tiles": b.value, "n_kmers": c.value}
+
+    def device_output(self):
+        dh, dc = vp(), vp()
+        ng, st = C.c_uint32(), C.c_uint32()
+        _check(lib().fpm_sketch_device_output(self.h, C.byref(dh), C.byref(dc), C.byref(ng),
+                                              C.byref(st)))
+        return dh.value, dc.value, ng.value, st.value
+
+    def fetch(self):
+        s = int(self.params.sketch_size)
+        out = np.zeros(max(self.n_groups, 1) * s, dtype=np.uint64)
+        cnt = np.zeros(max(self.n_groups, 1), dtype=np.uint32)
+        _check(lib().fpm_sketch_fetch(self.h, _p(out, u64p), _p(cnt, u32p)))
+        return out[: self.n_groups * s].reshape(self.n_groups, s), cnt[: self.n_groups]
+
+    def free(self):
+        if self.h:
+            lib().fpm_sketch_job_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One gfx950 device (fpm_ctx)."""
+
+    def __init__(self, device=0):
+        h = vp()
+        _check(lib().fpm_ctx_create(device, C.byref(h)))
+        self.h = h.value
+        self.device = device
+
+    def close(self):
+        if self.h:
+            lib().fpm_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    @property
+    def stream(self):
+        return lib().fpm_ctx_stream(self.h)
+
+    def synchronize(self):
+        _check(lib().fpm_ctx_synchronize(self.h))
+
+    def set_timing(self, on=True):
+        _check(lib().fpm_ctx_set_timing(self.h, int(on)))
+
+    def reset_timing(self):
+        _check(lib().fpm_ctx_reset_timing(self.h))
+
+    def kernel_time(self, kernel):
+        t, n = C.c_double(), C.c_uint64()
+        _check(lib().fpm_ctx_kernel_time(self.h, kernel, C.byref(t), C.byref(n)))
+        return t.value, n.value
+
+    # --- sketch -----------------------------------------------------------
+    def sketch(self, params, seqs, groups=None, n_groups=None):
+        """-> list of ascending u64 arrays (one per sketch)."""
+        job = SketchJob(self, params, seqs, groups, n_groups)
+        try:
+            job.run()
+            rows, cnt = job.fetch()
+        finally:
+            job.free()
+        return [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+
+    def sketch_job(self, params, seqs, groups=None, n_groups=None):
+        return SketchJob(self, params, seqs, groups, n_groups)
+
+    # --- -fp ----------------------------------------------------------------
+    def fp_hash_lines(self, values_per_line, seed=42, use64=False):
+        off = np.zeros(len(values_per_line) + 1, dtype=np.uint64)
+        if values_per_line:
+            off[1:] = np.cumsum([len(v) for v in values_per_line])
+        vals = (np.concatenate([np.asarray(v, dtype=np.uint64) for v in values_per_line])
+                if values_per_line else np.zeros(0, np.uint64))
+        return self.fp_hash_flat(vals, off, seed, use64)
+
+    def fp_hash_flat(self, vals, line_off, seed=42, use64=False):
+        vals = np.ascontiguousarray(vals, dtype=np.uint64)
+        line_off = np.ascontiguousarray(line_off, dtype=np.uint64)
+        n = len(line_off) - 1
+        out = np.zeros(max(n, 1), dtype=np.uint64 if use64 else np.uint32)
+        if vals.size == 0:
+            vals = np.zeros(1, np.uint64)
+        _check(lib().fpm_fp_hash_lines(self.h, _p(vals, u64p), _p(line_off, u64p), n, seed,
+                                       int(use64), out.ctypes.data))
+        return out[:n]
+
+    # --- dist ---------------------------------------------------------------
+    def dist(self, ref_lists, qry_lists, sketch_size, use64=True, k=21, kmer_space=None,
+             ref_lengths=None, qry_lengths=None, max_dist=-1.0, max_pvalue=-1.0,
+             finalize=True):
+        """All pairs, query-major: returns dict of flat arrays (index q*n_ref + r)."""
+        dt = np.uint64 if use64 else np.uint32
+        w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
+        R, rl = _dense(ref_lists, w, dt)
+        Q, ql = _dense(qry_lists, w, dt)
+        n = len(ref_lists) * len(qry_lists)
+        nu = np.zeros(max(n, 1), np.uint32)
+        de = np.zeros(max(n, 1), np.uint32)
+        if not finalize:
+            _check(lib().fpm_compare_grid(self.h, R.ctypes.data, _p(rl, u32p), w, len(ref_lists),
+                                          Q.ctypes.data, _p(ql, u32p), w, len(qry_lists),
+                                          8 if use64 else 4, sketch_size, _p(nu, u32p),
+                                          _p(de, u32p)))
+            return {"numer": nu[:n], "denom": de[:n]}
+        if kmer_space is None:
+            kmer_space = 4.0 ** k
+        rL = np.ascontiguousarray(ref_lengths, dtype=np.uint64)
+        qL = np.ascontiguousarray(qry_lengths, dtype=np.uint64)
+        di = np.zeros(max(n, 1), np.float64)
+        pv = np.zeros(max(n, 1), np.float64)
+        pa = np.zeros(max(n, 1), np.uint8)
+        _check(lib().fpm_dist(self.h, R.ctypes.data, _p(rl, u32p), _p(rL, u64p), w,
+                              len(ref_lists), Q.ctypes.data, _p(ql, u32p), _p(qL, u64p), w,
+                              len(qry_lists), 8 if use64 else 4, sketch_size, k, kmer_space,
+                              max_dist, max_pvalue, _p(nu, u32p), _p(de, u32p), _p(di, f64p),
+                              _p(pv, f64p), _p(pa, u8p)))
+        return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
+                "pass": pa[:n].astype(bool)}
+
+
+def _dense(lists, width, dtype):
+    m = np.zeros((max(len(lists), 1), max(width, 1)), dtype=dtype)
+    lens = np.zeros(max(len(lists), 1), dtype=np.uint32)
+    for i, l in enumerate(lists):
+        m[i, : len(l)] = l
+        lens[i] = len(l)
+    return m, lens

@@ -1,0 +1,169 @@
+/*
+ * fpmash.h — the drop-in C ABI of the MI355X (gfx950) sketch + dist hot path.
+ *
+ * Plain C: pointers, sizes and int status codes; no C++ or torch types.  Every
+ * entry point names the fp-mash interface (file:line under
+ * /root/reference/mash/src/mash) whose work it takes over.  The host side
+ * (fp-mash_amd/host: the Command/Sketch/-fp surface) and the Python binding
+ * (fp-mash_amd/fpmash) call only these symbols; INTEGRATION.md shows the binding
+ * a maintainer adds to the reference.
+ *
+ * Conventions
+ *  - Return FPM_OK (0) on success, a negative FPM_E* code otherwise; the message
+ *    is in fpm_last_error() (thread-local).  The reference has no status codes on
+ *    this path (it prints and exit(1)s: Sketch.cpp:75-76, 1446-1463); the host
+ *    maps a non-zero status to that behaviour.
+ *  - `*_dev` entry points take DEVICE pointers and a hipStream_t passed as
+ *    void* (NULL = the context's stream) and never synchronise; the others take
+ *    host buffers, stage them, run, copy back and synchronise.
+ *  - Hashes are returned as uint64_t; with use64 == 0 the value is the low 32
+ *    bits of h1, zero-extended (hash_u.hash32, hash.h:17-21).
+ *  - There is no CPU fallback: with no usable gfx950 device every compute call
+ *    fails with FPM_ENODEV.
+ *  - A context is bound to one device; contexts are independent and may be used
+ *    from different threads (one thread per context at a time).
+ */
+#ifndef FPMASH_H
+#define FPMASH_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FPM_OK 0
+#define FPM_EINVAL (-1)
+#define FPM_ENODEV (-2)
+#define FPM_EHIP (-3)
+#define FPM_ENOMEM (-4)
+
+#define FPM_ABI_VERSION 1
+
+typedef struct fpm_ctx fpm_ctx;
+typedef struct fpm_sketch_job fpm_sketch_job;
+
+/* Sketch::Parameters (Sketch.h:40-113) as filled by sketchParameterSetup
+ * (sketchParameterSetup.cpp:9-126) and setAlphabetFromString (Sketch.cpp:1260-1289). */
+typedef struct fpm_sketch_params {
+    uint32_t kmer_size;      /* 1..32 (Command.cpp:183-185) */
+    uint32_t sketch_size;    /* minHashesPerWindow, s */
+    uint32_t seed;           /* hash seed (default 42) */
+    uint32_t use64;          /* alphabetSize^k > 2^32 */
+    uint32_t noncanonical;   /* -n / -a / -z / -fp */
+    uint32_t preserve_case;  /* -Z */
+    uint8_t alphabet[256];   /* parameters.alphabet[] (1 = in alphabet) */
+} fpm_sketch_params;
+
+/* ---- context / device --------------------------------------------------- */
+int fpm_abi_version(void);
+const char *fpm_last_error(void);
+int fpm_device_count(int *count);
+int fpm_ctx_create(int device, fpm_ctx **out);
+void fpm_ctx_destroy(fpm_ctx *ctx);
+void *fpm_ctx_stream(fpm_ctx *ctx);          /* the context's hipStream_t */
+int fpm_ctx_synchronize(fpm_ctx *ctx);
+
+/* device memory helpers (for bindings that own no allocator) */
+int fpm_malloc(fpm_ctx *ctx, void **dptr, size_t bytes);
+int fpm_free(fpm_ctx *ctx, void *dptr);
+int fpm_memcpy_h2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
+int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
+int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
+
+/* Per-kernel timing with HIP events recorded on the launch stream.
+ * kernel ids: 0 sketch tiles, 1 sketch merge, 2 fp hash, 3 compare, 4 finalize. */
+#define FPM_K_SKETCH 0
+#define FPM_K_MERGE 1
+#define FPM_K_FPHASH 2
+#define FPM_K_COMPARE 3
+#define FPM_K_FINALIZE 4
+#define FPM_K_COUNT 5
+int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
+int fpm_ctx_reset_timing(fpm_ctx *ctx);
+/* total milliseconds and launch count since the last reset (synchronises) */
+int fpm_ctx_kernel_time(fpm_ctx *ctx, int kernel, double *total_ms, uint64_t *launches);
+
+/* ---- k-mer sketch ------------------------------------------------------------
+ * Replaces addMinHashes (Sketch.cpp:664-735) + MinHashHeap::tryInsert
+ * (MinHashHeap.cpp:68-146) + setMinHashesForReference/HashSet::toHashList
+ * (Sketch.cpp:1291-1297, HashSet.cpp:78-118), as driven by sketchSequence
+ * (Sketch.cpp:1490-1517, -i: one sketch per record) and sketchFile
+ * (Sketch.cpp:1299-1488, default: one sketch per file = group of records).
+ *
+ * Records: seq[rec_off[r] .. rec_off[r+1]).  Records shorter than k are skipped
+ * (Sketch.cpp:488-492, 1373-1377).  group_of_rec == NULL: record r is sketch r
+ * (n_groups is ignored); else record r belongs to sketch group_of_rec[r] and
+ * records of a group are streamed in record order.
+ * Output: sketch g's ascending distinct hashes at out_hashes[g*sketch_size ..],
+ * out_count[g] of them (= min(s, distinct k-mers)).
+ */
+int fpm_sketch_batch(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
+                     const uint64_t *rec_off, uint32_t n_rec, const uint32_t *group_of_rec,
+                     uint32_t n_groups, uint64_t *out_hashes, uint32_t *out_count);
+
+/* Staged form for device-resident pipelines: stage() packs and uploads the
+ * sequence and the tile plan (H2D), run() launches the kernels only (inputs
+ * already in HBM), device_output() exposes the [n_groups][s] u64 result matrix
+ * and the u32 counts on the device, fetch() copies them back. */
+int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
+                     const uint64_t *rec_off, uint32_t n_rec, const uint32_t *group_of_rec,
+                     uint32_t n_groups, fpm_sketch_job **job);
+int fpm_sketch_run(fpm_sketch_job *job, void *stream);
+int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,
+                             uint32_t *n_groups, uint32_t *row_stride);
+int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_count);
+/* bytes the run() kernels read + write by algorithm (for roofline accounting) */
+int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_tiles,
+                        uint64_t *n_kmers);
+void fpm_sketch_job_free(fpm_sketch_job *job);
+
+/* ---- -fp k-finger lines ------------------------------------------------------
+ * Replaces the per-line getHashFingerPrint of Sketch::initFromFingerprints
+ * (Sketch.cpp:131 -> hash.cpp:45-73): line l hashes the 8*n little-endian bytes
+ * of vals[line_off[l] .. line_off[l+1]).  use64 == 0 (the -fp setting) writes
+ * uint32_t, else uint64_t, into out. */
+int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_off,
+                      uint64_t n_lines, uint32_t seed, uint32_t use64, void *out);
+int fpm_fp_hash_lines_dev(fpm_ctx *ctx, const uint64_t *d_vals, const uint64_t *d_line_off,
+                          uint64_t n_lines, uint32_t seed, uint32_t use64, void *d_out,
+                          void *stream);
+
+/* ---- dist ---------------------------------------------------------------------
+ * Replaces compare()/compareSketches()/pValue() (CommandDistance.cpp:335-450) over
+ * the whole ref x query grid that CommandDistance::run chunks (:224-261).
+ * Sketch lists are rows of dense matrices (row stride in elements) holding
+ * hash_bytes = 8 (u64) or 4 (u32) values; lists may be unsorted and carry
+ * duplicates (-fp), the walk is the reference's literal one.  sketch_size =
+ * min(s_ref, s_query) (:342-344).  Outputs are query-major: index q*n_ref + r. */
+int fpm_compare_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                     uint64_t ref_stride, uint32_t n_ref, const void *qry,
+                     const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,
+                     uint32_t hash_bytes, uint32_t sketch_size, uint32_t *out_numer,
+                     uint32_t *out_denom);
+int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
+                         uint32_t *d_denom, void *stream);
+/* distance (:404-419), p-value (:433-450, FP64) and the -d/-v filter (:421-429);
+ * ref_length/qry_length are Reference::length (k-mer space scaling of pValue).
+ * max_dist / max_pvalue < 0 disable the filter.  pass may be NULL. */
+int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,
+                          const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+                          uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
+                          double kmer_space, double max_dist, double max_pvalue,
+                          double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream);
+/* host-buffer convenience: compare + finalize */
+int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
+             uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,
+             const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+             double max_dist, double max_pvalue, uint32_t *out_numer, uint32_t *out_denom,
+             double *out_dist, double *out_pvalue, uint8_t *out_pass);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FPMASH_H */

@@ -1,0 +1,168 @@
+"""GPU parity: the gfx950 kernels (through the C ABI) vs the CPU oracle.
+
+Integer outputs (hashes, sketch sets, shared-hash counts) must be bit-exact.
+Distance and p-value: relative tolerance 1e-12 (BASELINE.json north_star).
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-12
+
+
+def rand_seq(rng, n, p_bad=0.0, p_lower=0.0, alphabet=b"ACGT"):
+    a = np.frombuffer(alphabet, dtype=np.uint8)
+    s = a[rng.integers(0, len(a), size=n)].copy()
+    if p_bad:
+        m = rng.random(n) < p_bad
+        s[m] = np.frombuffer(b"NRY-*", dtype=np.uint8)[rng.integers(0, 5, size=int(m.sum()))]
+    if p_lower:
+        m = (rng.random(n) < p_lower) & (s >= 65) & (s <= 90)
+        s[m] += 32
+    return s.tobytes()
+
+
+def check_sketches(got, exp):
+    assert len(got) == len(exp)
+    for i, (g, e) in enumerate(zip(got, exp)):
+        assert len(g) == len(e), f"sketch {i}: {len(g)} vs {len(e)} hashes"
+        assert np.array_equal(g, e), f"sketch {i} differs"
+
+
+@pytest.mark.parametrize("k,s,canon", [(21, 1000, True), (21, 1000, False), (16, 200, True),
+                                       (32, 500, True), (9, 50, True), (1, 10, False),
+                                       (27, 5000, True)])
+def test_sketch_individual(ctx, oracle, k, s, canon):
+    import fpmash
+    rng = np.random.default_rng(1000 + k + s)
+    lens = [0, 1, k - 1, k, k + 1, 50, 300, 1000, 1980, 2000, 2100, 4000, 5000, 9000, 20000]
+    seqs = [rand_seq(rng, L, p_bad=0.01 if i % 3 == 0 else 0.0, p_lower=0.2 if i % 4 == 1 else 0.0)
+            for i, L in enumerate(lens)]
+    P = fpmash.make_params(k=k, s=s, noncanonical=not canon)
+    O = oracle.params(k=k, s=s, noncanonical=not canon)
+    assert P.use64 == O.use64
+    got = ctx.sketch(P, seqs)
+    exp = oracle.sketch_batch(O, seqs)
+    check_sketches(got, exp)
+
+
+def test_sketch_low_complexity(ctx, oracle):
+    """Repeats and palindromes: duplicates and canonical ties."""
+    import fpmash
+    seqs = [b"A" * 3000, b"ACGT" * 700, b"AC" * 1500, b"ACGTTGCA" * 300, b"N" * 100,
+            b"acgtNNNNacgtacgtacgtacgtacgtacgt" * 40]
+    for k, s in [(21, 1000), (21, 3), (4, 1000)]:
+        P = fpmash.make_params(k=k, s=s)
+        got = ctx.sketch(P, seqs)
+        exp = oracle.sketch_batch(oracle.params(k=k, s=s), seqs)
+        check_sketches(got, exp)
+
+
+def test_sketch_concatenated_groups(ctx, oracle):
+    """Default (non -i) mode: one sketch per group of records, incl. chunked long records
+    and many short records packed per tile (sketchFile Sketch.cpp:1354-1422)."""
+    import fpmash
+    rng = np.random.default_rng(7)
+    seqs, groups = [], []
+    plan = [(0, [150] * 300), (1, [60000]), (2, [5] * 10), (3, [2000, 30000, 100, 7000]),
+            (4, [20] * 40 + [22] * 5), (5, [])]
+    for g, lens in plan:
+        for L in lens:
+            seqs.append(rand_seq(rng, L, p_bad=0.002))
+            groups.append(g)
+    for k, s in [(21, 1000), (15, 3000)]:
+        P = fpmash.make_params(k=k, s=s)
+        got = ctx.sketch(P, seqs, groups=groups, n_groups=6)
+        exp = oracle.sketch_batch(oracle.params(k=k, s=s), seqs, groups=groups, n_groups=6)
+        check_sketches(got, exp)
+
+
+def test_sketch_seed_and_case(ctx, oracle):
+    import fpmash
+    rng = np.random.default_rng(3)
+    seqs = [rand_seq(rng, 1500, p_lower=0.5) for _ in range(20)]
+    for seed in (0, 1, 42, 0xFFFFFFFF):
+        for pc in (False, True):
+            P = fpmash.make_params(k=21, s=400, seed=seed, preserve_case=pc)
+            O = oracle.params(k=21, s=400, seed=seed, preserve_case=pc)
+            check_sketches(ctx.sketch(P, seqs), oracle.sketch_batch(O, seqs))
+
+
+def test_sketch_protein_alphabet(ctx, oracle):
+    import fpmash
+    rng = np.random.default_rng(11)
+    seqs = [rand_seq(rng, 800, alphabet=b"ACDEFGHIKLMNPQRSTVWYBXZ") for _ in range(10)]
+    P = fpmash.make_params(k=9, s=300, protein=True)
+    O = oracle.params(k=9, s=300, alphabet=fpmash.ALPHABET_PROTEIN, noncanonical=True)
+    check_sketches(ctx.sketch(P, seqs), oracle.sketch_batch(O, seqs))
+
+
+def test_fp_hash_lines(ctx, oracle):
+    rng = np.random.default_rng(5)
+    lines = [rng.integers(0, 2 ** 63, size=rng.integers(0, 40), dtype=np.uint64)
+             for _ in range(5000)]
+    lines += [np.array([8, 34, 57, 1], dtype=np.uint64), np.zeros(0, np.uint64)]
+    for use64 in (False, True):
+        for seed in (42, 7):
+            got = ctx.fp_hash_lines(lines, seed=seed, use64=use64)
+            exp = np.array([oracle.get_hash_fp(v, seed, use64) for v in lines],
+                           dtype=np.uint64 if use64 else np.uint32)
+            assert np.array_equal(got, exp)
+    assert int(ctx.fp_hash_lines([[8, 34, 57, 1]])[0]) == 819737709
+
+
+def _family_sketches(oracle, n_fam=6, members=8, L=2000, k=21, s=1000, seed=0):
+    import fpmash.datagen as D
+    seqs = D.family_dna(n_fam, members, L, sub_rate=(0.0, 0.08), seed=seed)
+    sk = oracle.sketch_batch(oracle.params(k=k, s=s), seqs)
+    return seqs, sk
+
+
+def test_dist_sorted_u64(ctx, oracle):
+    seqs, sk = _family_sketches(oracle)
+    lengths = [len(x) for x in seqs]
+    # uneven sketch sizes, empty lists, truncated sketch size
+    sk = sk + [sk[0][:10], np.zeros(0, np.uint64), sk[3][:999]]
+    lengths = lengths + [lengths[0], 100, lengths[3]]
+    for S in (1000, 500, 37):
+        got = ctx.dist(sk, sk[:20], S, use64=True, k=21, ref_lengths=lengths,
+                       qry_lengths=lengths[:20])
+        nu, de, di, pv = oracle.dist_grid(sk, lengths, sk[:20], lengths[:20], S, 21, 4.0 ** 21)
+        assert np.array_equal(got["numer"], nu)
+        assert np.array_equal(got["denom"], de)
+        np.testing.assert_allclose(got["distance"], di, rtol=RTOL, atol=0)
+        np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+    assert (got["numer"] > 0).any()
+
+
+def test_dist_unsorted_u32_fp(ctx, oracle):
+    """-fp lists: file-order u32 hashes with duplicates, walked literally."""
+    rng = np.random.default_rng(9)
+    base = rng.integers(0, 2 ** 32, size=3000, dtype=np.uint64).astype(np.uint32)
+    lists = []
+    for i in range(40):
+        n = int(rng.integers(0, 2100))
+        idx = rng.integers(0, 3000 if i % 2 else 200, size=n)
+        lists.append(base[idx])
+    lengths = [int(rng.integers(1, 20000)) for _ in lists]
+    for S in (1000, 2000, 5):
+        got = ctx.dist(lists, lists, S, use64=False, k=1, kmer_space=10.0, ref_lengths=lengths,
+                       qry_lengths=lengths)
+        nu, de, di, pv = oracle.dist_grid(lists, lengths, lists, lengths, S, 1, 10.0, use64=False)
+        assert np.array_equal(got["numer"], nu)
+        assert np.array_equal(got["denom"], de)
+        np.testing.assert_allclose(got["distance"], di, rtol=RTOL, atol=0)
+        np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+
+
+def test_dist_filters(ctx, oracle):
+    seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
+    lengths = [len(x) for x in seqs]
+    got = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths, max_dist=0.05,
+                   max_pvalue=1e-30)
+    nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, 1000, 21, 4.0 ** 21)
+    exp = (di <= 0.05) & (pv <= 1e-30)
+    assert np.array_equal(got["pass"], exp)
