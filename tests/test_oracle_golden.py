@@ -1,0 +1,172 @@
+"""CPU tests: pin the oracle to the reference's golden vectors and fixtures.
+
+tests/golden/ holds (a) data fixtures copied from the reference tree and
+(b) generated.json made by tests/golden/make_golden.py from the reference's own
+compiled hash/MinHashHeap sources (oracle/_ref) and 50-digit mpmath.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+import mshfmt
+import seqio
+
+GEN = json.load(open(os.path.join(GOLDEN, "generated.json")))
+
+
+def test_murmur_kats(oracle):
+    for c in GEN["murmur"]:
+        d = bytes.fromhex(c["data"])
+        assert oracle.get_hash(d, c["seed"], True) == int(c["h64"])
+        assert oracle.get_hash(d, c["seed"], False) == c["h32"]
+
+
+def test_survey_kats(oracle):
+    # SURVEY.md §8a rows a1, a5
+    assert oracle.get_hash(b"ACGTACGTACGTACGTACGTA", 42, True) == 13036166743686632327
+    assert oracle.get_hash_fp([8, 34, 57, 1], 42, False) == 819737709
+
+
+def test_fp_kats(oracle):
+    for c in GEN["fp"]:
+        v = [int(x) for x in c["vals"]]
+        assert oracle.get_hash_fp(v, 42, False) == c["h32"]
+        assert oracle.get_hash_fp(v, 42, True) == int(c["h64"])
+
+
+def test_sketch_kats_vs_reference_heap(oracle):
+    """Bottom-s sets + counts equal the reference MinHashHeap on the same k-mer stream."""
+    for c in GEN["sketch"]:
+        P = oracle.params(k=c["k"], s=c["s"], alphabet=c["alphabet"],
+                          noncanonical=bool(c["noncanonical"]))
+        assert P.use64 == c["use64"]
+        recs = [r.encode() for r in c["records"]]
+        got, cnt = oracle.sketch_batch(P, recs, groups=[0] * len(recs), n_groups=1, counts=True)
+        assert [int(x) for x in got[0]] == [int(x) for x in c["hashes"]]
+        assert [int(x) for x in cnt[0]] == c["counts"]
+
+
+def test_pvalue_vs_mpmath(oracle):
+    for row in GEN["pvalue"]:
+        q = float(row["q"])
+        got = oracle.binomial_q(row["x"] - 1, row["r"], row["n"])
+        if q < 1e-300:
+            assert got < 1e-290
+            continue
+        assert got == pytest.approx(q, rel=1e-12, abs=0), row
+
+
+def _fp_expected(name):
+    return mshfmt.read_msh(os.path.join(GOLDEN, name))
+
+
+@pytest.mark.parametrize("i", [1, 2, 3])
+def test_cfl_fixture_sketch(oracle, i):
+    """`mash sketch -fp DNA{i}-CFL.txt` == DNA{i}-sketch.msh (hashes in file order, names,
+    comments, the double-counted first-line length quirk)."""
+    text = open(os.path.join(GOLDEN, f"DNA{i}-CFL.txt"), "rb").read()
+    refs, used, _ = oracle.fp_references(text)
+    exp = _fp_expected(f"DNA{i}-sketch.msh")
+    assert exp["kmer"] == 1 and exp["alphabet"] == b"0123456789" and exp["noncanonical"]
+    assert used == 10000
+    assert len(refs) == len(exp["references"]) == 5
+    for (name, length, h), e in zip(refs, exp["references"]):
+        assert name == e["name"]
+        assert e["comment"] == b"FingerPrint : " + name
+        assert length == e["length"]
+        assert np.array_equal(h, e["hashes32"])
+
+
+def test_fp_line_cap(oracle):
+    """LIMIT_READ_FINGERPRINT (Sketch.cpp:37): at most 1,000,000 lines per invocation."""
+    text = b"".join(b"ID%d 1 2 3\n" % (i // 10) for i in range(25))
+    refs, used, _ = oracle.fp_references(text, limit=13)
+    assert used == 13
+    assert sum(len(h) for _, _, h in refs) == 13
+    # the cap carries across files
+    refs2, used2, _ = oracle.fp_references(b"X 1\nY 2\n", limit=13, lines_used=used)
+    assert refs2 == [] and used2 == 13
+
+
+def test_fp_parse_edge_cases(oracle):
+    ids, vals, used = oracle.fp_parse(b"A 1 2 3\nB\n\nC 4 x 5\r\nD -1 +7 18446744073709551615\n"
+                                      b"E 18446744073709551616 3\nF 12abc 4\nG")
+    assert ids == [b"A", b"B", b"", b"C", b"D", b"E", b"F", b"G"]
+    assert [list(map(int, v)) for v in vals] == [[1, 2, 3], [], [], [4], [2 ** 64 - 1, 7, 2 ** 64 - 1],
+                                                 [], [12], []]
+
+
+def test_reads_fixture_sketch(oracle):
+    """read1_2.msh: concatenated k=21 s=1000 sketches of reads1/2.fastq (reads with N)."""
+    exp = mshfmt.read_msh(os.path.join(GOLDEN, "read1_2.msh"))
+    P = oracle.params(k=21, s=1000)
+    for i, e in zip((1, 2), exp["references"]):
+        recs = seqio.read_records(os.path.join(GOLDEN, f"reads{i}.fastq.gz"))
+        seqs = [r[2] for r in recs]
+        got = oracle.sketch_batch(P, seqs, groups=[0] * len(seqs), n_groups=1)[0]
+        assert np.array_equal(got, e["hashes64"])
+        assert sum(len(s) for s in seqs if len(s) >= 21) == e["length"]
+        assert e["comment"].startswith(b"[%d seqs] " % len(seqs))
+
+
+def test_test_sequence_fixture(oracle):
+    exp = mshfmt.read_msh(os.path.join(GOLDEN, "test_sequence.msh"))
+    recs = seqio.read_records(os.path.join(GOLDEN, "test_sequence.fasta"))
+    seqs = [r[2] for r in recs]
+    got = oracle.sketch_batch(oracle.params(), seqs, groups=[0] * len(seqs), n_groups=1)[0]
+    e = exp["references"][0]
+    assert np.array_equal(got, e["hashes64"])
+    assert e["length"] == sum(len(s) for s in seqs) == 73
+    assert e["comment"] == b"[2 seqs] " + recs[0][0] + b" " + recs[0][1] + b" [...]"
+
+
+def _fmt(x):
+    """C++ ostream default formatting of a double (%g, precision 6)."""
+    return "%g" % x
+
+
+def test_genomes_dist_golden(oracle):
+    """mash/test/ref/genomes.dist: dist of genome{1,2,3}.fna.msh vs reads.msh."""
+    qry = mshfmt.read_msh(os.path.join(GOLDEN, "reads.msh"))["references"][0]
+    lines = open(os.path.join(GOLDEN, "genomes.dist")).read().splitlines()
+    for i, line in enumerate(lines, 1):
+        ref = mshfmt.read_msh(os.path.join(GOLDEN, f"genome{i}.fna.msh"))["references"][0]
+        nu, de = oracle.compare(ref["hashes64"], qry["hashes64"], 1000)
+        d = oracle.distance(nu, de, 21)
+        p = oracle.pvalue(nu, ref["length"], qry["length"], 4.0 ** 21, de)
+        name = os.path.basename(ref["name"].decode())
+        got = f"{name}\t{qry['name'].decode()}\t{_fmt(d)}\t{_fmt(p)}\t{nu}/{de}"
+        assert got == line
+
+
+def test_cfl_dist_self_and_cross(oracle):
+    """-fp dist on CFL sketches: self 1000/1000 (distance 0), DNA1 vs DNA2 0/1000."""
+    a = _fp_expected("DNA1-sketch.msh")["references"]
+    b = _fp_expected("DNA2-sketch.msh")["references"]
+    assert oracle.compare(a[0]["hashes32"], a[0]["hashes32"], 1000, use64=False) == (1000, 1000)
+    assert oracle.compare(a[0]["hashes32"], b[0]["hashes32"], 1000, use64=False) == (0, 1000)
+
+
+def test_cfl_generator_matches_lyn2vec_fixture():
+    """fpmash.datagen reproduces lyn2vec's DNA1-CFL.txt from DNA1.fasta byte for byte."""
+    from fpmash import datagen
+    recs = seqio.read_records(os.path.join(GOLDEN, "DNA1.fasta"))
+    out = b"".join(l.encode() for name, comment, seq in recs
+                   for l in datagen.cfl_lines(seq, comment.split()[0].decode()))
+    assert out == open(os.path.join(GOLDEN, "DNA1-CFL.txt"), "rb").read()
+
+
+def test_dist_grid_matches_pairwise(oracle):
+    rng = np.random.default_rng(1)
+    lists = [np.sort(rng.choice(2 ** 40, size=int(rng.integers(0, 300)), replace=False)).astype(np.uint64)
+             for _ in range(12)]
+    lengths = [int(rng.integers(100, 10000)) for _ in lists]
+    nu, de, di, pv = oracle.dist_grid(lists, lengths, lists[:5], lengths[:5], 200, 21, 4.0 ** 21,
+                                      threads=3)
+    for q in range(5):
+        for r in range(12):
+            n1, d1 = oracle.compare(lists[r], lists[q], 200)
+            assert (nu[q * 12 + r], de[q * 12 + r]) == (n1, d1)
