@@ -212,6 +212,7 @@ def main():
     ctx.set_timing(False)
     elapsed = grp.max(t1 - t0)
 
+    dstats = ctx.last_dist_stats()
     ktimes = {}
     for kid, name in fpmash.KERNEL_NAMES.items():
         tot, cnt = ctx.kernel_time(kid)
@@ -231,13 +232,19 @@ def main():
 
     # roofline of the dominant kernel (algorithmic bytes per launch / avg launch time)
     s = args.s
+    N = fpmash.KERNEL_NAMES
+    n_hash = int(cnt_host.sum())
     alg = {
-        "compare_grid_kernel": (2 * n * s * 8 + n_pairs * 8,
-                                f"(N_ref+N_qry)*s*8 B read + 8 B/pair written, N={n}, s={s}"),
-        "sketch_tiles_kernel": (info["seq_bytes"] + int(cnt_host.sum()) * 8,
-                                "packed sequence bytes read + 8 B per output hash"),
-        "dist_finalize_kernel": (n_pairs * (4 + 4 + 8 + 8 + 1),
-                                 "numer+denom read, dist+pvalue+pass written per pair"),
+        N[fpmash.K_SKETCH]: (info["seq_bytes"] + n_hash * 8,
+                             "packed sequence bytes read + 8 B per output hash"),
+        N[fpmash.K_INDEX]: (n_hash * 8,
+                            "reference sketch hashes read once (8 B each)"),
+        N[fpmash.K_PROBE]: (n_hash * 8 + n_pairs * 8,
+                            "query sketch hashes read + numer/denom (8 B/pair) written"),
+        N[fpmash.K_COMPARE]: (2 * n_hash * 8,
+                              "ref + query sketches read once (8 B per hash)"),
+        N[fpmash.K_FINALIZE]: (n_pairs * (4 + 4 + 8 + 8 + 1),
+                               "numer+denom read, distance+p-value+pass written per pair"),
     }
     dom = max(ktimes, key=lambda k_: ktimes[k_]["total_ms"])
     achieved = alg[dom][0] / (ktimes[dom]["avg_ms"] * 1e-3) / 1e9 if dom in alg else None
@@ -260,8 +267,11 @@ def main():
             per_kernel_roof[name] = {"avg_ms": ktimes[name]["avg_ms"], "alg_GBps": gbs,
                                      "frac_hbm": gbs / HBM_PEAK_GBS}
 
-    sk_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in ("sketch_tiles_kernel", "merge_kernel")) / args.steps
-    di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in ("compare_grid_kernel", "dist_finalize_kernel")) / args.steps
+    sk_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_SKETCH, fpmash.K_MERGE)]
+    di_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_INDEX, fpmash.K_PROBE,
+                                                  fpmash.K_COMPARE, fpmash.K_FINALIZE)]
+    sk_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in sk_names) / args.steps
+    di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in di_names) / args.steps
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
@@ -293,7 +303,10 @@ def main():
                        "kmers": info["n_kmers"]},
             "dist": {"mpairs_per_s": total_pairs / args.steps / (di_ms * 1e-3) / 1e6 if di_ms else None,
                      "device_ms_per_step": di_ms,
-                     "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean())},
+                     "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
+                     "path": ["dense walk", "inverted index + literal walk",
+                              "inverted index + sorted merge"][int(dstats["sparse"])],
+                     "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,

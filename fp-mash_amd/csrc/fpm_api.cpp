@@ -57,7 +57,31 @@ struct fpm_ctx {
     hipStream_t stream = nullptr;
     bool timing = false;
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
+    // grow-only device scratch, one buffer per named slot (no allocation in steady state)
+    struct Slot { void *p = nullptr; size_t bytes = 0; };
+    Slot scratch[12];
+    unsigned long long *host_counters = nullptr;   // pinned, for the events read-back
+    int dist_mode = FPM_DIST_AUTO;
+    int last_sparse = 0;
+    uint64_t last_events = 0, last_cand = 0;
 };
+
+// returns a device buffer of at least `bytes` for scratch slot `id`
+static hipError_t scratch(fpm_ctx *ctx, int id, size_t bytes, void **out)
+{
+    auto &s = ctx->scratch[id];
+    if (s.bytes < bytes) {
+        if (s.p) { hipError_t e = hipFree(s.p); if (e != hipSuccess) return e; }
+        s.p = nullptr;
+        s.bytes = 0;
+        size_t b = bytes + bytes / 8 + 256;
+        hipError_t e = hipMalloc(&s.p, b);
+        if (e != hipSuccess) return e;
+        s.bytes = b;
+    }
+    *out = s.p;
+    return hipSuccess;
+}
 
 // RAII-free event bracket: records start before and stop after a launch.
 struct TimedLaunch {
@@ -137,6 +161,9 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     fpm_ctx_reset_timing(ctx);
+    for (auto &s : ctx->scratch)
+        if (s.p) (void)hipFree(s.p);
+    if (ctx->host_counters) (void)hipHostFree(ctx->host_counters);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -186,6 +213,27 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes)
     if (int rc = set_device(ctx)) return rc;
     if (bytes) HIP_TRY(hipMemsetAsync(dptr, value, bytes, ctx->stream));
     HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return FPM_OK;
+}
+
+int fpm_ctx_set_dist_mode(fpm_ctx *ctx, int mode)
+{
+    if (!ctx || mode < FPM_DIST_AUTO || mode > FPM_DIST_SPARSE) return fail(FPM_EINVAL, "bad dist mode");
+    ctx->dist_mode = mode;
+    return FPM_OK;
+}
+
+int fpm_ctx_last_dist_stats(fpm_ctx *ctx, int *sparse, uint64_t *events, uint64_t *candidates)
+{
+    if (!ctx) return fail(FPM_EINVAL, "null context");
+    if (sparse) *sparse = ctx->last_sparse;
+    if (events) *events = ctx->last_events;
+    if (ctx->last_cand == (uint64_t)-1) {
+        if (int rc = set_device(ctx)) return rc;
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        ctx->last_cand = ctx->host_counters[65];
+    }
+    if (candidates) *candidates = ctx->last_cand;
     return FPM_OK;
 }
 
@@ -569,10 +617,99 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     if (int rc = set_device(ctx)) return rc;
     if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
     hipStream_t st = pick_stream(ctx, stream);
+    const uint64_t n_pairs = (uint64_t)n_ref * n_qry;
+    ctx->last_sparse = 0;
+    ctx->last_events = 0;
+    ctx->last_cand = 0;
+    if (n_pairs == 0) return FPM_OK;
+    const uint64_t E = (uint64_t)n_ref * ref_stride;   // index entries (upper bound)
+    bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
+                      (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
+    if (E == 0) try_sparse = false;
+    if (try_sparse) {
+        int log2t = 10;
+        while ((1ULL << log2t) < 2 * E) log2t++;
+        if (log2t > 31) return fail(FPM_EINVAL, "reference set too large for one index");
+        const uint64_t T = 1ULL << log2t;
+        void *keys, *cnt, *off, *cursor, *slot_of, *postings, *scan_s, *ctr;
+        HIP_TRY(scratch(ctx, 0, (T + 1) * 8, &keys));
+        HIP_TRY(scratch(ctx, 1, (T + 1) * 4, &cnt));
+        HIP_TRY(scratch(ctx, 2, (T + 2) * 4, &off));
+        HIP_TRY(scratch(ctx, 3, (T + 2) * 4, &cursor));
+        HIP_TRY(scratch(ctx, 4, E * 4, &slot_of));
+        HIP_TRY(scratch(ctx, 5, E * 4, &postings));
+        HIP_TRY(scratch(ctx, 6, scan_scratch_words(T + 1) * 4, &scan_s));
+        HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
+        if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
+        // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag
+        unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
+        uint32_t *unsorted = (uint32_t *)(events + 66);
+        {
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(hipMemsetAsync(keys, 0xFF, (T + 1) * 8, st));
+            HIP_TRY(hipMemsetAsync(cnt, 0, (T + 1) * 4, st));
+            HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+            HIP_TRY(launch_idx_insert(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
+                                      (uint64_t *)keys, (uint32_t *)cnt, (uint32_t *)slot_of, log2t,
+                                      unsorted, st));
+            HIP_TRY(launch_exscan((const uint32_t *)cnt, (uint32_t *)off, (uint32_t *)cursor, T + 1,
+                                  (uint32_t *)scan_s, (uint32_t *)off + T + 1, st));
+            HIP_TRY(launch_idx_scatter(d_ref_len, ref_stride, n_ref, (const uint32_t *)slot_of,
+                                       (uint32_t *)cursor, (uint32_t *)postings, st));
+            HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                       (const uint64_t *)keys, (const uint32_t *)off, log2t, events,
+                                       unsorted, st));
+            tl.done();
+        }
+        HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const uint64_t ev = ctx->host_counters[0];
+        const bool all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
+        ctx->last_events = ev;
+        const bool sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
+                            (long double)ev * 4.0L <= (long double)n_pairs * sketch_size;
+        if (sparse) {
+            const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(ev, n_pairs));
+            void *cand, *row_seg;
+            HIP_TRY(scratch(ctx, 8, cap * 8, &cand));
+            HIP_TRY(scratch(ctx, 9, (size_t)n_qry * 8, &row_seg));
+            const uint64_t lcap = std::max(ref_stride, qry_stride);
+            const bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
+                                    lcap <= 3072;
+            {
+                TimedLaunch tl(ctx, FPM_K_PROBE, st);
+                HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
+                                          (const uint64_t *)keys, (const uint32_t *)off,
+                                          (const uint32_t *)postings, log2t, d_ref_len, sketch_size,
+                                          d_numer, d_denom, (uint64_t *)cand, n_cand,
+                                          (uint64_t *)row_seg, st));
+                tl.done();
+            }
+            {
+                TimedLaunch tl(ctx, FPM_K_COMPARE, st);
+                if (rows_merge)
+                    HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
+                                              (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                                              (const uint64_t *)d_qry, d_qry_len, qry_stride,
+                                              sketch_size, d_numer, d_denom, st));
+                else
+                    HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
+                                                   d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
+                                                   qry_stride, hash_bytes, sketch_size, d_numer,
+                                                   d_denom, st));
+                tl.done();
+            }
+            HIP_TRY(hipMemcpyAsync(ctx->host_counters + 65, n_cand, 8, hipMemcpyDeviceToHost, st));
+            ctx->last_sparse = rows_merge ? 2 : 1;
+            ctx->last_cand = (uint64_t)-1;   // read lazily by fpm_ctx_last_dist_stats callers after sync
+            return FPM_OK;
+        }
+    }
     TimedLaunch tl(ctx, FPM_K_COMPARE, st);
     HIP_TRY(launch_compare_grid(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
                                 n_qry, hash_bytes, sketch_size, d_numer, d_denom, st));
     tl.done();
+    ctx->last_cand = n_pairs;
     return FPM_OK;
 }
 

@@ -54,6 +54,40 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
                                uint32_t sketch_size, uint32_t *d_numer, uint32_t *d_denom,
                                hipStream_t st);
 
+hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                  uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
+                                  uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                  const uint32_t *d_qry_len, uint64_t qry_stride,
+                                  uint32_t hash_bytes, uint32_t S, uint32_t *d_numer,
+                                  uint32_t *d_denom, hipStream_t st);
+
+// inverted index over ref hashes (dist_index.hip)
+hipError_t launch_idx_insert(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
+                             uint32_t n_ref, uint32_t hash_bytes, uint64_t *keys, uint32_t *cnt,
+                             uint32_t *slot_of, int log2t, uint32_t *unsorted, hipStream_t st);
+hipError_t launch_idx_scatter(const uint32_t *d_ref_len, uint64_t stride, uint32_t n_ref,
+                              const uint32_t *slot_of, uint32_t *cursor, uint32_t *postings,
+                              hipStream_t st);
+uint64_t scan_scratch_words(uint64_t n);
+hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
+                         uint32_t *scratch, uint32_t *total, hipStream_t st);
+hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
+                              uint32_t n_qry, uint32_t hash_bytes, const uint64_t *keys,
+                              const uint32_t *off, int log2t, unsigned long long *events,
+                              uint32_t *unsorted, hipStream_t st);
+hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
+                             uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes,
+                             const uint64_t *keys, const uint32_t *off, const uint32_t *postings,
+                             int log2t, const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
+                             uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
+                             uint64_t *row_seg, hipStream_t st);
+// sorted-distinct candidates: one workgroup per query row, one wave per pair
+hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
+                             const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                             uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
+                             uint64_t qry_stride, uint32_t S, uint32_t *d_numer,
+                             uint32_t *d_denom, hipStream_t st);
+
 hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
                                 const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,

@@ -20,10 +20,12 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfpmash.so")
 BIN_PATH = os.path.join(PKG_ROOT, "bin", "fpmash")
 
 FPM_OK, FPM_EINVAL, FPM_ENODEV, FPM_EHIP, FPM_ENOMEM = 0, -1, -2, -3, -4
-K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE = range(5)
+K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE, K_INDEX, K_PROBE = range(7)
 KERNEL_NAMES = {K_SKETCH: "sketch_tiles_kernel", K_MERGE: "merge_kernel",
-                K_FPHASH: "fp_hash_kernel", K_COMPARE: "compare_grid_kernel",
-                K_FINALIZE: "dist_finalize_kernel"}
+                K_FPHASH: "fp_hash_kernel", K_COMPARE: "walk (compare_grid/walk_cand)",
+                K_FINALIZE: "dist_finalize_kernel", K_INDEX: "dist index build",
+                K_PROBE: "probe_rows_kernel"}
+DIST_AUTO, DIST_DENSE, DIST_SPARSE = 0, 1, 2
 
 ALPHABET_NUCLEOTIDE = "ACGT"                     # Sketch.h alphabetNucleotide
 ALPHABET_PROTEIN = "ACDEFGHIKLMNPQRSTVWY"         # Sketch.h alphabetProtein
@@ -51,6 +53,8 @@ SYMBOLS = [
     ("fpm_ctx_set_timing", C.c_int, [vp, C.c_int]),
     ("fpm_ctx_reset_timing", C.c_int, [vp]),
     ("fpm_ctx_kernel_time", C.c_int, [vp, C.c_int, f64p, u64p]),
+    ("fpm_ctx_set_dist_mode", C.c_int, [vp, C.c_int]),
+    ("fpm_ctx_last_dist_stats", C.c_int, [vp, C.POINTER(C.c_int), u64p, u64p]),
     ("fpm_sketch_batch", C.c_int, [vp, vp, C.c_char_p, u64p, C.c_uint32, u32p, C.c_uint32,
                                    u64p, u32p]),
     ("fpm_sketch_stage", C.c_int, [vp, vp, C.c_char_p, u64p, C.c_uint32, u32p, C.c_uint32,
@@ -278,6 +282,14 @@ class Context:
         t, n = C.c_double(), C.c_uint64()
         _check(lib().fpm_ctx_kernel_time(self.h, kernel, C.byref(t), C.byref(n)))
         return t.value, n.value
+
+    def set_dist_mode(self, mode):
+        _check(lib().fpm_ctx_set_dist_mode(self.h, mode))
+
+    def last_dist_stats(self):
+        sp, ev, ca = C.c_int(), C.c_uint64(), C.c_uint64()
+        _check(lib().fpm_ctx_last_dist_stats(self.h, C.byref(sp), C.byref(ev), C.byref(ca)))
+        return {"sparse": sp.value, "events": ev.value, "candidates": ca.value}
 
     # --- sketch -----------------------------------------------------------
     def sketch(self, params, seqs, groups=None, n_groups=None):

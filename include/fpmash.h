@@ -73,17 +73,31 @@ int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 
 /* Per-kernel timing with HIP events recorded on the launch stream.
- * kernel ids: 0 sketch tiles, 1 sketch merge, 2 fp hash, 3 compare, 4 finalize. */
+ * kernel ids: sketch tiles, sketch merge, fp hash, compare walk, finalize,
+ * dist index build (insert + scan + scatter + probe count), dist row probe. */
 #define FPM_K_SKETCH 0
 #define FPM_K_MERGE 1
 #define FPM_K_FPHASH 2
 #define FPM_K_COMPARE 3
 #define FPM_K_FINALIZE 4
-#define FPM_K_COUNT 5
+#define FPM_K_INDEX 5
+#define FPM_K_PROBE 6
+#define FPM_K_COUNT 7
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */
 int fpm_ctx_kernel_time(fpm_ctx *ctx, int kernel, double *total_ms, uint64_t *launches);
+
+/* dist strategy: FPM_DIST_AUTO picks the inverted-index path unless the shared-hash
+ * events exceed pairs*S/4; DENSE walks every pair; SPARSE always uses the index.
+ * All three give identical results. */
+#define FPM_DIST_AUTO 0
+#define FPM_DIST_DENSE 1
+#define FPM_DIST_SPARSE 2
+int fpm_ctx_set_dist_mode(fpm_ctx *ctx, int mode);
+/* statistics of the last compare: path (0 dense walk, 1 index + literal walk of the
+ * candidates, 2 index + sorted-set merge of the candidates), posting events, candidates */
+int fpm_ctx_last_dist_stats(fpm_ctx *ctx, int *sparse, uint64_t *events, uint64_t *candidates);
 
 /* ---- k-mer sketch ------------------------------------------------------------
  * Replaces addMinHashes (Sketch.cpp:664-735) + MinHashHeap::tryInsert

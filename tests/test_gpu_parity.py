@@ -121,7 +121,16 @@ def _family_sketches(oracle, n_fam=6, members=8, L=2000, k=21, s=1000, seed=0):
     return seqs, sk
 
 
-def test_dist_sorted_u64(ctx, oracle):
+@pytest.fixture(params=["auto", "dense", "sparse"])
+def dist_mode(request, ctx):
+    import fpmash
+    ctx.set_dist_mode({"auto": fpmash.DIST_AUTO, "dense": fpmash.DIST_DENSE,
+                       "sparse": fpmash.DIST_SPARSE}[request.param])
+    yield request.param
+    ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
+def test_dist_sorted_u64(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle)
     lengths = [len(x) for x in seqs]
     # uneven sketch sizes, empty lists, truncated sketch size
@@ -138,7 +147,7 @@ def test_dist_sorted_u64(ctx, oracle):
     assert (got["numer"] > 0).any()
 
 
-def test_dist_unsorted_u32_fp(ctx, oracle):
+def test_dist_unsorted_u32_fp(ctx, oracle, dist_mode):
     """-fp lists: file-order u32 hashes with duplicates, walked literally."""
     rng = np.random.default_rng(9)
     base = rng.integers(0, 2 ** 32, size=3000, dtype=np.uint64).astype(np.uint32)
@@ -158,7 +167,7 @@ def test_dist_unsorted_u32_fp(ctx, oracle):
         np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
 
 
-def test_dist_filters(ctx, oracle):
+def test_dist_filters(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
     lengths = [len(x) for x in seqs]
     got = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths, max_dist=0.05,
@@ -166,3 +175,24 @@ def test_dist_filters(ctx, oracle):
     nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, 1000, 21, 4.0 ** 21)
     exp = (di <= 0.05) & (pv <= 1e-30)
     assert np.array_equal(got["pass"], exp)
+
+
+def test_dist_sparse_large_grid(ctx, oracle):
+    """A grid big enough for AUTO to pick the inverted index: counts match a dense run
+    and the oracle on a sampled block."""
+    import fpmash
+    seqs, sk = _family_sketches(oracle, n_fam=20, members=30, seed=3)
+    lengths = [len(x) for x in seqs]
+    ctx.set_dist_mode(fpmash.DIST_AUTO)
+    a = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths)
+    st = ctx.last_dist_stats()
+    assert st["sparse"] and 0 < st["candidates"] < len(sk) ** 2
+    ctx.set_dist_mode(fpmash.DIST_DENSE)
+    b = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths)
+    ctx.set_dist_mode(fpmash.DIST_AUTO)
+    for key in ("numer", "denom", "distance", "pvalue", "pass"):
+        assert np.array_equal(a[key], b[key]), key
+    nu, de, di, pv = oracle.dist_grid(sk, lengths, sk[:50], lengths[:50], 1000, 21, 4.0 ** 21)
+    n = len(sk)
+    assert np.array_equal(a["numer"][:50 * n], nu)
+    assert np.array_equal(a["denom"][:50 * n], de)
