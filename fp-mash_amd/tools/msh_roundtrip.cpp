@@ -1,0 +1,30 @@
+// msh_roundtrip — test tool: parse a .msh (no truncation) and re-serialize it with
+// the writer; prints "same" when the bytes are identical.  CPU only.
+#include "Msh.h"
+
+#include <fstream>
+#include <iostream>
+#include <sstream>
+
+int main(int argc, char **argv)
+{
+    if (argc < 2) { std::cerr << "usage: msh_roundtrip in.msh [out.msh]\n"; return 2; }
+    std::ifstream in(argv[1], std::ios::binary);
+    std::stringstream ss;
+    ss << in.rdbuf();
+    const std::string data = ss.str();
+    fpmhost::MshHeader h;
+    std::vector<fpmhost::MshReference> r64, r32;
+    std::string err;
+    if (!fpmhost::mshParse(data, h, &r64, true, ~0ULL, err) ||
+        !fpmhost::mshParse(data, h, &r32, false, ~0ULL, err)) { std::cerr << err << "\n"; return 2; }
+    bool use64 = false;
+    for (auto &r : r64) if (!r.hashes.empty()) use64 = true;
+    auto &refs = use64 ? r64 : r32;
+    bool counts = false;
+    for (auto &r : refs) if (!r.counts.empty()) counts = true;
+    const std::string out = fpmhost::mshSerialize(h, refs, use64, counts);
+    if (argc > 2) std::ofstream(argv[2], std::ios::binary) << out;
+    std::cout << (out == data ? "same" : "differs") << " " << data.size() << " " << out.size() << "\n";
+    return out == data ? 0 : 1;
+}
