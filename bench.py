@@ -54,6 +54,15 @@ def parse():
     return ap.parse_args()
 
 
+def parse_args_for_test(**kw):
+    """Defaults of parse() with overrides (tests)."""
+    a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
+                           k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0)
+    for k_, v in kw.items():
+        setattr(a, k_, v)
+    return a
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
