@@ -314,7 +314,7 @@ def main():
                      "device_ms_per_step": di_ms,
                      "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
                      "path": ["dense walk", "inverted index + literal walk",
-                              "inverted index + sorted merge"][int(dstats["sparse"])],
+                              "bucket index + bucketed rank"][int(dstats["sparse"])],
                      "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,

@@ -82,96 +82,187 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 }
 
 // Sorted, distinct lists (every sketch the k-mer path produces): the walk of
-// compareSketches is a merge of two sets, so with the shared values c_0 < c_1 < ...
-// at (i_k, j_k) in (A, B): walk step of c_k = union rank = i_k + j_k - k, hence
-//   numer = #{k : i_k + j_k - k < S},  denom = min(S, |A| + |B| - #shared).
-// One workgroup per query row (B staged in LDS once), one wave per candidate ref
-// (A staged in the wave's LDS slice with coalesced loads); lane l owns A's chunk
-// [l*CH, (l+1)*CH): one binary search into B, then a linear co-walk.
-constexpr int kMergeWaves = 8;
+// compareSketches (CommandDistance.cpp:365-398) is a merge of two sets and visits the
+// union elements in ascending order, so with U(c) = the union rank of value c
+//   numer = #{shared c : U(c) < S},   denom = min(S, |A| + |B| - #shared).
+// For A[i] = c with j = #{B < c} and k = #{shared values below c}: U(c) = i + j - k.
+//
+// Rank kernel, one workgroup per query row B, one wave per candidate ref row A:
+//  * B is staged once in LDS together with a bucket table over its value range
+//    (bucket = value >> shift, 4 buckets per B slot, so <= 0.5 B elements per bucket);
+//    bucket b holds the B positions [lo, hi) whose values fall in it.
+//  * lane l takes A[64t + l] (coalesced 512-byte buffer loads, prefetched one candidate
+//    ahead into registers); j comes from a fixed-length binary search inside the bucket
+//    (the row's largest bucket sets the step count, typically 2-3), equality from B[j].
+//  * k is a running ballot count: popc of this chunk's shared lanes below l + earlier chunks.
+//  * when max(|A|, |B|) >= S, denom is S whatever #shared is, and no A element after the
+//    first one whose union rank reaches S can count: the wave stops there (about half of A
+//    for unrelated pairs).
+// No per-wave LDS image and no merge walk: ~5 LDS reads and ~40 VALU per A element.
+constexpr int kRankWaves = 8;
 
-template <int CH>
-__global__ __launch_bounds__(512) void merge_rows_kernel(
-    const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg,
+template <int CAP>
+__global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
+    const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
     const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const uint64_t *__restrict__ qry, const uint32_t *__restrict__ qry_len,
     uint64_t qry_stride, uint32_t S, uint32_t *__restrict__ numer, uint32_t *__restrict__ denom)
 {
-    extern __shared__ __attribute__((aligned(16))) uint64_t Bs[];
-    const uint32_t q = blockIdx.x;
+    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 12 : 13;   // 4 * CAP buckets
+    constexpr uint32_t kBuckets = 1u << kLogBuckets;
+    constexpr int kChunks = CAP / 64;
+    __shared__ uint64_t Bs[CAP + 1];
+    __shared__ uint32_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
+    __shared__ uint32_t s_maxn;
+    const uint32_t q = xcd_row(blockIdx.x, n_qry);
+    if (q >= n_qry) return;
     const uint64_t seg = row_seg[q];
     const uint32_t n = (uint32_t)(seg & 0xFFFFFF);
     if (n == 0) return;
     const uint64_t base = seg >> 24;
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
     const uint64_t *B = qry + (uint64_t)q * qry_stride;
-    // B[m] lives at m + m/16: lanes co-walk B ~16 elements apart, and an unpadded
-    // 128-byte lane stride would put 16 lanes of a half-wave on one bank pair
-    auto P = [](uint32_t m) { return m + (m >> 4); };
-    for (uint32_t t = threadIdx.x; t < lb; t += blockDim.x) Bs[P(t)] = B[t];
+    if (threadIdx.x == 0) s_maxn = 0;
+    for (uint32_t t = threadIdx.x; t < lb; t += blockDim.x) Bs[t] = B[t];
+    if (threadIdx.x == 0) Bs[lb] = 0;
     __syncthreads();
-    constexpr uint32_t kInvalid = 0xFFFFFFFFu;
-    uint64_t o_next = wave < n ? cand[base + wave] : 0;
-    for (uint32_t c = wave; c < n; c += kMergeWaves) {
-        const uint64_t o = o_next;
-        const uint32_t r = (uint32_t)(o % n_ref);
-        const uint32_t la = ref_len[r];
-        if (c + kMergeWaves < n) o_next = cand[base + c + kMergeWaves];
-        const uint64_t *A = ref + (uint64_t)r * ref_stride;
-        // lane owns A[i0, i0+CH): batched 16-byte loads into registers
-        const uint32_t i0 = lane * CH;
-        uint64_t a[CH];
-        if (i0 + CH <= la && (((uintptr_t)(A + i0)) & 15) == 0) {
-            const ulonglong2 *p = reinterpret_cast<const ulonglong2 *>(A + i0);
-#pragma unroll
-            for (int t = 0; t < CH / 2; t++) { ulonglong2 v = p[t]; a[2 * t] = v.x; a[2 * t + 1] = v.y; }
+    const uint64_t bmax = lb ? Bs[lb - 1] : 0;
+    const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
+    const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
+    // bucket b = values [b << shift, (b + 1) << shift) = B positions [Bkt[b], Bkt[b + 1])
+    for (uint32_t b = threadIdx.x; b <= kBuckets; b += blockDim.x) {
+        uint32_t lo = 0;
+        if (b == kBuckets || ((uint64_t)b << shift) > bmax) {
+            lo = (b == 0) ? 0 : lb;                       // at or past the end of B
         } else {
-#pragma unroll
-            for (int t = 0; t < CH; t++) a[t] = (i0 + t < la) ? A[i0 + t] : ~0ULL;
-        }
-        // co-walk my chunk against B: position of each shared value
-        uint32_t sum_ij[CH];
-        uint32_t dups = 0;
-        uint32_t j = 0;
-        if (i0 < la) {
-            const uint64_t x = a[0];
-            uint32_t lo = 0, hi = lb;
-            while (lo < hi) { uint32_t m = (lo + hi) >> 1; if (Bs[P(m)] < x) lo = m + 1; else hi = m; }
-            j = lo;
-        }
-#pragma unroll
-        for (int t = 0; t < CH; t++) {
-            sum_ij[t] = kInvalid;
-            if (i0 + t < la) {
-                const uint64_t x = a[t];
-                while (j < lb && Bs[P(j)] < x) j++;
-                if (j < lb && Bs[P(j)] == x) { sum_ij[t] = i0 + t + j; dups++; j++; }
+            const uint64_t v = (uint64_t)b << shift;
+            uint32_t len = lb;
+            while (len > 0) {                             // lower_bound in Bs
+                const uint32_t half = len >> 1;
+                if (Bs[lo + half] < v) { lo += half + 1; len -= half + 1; }
+                else len = half;
             }
         }
-        // k of my first shared value = shared values owned by lower lanes
-        uint32_t incl = dups;
+        Bkt[b] = lo;
+    }
+    __syncthreads();
+    uint32_t mx = 0;
+    for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x) mx = max(mx, Bkt[b + 1] - Bkt[b]);
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            uint32_t y = __shfl_up(incl, d, 64);
-            if ((int)lane >= d) incl += y;
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+    if (lane == 0) atomicMax(&s_maxn, mx);
+    __syncthreads();
+    const uint32_t steps = 32 - __clz(s_maxn);          // lower_bound steps for the largest bucket
+
+    const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
+    const uint64_t pair_row = (uint64_t)q * n_ref;
+    uint64_t regs[kChunks];
+    auto issue_row = [&](uint64_t o, uint32_t &la_out) {
+        const uint32_t rr = __builtin_amdgcn_readfirstlane((uint32_t)(o - pair_row));
+        la_out = ref_len[rr];
+        const uintptr_t Ar = (uintptr_t)(ref + (uint64_t)rr * ref_stride);
+        const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)Ar);
+        const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(Ar >> 32));
+        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            (void *)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(ld * 8u),
+            0x00020000);
+#pragma unroll
+        for (int t = 0; t < kChunks; t++) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (t * 64 + lane) * 8u, 0, 0);
+            regs[t] = ((uint64_t)v[1] << 32) | v[0];
         }
-        uint32_t k = incl - dups;
-        const uint32_t total = __shfl(incl, 63, 64);
-        uint32_t cnt = 0;
+    };
+    auto cand_at = [&](uint32_t cc) -> uint64_t {
+        return cand[base + __builtin_amdgcn_readfirstlane(cc)];
+    };
+    // CAP 1024: the next candidate's row is in flight while this one is ranked (2 x 32
+    // VGPRs); CAP 2048 would need 128, so there the row is loaded at the top of its turn.
+    constexpr bool kPrefetch = CAP <= 1024;
+    uint64_t o_cur = 0, o_nxt = 0;
+    uint32_t la_cur = 0;
+    if (kPrefetch && wave < n) { o_cur = cand_at(wave); issue_row(o_cur, la_cur); }
+    if (kPrefetch && wave + kRankWaves < n) o_nxt = cand_at(wave + kRankWaves);
+    for (uint32_t c = wave; c < n; c += kRankWaves) {
+        uint64_t o;
+        uint32_t la;
+        uint64_t A[kChunks];
+        if (kPrefetch) {
+            o = o_cur;
+            la = la_cur;
 #pragma unroll
-        for (int t = 0; t < CH; t++) {
-            if (sum_ij[t] != kInvalid) {
-                if (sum_ij[t] - k < S) cnt++;
-                k++;
+            for (int t = 0; t < kChunks; t++) A[t] = regs[t];
+            if (c + kRankWaves < n) {
+                o_cur = o_nxt;
+                issue_row(o_cur, la_cur);
+                if (c + 2 * kRankWaves < n) o_nxt = cand_at(c + 2 * kRankWaves);
+            }
+        } else {
+            o = cand_at(c);
+            issue_row(o, la);
+#pragma unroll
+            for (int t = 0; t < kChunks; t++) A[t] = regs[t];
+        }
+        const bool need_all = la < S && lb < S;           // denom depends on #shared
+        const uint32_t nch = (la + 63) / 64;
+        uint32_t shared_below = 0, cnt = 0;
+        bool done = false;                                // wave-uniform
+        // kGroup chunks at a time: their bucket reads and search steps are independent,
+        // so each LDS round trip carries kGroup reads; the early-exit test is per group.
+        constexpr int kGroup = 4;
+#pragma unroll
+        for (int g0 = 0; g0 < kChunks; g0 += kGroup) {
+            if (done || (uint32_t)g0 >= nch) continue;
+            uint32_t lo[kGroup], len[kGroup];
+            bool act[kGroup];
+#pragma unroll
+            for (int g = 0; g < kGroup; g++) {
+                const uint32_t i = (g0 + g) * 64 + lane;
+                const uint64_t a = A[g0 + g];
+                act[g] = i < la && lb && a <= bmax;
+                // every index below stays inside the LDS arrays (bk < kBuckets, lo + half
+                // <= lb <= CAP), so the reads are unconditional and the tests bitwise: a
+                // short-circuit && would become a branch with its own lgkmcnt(0) wait
+                const uint32_t bk = act[g] ? (uint32_t)(a >> shift) : 0;
+                const uint32_t b0 = Bkt[bk], b1 = Bkt[bk + 1];
+                lo[g] = b0;
+                len[g] = act[g] ? b1 - b0 : 0;
+            }
+            for (uint32_t st = 0; st < steps; st++) {
+#pragma unroll
+                for (int g = 0; g < kGroup; g++) {
+                    const uint32_t half = len[g] >> 1;
+                    const uint64_t bv = Bs[lo[g] + half];
+                    const bool less = (len[g] != 0) & (bv < A[g0 + g]);
+                    lo[g] = less ? lo[g] + half + 1 : lo[g];
+                    len[g] = less ? len[g] - half - 1 : half;
+                }
+            }
+#pragma unroll
+            for (int g = 0; g < kGroup; g++) {
+                const uint32_t t = g0 + g;
+                if (t >= nch) break;                      // uniform
+                const uint32_t i = t * 64 + lane;
+                const uint32_t j = act[g] ? lo[g] : lb;
+                const uint64_t bj = Bs[j];
+                const bool eq = act[g] & (j < lb) & (bj == A[t]);
+                const uint64_t bal = __ballot(eq);
+                const uint32_t k = shared_below + __builtin_amdgcn_mbcnt_hi(
+                                       (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                const uint32_t u = i + j - k;             // union rank of A[i] (valid lanes)
+                cnt += __popcll(__ballot(eq && u < S));
+                shared_below += __popcll(bal);
+                if (!need_all && g == kGroup - 1) {
+                    // union rank of the group's last valid element; later A elements rank higher
+                    const uint32_t last = min(la - 1 - t * 64, 63u);
+                    if ((uint32_t)__builtin_amdgcn_readlane((int)u, (int)last) >= S) done = true;
+                }
             }
         }
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) cnt += __shfl_down(cnt, d, 64);
         if (lane == 0) {
-            const uint64_t u = (uint64_t)la + lb - total;
             numer[o] = cnt;
-            denom[o] = u < S ? (uint32_t)u : S;
+            const uint64_t un = (uint64_t)la + lb - shared_below;
+            denom[o] = need_all ? (un < S ? (uint32_t)un : S) : S;
         }
     }
 }
@@ -183,17 +274,16 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              uint32_t *d_denom, hipStream_t st)
 {
     if (!n_qry) return hipSuccess;
-    const size_t lds = (size_t)(qry_stride + qry_stride / 16 + 1) * 8;
-    const dim3 g(n_qry), b(64 * kMergeWaves);
-    if (ref_stride <= 64 * 16)
-        hipLaunchKernelGGL(merge_rows_kernel<16>, g, b, lds, st, d_cand, row_seg, d_ref, d_ref_len,
-                           ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
-    else if (ref_stride <= 64 * 32)
-        hipLaunchKernelGGL(merge_rows_kernel<32>, g, b, lds, st, d_cand, row_seg, d_ref, d_ref_len,
-                           ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
-    else if (ref_stride <= 64 * 48)
-        hipLaunchKernelGGL(merge_rows_kernel<48>, g, b, lds, st, d_cand, row_seg, d_ref, d_ref_len,
-                           ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
+    const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
+    const uint64_t cap = std::max(ref_stride, qry_stride);
+    if (cap <= 1024)
+        hipLaunchKernelGGL(rank_rows_kernel<1024>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
+                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer,
+                           d_denom);
+    else if (cap <= 2048)
+        hipLaunchKernelGGL(rank_rows_kernel<2048>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
+                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer,
+                           d_denom);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -1,18 +1,24 @@
-// dist_index.hip — sparse all-pairs dist for gfx950: inverted index + row bitmaps.
+// dist_index.hip — sparse all-pairs dist for gfx950: bucket index + row bitmaps.
 //
 // compareSketches (CommandDistance.cpp:365-430) walks <= S steps for EVERY pair.
 // Observation used here: if two lists share no value, the literal walk never hits
 // the equal branch, so it ends with common = 0 and denom = min(S, lenA + lenB) —
 // for sorted sketches and for the unsorted -fp lists alike.  So only pairs that
 // share at least one hash ("candidates") need the walk.  The candidates come from
-// an inverted index over the reference lists:
-//   1. insert every ref hash into an open-addressing table (key -> slot), count
-//      postings per slot, exclusive-scan, scatter ref ids into posting lists;
-//   2. one workgroup per query row probes its hashes and ORs the ref ids of every
-//      posting into a row bitmap held in LDS (no global atomics), then writes the
-//      row bitmap and appends the row's candidate pairs;
-//   3. the literal walk (dist.hip) runs on the candidates only; dist_finalize
-//      writes (0, min(S, la+lb)) for every other pair.
+// an index over the reference lists:
+//   1. bucket index: every ref hash becomes one packed u64 entry (key remainder << rbits
+//      | ref id) in a bucket array grouped by the key's top `nbits` bits, with a
+//      directory dir[b] = first entry of bucket b.  Hashes are uniform (MurmurHash3), so
+//      this is a two-level counting sort with no global atomics: per-tile LDS histograms
+//      of the top 10 bits + one exclusive scan place every entry in its partition, then
+//      one workgroup per partition counting-sorts it by the next l2 bits in LDS and
+//      writes its slice of the directory;
+//   2. one workgroup per query row looks up the bucket of each of its hashes; each wave
+//      flattens the buckets of 64 hashes into one event range and reads it coalesced,
+//      ORing the ref id of every entry whose remainder matches into a row bitmap in LDS
+//      (no global atomics), then appends the row's candidate pairs;
+//   3. the rank / literal-walk kernels (dist.hip) run on the candidates only; every other
+//      pair keeps the (0, min(S, la+lb)) written in step 2.
 // Work is O(N*S + sum_v n_v^2 + candidates*S) instead of O(pairs*S).  When the
 // posting events exceed a fraction of pairs*S (highly similar collections) the
 // host falls back to walking every pair.
@@ -21,12 +27,7 @@
 
 namespace fpm {
 
-constexpr uint64_t kEmpty = ~0ULL;
-
-__device__ __forceinline__ uint32_t slot_hash(uint64_t key, int log2t)
-{
-    return (uint32_t)((key * 0x9E3779B97F4A7C15ULL) >> (64 - log2t));
-}
+constexpr uint32_t kParts = 1u << kIdxL1;    // level-1 partitions (top 10 key bits)
 
 __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_bytes, uint64_t idx)
 {
@@ -34,65 +35,111 @@ __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_by
                            : (uint64_t) reinterpret_cast<const uint32_t *>(lists)[idx];
 }
 
-// key ~0 (only possible with 8-byte hashes) lives in the extra slot T
-__device__ __forceinline__ uint32_t idx_insert(uint64_t *keys, uint64_t key, int log2t)
+// 32-bit hashes move to the top of the word so the bucket bits are always the top bits
+__device__ __forceinline__ uint64_t norm_key(uint64_t h, uint32_t hash_bytes)
 {
-    const uint32_t T = 1u << log2t;
-    if (key == kEmpty) return T;
-    uint32_t s = slot_hash(key, log2t);
-    for (;;) {
-        unsigned long long old = atomicCAS((unsigned long long *)&keys[s], (unsigned long long)kEmpty,
-                                           (unsigned long long)key);
-        if (old == kEmpty || old == key) return s;
-        s = (s + 1) & (T - 1);
-    }
+    return hash_bytes == 8 ? h : (h << 32);
 }
 
-__device__ __forceinline__ int64_t idx_find(const uint64_t *keys, uint64_t key, int log2t)
-{
-    const uint32_t T = 1u << log2t;
-    if (key == kEmpty) return T;
-    uint32_t s = slot_hash(key, log2t);
-    for (;;) {
-        uint64_t k = keys[s];
-        if (k == key) return s;
-        if (k == kEmpty) return -1;
-        s = (s + 1) & (T - 1);
-    }
-}
+__device__ __forceinline__ uint64_t rem_mask(const IdxGeom &g) { return (1ULL << (64 - g.nbits)) - 1; }
 
-__global__ __launch_bounds__(256) void idx_insert_kernel(
-    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
-    uint32_t n_ref, uint32_t hash_bytes, uint64_t *__restrict__ keys, uint32_t *__restrict__ cnt,
-    uint32_t *__restrict__ slot_of, int log2t, uint32_t *__restrict__ unsorted)
+// ---- 1a. level-1 histogram: one tile = kIdxTile matrix cells, LDS counters per partition
+__global__ __launch_bounds__(256) void idx_part_hist_kernel(
+    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
+    uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles, uint32_t *__restrict__ tile_hist,
+    uint32_t *__restrict__ unsorted)
 {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t hist[kParts];
+    for (uint32_t p = threadIdx.x; p < kParts; p += 256) hist[p] = 0;
+    __syncthreads();
+    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
     bool uns = false;
-    if (e < (uint64_t)n_ref * stride) {
-        const uint32_t r = (uint32_t)(e / stride), i = (uint32_t)(e % stride);
+    for (uint32_t c = threadIdx.x; c < kIdxTile; c += 256) {
+        const uint32_t e = e0 + c;
+        if (e >= n) break;
+        const uint32_t r = e / stride, i = e - r * stride;
         const uint32_t la = ref_len[r];
         if (i < la) {
             const uint64_t key = load_key(ref, hash_bytes, e);
-            const uint32_t s = idx_insert(keys, key, log2t);
-            atomicAdd(&cnt[s], 1u);
-            slot_of[e] = s;
-            uns = i + 1 < la && !(key < load_key(ref, hash_bytes, e + 1));
+            atomicAdd(&hist[norm_key(key, hash_bytes) >> (64 - kIdxL1)], 1u);
+            uns |= i + 1 < la && !(key < load_key(ref, hash_bytes, (uint64_t)e + 1));
         }
     }
     if (__any(uns) && (threadIdx.x & 63) == 0) atomicOr(unsorted, 1u);
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < kParts; p += 256)
+        tile_hist[(uint64_t)p * ntiles + blockIdx.x] = hist[p];
 }
 
-__global__ __launch_bounds__(256) void idx_scatter_kernel(
-    const uint32_t *__restrict__ ref_len, uint64_t stride, uint32_t n_ref,
-    const uint32_t *__restrict__ slot_of, uint32_t *__restrict__ cursor,
-    uint32_t *__restrict__ postings)
+// ---- 1b. level-1 scatter into partitions (full key + ref id, temporary arrays)
+__global__ __launch_bounds__(256) void idx_part_scatter_kernel(
+    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
+    uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles, const uint32_t *__restrict__ tile_off,
+    uint64_t *__restrict__ tkey, uint32_t *__restrict__ tref)
 {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= (uint64_t)n_ref * stride) return;
-    const uint32_t r = (uint32_t)(e / stride), i = (uint32_t)(e % stride);
-    if (i >= ref_len[r]) return;
-    const uint32_t p = atomicAdd(&cursor[slot_of[e]], 1u);
-    postings[p] = r;
+    __shared__ uint32_t cur[kParts];
+    for (uint32_t p = threadIdx.x; p < kParts; p += 256)
+        cur[p] = tile_off[(uint64_t)p * ntiles + blockIdx.x];
+    __syncthreads();
+    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
+    for (uint32_t c = threadIdx.x; c < kIdxTile; c += 256) {
+        const uint32_t e = e0 + c;
+        if (e >= n) break;
+        const uint32_t r = e / stride, i = e - r * stride;
+        if (i < ref_len[r]) {
+            const uint64_t K = norm_key(load_key(ref, hash_bytes, e), hash_bytes);
+            const uint32_t pos = atomicAdd(&cur[K >> (64 - kIdxL1)], 1u);
+            tkey[pos] = K;
+            tref[pos] = r;
+        }
+    }
+}
+
+// ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits
+constexpr int kBucketThreads = 512;
+__global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
+    const uint64_t *__restrict__ tkey, const uint32_t *__restrict__ tref, uint32_t ntiles,
+    const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
+    uint64_t *__restrict__ entries)
+{
+    extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
+    __shared__ uint32_t wsum[kBucketThreads / 64];
+    const uint32_t p = blockIdx.x;
+    const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
+    const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
+    const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1, sh_sb = 64 - g.nbits;
+    for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
+    __syncthreads();
+    for (uint32_t e = s0 + threadIdx.x; e < s1; e += kBucketThreads)
+        atomicAdd(&sh[(uint32_t)(tkey[e] >> sh_sb) & sbmask], 1u);
+    __syncthreads();
+    // exclusive scan of the nsb counters: per-thread run of `per`, then a block scan
+    const uint32_t per = (nsb + kBucketThreads - 1) / kBucketThreads;
+    const uint32_t b0 = threadIdx.x * per;
+    uint32_t run = 0;
+    for (uint32_t b = b0; b < b0 + per && b < nsb; b++) run += sh[b];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = run;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t acc = x - run;
+    for (int w = 0; w < wave; w++) acc += wsum[w];
+    for (uint32_t b = b0; b < b0 + per && b < nsb; b++) {
+        const uint32_t c = sh[b];
+        sh[b] = acc;
+        dir[((uint64_t)p << g.l2) + b] = s0 + acc;
+        acc += c;
+    }
+    if (p == kParts - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
+    __syncthreads();
+    const uint64_t rm = rem_mask(g);
+    for (uint32_t e = s0 + threadIdx.x; e < s1; e += kBucketThreads) {
+        const uint64_t K = tkey[e];
+        const uint32_t pos = atomicAdd(&sh[(uint32_t)(K >> sh_sb) & sbmask], 1u);
+        entries[s0 + pos] = ((K & rm) << g.rbits) | tref[e];
+    }
 }
 
 // ---- exclusive scan of u32 counts (n <= 2^31), three launches ----
@@ -164,14 +211,14 @@ __global__ __launch_bounds__(256) void scan_add_kernel(uint32_t *__restrict__ ou
 }
 
 // ---- probing ----
-// Posting events = sum over query hashes of their posting-list length (= the work the
-// row probe will do).  Also flags unsorted / duplicate-carrying query rows.  One
-// atomic per workgroup into one of 64 spread counters (a single counter serialises).
+// Posting events = sum over query hashes of their bucket sizes (an upper bound of the
+// matching entries, and the work the row probe does).  Also flags unsorted /
+// duplicate-carrying query rows.  One atomic per workgroup into one of 64 spread
+// counters (a single counter serialises).
 __global__ __launch_bounds__(256) void probe_count_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
-    uint32_t n_qry, uint32_t hash_bytes, const uint64_t *__restrict__ keys,
-    const uint32_t *__restrict__ off, int log2t, unsigned long long *__restrict__ events,
-    uint32_t *__restrict__ unsorted)
+    uint32_t n_qry, uint32_t hash_bytes, IdxGeom g, const uint32_t *__restrict__ dir,
+    unsigned long long *__restrict__ events, uint32_t *__restrict__ unsorted)
 {
     __shared__ unsigned long long wsum[4];
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -182,8 +229,8 @@ __global__ __launch_bounds__(256) void probe_count_kernel(
         const uint32_t lq = qry_len[q];
         if (j < lq) {
             const uint64_t key = load_key(qry, hash_bytes, e);
-            int64_t s = idx_find(keys, key, log2t);
-            if (s >= 0) ev = off[s + 1] - off[s];
+            const uint64_t b = norm_key(key, hash_bytes) >> (64 - g.nbits);
+            ev = dir[b + 1] - dir[b];
             if (j + 1 < lq && !(key < load_key(qry, hash_bytes, e + 1))) uns = 1;
         }
     }
@@ -205,11 +252,15 @@ __global__ void sum64_kernel(unsigned long long *events)
     if (threadIdx.x == 0) events[0] = v;
 }
 
-// One workgroup per (query row, ref chunk): LDS bitmap of the chunk's refs.
+// One workgroup per (query row, ref chunk): LDS bitmap of the chunk's refs.  Each wave
+// takes 64 query hashes at a time: lane l looks up the bucket [st, st + cnt) of hash l,
+// a wave scan flattens the 64 buckets into one event range, and the lanes then read
+// consecutive entries of that range (coalesced) — the owner hash of an event comes from
+// a 6-step search over the wave's 64 prefix sums in LDS.
 __global__ __launch_bounds__(256) void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
-    uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, const uint64_t *__restrict__ keys,
-    const uint32_t *__restrict__ off, const uint32_t *__restrict__ postings, int log2t,
+    uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
+    const uint32_t *__restrict__ dir, const uint64_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S,
     uint32_t *__restrict__ numer, uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
@@ -217,7 +268,10 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long row_base;
-    const uint32_t q = blockIdx.x;
+    __shared__ uint32_t w_st[4][64], w_pre[4][64];
+    __shared__ uint64_t w_tgt[4][64];
+    const uint32_t q = xcd_row(blockIdx.x, n_qry);   // XCD-contiguous rows: shared buckets in L2
+    if (q >= n_qry) return;
     const uint32_t r0 = blockIdx.y * chunk_refs;
     const uint32_t r1 = min(n_ref, r0 + chunk_refs);
     const uint32_t nwords = (r1 - r0 + 31) / 32;
@@ -232,26 +286,56 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
         numer[o] = 0;
         denom[o] = d < S ? (uint32_t)d : S;
     }
-    for (uint32_t j = threadIdx.x; j < lq; j += 256) {
-        int64_t s = idx_find(keys, load_key(qry, hash_bytes, rowoff + j), log2t);
-        if (s < 0) continue;
-        for (uint32_t p = off[s], pe = off[s + 1]; p < pe; p++) {
-            uint32_t r = postings[p];
-            if (r >= r0 && r < r1) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t rm = rem_mask(g);
+    const uint64_t rmask = (1ULL << g.rbits) - 1;
+    for (uint32_t j0 = wave * 64; j0 < lq; j0 += 256) {
+        const uint32_t j = j0 + lane;
+        uint32_t st = 0, cnt = 0;
+        uint64_t tgt = 0;
+        if (j < lq) {
+            const uint64_t K = norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes);
+            const uint64_t b = K >> (64 - g.nbits);
+            st = dir[b];
+            cnt = dir[b + 1] - st;
+            tgt = K & rm;
         }
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(inc, d, 64);
+            if ((int)lane >= d) inc += y;
+        }
+        const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        // same wave writes and reads these slots: LDS ops of one wave complete in order
+        w_st[wave][lane] = st;
+        w_pre[wave][lane] = inc - cnt;
+        w_tgt[wave][lane] = tgt;
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t ev = lane; ev < total; ev += 64) {
+            uint32_t m = 0;                          // last m with w_pre[m] <= ev
+#pragma unroll
+            for (uint32_t step = 32; step > 0; step >>= 1)
+                m = (w_pre[wave][m + step] <= ev) ? m + step : m;
+            const uint64_t en = entries[w_st[wave][m] + (ev - w_pre[wave][m])];
+            if ((en >> g.rbits) == w_tgt[wave][m]) {
+                const uint32_t r = (uint32_t)(en & rmask);
+                if (r >= r0 && r < r1) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+            }
+        }
+        __builtin_amdgcn_wave_barrier();
     }
     __syncthreads();
     // candidates of this row: popcount per word -> block scan -> append
     uint32_t mycnt = 0;
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) mycnt += __popc(rowbits[w]);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = mycnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
     uint32_t wpre = 0, tot = 0;
-    for (int w = 0; w < 4; w++) { if (w < wave) wpre += wsum[w]; tot += wsum[w]; }
+    for (uint32_t w = 0; w < 4; w++) { if (w < wave) wpre += wsum[w]; tot += wsum[w]; }
     if (threadIdx.x == 0) {
         row_base = tot ? atomicAdd(n_cand, (unsigned long long)tot) : 0ULL;
         // (offset << 24 | count) of this row's candidates; one ref chunk per row here
@@ -271,28 +355,6 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     }
 }
 
-hipError_t launch_idx_insert(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
-                             uint32_t n_ref, uint32_t hash_bytes, uint64_t *keys, uint32_t *cnt,
-                             uint32_t *slot_of, int log2t, uint32_t *unsorted, hipStream_t st)
-{
-    uint64_t n = (uint64_t)n_ref * stride;
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(idx_insert_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, d_ref,
-                       d_ref_len, stride, n_ref, hash_bytes, keys, cnt, slot_of, log2t, unsorted);
-    return hipGetLastError();
-}
-
-hipError_t launch_idx_scatter(const uint32_t *d_ref_len, uint64_t stride, uint32_t n_ref,
-                              const uint32_t *slot_of, uint32_t *cursor, uint32_t *postings,
-                              hipStream_t st)
-{
-    uint64_t n = (uint64_t)n_ref * stride;
-    if (!n) return hipSuccess;
-    hipLaunchKernelGGL(idx_scatter_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st,
-                       d_ref_len, stride, n_ref, slot_of, cursor, postings);
-    return hipGetLastError();
-}
-
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock + 1; }
 
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
@@ -306,23 +368,42 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
     return hipGetLastError();
 }
 
+hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
+                            uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
+                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
+                            uint32_t *dir, uint64_t *entries, uint32_t *unsorted, hipStream_t st)
+{
+    const uint32_t ntiles = g.ntiles;
+    hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
+                       (uint32_t)stride, n_ref, hash_bytes, ntiles, tile_hist, unsorted);
+    const uint64_t nh = (uint64_t)kParts * ntiles;
+    if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
+        return e;
+    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
+                       (uint32_t)stride, n_ref, hash_bytes, ntiles, (const uint32_t *)tile_off,
+                       tkey, tref);
+    hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
+                       (size_t)4 << g.l2, st, (const uint64_t *)tkey, (const uint32_t *)tref,
+                       ntiles, (const uint32_t *)tile_off, g, dir, entries);
+    return hipGetLastError();
+}
+
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
-                              uint32_t n_qry, uint32_t hash_bytes, const uint64_t *keys,
-                              const uint32_t *off, int log2t, unsigned long long *events,
-                              uint32_t *unsorted, hipStream_t st)
+                              uint32_t n_qry, uint32_t hash_bytes, IdxGeom g, const uint32_t *dir,
+                              unsigned long long *events, uint32_t *unsorted, hipStream_t st)
 {
     uint64_t n = (uint64_t)n_qry * stride;
     if (n) hipLaunchKernelGGL(probe_count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
-                              st, d_qry, d_qry_len, stride, n_qry, hash_bytes, keys, off, log2t,
-                              events, unsorted);
+                              st, d_qry, d_qry_len, stride, n_qry, hash_bytes, g, dir, events,
+                              unsorted);
     hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, events);
     return hipGetLastError();
 }
 
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
-                             uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes,
-                             const uint64_t *keys, const uint32_t *off, const uint32_t *postings,
-                             int log2t, const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
+                             uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
+                             const uint32_t *dir, const uint64_t *entries,
+                             const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st)
 {
@@ -331,8 +412,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const uint32_t nchunks = (n_ref + chunk - 1) / chunk;
     const uint32_t cref = nchunks == 1 ? n_ref : chunk;
     const size_t lds = ((cref + 31) / 32) * 4;
-    hipLaunchKernelGGL(probe_rows_kernel, dim3(n_qry, nchunks), dim3(256), lds, st, d_qry, d_qry_len,
-                       stride, n_qry, n_ref, hash_bytes, keys, off, postings, log2t, cref,
+    hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
+                       d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
                        d_ref_len, S, d_numer, d_denom, cand, n_cand, row_seg);
     return hipGetLastError();
 }

@@ -626,19 +626,31 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
                       (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
     if (E == 0) try_sparse = false;
+    // bucket index geometry: ~1 entry per bucket (2^nbits >= E), ref ids packed into the
+    // entry's low rbits bits, so rbits <= nbits (n_ref <= 2^24)
+    IdxGeom geom{};
+    {
+        uint32_t rbits = 1, lg = 1;
+        while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
+        while (lg < 40 && (1ULL << lg) < E) lg++;
+        const uint32_t want = std::max(lg, rbits);
+        geom.l2 = want > kIdxL1 ? std::min<uint32_t>(want - kIdxL1, 14) : 1;
+        geom.nbits = kIdxL1 + geom.l2;
+        geom.rbits = rbits;
+        geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
+        if (rbits > geom.nbits || E >= (1ULL << 31)) try_sparse = false;
+    }
     if (try_sparse) {
-        int log2t = 10;
-        while ((1ULL << log2t) < 2 * E) log2t++;
-        if (log2t > 31) return fail(FPM_EINVAL, "reference set too large for one index");
-        const uint64_t T = 1ULL << log2t;
-        void *keys, *cnt, *off, *cursor, *slot_of, *postings, *scan_s, *ctr;
-        HIP_TRY(scratch(ctx, 0, (T + 1) * 8, &keys));
-        HIP_TRY(scratch(ctx, 1, (T + 1) * 4, &cnt));
-        HIP_TRY(scratch(ctx, 2, (T + 2) * 4, &off));
-        HIP_TRY(scratch(ctx, 3, (T + 2) * 4, &cursor));
-        HIP_TRY(scratch(ctx, 4, E * 4, &slot_of));
-        HIP_TRY(scratch(ctx, 5, E * 4, &postings));
-        HIP_TRY(scratch(ctx, 6, scan_scratch_words(T + 1) * 4, &scan_s));
+        const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
+        const uint64_t NB = 1ULL << geom.nbits;
+        void *tile_hist, *tile_off, *tkey, *tref, *dir, *entries, *scan_s, *ctr;
+        HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
+        HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
+        HIP_TRY(scratch(ctx, 2, E * 8, &tkey));
+        HIP_TRY(scratch(ctx, 3, E * 4, &tref));
+        HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir));
+        HIP_TRY(scratch(ctx, 5, E * 8, &entries));
+        HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
         HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
         if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
         // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag
@@ -646,19 +658,13 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         uint32_t *unsorted = (uint32_t *)(events + 66);
         {
             TimedLaunch tl(ctx, FPM_K_INDEX, st);
-            HIP_TRY(hipMemsetAsync(keys, 0xFF, (T + 1) * 8, st));
-            HIP_TRY(hipMemsetAsync(cnt, 0, (T + 1) * 4, st));
             HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
-            HIP_TRY(launch_idx_insert(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
-                                      (uint64_t *)keys, (uint32_t *)cnt, (uint32_t *)slot_of, log2t,
-                                      unsorted, st));
-            HIP_TRY(launch_exscan((const uint32_t *)cnt, (uint32_t *)off, (uint32_t *)cursor, T + 1,
-                                  (uint32_t *)scan_s, (uint32_t *)off + T + 1, st));
-            HIP_TRY(launch_idx_scatter(d_ref_len, ref_stride, n_ref, (const uint32_t *)slot_of,
-                                       (uint32_t *)cursor, (uint32_t *)postings, st));
-            HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                       (const uint64_t *)keys, (const uint32_t *)off, log2t, events,
-                                       unsorted, st));
+            HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
+                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                     (uint32_t *)scan_s, (uint64_t *)tkey, (uint32_t *)tref,
+                                     (uint32_t *)dir, (uint64_t *)entries, unsorted, st));
+            HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
+                                       (const uint32_t *)dir, events, unsorted, st));
             tl.done();
         }
         HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
@@ -675,14 +681,13 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
             HIP_TRY(scratch(ctx, 9, (size_t)n_qry * 8, &row_seg));
             const uint64_t lcap = std::max(ref_stride, qry_stride);
             const bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
-                                    lcap <= 3072;
+                                    lcap <= 2048;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
-                                          (const uint64_t *)keys, (const uint32_t *)off,
-                                          (const uint32_t *)postings, log2t, d_ref_len, sketch_size,
-                                          d_numer, d_denom, (uint64_t *)cand, n_cand,
-                                          (uint64_t *)row_seg, st));
+                                          geom, (const uint32_t *)dir, (const uint64_t *)entries,
+                                          d_ref_len, sketch_size, d_numer, d_denom,
+                                          (uint64_t *)cand, n_cand, (uint64_t *)row_seg, st));
                 tl.done();
             }
             {

@@ -82,4 +82,20 @@ __device__ __forceinline__ uint32_t lds_u32_at(const uint32_t *img, uint32_t byt
     return __builtin_amdgcn_alignbyte(img[q + 1], img[q], r);
 }
 
+// Row-major launches over query rows: workgroups are dealt round-robin over the 8 XCDs, so
+// block b runs on XCD b % 8. Map the blocks of one XCD to a CONTIGUOUS range of rows, so the
+// rows resident on an XCD at once are neighbours (same family / similar sketches) and the
+// ref rows and postings they share stay in that XCD's 4 MiB L2. Launch xcd_grid(n) blocks;
+// a block whose row is >= n returns.
+constexpr uint32_t kXcds = 8;
+__host__ __device__ __forceinline__ uint32_t xcd_grid(uint32_t n_rows)
+{
+    return (n_rows + kXcds - 1) / kXcds * kXcds;
+}
+__device__ __forceinline__ uint32_t xcd_row(uint32_t block, uint32_t n_rows)
+{
+    const uint32_t per = (n_rows + kXcds - 1) / kXcds;
+    return (block % kXcds) * per + block / kXcds;
+}
+
 }  // namespace fpm

@@ -61,24 +61,29 @@ hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long lo
                                   uint32_t hash_bytes, uint32_t S, uint32_t *d_numer,
                                   uint32_t *d_denom, hipStream_t st);
 
-// inverted index over ref hashes (dist_index.hip)
-hipError_t launch_idx_insert(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
-                             uint32_t n_ref, uint32_t hash_bytes, uint64_t *keys, uint32_t *cnt,
-                             uint32_t *slot_of, int log2t, uint32_t *unsorted, hipStream_t st);
-hipError_t launch_idx_scatter(const uint32_t *d_ref_len, uint64_t stride, uint32_t n_ref,
-                              const uint32_t *slot_of, uint32_t *cursor, uint32_t *postings,
-                              hipStream_t st);
+// bucket index over ref hashes (dist_index.hip)
+constexpr uint32_t kIdxL1 = 10;        // level-1 partition bits
+constexpr uint32_t kIdxTile = 4096;    // matrix cells per level-1 tile
+struct IdxGeom {
+    uint32_t l2;       // level-2 bits (1..14)
+    uint32_t nbits;    // bucket bits = kIdxL1 + l2
+    uint32_t rbits;    // ref-id bits in an entry (<= nbits)
+    uint32_t ntiles;   // level-1 tiles
+};
+hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
+                            uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
+                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
+                            uint32_t *dir, uint64_t *entries, uint32_t *unsorted, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
-                              uint32_t n_qry, uint32_t hash_bytes, const uint64_t *keys,
-                              const uint32_t *off, int log2t, unsigned long long *events,
-                              uint32_t *unsorted, hipStream_t st);
+                              uint32_t n_qry, uint32_t hash_bytes, IdxGeom g, const uint32_t *dir,
+                              unsigned long long *events, uint32_t *unsorted, hipStream_t st);
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
-                             uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes,
-                             const uint64_t *keys, const uint32_t *off, const uint32_t *postings,
-                             int log2t, const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
+                             uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
+                             const uint32_t *dir, const uint64_t *entries,
+                             const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st);
 // sorted-distinct candidates: one workgroup per query row, one wave per pair

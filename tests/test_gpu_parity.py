@@ -196,3 +196,46 @@ def test_dist_sparse_large_grid(ctx, oracle):
     n = len(sk)
     assert np.array_equal(a["numer"][:50 * n], nu)
     assert np.array_equal(a["denom"][:50 * n], de)
+
+
+def _sorted_lists(rng):
+    """Sorted distinct u64 lists that stress the rank kernel's bucket table: values near
+    2**64 (shift 52), tiny values (shift 0), one crowded bucket (long in-bucket search),
+    heavy overlap with lists shorter than S (denom < S), and long lists (CAP 2048)."""
+    pool = np.unique(rng.integers(0, 2 ** 64, size=6000, dtype=np.uint64))
+    lists = []
+    for i in range(24):
+        n = int(rng.integers(0, 1900))
+        lists.append(np.sort(rng.choice(pool[:2500], size=n, replace=False)))
+    small = np.arange(0, 6000, 3, dtype=np.uint64)                  # shift 0
+    lists += [small[:700], small[::2][:900], small[100:101]]
+    top = np.uint64(2 ** 64 - 1) - np.arange(0, 4000, 2, dtype=np.uint64)[::-1]
+    lists += [top[-1000:], top[-1500:][::3]]                           # bits = 64
+    crowd = np.concatenate([np.arange(1000, 1400, dtype=np.uint64),     # one bucket holds 400
+                            np.array([2 ** 62], dtype=np.uint64)])
+    lists += [crowd, crowd[::2], np.union1d(crowd[:50], small[:300])]
+    core = pool[:300]
+    lists += [core, core[:250], core[50:], pool[:2000], pool[1000:3000]]   # near-identical, long
+    return lists
+
+
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_dist_rank_kernel_edges(ctx, oracle, mode):
+    import fpmash
+    rng = np.random.default_rng(21)
+    lists = _sorted_lists(rng)
+    lengths = [int(x) for x in rng.integers(1000, 10 ** 6, size=len(lists))]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE if mode == "sparse" else fpmash.DIST_DENSE)
+    try:
+        for S in (1000, 2000, 260, 1):
+            got = ctx.dist(lists, lists, S, use64=True, k=21, ref_lengths=lengths,
+                           qry_lengths=lengths)
+            nu, de, di, pv = oracle.dist_grid(lists, lengths, lists, lengths, S, 21, 4.0 ** 21)
+            assert np.array_equal(got["numer"], nu), S
+            assert np.array_equal(got["denom"], de), S
+            np.testing.assert_allclose(got["distance"], di, rtol=RTOL, atol=0)
+            np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+            if mode == "sparse":
+                assert ctx.last_dist_stats()["sparse"] == 2
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
