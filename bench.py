@@ -313,7 +313,7 @@ def main():
             "dist": {"mpairs_per_s": total_pairs / args.steps / (di_ms * 1e-3) / 1e6 if di_ms else None,
                      "device_ms_per_step": di_ms,
                      "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
-                     "path": ["dense walk", "inverted index + literal walk",
+                     "path": ["dense walk", "bucket index + literal walk",
                               "bucket index + bucketed rank"][int(dstats["sparse"])],
                      "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
             "kernels": ktimes,

@@ -6,7 +6,7 @@
 // for sorted sketches and for the unsorted -fp lists alike.  So only pairs that
 // share at least one hash ("candidates") need the walk.  The candidates come from
 // an index over the reference lists:
-//   1. bucket index: every ref hash becomes one packed u64 entry (key remainder << rbits
+//   1. bucket index: every ref hash becomes one packed u32 entry (key fingerprint << rbits
 //      | ref id) in a bucket array grouped by the key's top `nbits` bits, with a
 //      directory dir[b] = first entry of bucket b.  Hashes are uniform (MurmurHash3), so
 //      this is a two-level counting sort with no global atomics: per-tile LDS histograms
@@ -15,7 +15,7 @@
 //      writes its slice of the directory;
 //   2. one workgroup per query row looks up the bucket of each of its hashes; each wave
 //      flattens the buckets of 64 hashes into one event range and reads it coalesced,
-//      ORing the ref id of every entry whose remainder matches into a row bitmap in LDS
+//      ORing the ref id of every entry whose fingerprint matches into a row bitmap in LDS
 //      (no global atomics), then appends the row's candidate pairs;
 //   3. the rank / literal-walk kernels (dist.hip) run on the candidates only; every other
 //      pair keeps the (0, min(S, la+lb)) written in step 2.
@@ -41,7 +41,13 @@ __device__ __forceinline__ uint64_t norm_key(uint64_t h, uint32_t hash_bytes)
     return hash_bytes == 8 ? h : (h << 32);
 }
 
-__device__ __forceinline__ uint64_t rem_mask(const IdxGeom &g) { return (1ULL << (64 - g.nbits)) - 1; }
+// u32 entry = fingerprint << rbits | ref id, fingerprint = the fbits key bits just below the
+// bucket bits.  A fingerprint collision only adds a candidate pair that shares no hash; the
+// exact candidate kernels then produce the same (0, min(S, la+lb)) the probe already wrote.
+__device__ __forceinline__ uint32_t key_fp(uint64_t K, const IdxGeom &g)
+{
+    return (uint32_t)(K >> (64 - g.nbits - g.fbits)) & ((1u << g.fbits) - 1);
+}
 
 // ---- 1a. level-1 histogram: one tile = kIdxTile matrix cells, LDS counters per partition
 __global__ __launch_bounds__(256) void idx_part_hist_kernel(
@@ -100,7 +106,7 @@ constexpr int kBucketThreads = 512;
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tkey, const uint32_t *__restrict__ tref, uint32_t ntiles,
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
-    uint64_t *__restrict__ entries)
+    uint32_t *__restrict__ entries)
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
     __shared__ uint32_t wsum[kBucketThreads / 64];
@@ -134,11 +140,10 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     }
     if (p == kParts - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
     __syncthreads();
-    const uint64_t rm = rem_mask(g);
     for (uint32_t e = s0 + threadIdx.x; e < s1; e += kBucketThreads) {
         const uint64_t K = tkey[e];
         const uint32_t pos = atomicAdd(&sh[(uint32_t)(K >> sh_sb) & sbmask], 1u);
-        entries[s0 + pos] = ((K & rm) << g.rbits) | tref[e];
+        entries[s0 + pos] = (key_fp(K, g) << g.rbits) | tref[e];
     }
 }
 
@@ -260,7 +265,7 @@ __global__ void sum64_kernel(unsigned long long *events)
 __global__ __launch_bounds__(256) void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
-    const uint32_t *__restrict__ dir, const uint64_t *__restrict__ entries,
+    const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S,
     uint32_t *__restrict__ numer, uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
@@ -269,7 +274,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long row_base;
     __shared__ uint32_t w_st[4][64], w_pre[4][64];
-    __shared__ uint64_t w_tgt[4][64];
+    __shared__ uint32_t w_tgt[4][64];
     const uint32_t q = xcd_row(blockIdx.x, n_qry);   // XCD-contiguous rows: shared buckets in L2
     if (q >= n_qry) return;
     const uint32_t r0 = blockIdx.y * chunk_refs;
@@ -287,19 +292,26 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
         denom[o] = d < S ? (uint32_t)d : S;
     }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t rm = rem_mask(g);
-    const uint64_t rmask = (1ULL << g.rbits) - 1;
-    for (uint32_t j0 = wave * 64; j0 < lq; j0 += 256) {
-        const uint32_t j = j0 + lane;
-        uint32_t st = 0, cnt = 0;
-        uint64_t tgt = 0;
-        if (j < lq) {
-            const uint64_t K = norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes);
+    const uint32_t rmask = (uint32_t)((1ULL << g.rbits) - 1);
+    // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
+    // loaded together (their global loads overlap) before the batches are expanded
+    constexpr int kB = 4;
+    for (uint32_t jb = wave * 64; jb < lq; jb += 256 * kB) {
+        uint32_t st_b[kB], cnt_b[kB], tgt_b[kB];
+#pragma unroll
+        for (int bi = 0; bi < kB; bi++) {
+            const uint32_t j = jb + 256 * bi + lane;
+            const uint64_t K = j < lq ? norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes) : 0;
             const uint64_t b = K >> (64 - g.nbits);
-            st = dir[b];
-            cnt = dir[b + 1] - st;
-            tgt = K & rm;
+            const uint32_t d0 = j < lq ? dir[b] : 0u, d1 = j < lq ? dir[b + 1] : 0u;
+            st_b[bi] = d0;
+            cnt_b[bi] = d1 - d0;
+            tgt_b[bi] = key_fp(K, g);
         }
+#pragma unroll
+      for (int bi = 0; bi < kB; bi++) {
+        if (jb + 256 * bi >= lq) break;                   // wave-uniform
+        const uint32_t st = st_b[bi], cnt = cnt_b[bi], tgt = tgt_b[bi];
         uint32_t inc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -312,18 +324,39 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
         w_pre[wave][lane] = inc - cnt;
         w_tgt[wave][lane] = tgt;
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t ev = lane; ev < total; ev += 64) {
-            uint32_t m = 0;                          // last m with w_pre[m] <= ev
+        // 4 events per lane per pass (ev, ev+64, ev+128, ev+192): their owner searches and
+        // entry loads are independent, so the LDS reads and global loads overlap
+        constexpr int kU = 4;
+        for (uint32_t ev0 = lane; ev0 < total; ev0 += 64 * kU) {
+            uint32_t m[kU];
 #pragma unroll
-            for (uint32_t step = 32; step > 0; step >>= 1)
-                m = (w_pre[wave][m + step] <= ev) ? m + step : m;
-            const uint64_t en = entries[w_st[wave][m] + (ev - w_pre[wave][m])];
-            if ((en >> g.rbits) == w_tgt[wave][m]) {
-                const uint32_t r = (uint32_t)(en & rmask);
-                if (r >= r0 && r < r1) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+            for (int u = 0; u < kU; u++) m[u] = 0;
+#pragma unroll
+            for (uint32_t step = 32; step > 0; step >>= 1) {
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const uint32_t pv = w_pre[wave][m[u] + step];      // last m with pre <= ev
+                    m[u] = (pv <= ev0 + 64 * u) ? m[u] + step : m[u];
+                }
+            }
+            uint32_t en[kU];
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint32_t ev = ev0 + 64 * u;
+                const uint32_t at = ev < total ? w_st[wave][m[u]] + (ev - w_pre[wave][m[u]]) : 0u;
+                en[u] = ev < total ? entries[at] : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; u++) {
+                const uint32_t ev = ev0 + 64 * u;
+                if (ev < total && (en[u] >> g.rbits) == w_tgt[wave][m[u]]) {
+                    const uint32_t r = en[u] & rmask;
+                    if (r >= r0 && r < r1) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+                }
             }
         }
         __builtin_amdgcn_wave_barrier();
+      }
     }
     __syncthreads();
     // candidates of this row: popcount per word -> block scan -> append
@@ -371,7 +404,7 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
-                            uint32_t *dir, uint64_t *entries, uint32_t *unsorted, hipStream_t st)
+                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
@@ -402,7 +435,7 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
 
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
-                             const uint32_t *dir, const uint64_t *entries,
+                             const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st)

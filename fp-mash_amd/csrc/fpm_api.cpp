@@ -626,19 +626,19 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
                       (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
     if (E == 0) try_sparse = false;
-    // bucket index geometry: ~1 entry per bucket (2^nbits >= E), ref ids packed into the
-    // entry's low rbits bits, so rbits <= nbits (n_ref <= 2^24)
+    // bucket index geometry: ~1 entry per bucket (2^nbits >= E, at most 2^24 buckets);
+    // entries are u32 (ref id in rbits, key fingerprint in the other >= 8 bits)
     IdxGeom geom{};
     {
         uint32_t rbits = 1, lg = 1;
         while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
         while (lg < 40 && (1ULL << lg) < E) lg++;
-        const uint32_t want = std::max(lg, rbits);
-        geom.l2 = want > kIdxL1 ? std::min<uint32_t>(want - kIdxL1, 14) : 1;
+        geom.l2 = lg > kIdxL1 ? std::min<uint32_t>(lg - kIdxL1, 14) : 1;
         geom.nbits = kIdxL1 + geom.l2;
         geom.rbits = rbits;
+        geom.fbits = 32 - rbits;
         geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
-        if (rbits > geom.nbits || E >= (1ULL << 31)) try_sparse = false;
+        if (rbits > 24 || E >= (1ULL << 31)) try_sparse = false;
     }
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
@@ -649,7 +649,7 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         HIP_TRY(scratch(ctx, 2, E * 8, &tkey));
         HIP_TRY(scratch(ctx, 3, E * 4, &tref));
         HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir));
-        HIP_TRY(scratch(ctx, 5, E * 8, &entries));
+        HIP_TRY(scratch(ctx, 5, E * 4, &entries));
         HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
         HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
         if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
@@ -662,7 +662,7 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
             HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
                                      (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                      (uint32_t *)scan_s, (uint64_t *)tkey, (uint32_t *)tref,
-                                     (uint32_t *)dir, (uint64_t *)entries, unsorted, st));
+                                     (uint32_t *)dir, (uint32_t *)entries, unsorted, st));
             HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
                                        (const uint32_t *)dir, events, unsorted, st));
             tl.done();
@@ -685,7 +685,7 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
-                                          geom, (const uint32_t *)dir, (const uint64_t *)entries,
+                                          geom, (const uint32_t *)dir, (const uint32_t *)entries,
                                           d_ref_len, sketch_size, d_numer, d_denom,
                                           (uint64_t *)cand, n_cand, (uint64_t *)row_seg, st));
                 tl.done();

@@ -67,13 +67,14 @@ constexpr uint32_t kIdxTile = 4096;    // matrix cells per level-1 tile
 struct IdxGeom {
     uint32_t l2;       // level-2 bits (1..14)
     uint32_t nbits;    // bucket bits = kIdxL1 + l2
-    uint32_t rbits;    // ref-id bits in an entry (<= nbits)
+    uint32_t rbits;    // ref-id bits in a u32 entry
+    uint32_t fbits;    // key-fingerprint bits in a u32 entry (32 - rbits, >= 8)
     uint32_t ntiles;   // level-1 tiles
 };
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
-                            uint32_t *dir, uint64_t *entries, uint32_t *unsorted, hipStream_t st);
+                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
@@ -82,7 +83,7 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
                               unsigned long long *events, uint32_t *unsorted, hipStream_t st);
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
-                             const uint32_t *dir, const uint64_t *entries,
+                             const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st);
