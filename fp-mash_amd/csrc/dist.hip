@@ -99,14 +99,15 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
 // No per-wave LDS image and no merge walk: ~5 LDS reads and ~40 VALU per A element.
-constexpr int kRankWaves = 8;
+constexpr int kRankWaves = 4;
 
 template <int CAP>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
     const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const uint64_t *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, uint32_t *__restrict__ numer, uint32_t *__restrict__ denom)
+    uint64_t qry_stride, uint32_t S, uint32_t sym, uint32_t *__restrict__ numer,
+    uint32_t *__restrict__ denom)
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 12 : 13;   // 4 * CAP buckets
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
@@ -130,21 +131,13 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
     const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
-    // bucket b = values [b << shift, (b + 1) << shift) = B positions [Bkt[b], Bkt[b + 1])
-    for (uint32_t b = threadIdx.x; b <= kBuckets; b += blockDim.x) {
-        uint32_t lo = 0;
-        if (b == kBuckets || ((uint64_t)b << shift) > bmax) {
-            lo = (b == 0) ? 0 : lb;                       // at or past the end of B
-        } else {
-            const uint64_t v = (uint64_t)b << shift;
-            uint32_t len = lb;
-            while (len > 0) {                             // lower_bound in Bs
-                const uint32_t half = len >> 1;
-                if (Bs[lo + half] < v) { lo += half + 1; len -= half + 1; }
-                else len = half;
-            }
-        }
-        Bkt[b] = lo;
+    // bucket b = values [b << shift, (b + 1) << shift) = B positions [Bkt[b], Bkt[b + 1]).
+    // Bkt[b] = #{B < b << shift}: element j owns the buckets after its predecessor's bucket
+    // up to its own, so each thread fills one gap (O(lb + buckets) writes, no searches).
+    for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
+        const uint32_t bj = j < lb ? (uint32_t)(Bs[j] >> shift) : kBuckets;
+        const uint32_t bp = j > 0 ? (uint32_t)(Bs[j - 1] >> shift) + 1 : 0;
+        for (uint32_t b = bp; b <= bj; b++) Bkt[b] = j;
     }
     __syncthreads();
     uint32_t mx = 0;
@@ -260,9 +253,16 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             }
         }
         if (lane == 0) {
-            numer[o] = cnt;
             const uint64_t un = (uint64_t)la + lb - shared_below;
-            denom[o] = need_all ? (un < S ? (uint32_t)un : S) : S;
+            const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
+            numer[o] = cnt;
+            denom[o] = dn;
+            const uint32_t r = (uint32_t)(o - pair_row);
+            if (sym && r != q) {                          // mirror cell (r, q)
+                const uint64_t o2 = (uint64_t)r * n_ref + q;
+                numer[o2] = cnt;
+                denom[o2] = dn;
+            }
         }
     }
 }
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
-                             uint64_t qry_stride, uint32_t S, uint32_t *d_numer,
+                             uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, hipStream_t st)
 {
     if (!n_qry) return hipSuccess;
@@ -278,12 +278,12 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
     const uint64_t cap = std::max(ref_stride, qry_stride);
     if (cap <= 1024)
         hipLaunchKernelGGL(rank_rows_kernel<1024>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
-                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer,
-                           d_denom);
+                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
+                           (uint32_t)sym, d_numer, d_denom);
     else if (cap <= 2048)
         hipLaunchKernelGGL(rank_rows_kernel<2048>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
-                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S, d_numer,
-                           d_denom);
+                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
+                           (uint32_t)sym, d_numer, d_denom);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();

@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
-    uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S,
+    uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
     uint32_t *__restrict__ numer, uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
 {
@@ -279,6 +279,8 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     if (q >= n_qry) return;
     const uint32_t r0 = blockIdx.y * chunk_refs;
     const uint32_t r1 = min(n_ref, r0 + chunk_refs);
+    // symmetric self-comparison: only refs r <= q become candidates of row q
+    const uint32_t r1c = sym ? min(r1, q + 1) : r1;
     const uint32_t nwords = (r1 - r0 + 31) / 32;
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) rowbits[w] = 0;
     __syncthreads();
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
                 const uint32_t ev = ev0 + 64 * u;
                 if (ev < total && (en[u] >> g.rbits) == w_tgt[wave][m[u]]) {
                     const uint32_t r = en[u] & rmask;
-                    if (r >= r0 && r < r1) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+                    if (r >= r0 && r < r1c) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
                 }
             }
         }
@@ -436,7 +438,7 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
-                             const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
+                             const uint32_t *d_ref_len, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st)
 {
@@ -447,7 +449,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const size_t lds = ((cref + 31) / 32) * 4;
     hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
-                       d_ref_len, S, d_numer, d_denom, cand, n_cand, row_seg);
+                       d_ref_len, S, (uint32_t)sym, d_numer, d_denom, cand, n_cand, row_seg);
     return hipGetLastError();
 }
 

@@ -682,11 +682,16 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
             const uint64_t lcap = std::max(ref_stride, qry_stride);
             const bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
                                     lcap <= 2048;
+            // one sorted set against itself: (numer, denom) of sorted distinct lists is
+            // symmetric in the two sets, so only candidates r <= q are ranked and each result
+            // is written to both cells (q, r) and (r, q)
+            const bool sym = rows_merge && d_ref == d_qry && d_ref_len == d_qry_len &&
+                             ref_stride == qry_stride && n_ref == n_qry;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
-                                          d_ref_len, sketch_size, d_numer, d_denom,
+                                          d_ref_len, sketch_size, sym, d_numer, d_denom,
                                           (uint64_t *)cand, n_cand, (uint64_t *)row_seg, st));
                 tl.done();
             }
@@ -696,7 +701,7 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
-                                              sketch_size, d_numer, d_denom, st));
+                                              sketch_size, sym, d_numer, d_denom, st));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
@@ -761,10 +766,16 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
         e = hipMalloc(&b.p, bytes ? bytes : 16);
         if (e == hipSuccess && h && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
     };
+    // one set against itself (dist X.msh X.msh): upload once; the grid call then sees
+    // identical device inputs and may use the pair symmetry
+    const bool same = ref == qry && ref_len == qry_len && ref_stride == qry_stride &&
+                      n_ref == n_qry;
     up(r, ref, (size_t)n_ref * ref_stride * hash_bytes);
     up(rl, ref_len, (size_t)n_ref * 4);
-    up(q, qry, (size_t)n_qry * qry_stride * hash_bytes);
-    up(ql, qry_len, (size_t)n_qry * 4);
+    if (!same) {
+        up(q, qry, (size_t)n_qry * qry_stride * hash_bytes);
+        up(ql, qry_len, (size_t)n_qry * 4);
+    }
     up(nu, nullptr, np * 4);
     up(de, nullptr, np * 4);
     if (fin) {
@@ -775,9 +786,10 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
         up(pa, nullptr, np);
     }
     if (e != hipSuccess) return fail(FPM_ENOMEM, std::string("dist staging: ") + hipGetErrorString(e));
-    int rc = fpm_compare_grid_dev(ctx, r.p, (const uint32_t *)rl.p, ref_stride, n_ref, q.p,
-                                  (const uint32_t *)ql.p, qry_stride, n_qry, hash_bytes, sketch_size,
-                                  (uint32_t *)nu.p, (uint32_t *)de.p, nullptr);
+    int rc = fpm_compare_grid_dev(ctx, r.p, (const uint32_t *)rl.p, ref_stride, n_ref,
+                                  same ? r.p : q.p, (const uint32_t *)(same ? rl.p : ql.p),
+                                  qry_stride, n_qry, hash_bytes, sketch_size, (uint32_t *)nu.p,
+                                  (uint32_t *)de.p, nullptr);
     if (!rc && fin)
         rc = fpm_dist_finalize_dev(ctx, (const uint32_t *)nu.p, (const uint32_t *)de.p,
                                    (const uint64_t *)rL.p, (const uint64_t *)qL.p, n_ref, n_qry,

@@ -84,14 +84,14 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
-                             const uint32_t *d_ref_len, uint32_t S, uint32_t *d_numer,
+                             const uint32_t *d_ref_len, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
                              uint64_t *row_seg, hipStream_t st);
 // sorted-distinct candidates: one workgroup per query row, one wave per pair
 hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
-                             uint64_t qry_stride, uint32_t S, uint32_t *d_numer,
+                             uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, hipStream_t st);
 
 hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,

@@ -333,7 +333,9 @@ class Context:
         dt = np.uint64 if use64 else np.uint32
         w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
         R, rl = _dense(ref_lists, w, dt)
-        Q, ql = _dense(qry_lists, w, dt)
+        # the same list object on both sides: one upload, and the library may use the
+        # pair symmetry of one set against itself
+        Q, ql = (R, rl) if qry_lists is ref_lists else _dense(qry_lists, w, dt)
         n = len(ref_lists) * len(qry_lists)
         nu = np.zeros(max(n, 1), np.uint32)
         de = np.zeros(max(n, 1), np.uint32)

@@ -239,3 +239,24 @@ def test_dist_rank_kernel_edges(ctx, oracle, mode):
                 assert ctx.last_dist_stats()["sparse"] == 2
     finally:
         ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
+def test_dist_self_symmetric_path(ctx, oracle):
+    """One sorted set against itself (same buffers) ranks only r <= q and mirrors; the result
+    equals the same data passed as a separate copy and the oracle."""
+    import fpmash
+    seqs, sk = _family_sketches(oracle, n_fam=8, members=12, seed=11)
+    sk = sk + [sk[0][:10], np.zeros(0, np.uint64), sk[5][:700]]
+    lengths = [len(x) for x in seqs] + [50, 100, 3000]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE)
+    try:
+        for S in (1000, 300):
+            a = ctx.dist(sk, sk, S, ref_lengths=lengths, qry_lengths=lengths)
+            assert ctx.last_dist_stats()["sparse"] == 2
+            b = ctx.dist(sk, [x.copy() for x in sk], S, ref_lengths=lengths, qry_lengths=lengths)
+            for key in ("numer", "denom", "distance", "pvalue", "pass"):
+                assert np.array_equal(a[key], b[key]), key
+            nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, S, 21, 4.0 ** 21)
+            assert np.array_equal(a["numer"], nu) and np.array_equal(a["denom"], de)
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
