@@ -5,7 +5,8 @@
 // HashSet::toHashList sort (HashSet.cpp:78-118): instead of a heap walked one
 // k-mer at a time, one workgroup owns a tile of up to P k-mer starts, stages the
 // tile's bytes (and their reverse complement) in LDS, hashes every window in
-// parallel, bitonic-sorts the P keys in LDS and keeps the first s distinct.
+// parallel (keys stay in registers), counting-sorts them by their top bits into LDS,
+// insertion-sorts each ~2-key bucket and keeps the first s distinct.
 // Result: the s smallest distinct hashes, ascending — exactly the set the
 // reference heap holds at the end of the stream.
 #include "fpm_device.hpp"
@@ -41,6 +42,25 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *tmp, uint
     return ex;
 }
 
+// Bitonic sort of P keys in LDS, ascending (fallback for tiles with crowded buckets).
+template <int P>
+__device__ void bitonic_sort(uint64_t *keys)
+{
+    const int tid = threadIdx.x;
+    for (int ks = 2; ks <= P; ks <<= 1) {
+        for (int j = ks >> 1; j > 0; j >>= 1) {
+            for (int t = tid; t < P / 2; t += kBlock) {
+                int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
+                int l = i + j;
+                bool up = (i & ks) == 0;
+                uint64_t a = keys[i], b = keys[l];
+                if ((a > b) == up) { keys[i] = b; keys[l] = a; }
+            }
+            __syncthreads();
+        }
+    }
+}
+
 template <int P>
 __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
@@ -55,6 +75,8 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     __shared__ uint8_t alpha[256];
     __shared__ uint8_t compl_tab[256];
     __shared__ uint32_t scan_tmp[kWaves + 1];
+    __shared__ uint32_t bins[P / 2 + 1];
+    __shared__ uint32_t big_bucket;
 
     const TileDesc td = tiles[blockIdx.x];
     const uint32_t n = td.n_bytes;
@@ -92,8 +114,12 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     const int nw = (k + 3) >> 2;                           // dwords per k-mer
     const uint32_t tail_mask = (k & 3) ? ((1u << (8 * (k & 3))) - 1u) : 0xffffffffu;
     const uint32_t kmask = (k == 32) ? 0xffffffffu : ((1u << k) - 1u);
-    uint32_t nvalid_local = 0;
-    for (int i = tid; i < P; i += kBlock) {
+    constexpr int E = P / kBlock;                          // keys per thread (P >= 256)
+    uint64_t kr[E];                                        // this thread's keys: i = tid + e*kBlock
+    uint32_t vbits = 0;                                    // bit e: kr[e] is a valid k-mer hash
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const int i = tid + e * kBlock;
         uint64_t key = ~0ULL;
         if ((uint32_t)i < nk) {
             // window [i, i+k) must hold alphabet bytes only (Sketch.cpp:696-713)
@@ -129,30 +155,70 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
                 for (int j = 0; j < 4; j++) wd[j] = (uint64_t)d[2 * j] | ((uint64_t)d[2 * j + 1] << 32);
                 uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
                 key = p.use64 ? h : (h & 0xffffffffULL);   // getHash hash.cpp:30-37
-                nvalid_local++;
+                vbits |= 1u << e;
             }
         }
-        keys[i] = key;
+        kr[e] = key;
+    }
+
+    // ---- sort: counting sort by the top log2(P/2) bits of the (uniform) hash values,
+    // then insertion sort inside each bucket (~2 keys per bucket).  A bucket holding
+    // more than kMaxBucket keys (low-complexity input: many copies of few k-mers) sends
+    // the whole tile to the bitonic sort instead.
+    constexpr int NB = P / 2;
+    constexpr int LB = __builtin_ctz(NB);
+    constexpr uint32_t kMaxBucket = 32;
+    const uint32_t bshift = p.use64 ? 64 - LB : 32 - LB;
+    for (int b = tid; b <= NB; b += kBlock) bins[b] = 0;
+    if (tid == 0) big_bucket = 0;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (vbits >> e & 1) atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
+    __syncthreads();
+    // exclusive scan of the bucket counts: thread t owns buckets [t*per, t*per + per)
+    constexpr int per = NB >= kBlock ? NB / kBlock : 1;
+    uint32_t run = 0, bmax = 0;
+#pragma unroll
+    for (int u = 0; u < per; u++) {
+        const int b = tid * per + u;
+        const uint32_t c = b < NB ? bins[b] : 0u;
+        run += c;
+        bmax = max(bmax, c);
     }
     uint32_t nvalid;
-    block_exscan(nvalid_local, scan_tmp, &nvalid);   // also a barrier over keys[]
-
-    // ---- bitonic sort of P keys, ascending
-    for (int ks = 2; ks <= P; ks <<= 1) {
-        for (int j = ks >> 1; j > 0; j >>= 1) {
-            for (int t = tid; t < P / 2; t += kBlock) {
-                int i = ((t & ~(j - 1)) << 1) | (t & (j - 1));
-                int l = i + j;
-                bool up = (i & ks) == 0;
-                uint64_t a = keys[i], b = keys[l];
-                if ((a > b) == up) { keys[i] = b; keys[l] = a; }
+    uint32_t acc = block_exscan(run, scan_tmp, &nvalid);   // also a barrier over bins[]
+#pragma unroll
+    for (int u = 0; u < per; u++) {
+        const int b = tid * per + u;
+        if (b < NB) { const uint32_t c = bins[b]; bins[b] = acc; acc += c; }
+    }
+    if (bmax > kMaxBucket) big_bucket = 1;
+    __syncthreads();
+    // scatter: afterwards bins[b] = end of bucket b, start = bins[b - 1]
+#pragma unroll
+    for (int e = 0; e < E; e++)
+        if (vbits >> e & 1) keys[atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u)] = kr[e];
+    __syncthreads();
+    if (!big_bucket) {
+        for (int b = tid; b < NB; b += kBlock) {
+            const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
+            for (uint32_t i = s0 + 1; i < s1; i++) {
+                const uint64_t x = keys[i];
+                uint32_t j = i;
+                while (j > s0 && keys[j - 1] > x) { keys[j] = keys[j - 1]; j--; }
+                keys[j] = x;
             }
-            __syncthreads();
         }
+        __syncthreads();
+    } else {
+        for (int i = tid; i < P; i += kBlock)
+            if ((uint32_t)i >= nvalid) keys[i] = ~0ULL;
+        __syncthreads();
+        bitonic_sort<P>(keys);
     }
 
     // ---- first s distinct (ties removed: the heap is a set, MinHashHeap.cpp:74)
-    constexpr int E = P / kBlock > 0 ? P / kBlock : 1;
     const int base = tid * E;
     uint32_t cnt = 0;
 #pragma unroll

@@ -52,8 +52,11 @@ def test_sketch_individual(ctx, oracle, k, s, canon):
 def test_sketch_low_complexity(ctx, oracle):
     """Repeats and palindromes: duplicates and canonical ties."""
     import fpmash
+    rng = np.random.default_rng(77)
     seqs = [b"A" * 3000, b"ACGT" * 700, b"AC" * 1500, b"ACGTTGCA" * 300, b"N" * 100,
-            b"acgtNNNNacgtacgtacgtacgtacgtacgt" * 40]
+            b"acgtNNNNacgtacgtacgtacgtacgtacgt" * 40,
+            # repeats of a random unit: every hash 4-14 times (crowded, sortable buckets)
+            rand_seq(rng, 150) * 14, rand_seq(rng, 600) * 4, rand_seq(rng, 37) * 60]
     for k, s in [(21, 1000), (21, 3), (4, 1000)]:
         P = fpmash.make_params(k=k, s=s)
         got = ctx.sketch(P, seqs)
