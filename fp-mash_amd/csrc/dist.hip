@@ -371,6 +371,8 @@ __device__ double pvalue_dev(uint32_t x, uint64_t len_ref, uint64_t len_qry, dou
     return beta_P(r, (double)k + 1.0, (double)n - (double)k);
 }
 
+// distance (CommandDistance.cpp:404-419), p-value and the -d / -v filters, one pair per
+// thread (a candidate's p-value continued fraction stays on its own lane)
 __global__ __launch_bounds__(256) void dist_finalize_kernel(
     const uint32_t *__restrict__ numer, const uint32_t *__restrict__ denom,
     const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
@@ -453,7 +455,7 @@ hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom
 {
     uint64_t n = (uint64_t)n_ref * n_qry;
     if (n == 0) return hipSuccess;
-    uint64_t blocks = (n + 255) / 256;
+    const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(dist_finalize_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, d_numer,
                        d_denom, d_ref_length, d_qry_length, n_ref, n, kmer_size, kmer_space,
                        max_dist, max_pvalue, d_dist, d_pvalue, d_pass);

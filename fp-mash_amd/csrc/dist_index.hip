@@ -106,7 +106,7 @@ constexpr int kBucketThreads = 512;
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tkey, const uint32_t *__restrict__ tref, uint32_t ntiles,
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
-    uint32_t *__restrict__ entries)
+    uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
     __shared__ uint32_t wsum[kBucketThreads / 64];
@@ -116,8 +116,19 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1, sh_sb = 64 - g.nbits;
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
-    for (uint32_t e = s0 + threadIdx.x; e < s1; e += kBucketThreads)
-        atomicAdd(&sh[(uint32_t)(tkey[e] >> sh_sb) & sbmask], 1u);
+    // 4 independent loads in flight per thread
+    constexpr uint32_t kU = 4;
+    for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
+        uint64_t K[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = e0 + u * kBucketThreads;
+            K[u] = e < s1 ? tkey[e] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+            if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(K[u] >> sh_sb) & sbmask], 1u);
+    }
     __syncthreads();
     // exclusive scan of the nsb counters: per-thread run of `per`, then a block scan
     const uint32_t per = (nsb + kBucketThreads - 1) / kBucketThreads;
@@ -132,18 +143,37 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     __syncthreads();
     uint32_t acc = x - run;
     for (int w = 0; w < wave; w++) acc += wsum[w];
+    unsigned long long sq = 0;
     for (uint32_t b = b0; b < b0 + per && b < nsb; b++) {
         const uint32_t c = sh[b];
         sh[b] = acc;
         dir[((uint64_t)p << g.l2) + b] = s0 + acc;
         acc += c;
+        sq += (unsigned long long)c * c;
+    }
+    // a set probed against itself does sum_b |b|^2 posting events: no separate count pass
+    if (sqsum) {
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) sq += __shfl_down(sq, d, 64);
+        if (lane == 0 && sq) atomicAdd(sqsum, sq);
     }
     if (p == kParts - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
     __syncthreads();
-    for (uint32_t e = s0 + threadIdx.x; e < s1; e += kBucketThreads) {
-        const uint64_t K = tkey[e];
-        const uint32_t pos = atomicAdd(&sh[(uint32_t)(K >> sh_sb) & sbmask], 1u);
-        entries[s0 + pos] = (key_fp(K, g) << g.rbits) | tref[e];
+    for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
+        uint64_t K[kU];
+        uint32_t R[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++) {
+            const uint32_t e = e0 + u * kBucketThreads;
+            K[u] = e < s1 ? tkey[e] : 0;
+            R[u] = e < s1 ? tref[e] : 0;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; u++)
+            if (e0 + u * kBucketThreads < s1) {
+                const uint32_t pos = atomicAdd(&sh[(uint32_t)(K[u] >> sh_sb) & sbmask], 1u);
+                entries[s0 + pos] = (key_fp(K[u], g) << g.rbits) | R[u];
+            }
     }
 }
 
@@ -406,7 +436,8 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
-                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted, hipStream_t st)
+                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
+                            unsigned long long *self_events, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
@@ -419,7 +450,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                        tkey, tref);
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)4 << g.l2, st, (const uint64_t *)tkey, (const uint32_t *)tref,
-                       ntiles, (const uint32_t *)tile_off, g, dir, entries);
+                       ntiles, (const uint32_t *)tile_off, g, dir, entries, self_events);
     return hipGetLastError();
 }
 

@@ -633,13 +633,17 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         uint32_t rbits = 1, lg = 1;
         while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
         while (lg < 40 && (1ULL << lg) < E) lg++;
-        geom.l2 = lg > kIdxL1 ? std::min<uint32_t>(lg - kIdxL1, 14) : 1;
+        // 2^nbits >= E/2 buckets (<= ~1.2 entries per bucket): 8K level-2 counters (32 KiB
+        // of LDS) at the bench's E = 1e7
+        geom.l2 = lg > kIdxL1 + 1 ? std::min<uint32_t>(lg - 1 - kIdxL1, 14) : 1;
         geom.nbits = kIdxL1 + geom.l2;
         geom.rbits = rbits;
         geom.fbits = 32 - rbits;
         geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
         if (rbits > 24 || E >= (1ULL << 31)) try_sparse = false;
     }
+    const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
+                          n_ref == n_qry;
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
@@ -659,12 +663,16 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         {
             TimedLaunch tl(ctx, FPM_K_INDEX, st);
             HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+            // one set against itself: the query side is the ref side, so its sortedness is
+            // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
             HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
                                      (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                      (uint32_t *)scan_s, (uint64_t *)tkey, (uint32_t *)tref,
-                                     (uint32_t *)dir, (uint32_t *)entries, unsorted, st));
-            HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
-                                       (const uint32_t *)dir, events, unsorted, st));
+                                     (uint32_t *)dir, (uint32_t *)entries, unsorted,
+                                     self_set ? events : nullptr, st));
+            if (!self_set)
+                HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
+                                           (const uint32_t *)dir, events, unsorted, st));
             tl.done();
         }
         HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
@@ -685,8 +693,7 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
             // one sorted set against itself: (numer, denom) of sorted distinct lists is
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
-            const bool sym = rows_merge && d_ref == d_qry && d_ref_len == d_qry_len &&
-                             ref_stride == qry_stride && n_ref == n_qry;
+            const bool sym = rows_merge && self_set;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,

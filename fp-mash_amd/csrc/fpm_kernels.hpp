@@ -74,7 +74,8 @@ struct IdxGeom {
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
-                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted, hipStream_t st);
+                            uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
+                            unsigned long long *self_events, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
