@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //
 // Rank kernel, one workgroup per query row B, one wave per candidate ref row A:
 //  * B is staged once in LDS together with a bucket table over its value range
-//    (bucket = value >> shift, 4 buckets per B slot, so <= 0.5 B elements per bucket);
+//    (bucket = value >> shift, 2 buckets per B slot, so <= 1 B element per bucket);
 //    bucket b holds the B positions [lo, hi) whose values fall in it.
 //  * lane l takes A[64t + l] (coalesced 512-byte buffer loads, prefetched one candidate
 //    ahead into registers); j comes from a fixed-length binary search inside the bucket
@@ -109,7 +109,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     uint64_t qry_stride, uint32_t S, uint32_t sym, uint32_t *__restrict__ numer,
     uint32_t *__restrict__ denom)
 {
-    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 12 : 13;   // 4 * CAP buckets
+    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 11 : 12;   // 2 * CAP buckets
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
     constexpr int kChunks = CAP / 64;
     __shared__ uint64_t Bs[CAP + 1];
@@ -150,68 +150,62 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
-    uint64_t regs[kChunks];
-    auto issue_row = [&](uint64_t o, uint32_t &la_out) {
+    // A rows are read in groups of kGroup chunks (64 x u64 each) through a bounds-checked
+    // buffer descriptor (reads past ld return 0).  Three register groups: `cur` (being
+    // ranked), `nxt` (this candidate's next group, issued before `cur` is ranked) and `pf`
+    // (the next candidate's first group, issued when a candidate starts): 24 VGPRs of row
+    // data, and the groups after an early exit are never loaded.
+    constexpr int kGroup = 4;
+    struct Row { __amdgpu_buffer_rsrc_t rsrc; uint32_t la; uint64_t o; };
+    auto open_row = [&](uint64_t o) -> Row {
         const uint32_t rr = __builtin_amdgcn_readfirstlane((uint32_t)(o - pair_row));
-        la_out = ref_len[rr];
         const uintptr_t Ar = (uintptr_t)(ref + (uint64_t)rr * ref_stride);
         const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)Ar);
         const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(Ar >> 32));
-        const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc(
-            (void *)(((uintptr_t)phi << 32) | plo), 0, (int)__builtin_amdgcn_readfirstlane(ld * 8u),
-            0x00020000);
+        Row R;
+        R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)phi << 32) | plo), 0,
+                                                   (int)__builtin_amdgcn_readfirstlane(ld * 8u),
+                                                   0x00020000);
+        R.la = ref_len[rr];
+        R.o = o;
+        return R;
+    };
+    auto load_group = [&](const Row &R, uint32_t gi, uint64_t (&dst)[kGroup]) {
 #pragma unroll
-        for (int t = 0; t < kChunks; t++) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, (t * 64 + lane) * 8u, 0, 0);
-            regs[t] = ((uint64_t)v[1] << 32) | v[0];
+        for (int u = 0; u < kGroup; u++) {
+            const uint32_t t = gi * kGroup + u;
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * 64 + lane) * 8u, 0, 0);
+            dst[u] = ((uint64_t)v[1] << 32) | v[0];
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
         return cand[base + __builtin_amdgcn_readfirstlane(cc)];
     };
-    // CAP 1024: the next candidate's row is in flight while this one is ranked (2 x 32
-    // VGPRs); CAP 2048 would need 128, so there the row is loaded at the top of its turn.
-    constexpr bool kPrefetch = CAP <= 1024;
-    uint64_t o_cur = 0, o_nxt = 0;
-    uint32_t la_cur = 0;
-    if (kPrefetch && wave < n) { o_cur = cand_at(wave); issue_row(o_cur, la_cur); }
-    if (kPrefetch && wave + kRankWaves < n) o_nxt = cand_at(wave + kRankWaves);
+    uint64_t cur[kGroup], nxt[kGroup], pf[kGroup];
+    Row Rc{};
+    if (wave < n) { Rc = open_row(cand_at(wave)); load_group(Rc, 0, pf); }
     for (uint32_t c = wave; c < n; c += kRankWaves) {
-        uint64_t o;
-        uint32_t la;
-        uint64_t A[kChunks];
-        if (kPrefetch) {
-            o = o_cur;
-            la = la_cur;
+        const Row R = Rc;
 #pragma unroll
-            for (int t = 0; t < kChunks; t++) A[t] = regs[t];
-            if (c + kRankWaves < n) {
-                o_cur = o_nxt;
-                issue_row(o_cur, la_cur);
-                if (c + 2 * kRankWaves < n) o_nxt = cand_at(c + 2 * kRankWaves);
-            }
-        } else {
-            o = cand_at(c);
-            issue_row(o, la);
-#pragma unroll
-            for (int t = 0; t < kChunks; t++) A[t] = regs[t];
-        }
+        for (int u = 0; u < kGroup; u++) cur[u] = pf[u];
+        if (c + kRankWaves < n) { Rc = open_row(cand_at(c + kRankWaves)); load_group(Rc, 0, pf); }
+        const uint32_t la = R.la;
+        const uint64_t o = R.o;
         const bool need_all = la < S && lb < S;           // denom depends on #shared
         const uint32_t nch = (la + 63) / 64;
+        const uint32_t ngr = (nch + kGroup - 1) / kGroup;
         uint32_t shared_below = 0, cnt = 0;
-        bool done = false;                                // wave-uniform
-        // kGroup chunks at a time: their bucket reads and search steps are independent,
-        // so each LDS round trip carries kGroup reads; the early-exit test is per group.
-        constexpr int kGroup = 4;
-#pragma unroll
-        for (int g0 = 0; g0 < kChunks; g0 += kGroup) {
-            if (done || (uint32_t)g0 >= nch) continue;
+        for (uint32_t gi = 0; gi < ngr; gi++) {
+            if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
+            const uint32_t g0 = gi * kGroup;
+            // bucket reads and search steps of the group's chunks are independent, so each
+            // LDS round trip carries kGroup reads
             uint32_t lo[kGroup], len[kGroup];
             bool act[kGroup];
 #pragma unroll
             for (int g = 0; g < kGroup; g++) {
                 const uint32_t i = (g0 + g) * 64 + lane;
-                const uint64_t a = A[g0 + g];
+                const uint64_t a = cur[g];
                 act[g] = i < la && lb && a <= bmax;
                 // every index below stays inside the LDS arrays (bk < kBuckets, lo + half
                 // <= lb <= CAP), so the reads are unconditional and the tests bitwise: a
@@ -226,11 +220,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 for (int g = 0; g < kGroup; g++) {
                     const uint32_t half = len[g] >> 1;
                     const uint64_t bv = Bs[lo[g] + half];
-                    const bool less = (len[g] != 0) & (bv < A[g0 + g]);
+                    const bool less = (len[g] != 0) & (bv < cur[g]);
                     lo[g] = less ? lo[g] + half + 1 : lo[g];
                     len[g] = less ? len[g] - half - 1 : half;
                 }
             }
+            bool done = false;
 #pragma unroll
             for (int g = 0; g < kGroup; g++) {
                 const uint32_t t = g0 + g;
@@ -238,7 +233,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 const uint32_t i = t * 64 + lane;
                 const uint32_t j = act[g] ? lo[g] : lb;
                 const uint64_t bj = Bs[j];
-                const bool eq = act[g] & (j < lb) & (bj == A[t]);
+                const bool eq = act[g] & (j < lb) & (bj == cur[g]);
                 const uint64_t bal = __ballot(eq);
                 const uint32_t k = shared_below + __builtin_amdgcn_mbcnt_hi(
                                        (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
@@ -251,6 +246,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                     if ((uint32_t)__builtin_amdgcn_readlane((int)u, (int)last) >= S) done = true;
                 }
             }
+            if (done) break;
+#pragma unroll
+            for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
         }
         if (lane == 0) {
             const uint64_t un = (uint64_t)la + lb - shared_below;
