@@ -111,7 +111,6 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 11 : 12;   // 2 * CAP buckets
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
-    constexpr int kChunks = CAP / 64;
     __shared__ uint64_t Bs[CAP + 1];
     __shared__ uint32_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
     __shared__ uint32_t s_maxn;
