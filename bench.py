@@ -198,12 +198,11 @@ def main():
 
     def step():
         job.run(st)
-        fpmash._check(L.fpm_compare_grid_dev(ctx.h, d_rows, d_cnt, stride, n, d_rows, d_cnt,
-                                             stride, n, 8, args.s, d_numer.ptr, d_denom.ptr,
-                                             st))
-        fpmash._check(L.fpm_dist_finalize_dev(ctx.h, d_numer.ptr, d_denom.ptr, d_len.ptr,
-                                              d_len.ptr, n, n, args.k, 4.0 ** args.k, 1.0, 1.0,
-                                              d_dist.ptr, d_pval.ptr, d_pass.ptr, st))
+        # compare + distance + p-value + pass in one call
+        fpmash._check(L.fpm_dist_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
+                                     d_len.ptr, stride, n, 8, args.s, args.k, 4.0 ** args.k,
+                                     1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
+                                     d_pass.ptr, st))
 
     for _ in range(args.warmup):
         step()

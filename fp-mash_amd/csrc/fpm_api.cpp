@@ -608,11 +608,14 @@ int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_o
 // dist
 // ----------------------------------------------------------------------------
 
-int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
-                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
-                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
-                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
-                         uint32_t *d_denom, void *stream)
+}  // extern "C"
+
+// The grid compare: dense walk, or bucket index + probe + candidate kernel (sparse).
+static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                        uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                        const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                        uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
+                        uint32_t *d_denom, void *stream)
 {
     if (int rc = set_device(ctx)) return rc;
     if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
@@ -730,6 +733,37 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     return FPM_OK;
 }
 
+extern "C" {
+
+int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
+                         uint32_t *d_denom, void *stream)
+{
+    return compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
+                        n_qry, hash_bytes, sketch_size, d_numer, d_denom, stream);
+}
+
+int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                 const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                 const void *d_qry, const uint32_t *d_qry_len, const uint64_t *d_qry_length,
+                 uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes, uint32_t sketch_size,
+                 uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
+                 uint32_t *d_numer, uint32_t *d_denom, double *d_dist, double *d_pvalue,
+                 uint8_t *d_pass, void *stream)
+{
+    if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
+        return fail(FPM_EINVAL, "fpm_dist_dev: lengths, distance and p-value buffers required");
+    if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
+                              qry_stride, n_qry, hash_bytes, sketch_size, d_numer, d_denom,
+                              stream))
+        return rc;
+    return fpm_dist_finalize_dev(ctx, d_numer, d_denom, d_ref_length, d_qry_length, n_ref, n_qry,
+                                 kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue,
+                                 d_pass, stream);
+}
+
 int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,
                           const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                           uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
@@ -793,15 +827,16 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
         up(pa, nullptr, np);
     }
     if (e != hipSuccess) return fail(FPM_ENOMEM, std::string("dist staging: ") + hipGetErrorString(e));
-    int rc = fpm_compare_grid_dev(ctx, r.p, (const uint32_t *)rl.p, ref_stride, n_ref,
-                                  same ? r.p : q.p, (const uint32_t *)(same ? rl.p : ql.p),
-                                  qry_stride, n_qry, hash_bytes, sketch_size, (uint32_t *)nu.p,
-                                  (uint32_t *)de.p, nullptr);
-    if (!rc && fin)
-        rc = fpm_dist_finalize_dev(ctx, (const uint32_t *)nu.p, (const uint32_t *)de.p,
-                                   (const uint64_t *)rL.p, (const uint64_t *)qL.p, n_ref, n_qry,
-                                   kmer_size, kmer_space, max_dist, max_pvalue, (double *)di.p,
-                                   (double *)pv.p, (uint8_t *)pa.p, nullptr);
+    const void *dq = same ? r.p : q.p;
+    const uint32_t *dql = (const uint32_t *)(same ? rl.p : ql.p);
+    int rc = fin ? fpm_dist_dev(ctx, r.p, (const uint32_t *)rl.p, (const uint64_t *)rL.p,
+                                ref_stride, n_ref, dq, dql, (const uint64_t *)qL.p, qry_stride,
+                                n_qry, hash_bytes, sketch_size, kmer_size, kmer_space, max_dist,
+                                max_pvalue, (uint32_t *)nu.p, (uint32_t *)de.p, (double *)di.p,
+                                (double *)pv.p, (uint8_t *)pa.p, nullptr)
+                 : fpm_compare_grid_dev(ctx, r.p, (const uint32_t *)rl.p, ref_stride, n_ref, dq,
+                                        dql, qry_stride, n_qry, hash_bytes, sketch_size,
+                                        (uint32_t *)nu.p, (uint32_t *)de.p, nullptr);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     if (out_numer) HIP_TRY(hipMemcpy(out_numer, nu.p, np * 4, hipMemcpyDeviceToHost));
