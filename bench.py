@@ -35,6 +35,9 @@ import fpmash  # noqa: E402
 from fpmash import datagen  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+# per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py,
+# regenerated on the GPU box whenever the kernels change)
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
 METRIC = "bases/s sketched + Mpairs/s dist, k=21 s=1000, 1/2/4/8 MI355X; %HBM roofline"
 
 
@@ -254,6 +257,9 @@ def main():
         N[fpmash.K_FINALIZE]: (n_pairs * (4 + 4 + 8 + 8 + 1),
                                "numer+denom read, distance+p-value+pass written per pair"),
     }
+    traffic = {}
+    if os.path.exists(PMC_TRAFFIC):
+        traffic = json.load(open(PMC_TRAFFIC)).get("kernels", {})
     dom = max(ktimes, key=lambda k_: ktimes[k_]["total_ms"])
     achieved = alg[dom][0] / (ktimes[dom]["avg_ms"] * 1e-3) / 1e9 if dom in alg else None
     roof = {
@@ -263,7 +269,8 @@ def main():
         "peak": HBM_PEAK_GBS,
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
-        "traffic": None,
+        "traffic": traffic.get(dom, {}).get("traffic_bytes"),
+        "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if dom in traffic else None,
         "alg_bytes_per_launch": alg.get(dom, (None, ""))[0],
         "alg_bytes_formula": alg.get(dom, (None, ""))[1],
         "avg_launch_ms": ktimes[dom]["avg_ms"],
@@ -273,7 +280,8 @@ def main():
         if name in ktimes:
             gbs = b / (ktimes[name]["avg_ms"] * 1e-3) / 1e9
             per_kernel_roof[name] = {"avg_ms": ktimes[name]["avg_ms"], "alg_GBps": gbs,
-                                     "frac_hbm": gbs / HBM_PEAK_GBS}
+                                     "frac_hbm": gbs / HBM_PEAK_GBS,
+                                     "traffic_bytes": traffic.get(name, {}).get("traffic_bytes")}
 
     sk_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_SKETCH, fpmash.K_MERGE)]
     di_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_INDEX, fpmash.K_PROBE,

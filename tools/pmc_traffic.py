@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""tools/pmc_traffic.py — HBM traffic per kernel launch from rocprofv3 PMC counters.
+
+Runs `bench.py` under rocprofv3 twice (FETCH_SIZE and WRITE_SIZE do not fit one pass on
+gfx950), then writes per-kernel bytes per launch to a JSON file that bench.py reads for
+`roofline.traffic`.  Corrections follow MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950
+tallies 128-B requests at 64 B, so it is doubled; WRITE_SIZE is taken as reported; both
+count Infinity-Cache traffic (L2 memory-side requests), so they are an upper bound on
+HBM bytes.  rocprofv3 reports both in KiB.
+
+Run it on the GPU box (this process never touches the GPU itself):
+    python3 tools/pmc_traffic.py --out profiles/r01/pmc_traffic.json
+"""
+from __future__ import annotations
+
+import argparse
+import collections
+import csv
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# kernel-name fragments -> bench.py KERNEL_NAMES group (one launch of the group = the sum)
+GROUPS = [
+    ("sketch_tiles_kernel", "sketch_tiles_kernel"),
+    ("merge_kernel", "merge_kernel"),
+    ("fp_hash_kernel", "fp_hash_kernel"),
+    ("rank_rows_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
+    ("walk_cand_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
+    ("compare_grid_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
+    ("dist_finalize_kernel", "dist_finalize_kernel"),
+    ("probe_rows_kernel", "probe_rows_kernel"),
+    ("idx_", "dist index build"),
+    ("scan_", "dist index build"),
+    ("probe_count_kernel", "dist index build"),
+    ("sum64_kernel", "dist index build"),
+]
+
+
+def group_of(name: str):
+    for frag, g in GROUPS:
+        if frag in name:
+            return g
+    return None
+
+
+def run_pass(counter: str, outdir: str, bench_args: list[str]) -> dict:
+    cmd = ["rocprofv3", "--pmc", counter, "-d", outdir, "-o", "pmc", "--output-format", "csv",
+           "--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+    env = dict(os.environ, TMPDIR="/tmp")
+    with open(os.path.join(outdir + ".log"), "w") as log:
+        subprocess.run(cmd, check=True, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
+                       timeout=600)
+    files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no counter file under {outdir}")
+    per_disp = collections.defaultdict(float)     # (group, dispatch) -> KiB
+    for row in csv.DictReader(open(files[0])):
+        if row["Counter_Name"] != counter:
+            continue
+        g = group_of(row["Kernel_Name"])
+        if g is None:
+            continue
+        per_disp[(g, row["Dispatch_Id"])] += float(row["Counter_Value"])
+    return per_disp
+
+
+def per_launch(per_disp: dict, launches: dict) -> dict:
+    tot = collections.defaultdict(float)
+    for (g, _), v in per_disp.items():
+        tot[g] += v
+    return {g: tot[g] * 1024.0 / launches[g] for g in tot if launches.get(g)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
+    ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    a = ap.parse_args()
+    os.makedirs(a.work, exist_ok=True)
+    bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"]
+    fetch = run_pass("FETCH_SIZE", os.path.join(a.work, "fetch"), bench_args)
+    write = run_pass("WRITE_SIZE", os.path.join(a.work, "write"), bench_args)
+    # every group runs once per bench step (warmup included): one "launch" of a group that
+    # is several kernels (the index build) is one step's worth of them
+    steps = a.steps + a.warmup
+    launches = {g: steps for (g, _d) in list(fetch) + list(write)}
+    f = per_launch(fetch, launches)
+    w = per_launch(write, launches)
+    res = {}
+    for g in sorted(set(f) | set(w)):
+        fb = 2.0 * f.get(g, 0.0)          # gfx950: FETCH_SIZE = half the streamed bytes
+        wb = w.get(g, 0.0)
+        res[g] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb}
+    out = {
+        "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
+                  f"bench.py --steps {a.steps} --warmup {a.warmup}; bytes per launch = "
+                  "2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB x 1024; includes "
+                  "Infinity-Cache traffic",
+        "kernels": res,
+    }
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    with open(a.out, "w") as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
