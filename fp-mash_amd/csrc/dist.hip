@@ -400,6 +400,59 @@ __global__ __launch_bounds__(256) void dist_finalize_kernel(
     if (pass) pass[o] = ok ? 1 : 0;
 }
 
+// triangle -fp's compareFingerprints (CommandTriangle.cpp:255-302): positional compare of
+// two lists over min(len) entries.  The fork reads the hash64 half of a u32 union whose
+// upper bits are uninitialised (:279); here u32 values are zero-extended, so a match is
+// an equal value at the same position.  distance = 1 - m/min(len) (NaN for an empty
+// list, as the reference), p-value = gsl_cdf_chisq_Q(m, 1) = erfc(sqrt(m/2)), pass =
+// distance <= max_dist && p <= max_pvalue.  One lane per pair, query-major output.
+template <typename H>
+__global__ __launch_bounds__(256) void positional_grid_kernel(
+    const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
+    uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
+    uint64_t qry_stride, uint32_t n_qry, double max_dist, double max_pvalue,
+    uint32_t *__restrict__ numer, uint32_t *__restrict__ denom, double *__restrict__ dist,
+    double *__restrict__ pval, uint8_t *__restrict__ pass)
+{
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x, q = blockIdx.y;
+    if (r >= n_ref) return;
+    const H *a = ref + (uint64_t)r * ref_stride, *b = qry + (uint64_t)q * qry_stride;
+    const uint32_t m = min(ref_len[r], qry_len[q]);
+    uint32_t matches = 0;
+    for (uint32_t i = 0; i < m; i++) matches += a[i] == b[i];
+    const double dv = 1.0 - (double)matches / (double)m;
+    const double pv = erfc(sqrt((double)matches / 2.0));
+    const uint64_t o = (uint64_t)q * n_ref + r;
+    numer[o] = matches;
+    denom[o] = m;
+    dist[o] = dv;
+    pval[o] = pv;
+    pass[o] = (dv <= max_dist && pv <= max_pvalue) ? 1 : 0;
+}
+
+hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
+                                  uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                  const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                                  uint32_t hash_bytes, double max_dist, double max_pvalue,
+                                  uint32_t *d_numer, uint32_t *d_denom, double *d_dist,
+                                  double *d_pvalue, uint8_t *d_pass, hipStream_t st)
+{
+    if (!n_ref || !n_qry) return hipSuccess;
+    const dim3 g((n_ref + 255) / 256, n_qry);
+    if (n_qry > 65535) return hipErrorInvalidValue;
+    if (hash_bytes == 8)
+        hipLaunchKernelGGL(positional_grid_kernel<uint64_t>, g, dim3(256), 0, st,
+                           (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                           (const uint64_t *)d_qry, d_qry_len, qry_stride, n_qry, max_dist,
+                           max_pvalue, d_numer, d_denom, d_dist, d_pvalue, d_pass);
+    else
+        hipLaunchKernelGGL(positional_grid_kernel<uint32_t>, g, dim3(256), 0, st,
+                           (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                           (const uint32_t *)d_qry, d_qry_len, qry_stride, n_qry, max_dist,
+                           max_pvalue, d_numer, d_denom, d_dist, d_pvalue, d_pass);
+    return hipGetLastError();
+}
+
 hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                                uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
                                uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,

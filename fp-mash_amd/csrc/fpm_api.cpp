@@ -847,6 +847,49 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
     return FPM_OK;
 }
 
+int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                           uint64_t ref_stride, uint32_t n_ref, const void *qry,
+                           const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,
+                           uint32_t hash_bytes, double max_dist, double max_pvalue,
+                           uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
+                           double *out_pvalue, uint8_t *out_pass)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
+    if (n_qry > 65535) return fail(FPM_EINVAL, "positional grid: at most 65535 queries per call");
+    const uint64_t np = (uint64_t)n_ref * n_qry;
+    if (np == 0) return FPM_OK;
+    DevBuf r, rl, q, ql, nu, de, di, pv, pa;
+    hipError_t e = hipSuccess;
+    auto up = [&](DevBuf &b, const void *h, size_t bytes) {
+        if (e != hipSuccess) return;
+        e = hipMalloc(&b.p, bytes ? bytes : 16);
+        if (e == hipSuccess && h && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+    };
+    up(r, ref, (size_t)n_ref * ref_stride * hash_bytes);
+    up(rl, ref_len, (size_t)n_ref * 4);
+    up(q, qry, (size_t)n_qry * qry_stride * hash_bytes);
+    up(ql, qry_len, (size_t)n_qry * 4);
+    up(nu, nullptr, np * 4);
+    up(de, nullptr, np * 4);
+    up(di, nullptr, np * 8);
+    up(pv, nullptr, np * 8);
+    up(pa, nullptr, np);
+    if (e != hipSuccess) return fail(FPM_ENOMEM, std::string("positional staging: ") + hipGetErrorString(e));
+    hipStream_t st = ctx->stream;
+    HIP_TRY(launch_positional_grid(r.p, (const uint32_t *)rl.p, ref_stride, n_ref, q.p,
+                                   (const uint32_t *)ql.p, qry_stride, n_qry, hash_bytes, max_dist,
+                                   max_pvalue, (uint32_t *)nu.p, (uint32_t *)de.p, (double *)di.p,
+                                   (double *)pv.p, (uint8_t *)pa.p, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (out_numer) HIP_TRY(hipMemcpy(out_numer, nu.p, np * 4, hipMemcpyDeviceToHost));
+    if (out_denom) HIP_TRY(hipMemcpy(out_denom, de.p, np * 4, hipMemcpyDeviceToHost));
+    if (out_dist) HIP_TRY(hipMemcpy(out_dist, di.p, np * 8, hipMemcpyDeviceToHost));
+    if (out_pvalue) HIP_TRY(hipMemcpy(out_pvalue, pv.p, np * 8, hipMemcpyDeviceToHost));
+    if (out_pass) HIP_TRY(hipMemcpy(out_pass, pa.p, np, hipMemcpyDeviceToHost));
+    return FPM_OK;
+}
+
 int fpm_compare_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
                      uint64_t ref_stride, uint32_t n_ref, const void *qry,
                      const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,

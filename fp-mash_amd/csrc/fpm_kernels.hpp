@@ -95,6 +95,14 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, hipStream_t st);
 
+// triangle -fp positional compare (dist.hip)
+hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
+                                  uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                  const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                                  uint32_t hash_bytes, double max_dist, double max_pvalue,
+                                  uint32_t *d_numer, uint32_t *d_denom, double *d_dist,
+                                  double *d_pvalue, uint8_t *d_pass, hipStream_t st);
+
 hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
                                 const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,

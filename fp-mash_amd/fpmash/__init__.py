@@ -76,6 +76,9 @@ SYMBOLS = [
     ("fpm_dist_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
                                C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
+    ("fpm_fp_positional_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p,
+                                         C.c_uint64, C.c_uint32, C.c_uint32, C.c_double,
+                                         C.c_double, u32p, u32p, f64p, f64p, u8p]),
     ("fpm_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, vp, u32p, u64p,
                            C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_double, C.c_double, C.c_double, u32p, u32p, f64p, f64p, u8p]),
@@ -360,6 +363,25 @@ class Context:
                               len(qry_lists), 8 if use64 else 4, sketch_size, k, kmer_space,
                               max_dist, max_pvalue, _p(nu, u32p), _p(de, u32p), _p(di, f64p),
                               _p(pv, f64p), _p(pa, u8p)))
+        return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
+                "pass": pa[:n].astype(bool)}
+
+    def positional(self, ref_lists, qry_lists, use64=False, max_dist=1.0, max_pvalue=1.0):
+        """triangle -fp's positional compare over the grid (query-major)."""
+        dt = np.uint64 if use64 else np.uint32
+        w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
+        R, rl = _dense(ref_lists, w, dt)
+        Q, ql = _dense(qry_lists, w, dt)
+        n = len(ref_lists) * len(qry_lists)
+        nu = np.zeros(max(n, 1), np.uint32)
+        de = np.zeros(max(n, 1), np.uint32)
+        di = np.zeros(max(n, 1), np.float64)
+        pv = np.zeros(max(n, 1), np.float64)
+        pa = np.zeros(max(n, 1), np.uint8)
+        _check(lib().fpm_fp_positional_grid(self.h, R.ctypes.data, _p(rl, u32p), w, len(ref_lists),
+                                            Q.ctypes.data, _p(ql, u32p), w, len(qry_lists),
+                                            8 if use64 else 4, max_dist, max_pvalue, _p(nu, u32p),
+                                            _p(de, u32p), _p(di, f64p), _p(pv, f64p), _p(pa, u8p)))
         return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
                 "pass": pa[:n].astype(bool)}
 

@@ -84,6 +84,18 @@ public:
     int run() const override;
 };
 
+class CommandPaste : public Command {
+public:
+    CommandPaste();
+    int run() const override;
+};
+
+class CommandTriangle : public Command {
+public:
+    CommandTriangle();
+    int run() const override;
+};
+
 // sketchParameterSetup (sketchParameterSetup.cpp:9-126)
 struct Parameters;
 int sketchParameterSetup(Parameters &p, const Command &c);

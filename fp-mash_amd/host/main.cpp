@@ -1,5 +1,6 @@
 // main.cpp — `fpmash`: the reference's CLI entry (mash.cpp:19-40) for the hot-path
-// verbs.  `fpmash sketch|dist [-fp] ...` is a drop-in for `mash sketch|dist [-fp] ...`.
+// verbs.  `fpmash sketch|dist|info|paste|triangle [-fp] ...` is a drop-in for the same
+// `mash` verbs.
 #include "Command.h"
 
 int main(int argc, const char **argv)
@@ -8,5 +9,7 @@ int main(int argc, const char **argv)
     commandList.addCommand(new fpmhost::CommandSketch());
     commandList.addCommand(new fpmhost::CommandDistance());
     commandList.addCommand(new fpmhost::CommandInfo());
+    commandList.addCommand(new fpmhost::CommandPaste());
+    commandList.addCommand(new fpmhost::CommandTriangle());
     return commandList.run(argc, argv);
 }

@@ -8,7 +8,14 @@
 
 int main(int argc, char **argv)
 {
-    if (argc < 2) { std::cerr << "usage: msh_roundtrip in.msh [out.msh]\n"; return 2; }
+    if (argc < 2) {
+        std::cerr << "usage: msh_roundtrip in.msh [out.msh]\n"
+                     "       msh_roundtrip --split in.msh out_prefix  (one .msh per sketch)\n";
+        return 2;
+    }
+    const bool split = std::string(argv[1]) == "--split";
+    if (split && argc < 4) return 2;
+    if (split) { argv++; argc--; }
     std::ifstream in(argv[1], std::ios::binary);
     std::stringstream ss;
     ss << in.rdbuf();
@@ -23,6 +30,14 @@ int main(int argc, char **argv)
     auto &refs = use64 ? r64 : r32;
     bool counts = false;
     for (auto &r : refs) if (!r.counts.empty()) counts = true;
+    if (split) {
+        for (size_t i = 0; i < refs.size(); i++) {
+            const std::string one = fpmhost::mshSerialize(h, {refs[i]}, use64, counts);
+            std::ofstream(std::string(argv[2]) + std::to_string(i) + ".msh", std::ios::binary) << one;
+        }
+        std::cout << refs.size() << "\n";
+        return 0;
+    }
     const std::string out = fpmhost::mshSerialize(h, refs, use64, counts);
     if (argc > 2) std::ofstream(argv[2], std::ios::binary) << out;
     std::cout << (out == data ? "same" : "differs") << " " << data.size() << " " << out.size() << "\n";

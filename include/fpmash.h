@@ -186,6 +186,20 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
              double max_dist, double max_pvalue, uint32_t *out_numer, uint32_t *out_denom,
              double *out_dist, double *out_pvalue, uint8_t *out_pass);
 
+/* ---- triangle -fp ---------------------------------------------------------------
+ * Replaces compareFingerprints (CommandTriangle.cpp:255-302): positional compare of
+ * two lists over min(len) entries, matches = equal values at the same position (the
+ * fork reads an uninitialised union half, :279; u32 values are zero-extended here).
+ * distance = 1 - matches/min(len), p-value = gsl_cdf_chisq_Q(matches, 1) =
+ * erfc(sqrt(matches/2)), pass = distance <= max_dist && p <= max_pvalue.
+ * Host buffers, query-major output (q*n_ref + r); n_qry <= 65535 per call. */
+int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                           uint64_t ref_stride, uint32_t n_ref, const void *qry,
+                           const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,
+                           uint32_t hash_bytes, double max_dist, double max_pvalue,
+                           uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
+                           double *out_pvalue, uint8_t *out_pass);
+
 #ifdef __cplusplus
 }
 #endif

@@ -673,3 +673,22 @@ int orc_dist_grid(const void *ref, const uint32_t *ref_len, const uint64_t *ref_
     pthread_mutex_destroy(&J.mu);
     return 0;
 }
+
+/* ---- triangle -fp positional compare (CommandTriangle.cpp:255-302) ---- */
+void orc_positional(const void *a, uint64_t len_a, const void *b, uint64_t len_b, int use64,
+                    uint64_t *matches, uint64_t *min_len, double *distance, double *pvalue)
+{
+    const uint64_t m = len_a < len_b ? len_a : len_b;
+    uint64_t c = 0;
+    for (uint64_t i = 0; i < m; i++) {
+        /* hash1.hash64 != 0 || hash2.hash64 != 0 ? compare hash64 : compare hash32 -- with
+         * zero-extended u32 values both branches are "equal values" (:276-290) */
+        const uint64_t x = use64 ? ((const uint64_t *)a)[i] : ((const uint32_t *)a)[i];
+        const uint64_t y = use64 ? ((const uint64_t *)b)[i] : ((const uint32_t *)b)[i];
+        c += x == y;
+    }
+    *matches = c;
+    *min_len = m;
+    *distance = 1.0 - ((double)c / (double)m);       /* :292, NaN when m == 0 */
+    *pvalue = erfc(sqrt((double)c / 2.0));          /* gsl_cdf_chisq_Q(c, 1), :293 */
+}

@@ -93,6 +93,12 @@ double orc_pvalue(uint64_t x, uint64_t len_ref, uint64_t len_qry, double kmer_sp
 /* gsl_cdf_binomial_Q(k, p, n) */
 double orc_binomial_q(uint64_t k, double p, uint64_t n);
 
+/* compareFingerprints (CommandTriangle.cpp:255-302), triangle -fp: positional matches over
+ * min(len); u32 values zero-extended (the fork reads an uninitialised union half, :279).
+ * distance = 1 - m/min(len); p = gsl_cdf_chisq_Q(m, 1) = erfc(sqrt(m/2)). */
+void orc_positional(const void *a, uint64_t len_a, const void *b, uint64_t len_b, int use64,
+                    uint64_t *matches, uint64_t *min_len, double *distance, double *pvalue);
+
 /*
  * All-pairs dist grid, query-major / ref-minor (CommandDistance.cpp:224-261 order),
  * chunked like the reference (pairs/threads capped at 4096 per task) across

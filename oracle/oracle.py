@@ -64,6 +64,8 @@ def lib():
         L.orc_pvalue.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_double, C.c_uint64]
         L.orc_binomial_q.restype = C.c_double
         L.orc_binomial_q.argtypes = [C.c_uint64, C.c_double, C.c_uint64]
+        L.orc_positional.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,
+                                     u64p, u64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.orc_dist_grid.restype = C.c_int
         L.orc_dist_grid.argtypes = [C.c_void_p, u32p, u64p, C.c_uint64, C.c_uint32,
                                     C.c_void_p, u32p, u64p, C.c_uint64, C.c_uint32,
@@ -201,6 +203,17 @@ def compare(a, b, sketch_size, use64=True):
     lib().orc_compare(a.ctypes.data, len(a), b.ctypes.data, len(b), int(use64), sketch_size,
                       C.byref(nu), C.byref(de))
     return nu.value, de.value
+
+
+def positional(a, b, use64=False):
+    """triangle -fp compareFingerprints: (matches, min_len, distance, pvalue)."""
+    a = np.ascontiguousarray(a, dtype=np.uint64 if use64 else np.uint32)
+    b = np.ascontiguousarray(b, dtype=np.uint64 if use64 else np.uint32)
+    m, n = C.c_uint64(), C.c_uint64()
+    d, p = C.c_double(), C.c_double()
+    lib().orc_positional(a.ctypes.data, len(a), b.ctypes.data, len(b), int(use64), C.byref(m),
+                         C.byref(n), C.byref(d), C.byref(p))
+    return m.value, n.value, d.value, p.value
 
 
 def distance(common, denom, k):

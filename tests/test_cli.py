@@ -180,3 +180,113 @@ def test_dist_fp_msh_and_table(tmp_path, oracle):
             nu, de = oracle.compare(r[ri]["hashes32"][:1000], q[qi]["hashes32"][:1000], 1000,
                                     use64=False)
             assert c == "%g" % oracle.distance(nu, de, 1)
+
+
+# ----------------------------------------------------------------------------- paste
+
+
+@pytest.mark.parametrize("name,fp", [("read1_2.msh", False), ("fingerprint_example1_2.msh", True)])
+def test_paste_reassembles_fixture(tmp_path, name, fp):
+    """Split a two-sketch fixture into one .msh per sketch (the byte-exact writer), paste
+    them back: the result is the fixture, byte for byte (read1_2.msh: the fork's
+    test/paste_example, fingerprint_example1_2.msh: its `paste -fp` example)."""
+    p = subprocess.run([ROUNDTRIP, "--split", os.path.join(GOLDEN, name), str(tmp_path / "part")],
+                       capture_output=True, text=True)
+    assert p.returncode == 0 and p.stdout.strip() == "2"
+    if fp:
+        for i in (0, 1):
+            (tmp_path / f"part{i}.txt").write_text("")      # -fp wants the .txt siblings
+        args = ["paste", "-fp", "part0.txt", "part1.msh", "-o", "joined"]
+    else:
+        args = ["paste", "joined", "part0.msh", "part1.msh"]
+    r = run(args, cwd=tmp_path)
+    assert r.stderr.decode() == "Writing joined.msh...\n"
+    assert (tmp_path / "joined.msh").read_bytes() == open(os.path.join(GOLDEN, name), "rb").read()
+
+
+def test_paste_errors(tmp_path):
+    shutil.copy(os.path.join(GOLDEN, "read1_2.msh"), tmp_path)
+    p = run(["paste", "-l", "-fp", "o", "read1_2.msh"], cwd=tmp_path, check=False)
+    assert p.returncode == 1 and b"The options -l and -fp are incompatible." in p.stderr
+    p = run(["paste", "o", "x.fa"], cwd=tmp_path, check=False)
+    assert p.returncode == 1 and b'"x.fa" does not look like a sketch.' in p.stderr
+    p = run(["paste", "-fp", "o", "a.txt"], cwd=tmp_path, check=False)
+    assert p.returncode == 1 and b'"a.msh" does not exist but is required.' in p.stderr
+    p = run(["paste", "-fp", "o", "read1_2.msh"], cwd=tmp_path, check=False)
+    assert p.returncode == 1 and b'"read1_2.txt" does not exist but is required.' in p.stderr
+    run(["paste", "o", "read1_2.msh"], cwd=tmp_path)
+    p = run(["paste", "o", "read1_2.msh"], cwd=tmp_path, check=False)
+    assert p.returncode == 1 and b'"o.msh" exists; remove to write.' in p.stderr
+
+
+# ----------------------------------------------------------------------------- triangle
+
+
+def _triangle_rows(text):
+    lines = text.splitlines()
+    n = int(lines[0].strip())
+    names = [lines[1]] + [l.split("\t")[0] for l in lines[2:]]
+    vals = [[float(x) for x in l.split("\t")[1:]] for l in lines[2:]]
+    return n, names, vals
+
+
+@pytest.mark.gpu
+def test_triangle_msh_matrix_and_edges(oracle):
+    files = [os.path.join(GOLDEN, f) for f in
+             ("genome1.fna.msh", "genome2.fna.msh", "genome3.fna.msh", "reads.msh")]
+    p = run(["triangle"] + files)
+    n, names, vals = _triangle_rows(p.stdout.decode())
+    refs = [r for f in files for r in mshfmt.read_msh(f)["references"]]
+    assert n == 4 and names == [r["name"].decode() for r in refs]
+    peak = 0.0
+    for i in range(1, n):
+        assert len(vals[i - 1]) == i
+        for j in range(i):
+            nu, de = oracle.compare(refs[i]["hashes64"], refs[j]["hashes64"], 1000)
+            d = oracle.distance(nu, de, 21)
+            pv = oracle.pvalue(nu, refs[i]["length"], refs[j]["length"], 4.0 ** 21, de)
+            assert ("%g" % vals[i - 1][j]) == ("%g" % d)
+            peak = max(peak, pv)
+    assert p.stderr.decode().startswith("Max p-value: ")
+    assert float(p.stderr.decode().split(":")[1]) == pytest.approx(float("%g" % peak), rel=1e-5)
+    e = run(["triangle", "-E"] + files).stdout.decode().splitlines()
+    assert len(e) == n * (n - 1) // 2
+    f1 = e[0].split("\t")
+    assert f1[0] == names[1] and f1[1] == names[0] and "/" in f1[4]
+    d = run(["triangle", "-d", "0.1"] + files).stdout.decode().splitlines()
+    assert all(float(x.split("\t")[2]) <= 0.1 for x in d)
+
+
+@pytest.mark.gpu
+def test_triangle_fp_positional(oracle):
+    """triangle -fp: positional compare (matches at equal positions), chi-square p-value."""
+    f = os.path.join(GOLDEN, "DNA1-CFL.txt")
+    p = run(["triangle", "-fp", "-E", f])
+    refs, _, _ = oracle.fp_references(open(f, "rb").read())
+    exp = []
+    for i in range(1, len(refs)):
+        for j in range(i):
+            m, mn, dv, pv = oracle.positional(refs[i][2], refs[j][2])
+            exp.append((refs[i][0].decode(), refs[j][0].decode(), "%g" % dv, "%g" % pv,
+                        f"{m}/{mn}"))
+    got = [tuple(l.split("\t")) for l in p.stdout.decode().splitlines()
+           if not l.startswith(("Initializing", "Processing", "Initialization"))]
+    assert got == exp
+
+
+@pytest.mark.gpu
+def test_positional_grid_abi(ctx, oracle):
+    rng = np.random.default_rng(5)
+    lists = [rng.integers(0, 20, size=int(rng.integers(0, 60))).astype(np.uint32) for _ in range(9)]
+    got = ctx.positional(lists, lists, max_dist=0.9, max_pvalue=0.5)
+    for q, b in enumerate(lists):
+        for r, a in enumerate(lists):
+            m, mn, dv, pv = oracle.positional(a, b)
+            k = q * len(lists) + r
+            assert got["numer"][k] == m and got["denom"][k] == mn
+            if mn:
+                assert got["distance"][k] == pytest.approx(dv, rel=1e-12)
+            else:
+                assert np.isnan(got["distance"][k])
+            assert got["pvalue"][k] == pytest.approx(pv, rel=1e-12)
+            assert got["pass"][k] == (dv <= 0.9 and pv <= 0.5)
