@@ -1,4 +1,4 @@
-// fingerprint.hip — the -fp k-finger line hash for gfx950.
+// fingerprint.hip — the -fp k-finger text parse and line hash for gfx950.
 //
 // Replaces the per-line getHashFingerPrint call of Sketch::initFromFingerprints
 // (Sketch.cpp:131, hash.cpp:45-73): Murmur over the 8*n little-endian bytes of
@@ -31,6 +31,154 @@ hipError_t launch_fp_hash(const uint64_t *d_vals, const uint64_t *d_line_off, ui
     uint64_t blocks = (n_lines + 255) / 256;
     hipLaunchKernelGGL(fp_hash_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, d_vals, d_line_off,
                        n_lines, seed, use64, d_out);
+    return hipGetLastError();
+}
+
+// ---- CFL k-finger text → per-line (ID, value count, hash), the parse of
+// Sketch::initFromFingerprints (Sketch.cpp:82-101: getline, `iss >> id`, `while (iss >> v)`)
+// and its getHashFingerPrint call (:131), with the values streamed into Murmur instead of
+// being stored.  Lines: split on '\n'; a last line without '\n' counts (getline).
+
+constexpr int kTextChunk = 4096;   // text bytes per workgroup (256 threads x 16)
+
+__device__ __forceinline__ bool fp_is_space(uint8_t c)
+{
+    return c == ' ' || (c >= '\t' && c <= '\r');   // isspace in the "C" locale
+}
+
+__global__ __launch_bounds__(256) void nl_count_kernel(const uint8_t *__restrict__ text,
+                                                      uint64_t len, uint32_t *__restrict__ cnt)
+{
+    __shared__ uint32_t wsum[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kTextChunk + threadIdx.x * 16;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) c += (b0 + i < len && text[b0 + i] == '\n');
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// line_start[k + 1] = 1 + position of the k-th '\n' (line_start[0] = 0, set by the host)
+__global__ __launch_bounds__(256) void nl_scatter_kernel(const uint8_t *__restrict__ text,
+                                                        uint64_t len,
+                                                        const uint32_t *__restrict__ blk_off,
+                                                        uint64_t *__restrict__ line_start)
+{
+    __shared__ uint32_t wsum[4];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kTextChunk + threadIdx.x * 16;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) c += (b0 + i < len && text[b0 + i] == '\n');
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t k = blk_off[blockIdx.x] + x - c;
+    for (int w = 0; w < wave; w++) k += wsum[w];
+    for (int i = 0; i < 16; i++)
+        if (b0 + i < len && text[b0 + i] == '\n') line_start[++k] = b0 + i + 1;
+}
+
+// one lane per line
+__global__ __launch_bounds__(256) void fp_line_kernel(
+    const uint8_t *__restrict__ text, uint64_t len, const uint64_t *__restrict__ line_start,
+    uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
+    uint64_t *__restrict__ id_off, uint32_t *__restrict__ id_len, uint32_t *__restrict__ n_vals,
+    void *__restrict__ hash, uint8_t *__restrict__ new_id)
+{
+    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (li >= n_lines) return;
+    const uint64_t b = line_start[li], e = li < n_nl ? line_start[li + 1] - 1 : len;
+    uint64_t p = b;
+    while (p < e && fp_is_space(text[p])) p++;
+    const uint64_t ib = p;
+    while (p < e && !fp_is_space(text[p])) p++;
+    const uint64_t ie = p;
+    // `while (iss >> v)`: optional sign, digits; a non-digit or an overflow ends the line
+    uint64_t h1 = seed, h2 = seed, pend = 0, nv = 0;
+    if (ie > ib) {
+        for (;;) {
+            while (p < e && fp_is_space(text[p])) p++;
+            bool neg = false;
+            if (p < e && (text[p] == '+' || text[p] == '-')) { neg = text[p] == '-'; p++; }
+            if (p >= e || text[p] < '0' || text[p] > '9') break;
+            uint64_t v = 0;
+            bool ovf = false;
+            while (p < e && text[p] >= '0' && text[p] <= '9') {
+                const uint64_t d = (uint64_t)(text[p] - '0');
+                if (v > (~0ULL - d) / 10) ovf = true;
+                v = v * 10 + d;
+                p++;
+            }
+            if (ovf) break;
+            if (neg) v = 0 - v;
+            if (nv & 1) mur_block(h1, h2, pend, v);          // value pairs are Murmur blocks
+            else pend = v;
+            nv++;
+        }
+    }
+    if (nv & 1) {                                            // odd last value: the k1 tail
+        uint64_t k1 = pend;
+        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+    }
+    const uint64_t h = mur_final(h1, h2, (uint64_t)(int64_t)(int)(nv * 8));
+    id_off[li] = ib;
+    id_len[li] = (uint32_t)(ie - ib);
+    n_vals[li] = (uint32_t)nv;
+    if (use64) reinterpret_cast<uint64_t *>(hash)[li] = h;
+    else reinterpret_cast<uint32_t *>(hash)[li] = (uint32_t)h;
+    // a new Reference starts where the ID differs from the previous line's (:104-129);
+    // line 0 is compared with the previous file's last ID by the host (2 = unknown)
+    uint8_t nid = 2;
+    if (li > 0) {
+        uint64_t q = line_start[li - 1];
+        const uint64_t qe = line_start[li] - 1;
+        while (q < qe && fp_is_space(text[q])) q++;
+        const uint64_t pb = q;
+        while (q < qe && !fp_is_space(text[q])) q++;
+        nid = 0;
+        if (q - pb != ie - ib) nid = 1;
+        else
+            for (uint64_t t = 0; t < ie - ib; t++)
+                if (text[pb + t] != text[ib + t]) { nid = 1; break; }
+    }
+    new_id[li] = nid;
+}
+
+uint32_t text_blocks(uint64_t len) { return (uint32_t)((len + kTextChunk - 1) / kTextChunk); }
+
+hipError_t launch_fp_nl_count(const uint8_t *d_text, uint64_t len, uint32_t *blk_cnt,
+                              uint32_t *blk_off, uint32_t *scan_s, hipStream_t st)
+{
+    const uint32_t nb = text_blocks(len);
+    if (!nb) return hipSuccess;
+    hipLaunchKernelGGL(nl_count_kernel, dim3(nb), dim3(256), 0, st, d_text, len, blk_cnt);
+    return launch_exscan(blk_cnt, blk_off, nullptr, nb, scan_s, blk_off + nb, st);
+}
+
+hipError_t launch_fp_nl_scatter(const uint8_t *d_text, uint64_t len, const uint32_t *blk_off,
+                                uint64_t *d_line_start, hipStream_t st)
+{
+    const uint32_t nb = text_blocks(len);
+    if (!nb) return hipSuccess;
+    hipLaunchKernelGGL(nl_scatter_kernel, dim3(nb), dim3(256), 0, st, d_text, len, blk_off,
+                       d_line_start);
+    return hipGetLastError();
+}
+
+hipError_t launch_fp_lines(const uint8_t *d_text, uint64_t len, const uint64_t *d_line_start,
+                           uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
+                           uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals, void *hash,
+                           uint8_t *new_id, hipStream_t st)
+{
+    if (!n_lines) return hipSuccess;
+    hipLaunchKernelGGL(fp_line_kernel, dim3((uint32_t)((n_lines + 255) / 256)), dim3(256), 0, st,
+                       d_text, len, d_line_start, n_nl, n_lines, seed, use64, id_off, id_len,
+                       n_vals, hash, new_id);
     return hipGetLastError();
 }
 

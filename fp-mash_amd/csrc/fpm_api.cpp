@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -602,6 +603,119 @@ int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_o
     }
     (void)hipFree(dv); (void)hipFree(doff); (void)hipFree(dout);
     return rc;
+}
+
+// ----------------------------------------------------------------------------
+// -fp text
+// ----------------------------------------------------------------------------
+
+}  // extern "C"
+
+struct fpm_fptext {
+    fpm_ctx *ctx = nullptr;
+    uint64_t n_lines = 0;
+    uint32_t use64 = 0;
+    uint8_t *d_text = nullptr;
+    uint64_t *d_line_start = nullptr;
+    uint32_t *d_blk = nullptr;
+    uint64_t *d_id_off = nullptr;
+    uint32_t *d_id_len = nullptr, *d_n_vals = nullptr;
+    void *d_hash = nullptr;
+    uint8_t *d_new_id = nullptr;
+};
+
+static void fptext_release(fpm_fptext *j)
+{
+    if (!j) return;
+    (void)hipSetDevice(j->ctx->device);
+    for (void *p : {(void *)j->d_text, (void *)j->d_line_start, (void *)j->d_blk,
+                    (void *)j->d_id_off, (void *)j->d_id_len, (void *)j->d_n_vals, j->d_hash,
+                    (void *)j->d_new_id})
+        if (p) (void)hipFree(p);
+}
+
+extern "C" {
+
+int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_t max_lines,
+                      uint32_t seed, uint32_t use64, fpm_fptext **job, uint64_t *n_lines)
+{
+    if (!job || !n_lines) return fail(FPM_EINVAL, "fp_text_stage: null output");
+    *job = nullptr;
+    *n_lines = 0;
+    if (int rc = set_device(ctx)) return rc;
+    std::unique_ptr<fpm_fptext, void (*)(fpm_fptext *)> j(new fpm_fptext,
+        [](fpm_fptext *p) { fptext_release(p); delete p; });
+    j->ctx = ctx;
+    j->use64 = use64;
+    hipStream_t st = ctx->stream;
+    const uint32_t nb = text_blocks(text_len);
+    const uint64_t scan_w = scan_scratch_words(nb ? nb : 1);
+    HIP_TRY(hipMalloc(&j->d_text, text_len + 16));
+    HIP_TRY(hipMalloc(&j->d_blk, ((size_t)2 * nb + 2 + scan_w) * 4));
+    if (text_len) HIP_TRY(hipMemcpyAsync(j->d_text, text, text_len, hipMemcpyHostToDevice, st));
+    uint32_t *blk_cnt = j->d_blk, *blk_off = j->d_blk + nb, *scan_s = j->d_blk + 2 * nb + 2;
+    // newline count first: it sizes the line index
+    uint64_t n_nl = 0;
+    if (nb) {
+        {
+            TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
+            HIP_TRY(launch_fp_nl_count(j->d_text, text_len, blk_cnt, blk_off, scan_s, st));
+            tl.done();
+        }
+        uint32_t tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, blk_off + nb, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        n_nl = tot;
+    }
+    HIP_TRY(hipMalloc(&j->d_line_start, (n_nl + 1) * 8));
+    HIP_TRY(hipMemsetAsync(j->d_line_start, 0, 8, st));
+    if (n_nl) {
+        TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
+        HIP_TRY(launch_fp_nl_scatter(j->d_text, text_len, blk_off, j->d_line_start, st));
+        tl.done();
+    }
+    const uint64_t total = n_nl + ((text_len && text[text_len - 1] != '\n') ? 1 : 0);
+    const uint64_t nl = std::min(total, max_lines);
+    j->n_lines = nl;
+    if (nl) {
+        HIP_TRY(hipMalloc(&j->d_id_off, nl * 8));
+        HIP_TRY(hipMalloc(&j->d_id_len, nl * 4));
+        HIP_TRY(hipMalloc(&j->d_n_vals, nl * 4));
+        HIP_TRY(hipMalloc(&j->d_hash, nl * (use64 ? 8 : 4)));
+        HIP_TRY(hipMalloc(&j->d_new_id, nl));
+        TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
+        HIP_TRY(launch_fp_lines(j->d_text, text_len, j->d_line_start, n_nl, nl, seed, use64,
+                                j->d_id_off, j->d_id_len, j->d_n_vals, j->d_hash, j->d_new_id, st));
+        tl.done();
+    }
+    *n_lines = nl;
+    *job = j.release();
+    return FPM_OK;
+}
+
+int fpm_fp_text_fetch(fpm_fptext *j, uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals,
+                      void *hash, uint8_t *new_id)
+{
+    if (!j) return fail(FPM_EINVAL, "fp_text_fetch: null job");
+    if (int rc = set_device(j->ctx)) return rc;
+    hipStream_t st = j->ctx->stream;
+    const uint64_t n = j->n_lines;
+    if (n) {
+        if (id_off) HIP_TRY(hipMemcpyAsync(id_off, j->d_id_off, n * 8, hipMemcpyDeviceToHost, st));
+        if (id_len) HIP_TRY(hipMemcpyAsync(id_len, j->d_id_len, n * 4, hipMemcpyDeviceToHost, st));
+        if (n_vals) HIP_TRY(hipMemcpyAsync(n_vals, j->d_n_vals, n * 4, hipMemcpyDeviceToHost, st));
+        if (hash)
+            HIP_TRY(hipMemcpyAsync(hash, j->d_hash, n * (j->use64 ? 8 : 4), hipMemcpyDeviceToHost, st));
+        if (new_id) HIP_TRY(hipMemcpyAsync(new_id, j->d_new_id, n, hipMemcpyDeviceToHost, st));
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return FPM_OK;
+}
+
+void fpm_fp_text_free(fpm_fptext *j)
+{
+    fptext_release(j);
+    delete j;
 }
 
 // ----------------------------------------------------------------------------

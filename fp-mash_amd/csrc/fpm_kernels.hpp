@@ -95,6 +95,17 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
                              uint32_t *d_denom, hipStream_t st);
 
+// -fp CFL text: newline index, then one lane per line (fingerprint.hip)
+uint32_t text_blocks(uint64_t len);
+hipError_t launch_fp_nl_count(const uint8_t *d_text, uint64_t len, uint32_t *blk_cnt,
+                              uint32_t *blk_off, uint32_t *scan_s, hipStream_t st);
+hipError_t launch_fp_nl_scatter(const uint8_t *d_text, uint64_t len, const uint32_t *blk_off,
+                                uint64_t *d_line_start, hipStream_t st);
+hipError_t launch_fp_lines(const uint8_t *d_text, uint64_t len, const uint64_t *d_line_start,
+                           uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
+                           uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals, void *hash,
+                           uint8_t *new_id, hipStream_t st);
+
 // triangle -fp positional compare (dist.hip)
 hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,

@@ -67,6 +67,10 @@ SYMBOLS = [
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
     ("fpm_fp_hash_lines_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32, vp,
                                         vp]),
+    ("fpm_fp_text_stage", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32,
+                                    C.c_uint32, C.POINTER(vp), u64p]),
+    ("fpm_fp_text_fetch", C.c_int, [vp, u64p, u32p, u32p, vp, u8p]),
+    ("fpm_fp_text_free", None, [vp]),
     ("fpm_compare_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p, C.c_uint64,
                                    C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p]),
     ("fpm_compare_grid_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, C.c_uint64,
@@ -365,6 +369,25 @@ class Context:
                               _p(pv, f64p), _p(pa, u8p)))
         return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
                 "pass": pa[:n].astype(bool)}
+
+    def fp_text(self, text, max_lines=1_000_000, seed=42, use64=False):
+        """-fp file image -> per line: ID (offset, length), value count, hash, new-ID flag."""
+        job, n = vp(), C.c_uint64()
+        _check(lib().fpm_fp_text_stage(self.h, text, len(text), max_lines, seed, int(use64),
+                                       C.byref(job), C.byref(n)))
+        n = n.value
+        io = np.zeros(max(n, 1), np.uint64)
+        il = np.zeros(max(n, 1), np.uint32)
+        nv = np.zeros(max(n, 1), np.uint32)
+        h = np.zeros(max(n, 1), np.uint64 if use64 else np.uint32)
+        ni = np.zeros(max(n, 1), np.uint8)
+        try:
+            _check(lib().fpm_fp_text_fetch(job, _p(io, u64p), _p(il, u32p), _p(nv, u32p),
+                                           h.ctypes.data, _p(ni, u8p)))
+        finally:
+            lib().fpm_fp_text_free(job)
+        return {"id_off": io[:n], "id_len": il[:n], "n_vals": nv[:n], "hash": h[:n],
+                "new_id": ni[:n]}
 
     def positional(self, ref_lists, qry_lists, use64=False, max_dist=1.0, max_pvalue=1.0):
         """triangle -fp's positional compare over the grid (query-major)."""

@@ -311,26 +311,6 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
     return 0;
 }
 
-// istream >> unsigned long long, for the cases CFL k-finger files hold
-static bool readU64(const char *&p, const char *end, uint64_t &out)
-{
-    while (p < end && isspace((unsigned char)*p)) p++;
-    bool neg = false;
-    if (p < end && (*p == '+' || *p == '-')) { neg = *p == '-'; p++; }
-    if (p >= end || *p < '0' || *p > '9') return false;
-    uint64_t v = 0;
-    bool ovf = false;
-    while (p < end && *p >= '0' && *p <= '9') {
-        uint64_t d = (uint64_t)(*p - '0');
-        if (v > (UINT64_MAX - d) / 10) ovf = true;
-        v = v * 10 + d;
-        p++;
-    }
-    if (ovf) return false;
-    out = neg ? (uint64_t)(0 - v) : v;
-    return true;
-}
-
 void Sketch::initFromFingerprints(const std::vector<std::string> &files, const Parameters &p)
 {
     parameters = p;
@@ -345,57 +325,50 @@ void Sketch::initFromFingerprints(const std::vector<std::string> &files, const P
                       << std::endl;
             exit(1);
         }
-        // parse lines (getline on '\n'; ID token; u64 values) up to the global cap
-        std::vector<uint64_t> vals, line_off{0};
-        std::vector<std::pair<uint64_t, uint32_t>> ids;
-        const char *t = text.data(), *end = text.data() + text.size();
-        while (t < end && counterLine < kLimitReadFingerprint) {
-            const char *eol = (const char *)memchr(t, '\n', (size_t)(end - t));
-            const char *le = eol ? eol : end;
-            counterLine++;
-            const char *q = t;
-            while (q < le && isspace((unsigned char)*q)) q++;
-            const char *ib = q;
-            while (q < le && !isspace((unsigned char)*q)) q++;
-            ids.push_back({(uint64_t)(ib - text.data()), (uint32_t)(q - ib)});
-            if (q > ib) {
-                uint64_t v;
-                while (readU64(q, le, v)) vals.push_back(v);
-            }
-            line_off.push_back(vals.size());
-            t = eol ? eol + 1 : end;
-        }
-        const uint64_t n = ids.size();
-        std::vector<uint32_t> h(n);
-        if (n) {
-            if (vals.empty()) vals.push_back(0);
-            check(fpm_fp_hash_lines(device(), vals.data(), line_off.data(), n, parameters.seed,
-                                    parameters.use64, h.data()),
-                  "fingerprint hash");
-        }
+        // parse + hash on the device (getline / `iss >> id` / `while (iss >> v)` /
+        // getHashFingerPrint per line, Sketch.cpp:82-101, 131), at most the lines left
+        // of the global cap
+        const uint64_t remaining = kLimitReadFingerprint - counterLine;
+        fpm_fptext *job = nullptr;
+        uint64_t n = 0;
+        check(fpm_fp_text_stage(device(), text.data(), text.size(), remaining, parameters.seed,
+                                parameters.use64, &job, &n),
+              "fingerprint parse");
+        std::vector<uint64_t> idOff(n), h64(parameters.use64 ? n : 0);
+        std::vector<uint32_t> idLen(n), nVals(n), h32(parameters.use64 ? 0 : n);
+        std::vector<uint8_t> newId(n);
+        const int rc = fpm_fp_text_fetch(job, idOff.data(), idLen.data(), nVals.data(),
+                                         parameters.use64 ? (void *)h64.data() : (void *)h32.data(),
+                                         newId.data());
+        fpm_fp_text_free(job);
+        check(rc, "fingerprint parse");
+        counterLine += n;
+        // group lines into References: a new one wherever the ID changes (:104-129)
         Reference *cur = nullptr;
         std::vector<Reference> fileRefs;
         for (uint64_t i = 0; i < n; i++) {
-            std::string id(text.data() + ids[i].first, ids[i].second);
-            const uint64_t nv = line_off[i + 1] - line_off[i];
-            if (id != lastID) {
+            const uint64_t nv = nVals[i];
+            const bool isNew = i == 0 ? std::string(text.data() + idOff[0], idLen[0]) != lastID
+                                      : newId[i] != 0;
+            if (isNew) {
+                const std::string id(text.data() + idOff[i], idLen[i]);
                 fileRefs.emplace_back();
                 cur = &fileRefs.back();
                 cur->id = id;
                 cur->length = nv;
                 cur->name = id;
                 cur->comment = "FingerPrint : " + id;
-                lastID = id;
             }
             if (!cur) {
                 // the reference dereferences a null Reference here (Sketch.cpp:131-134)
                 std::cerr << "ERROR: fingerprint line " << i + 1 << " of " << file
-                          << " continues ID \"" << id << "\" from a previous file." << std::endl;
+                          << " continues ID \"" << lastID << "\" from a previous file." << std::endl;
                 exit(1);
             }
-            cur->hashes.push_back(h[i]);
+            cur->hashes.push_back(parameters.use64 ? h64[i] : (uint64_t)h32[i]);
             cur->length += nv;
         }
+        if (n) lastID.assign(text.data() + idOff[n - 1], idLen[n - 1]);
         for (auto &r : fileRefs) references.push_back(std::move(r));
     }
     createIndex();

@@ -82,7 +82,8 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 #define FPM_K_FINALIZE 4
 #define FPM_K_INDEX 5
 #define FPM_K_PROBE 6
-#define FPM_K_COUNT 7
+#define FPM_K_FPTEXT 7
+#define FPM_K_COUNT 8
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */
@@ -143,6 +144,23 @@ int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_o
 int fpm_fp_hash_lines_dev(fpm_ctx *ctx, const uint64_t *d_vals, const uint64_t *d_line_off,
                           uint64_t n_lines, uint32_t seed, uint32_t use64, void *d_out,
                           void *stream);
+
+/* ---- -fp text ------------------------------------------------------------------
+ * Replaces the parse loop of Sketch::initFromFingerprints (Sketch.cpp:82-101: getline,
+ * `iss >> id`, `while (iss >> v)` over u64 values) and its per-line getHashFingerPrint
+ * (:131): the whole file image goes to the device, lines are split on '\n' (a last line
+ * without '\n' counts), at most max_lines are parsed (the caller passes what is left of
+ * the 1,000,000-line budget, :37, :82).  Per line: the ID token (byte offset, length),
+ * the number of values, the line hash (u32, or u64 when use64), and new_id = 1 when the
+ * ID differs from the previous line's, 0 when equal, 2 on line 0 (the caller compares
+ * it with the previous file's last ID).  Grouping lines into References stays with the
+ * caller (it owns names/comments).  fetch may be given NULL for outputs it does not need. */
+typedef struct fpm_fptext fpm_fptext;
+int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_t max_lines,
+                      uint32_t seed, uint32_t use64, fpm_fptext **job, uint64_t *n_lines);
+int fpm_fp_text_fetch(fpm_fptext *job, uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals,
+                      void *hash, uint8_t *new_id);
+void fpm_fp_text_free(fpm_fptext *job);
 
 /* ---- dist ---------------------------------------------------------------------
  * Replaces compare()/compareSketches()/pValue() (CommandDistance.cpp:335-450) over

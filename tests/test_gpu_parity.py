@@ -8,6 +8,8 @@ import os
 import numpy as np
 import pytest
 
+from conftest import GOLDEN
+
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-12
@@ -263,3 +265,45 @@ def test_dist_self_symmetric_path(ctx, oracle):
             assert np.array_equal(a["numer"], nu) and np.array_equal(a["denom"], de)
     finally:
         ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
+def _fp_texts():
+    rng = np.random.default_rng(31)
+    import fpmash.datagen as D
+    texts = [open(os.path.join(GOLDEN, "DNA2-CFL.txt"), "rb").read()[:200000],
+             b"", b"\n", b"\n\n\nX 1 2\n", b"ID 1 2 3", b"ID\n", b"   \t \n",
+             b"A 1 2\nA 3\nB 4\n\nB 5\nB\t6\r\nC +7 -8 9x 10\nD 18446744073709551615 "
+             b"18446744073709551616 3\nE 1\x0b2\x0c3\r\nF abc 1\n  G   5  6  \n",
+             b"X " + b" ".join(str(v).encode() for v in rng.integers(0, 2 ** 63, 40)) + b"\n"]
+    # random CFL-like lines with mixed separators and ID runs
+    lines = []
+    for i in range(3000):
+        idv = b"T%05d" % (i // int(rng.integers(1, 40)))
+        vals = rng.integers(0, 200, size=int(rng.integers(0, 16)))
+        sep = [b" ", b"\t", b"  "][int(rng.integers(0, 3))]
+        lines.append(idv + sep + sep.join(str(v).encode() for v in vals))
+    texts.append(b"\n".join(lines))
+    texts.append(D.cfl_text(D.random_dna(30, 300, seed=4), D.lyn2vec_ids(30)))
+    return texts
+
+
+@pytest.mark.parametrize("use64", [False, True])
+def test_fp_text_parse_matches_oracle(ctx, oracle, use64):
+    """GPU -fp text parse + line hash == the istream-semantics oracle, incl. blank lines,
+    \\t \\r \\v \\f, signs, overflow, non-numeric tokens, no trailing newline, line caps."""
+    for t in _fp_texts():
+        for cap in (1_000_000, 7, 1, 0):
+            got = ctx.fp_text(t, max_lines=cap, seed=42, use64=use64)
+            ids, vals, used = oracle.fp_parse(t, limit=cap)
+            assert len(got["id_off"]) == len(ids) == used
+            prev = None
+            for i, (idv, v) in enumerate(zip(ids, vals)):
+                o, n = int(got["id_off"][i]), int(got["id_len"][i])
+                assert t[o:o + n] == idv
+                assert got["n_vals"][i] == len(v)
+                assert int(got["hash"][i]) == oracle.get_hash_fp(v, 42, use64)
+                if i:
+                    assert got["new_id"][i] == (1 if idv != prev else 0)
+                else:
+                    assert got["new_id"][0] == 2
+                prev = idv
