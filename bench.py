@@ -175,6 +175,32 @@ def _cpu_model():
     return "unknown"
 
 
+def fp_text_leg(ctx, reps=3):
+    """C3's -fp input step, reported beside the metric (not part of `value`): parse + hash
+    the 1,000,000 CFL k-finger lines `sketch -fp` reads (50 lyn2vec-shaped sequences' CFL
+    text, tiled to the line cap: ~30 MB).  Device rate = the parse kernels' HIP-event time;
+    the wall rate includes the H2D copy of the text and the D2H of the per-line results."""
+    base = datagen.cfl_text(datagen.random_dna(50, 2000, seed=3), datagen.lyn2vec_ids(50))
+    text = base * 10
+    lines = text.count(b"\n")
+    ctx.fp_text(text[:100000])                                     # warm
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = ctx.fp_text(text, max_lines=1_000_000)
+    wall = (time.perf_counter() - t0) / reps
+    ctx.set_timing(False)
+    tot, _cnt = ctx.kernel_time(fpmash.K_FPTEXT)
+    ctx.reset_timing()
+    dev = tot / reps * 1e-3
+    n = len(r["hash"])
+    return {"lines": n, "text_bytes": len(text), "device_ms": dev * 1e3,
+            "lines_per_s_device": n / dev, "text_GBps_device": len(text) / dev / 1e9,
+            "lines_per_s_wall_pcie": n / wall, "wall_ms": wall * 1e3,
+            "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap)"}
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -289,6 +315,8 @@ def main():
     sk_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in sk_names) / args.steps
     di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in di_names) / args.steps
 
+    fp_leg = fp_text_leg(ctx) if rank == 0 else None
+
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seqs)
@@ -323,6 +351,7 @@ def main():
                      "path": ["dense walk", "bucket index + literal walk",
                               "bucket index + bucketed rank"][int(dstats["sparse"])],
                      "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
+            "fp_text": fp_leg,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
