@@ -298,6 +298,15 @@ struct fpm_sketch_job {
     MergeDesc *d_merge = nullptr;
     uint32_t class_begin[kTileClasses + 1] = {0};
     std::vector<uint32_t> round_begin;
+    // long groups: a 1-in-kSampleEvery sample of their tiles is sketched first; its s-th
+    // smallest hash bounds what every tile of the group keeps
+    uint32_t n_slots = 0;
+    TileDesc *d_stiles = nullptr;
+    MergeDesc *d_smerge = nullptr;
+    uint32_t *d_srow = nullptr;
+    uint64_t *d_thr = nullptr;
+    uint32_t sclass_begin[kTileClasses + 1] = {0};
+    std::vector<uint32_t> sround_begin;
 };
 
 static void job_release(fpm_sketch_job *j)
@@ -306,6 +315,8 @@ static void job_release(fpm_sketch_job *j)
     (void)hipSetDevice(j->ctx->device);
     (void)hipFree(j->d_seq); (void)hipFree(j->d_tiles); (void)hipFree(j->d_rows); (void)hipFree(j->d_count);
     (void)hipFree(j->d_merge);
+    (void)hipFree(j->d_stiles); (void)hipFree(j->d_smerge); (void)hipFree(j->d_srow);
+    (void)hipFree(j->d_thr);
 }
 
 extern "C" {
@@ -397,39 +408,86 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
         if (ntile_of[g] == 1) tiles[t].out_row = g;
         else { tiles[t].out_row = n_rows; lists[g].push_back(n_rows); n_rows++; }
     }
-    struct Plan { uint32_t a, b, c; };
-    std::vector<Plan> mplan;
-    std::vector<uint32_t> rb{0};
-    for (;;) {
-        bool any = false;
-        for (uint32_t g = 0; g < n_groups; g++) {
-            auto &L = lists[g];
-            if (L.size() < 2) continue;
-            any = true;
-            std::vector<uint32_t> next;
-            for (size_t i = 0; i + 1 < L.size(); i += 2) {
-                uint32_t c = (L.size() == 2) ? g : n_rows++;
-                mplan.push_back({L[i], L[i + 1], c});
-                next.push_back(c);
+    // long groups (many 4096-k-mer chunks: C5 genomes): every kSampleEvery-th tile is also
+    // sketched in a sample pass (own temp rows and merge plan); the sample's s-th smallest
+    // hash is >= the group's s-th smallest, so the full pass drops every hash above it and
+    // its merges move ~kSampleEvery*s hashes per group instead of every tile's bottom-s.
+    constexpr uint32_t kSampleEvery = 16;
+    std::vector<uint32_t> slot_of(n_groups, 0);          // 0: not sampled, else slot + 1
+    std::vector<TileDesc> stiles;
+    std::vector<std::vector<uint32_t>> slists(n_groups);
+    std::vector<uint32_t> srow;
+    {
+        std::vector<uint32_t> seen(n_groups, 0);
+        for (size_t t = 0; t < tiles.size(); t++) {
+            const uint32_t g = tile_group[t];
+            const uint64_t sample_kmers = (uint64_t)(ntile_of[g] / kSampleEvery) * kChunkKmers;
+            if (ntile_of[g] < 2 * kSampleEvery || sample_kmers < 4ULL * s) continue;
+            if (!slot_of[g]) { srow.push_back(0); slot_of[g] = (uint32_t)srow.size(); }
+            if (seen[g]++ % kSampleEvery == 0) {
+                TileDesc st = tiles[t];
+                st.out_row = n_rows;
+                st.thr_slot = 0;
+                slists[g].push_back(n_rows++);
+                stiles.push_back(st);
             }
-            if (L.size() % 2) next.push_back(L.back());
-            if (next.size() == 1) next.clear();   // reached the final row
-            L.swap(next);
         }
-        if (!any) break;
-        rb.push_back((uint32_t)mplan.size());
+        for (size_t t = 0; t < tiles.size(); t++) tiles[t].thr_slot = slot_of[tile_group[t]];
     }
+    struct Plan { uint32_t a, b, c; };
+    // pairwise merge rounds of each group's lists; the last merge writes final_row(g)
+    auto plan_rounds = [&](std::vector<std::vector<uint32_t>> &L_of, auto final_row,
+                           std::vector<Plan> &plan, std::vector<uint32_t> &rounds) {
+        rounds.assign(1, 0);
+        for (;;) {
+            bool any = false;
+            for (uint32_t g = 0; g < n_groups; g++) {
+                auto &L = L_of[g];
+                if (L.size() < 2) continue;
+                any = true;
+                std::vector<uint32_t> next;
+                for (size_t i = 0; i + 1 < L.size(); i += 2) {
+                    uint32_t c = (L.size() == 2) ? final_row(g) : n_rows++;
+                    plan.push_back({L[i], L[i + 1], c});
+                    next.push_back(c);
+                }
+                if (L.size() % 2) next.push_back(L.back());
+                if (next.size() == 1) next.clear();   // reached the final row
+                L.swap(next);
+            }
+            if (!any) break;
+            rounds.push_back((uint32_t)plan.size());
+        }
+    };
+    std::vector<Plan> splan, mplan;
+    std::vector<uint32_t> srb, rb;
+    for (uint32_t g = 0; g < n_groups; g++)
+        if (slot_of[g]) srow[slot_of[g] - 1] = slists[g].size() == 1 ? slists[g][0] : 0;
+    plan_rounds(slists, [&](uint32_t g) {
+        const uint32_t r = n_rows++;
+        srow[slot_of[g] - 1] = r;
+        return r;
+    }, splan, srb);
+    plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb);
 
     // tiles ordered by capacity class
-    std::vector<TileDesc> by_class;
-    by_class.reserve(tiles.size());
-    uint32_t class_begin[kTileClasses + 1] = {0};
-    for (int c = 0; c < kTileClasses; c++) {
-        for (auto &t : tiles)
-            if (tile_class(t.n_bytes - k + 1) == c) by_class.push_back(t);
-        class_begin[c + 1] = (uint32_t)by_class.size();
-    }
-    if (by_class.size() != tiles.size()) return fail(FPM_EINVAL, "internal: tile exceeds capacity");
+    auto order_by_class = [&](const std::vector<TileDesc> &in, std::vector<TileDesc> &out,
+                              uint32_t *begin) {
+        out.clear();
+        out.reserve(in.size());
+        begin[0] = 0;
+        for (int c = 0; c < kTileClasses; c++) {
+            for (auto &t : in)
+                if (tile_class(t.n_bytes - k + 1) == c) out.push_back(t);
+            begin[c + 1] = (uint32_t)out.size();
+        }
+        return out.size() == in.size();
+    };
+    std::vector<TileDesc> by_class, sby_class;
+    uint32_t class_begin[kTileClasses + 1] = {0}, sclass_begin[kTileClasses + 1] = {0};
+    if (!order_by_class(tiles, by_class, class_begin) ||
+        !order_by_class(stiles, sby_class, sclass_begin))
+        return fail(FPM_EINVAL, "internal: tile exceeds capacity");
 
     auto *job = new fpm_sketch_job();
     job->ctx = ctx;
@@ -440,7 +498,10 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     job->n_kmers = n_kmers;
     job->n_tiles = tiles.size();
     memcpy(job->class_begin, class_begin, sizeof(class_begin));
+    memcpy(job->sclass_begin, sclass_begin, sizeof(sclass_begin));
     job->round_begin = rb;
+    job->sround_begin = srb;
+    job->n_slots = (uint32_t)srow.size();
 
     hipError_t e = hipSuccess;
     auto alloc = [&](void **ptr, size_t bytes) {
@@ -451,26 +512,41 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     alloc((void **)&job->d_rows, (size_t)n_rows * s * sizeof(uint64_t));
     alloc((void **)&job->d_count, (size_t)n_rows * sizeof(uint32_t));
     alloc((void **)&job->d_merge, mplan.size() * sizeof(MergeDesc));
+    alloc((void **)&job->d_stiles, sby_class.size() * sizeof(TileDesc));
+    alloc((void **)&job->d_smerge, splan.size() * sizeof(MergeDesc));
+    alloc((void **)&job->d_srow, srow.size() * sizeof(uint32_t));
+    alloc((void **)&job->d_thr, srow.size() * sizeof(uint64_t));
     if (e != hipSuccess) {
         job_release(job);
         delete job;
         return fail(FPM_ENOMEM, std::string("sketch staging alloc: ") + hipGetErrorString(e));
     }
-    std::vector<MergeDesc> md(mplan.size());
-    for (size_t i = 0; i < mplan.size(); i++) {
-        md[i].a = job->d_rows + (uint64_t)mplan[i].a * s;
-        md[i].alen = job->d_count + mplan[i].a;
-        md[i].b = job->d_rows + (uint64_t)mplan[i].b * s;
-        md[i].blen = job->d_count + mplan[i].b;
-        md[i].c = job->d_rows + (uint64_t)mplan[i].c * s;
-        md[i].clen = job->d_count + mplan[i].c;
-    }
+    auto descs = [&](const std::vector<Plan> &plan) {
+        std::vector<MergeDesc> md(plan.size());
+        for (size_t i = 0; i < plan.size(); i++) {
+            md[i].a = job->d_rows + (uint64_t)plan[i].a * s;
+            md[i].alen = job->d_count + plan[i].a;
+            md[i].b = job->d_rows + (uint64_t)plan[i].b * s;
+            md[i].blen = job->d_count + plan[i].b;
+            md[i].c = job->d_rows + (uint64_t)plan[i].c * s;
+            md[i].clen = job->d_count + plan[i].c;
+        }
+        return md;
+    };
+    const std::vector<MergeDesc> md = descs(mplan), smd = descs(splan);
     if (!packed.empty()) e = hipMemcpy(job->d_seq, packed.data(), packed.size(), hipMemcpyHostToDevice);
     if (e == hipSuccess && !by_class.empty())
         e = hipMemcpy(job->d_tiles, by_class.data(), by_class.size() * sizeof(TileDesc),
                       hipMemcpyHostToDevice);
     if (e == hipSuccess && !md.empty())
         e = hipMemcpy(job->d_merge, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !sby_class.empty())
+        e = hipMemcpy(job->d_stiles, sby_class.data(), sby_class.size() * sizeof(TileDesc),
+                      hipMemcpyHostToDevice);
+    if (e == hipSuccess && !smd.empty())
+        e = hipMemcpy(job->d_smerge, smd.data(), smd.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !srow.empty())
+        e = hipMemcpy(job->d_srow, srow.data(), srow.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -488,21 +564,34 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     hipStream_t st = pick_stream(ctx, stream);
     // groups without any k-mer keep count 0
     HIP_TRY(hipMemsetAsync(job->d_count, 0, (size_t)job->n_groups * sizeof(uint32_t), st));
-    for (int c = 0; c < kTileClasses; c++) {
-        uint32_t b = job->class_begin[c], n = job->class_begin[c + 1] - b;
-        if (!n) continue;
-        TimedLaunch tl(ctx, FPM_K_SKETCH, st);
-        HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_tiles + b, n, job->kp, job->d_rows,
-                                    job->d_count, st));
-        tl.done();
+    auto tiles_pass = [&](const TileDesc *d_t, const uint32_t *begin) -> int {
+        for (int c = 0; c < kTileClasses; c++) {
+            uint32_t b = begin[c], n = begin[c + 1] - b;
+            if (!n) continue;
+            TimedLaunch tl(ctx, FPM_K_SKETCH, st);
+            HIP_TRY(launch_sketch_tiles(c, job->d_seq, d_t + b, n, job->kp, job->d_thr,
+                                        job->d_rows, job->d_count, st));
+            tl.done();
+        }
+        return FPM_OK;
+    };
+    auto merge_pass = [&](const MergeDesc *d_m, const std::vector<uint32_t> &rounds) -> int {
+        for (size_t r = 0; r + 1 < rounds.size(); r++) {
+            uint32_t b = rounds[r], n = rounds[r + 1] - b;
+            TimedLaunch tl(ctx, FPM_K_MERGE, st);
+            HIP_TRY(launch_merge(d_m + b, n, job->kp.s, st));
+            tl.done();
+        }
+        return FPM_OK;
+    };
+    if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
+        if (int rc = tiles_pass(job->d_stiles, job->sclass_begin)) return rc;
+        if (int rc = merge_pass(job->d_smerge, job->sround_begin)) return rc;
+        HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
+                                        job->kp.s, job->d_thr, st));
     }
-    for (size_t r = 0; r + 1 < job->round_begin.size(); r++) {
-        uint32_t b = job->round_begin[r], n = job->round_begin[r + 1] - b;
-        TimedLaunch tl(ctx, FPM_K_MERGE, st);
-        HIP_TRY(launch_merge(job->d_merge + b, n, job->kp.s, st));
-        tl.done();
-    }
-    return FPM_OK;
+    if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
+    return merge_pass(job->d_merge, job->round_begin);
 }
 
 int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,

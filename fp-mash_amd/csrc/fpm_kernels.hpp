@@ -15,6 +15,8 @@ struct TileDesc {
     uint64_t byte_off;
     uint32_t n_bytes;
     uint32_t out_row;   // row of the output (or temp) matrix this tile writes
+    uint32_t thr_slot;  // 0: keep every hash; i > 0: keep hashes <= thr[i - 1] (long groups)
+    uint32_t pad;
 };
 
 struct SketchKParams {
@@ -41,8 +43,12 @@ constexpr int kTileClasses = 6;
 constexpr uint32_t kTileCap[kTileClasses] = {256, 512, 1024, 2048, 4096, 8192};
 
 hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
-                               uint32_t n_tiles, const SketchKParams &p, uint64_t *d_out,
-                               uint32_t *d_count, hipStream_t st);
+                               uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_thr,
+                               uint64_t *d_out, uint32_t *d_count, hipStream_t st);
+// thr[i] = s-th smallest of sample row srow[i] when it holds s hashes, else no bound
+hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
+                                   const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
+                                   hipStream_t st);
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st);
 
 hipError_t launch_fp_hash(const uint64_t *d_vals, const uint64_t *d_line_off, uint64_t n_lines,

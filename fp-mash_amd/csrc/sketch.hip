@@ -64,7 +64,7 @@ __device__ void bitonic_sort(uint64_t *keys)
 template <int P>
 __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
-    uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
 {
     // byte images padded so that 9-dword window reads past the end stay in bounds
     constexpr int kImgWords = (P + 32 + 64) / 4;
@@ -161,14 +161,25 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
         kr[e] = key;
     }
 
-    // ---- sort: counting sort by the top log2(P/2) bits of the (uniform) hash values,
-    // then insertion sort inside each bucket (~2 keys per bucket).  A bucket holding
-    // more than kMaxBucket keys (low-complexity input: many copies of few k-mers) sends
-    // the whole tile to the bitonic sort instead.
+    // ---- long groups: keep only hashes <= the group's bound (the s-th smallest hash of a
+    // sample of the group's tiles, an upper bound of the group's own s-th smallest)
+    uint64_t hmax = p.use64 ? ~0ULL : 0xffffffffULL;
+    if (td.thr_slot) {
+        hmax = min(hmax, thr[td.thr_slot - 1]);
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if (kr[e] > hmax) vbits &= ~(1u << e);
+    }
+
+    // ---- sort: counting sort by the top log2(P/2) bits of the (uniform) hash values in
+    // [0, hmax], then insertion sort inside each bucket (~2 keys per bucket).  A bucket
+    // holding more than kMaxBucket keys (low-complexity input: many copies of few k-mers)
+    // sends the whole tile to the bitonic sort instead.
     constexpr int NB = P / 2;
     constexpr int LB = __builtin_ctz(NB);
     constexpr uint32_t kMaxBucket = 32;
-    const uint32_t bshift = p.use64 ? 64 - LB : 32 - LB;
+    const uint32_t hbits = hmax ? 64 - __clzll(hmax) : 1;
+    const uint32_t bshift = hbits > (uint32_t)LB ? hbits - LB : 0;
     for (int b = tid; b <= NB; b += kBlock) bins[b] = 0;
     if (tid == 0) big_bucket = 0;
     __syncthreads();
@@ -307,28 +318,49 @@ __global__ __launch_bounds__(kBlock) void merge_kernel(const MergeDesc *__restri
 
 template <int P>
 static hipError_t launch_p(const uint8_t *d_seq, const TileDesc *d_tiles, uint32_t n_tiles,
-                           const SketchKParams &p, uint64_t *d_out, uint32_t *d_count,
-                           hipStream_t st)
+                           const SketchKParams &p, const uint64_t *d_thr, uint64_t *d_out,
+                           uint32_t *d_count, hipStream_t st)
 {
     if (n_tiles == 0) return hipSuccess;
     hipLaunchKernelGGL(sketch_tiles_kernel<P>, dim3(n_tiles), dim3(kBlock), 0, st, d_seq, d_tiles,
-                       p, d_out, d_count);
+                       p, d_thr, d_out, d_count);
     return hipGetLastError();
 }
 
 hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
-                               uint32_t n_tiles, const SketchKParams &p, uint64_t *d_out,
-                               uint32_t *d_count, hipStream_t st)
+                               uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_thr,
+                               uint64_t *d_out, uint32_t *d_count, hipStream_t st)
 {
     switch (cls) {
-    case 0: return launch_p<256>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
-    case 1: return launch_p<512>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
-    case 2: return launch_p<1024>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
-    case 3: return launch_p<2048>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
-    case 4: return launch_p<4096>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
-    case 5: return launch_p<8192>(d_seq, d_tiles, n_tiles, p, d_out, d_count, st);
+    case 0: return launch_p<256>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
+    case 1: return launch_p<512>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
+    case 2: return launch_p<1024>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
+    case 3: return launch_p<2048>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
+    case 4: return launch_p<4096>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
+    case 5: return launch_p<8192>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+__global__ void sketch_threshold_kernel(const uint32_t *__restrict__ srow, uint32_t n_slots,
+                                        const uint64_t *__restrict__ rows,
+                                        const uint32_t *__restrict__ count, uint32_t s,
+                                        uint64_t *__restrict__ thr)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    const uint32_t r = srow[i];
+    thr[i] = count[r] >= s ? rows[(uint64_t)r * s + s - 1] : ~0ULL;
+}
+
+hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
+                                   const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
+                                   hipStream_t st)
+{
+    if (!n_slots) return hipSuccess;
+    hipLaunchKernelGGL(sketch_threshold_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
+                       d_srow, n_slots, d_rows, d_count, s, d_thr);
+    return hipGetLastError();
 }
 
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st)

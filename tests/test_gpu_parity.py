@@ -307,3 +307,21 @@ def test_fp_text_parse_matches_oracle(ctx, oracle, use64):
                 else:
                     assert got["new_id"][0] == 2
                 prev = idv
+
+
+@pytest.mark.parametrize("k,s", [(21, 1000), (21, 5000), (12, 2000), (21, 50000)])
+def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
+    """Groups of >= 32 tiles take the sample pass (every 16th tile sketched first; its s-th
+    smallest hash bounds every tile): the sets still equal the reference heap's."""
+    import fpmash
+    rng = np.random.default_rng(k * 7 + s)
+    unit = rand_seq(rng, 3000)
+    recs = [rand_seq(rng, 300_000),                        # one long record
+            unit * 70,                                     # 210 kb of a repeated unit
+            rand_seq(rng, 150_000, p_bad=0.001),           # long, with N windows
+            ] + [rand_seq(rng, 60_000) for _ in range(4)]  # a group of 4 x 60 kb records
+    groups = [0, 1, 2, 3, 3, 3, 3]
+    P = fpmash.make_params(k=k, s=s)
+    got = ctx.sketch(P, recs, groups=groups, n_groups=4)
+    exp = oracle.sketch_batch(oracle.params(k=k, s=s), recs, groups=groups, n_groups=4)
+    check_sketches(got, exp)
