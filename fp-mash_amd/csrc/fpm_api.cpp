@@ -209,6 +209,13 @@ int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
     return FPM_OK;
 }
 
+int fpm_memcpy_d2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return FPM_OK;
+}
+
 int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes)
 {
     if (int rc = set_device(ctx)) return rc;

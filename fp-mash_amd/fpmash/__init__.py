@@ -49,6 +49,7 @@ SYMBOLS = [
     ("fpm_free", C.c_int, [vp, vp]),
     ("fpm_memcpy_h2d", C.c_int, [vp, vp, vp, C.c_size_t]),
     ("fpm_memcpy_d2h", C.c_int, [vp, vp, vp, C.c_size_t]),
+    ("fpm_memcpy_d2d", C.c_int, [vp, vp, vp, C.c_size_t]),
     ("fpm_memset", C.c_int, [vp, vp, C.c_int, C.c_size_t]),
     ("fpm_ctx_set_timing", C.c_int, [vp, C.c_int]),
     ("fpm_ctx_reset_timing", C.c_int, [vp]),

@@ -70,6 +70,9 @@ int fpm_malloc(fpm_ctx *ctx, void **dptr, size_t bytes);
 int fpm_free(fpm_ctx *ctx, void *dptr);
 int fpm_memcpy_h2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* device-to-device copy, ordered on the context stream (e.g. sketch rows into a buffer
+ * handed to a collective) */
+int fpm_memcpy_d2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes);
 int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 
 /* Per-kernel timing with HIP events recorded on the launch stream.
