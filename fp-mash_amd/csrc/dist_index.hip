@@ -77,11 +77,19 @@ __global__ __launch_bounds__(256) void idx_part_hist_kernel(
         tile_hist[(uint64_t)p * ntiles + blockIdx.x] = hist[p];
 }
 
-// ---- 1b. level-1 scatter into partitions (full key + ref id, temporary arrays)
+// ---- 1b. level-1 scatter into partitions.  One u64 per entry: the key bits below the
+// partition bits that level 2 needs (l2 sub-bucket bits, then the fbits fingerprint) over
+// the ref id, i.e. (sub << 32) | final u32 entry, since fbits + rbits = 32.
+__device__ __forceinline__ uint64_t pack_l1(uint64_t K, uint32_t r, const IdxGeom &g)
+{
+    const uint64_t mid = (K << kIdxL1) >> (64 - (g.l2 + g.fbits));
+    return (mid << g.rbits) | r;
+}
+
 __global__ __launch_bounds__(256) void idx_part_scatter_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
     uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles, const uint32_t *__restrict__ tile_off,
-    uint64_t *__restrict__ tkey, uint32_t *__restrict__ tref)
+    IdxGeom g, uint64_t *__restrict__ tent)
 {
     __shared__ uint32_t cur[kParts];
     for (uint32_t p = threadIdx.x; p < kParts; p += 256)
@@ -95,8 +103,7 @@ __global__ __launch_bounds__(256) void idx_part_scatter_kernel(
         if (i < ref_len[r]) {
             const uint64_t K = norm_key(load_key(ref, hash_bytes, e), hash_bytes);
             const uint32_t pos = atomicAdd(&cur[K >> (64 - kIdxL1)], 1u);
-            tkey[pos] = K;
-            tref[pos] = r;
+            tent[pos] = pack_l1(K, r, g);
         }
     }
 }
@@ -104,7 +111,7 @@ __global__ __launch_bounds__(256) void idx_part_scatter_kernel(
 // ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits
 constexpr int kBucketThreads = 512;
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
-    const uint64_t *__restrict__ tkey, const uint32_t *__restrict__ tref, uint32_t ntiles,
+    const uint64_t *__restrict__ tent, uint32_t ntiles,
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
     uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
 {
@@ -113,7 +120,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint32_t p = blockIdx.x;
     const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
     const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
-    const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1, sh_sb = 64 - g.nbits;
+    const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
     // 4 independent loads in flight per thread
@@ -123,11 +130,11 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tkey[e] : 0;
+            K[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
-            if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(K[u] >> sh_sb) & sbmask], 1u);
+            if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
     }
     __syncthreads();
     // exclusive scan of the nsb counters: per-thread run of `per`, then a block scan
@@ -161,18 +168,16 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     __syncthreads();
     for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
         uint64_t K[kU];
-        uint32_t R[kU];
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tkey[e] : 0;
-            R[u] = e < s1 ? tref[e] : 0;
+            K[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
             if (e0 + u * kBucketThreads < s1) {
-                const uint32_t pos = atomicAdd(&sh[(uint32_t)(K[u] >> sh_sb) & sbmask], 1u);
-                entries[s0 + pos] = (key_fp(K[u], g) << g.rbits) | R[u];
+                const uint32_t pos = atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
+                entries[s0 + pos] = (uint32_t)K[u];
             }
     }
 }
@@ -435,7 +440,7 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
 
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
-                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
+                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, hipStream_t st)
 {
@@ -447,10 +452,9 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
         return e;
     hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
                        (uint32_t)stride, n_ref, hash_bytes, ntiles, (const uint32_t *)tile_off,
-                       tkey, tref);
+                       g, tent);
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
-                       (size_t)4 << g.l2, st, (const uint64_t *)tkey, (const uint32_t *)tref,
-                       ntiles, (const uint32_t *)tile_off, g, dir, entries, self_events);
+                       (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles, (const uint32_t *)tile_off, g, dir, entries, self_events);
     return hipGetLastError();
 }
 

@@ -860,11 +860,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
-        void *tile_hist, *tile_off, *tkey, *tref, *dir, *entries, *scan_s, *ctr;
+        void *tile_hist, *tile_off, *tent, *dir, *entries, *scan_s, *ctr;
         HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
         HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
-        HIP_TRY(scratch(ctx, 2, E * 8, &tkey));
-        HIP_TRY(scratch(ctx, 3, E * 4, &tref));
+        HIP_TRY(scratch(ctx, 2, E * 8, &tent));
         HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir));
         HIP_TRY(scratch(ctx, 5, E * 4, &entries));
         HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
@@ -880,7 +879,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
             HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
                                      (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                     (uint32_t *)scan_s, (uint64_t *)tkey, (uint32_t *)tref,
+                                     (uint32_t *)scan_s, (uint64_t *)tent,
                                      (uint32_t *)dir, (uint32_t *)entries, unsorted,
                                      self_set ? events : nullptr, st));
             if (!self_set)

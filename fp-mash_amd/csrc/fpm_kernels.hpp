@@ -69,7 +69,7 @@ hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long lo
 
 // bucket index over ref hashes (dist_index.hip)
 constexpr uint32_t kIdxL1 = 10;        // level-1 partition bits
-constexpr uint32_t kIdxTile = 4096;    // matrix cells per level-1 tile
+constexpr uint32_t kIdxTile = 16384;   // matrix cells per level-1 tile (~16 entries per partition)
 struct IdxGeom {
     uint32_t l2;       // level-2 bits (1..14)
     uint32_t nbits;    // bucket bits = kIdxL1 + l2
@@ -79,7 +79,7 @@ struct IdxGeom {
 };
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
-                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tkey, uint32_t *tref,
+                            uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
