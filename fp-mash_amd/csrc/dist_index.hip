@@ -295,8 +295,8 @@ __global__ void sum64_kernel(unsigned long long *events)
 // One workgroup per (query row, ref chunk): LDS bitmap of the chunk's refs.  Each wave
 // takes 64 query hashes at a time: lane l looks up the bucket [st, st + cnt) of hash l,
 // a wave scan flattens the 64 buckets into one event range, and the lanes then read
-// consecutive entries of that range (coalesced) — the owner hash of an event comes from
-// a 6-step search over the wave's 64 prefix sums in LDS.
+// consecutive entries of that range (coalesced).  The owner hash of each event comes from
+// a per-wave byte map filled by the lanes for 1024-event windows (one LDS read per event).
 __global__ __launch_bounds__(256) void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
@@ -308,8 +308,11 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long row_base;
-    __shared__ uint32_t w_st[4][64], w_pre[4][64];
-    __shared__ uint32_t w_tgt[4][64];
+    // per wave: (entry base, fingerprint) of its 64 hashes, and the owner map of an event
+    // window (which of the 64 hashes each event belongs to)
+    constexpr uint32_t kWin = 1024;
+    __shared__ uint64_t w_tab[4][64];
+    __shared__ uint8_t w_own[4][kWin];
     const uint32_t q = xcd_row(blockIdx.x, n_qry);   // XCD-contiguous rows: shared buckets in L2
     if (q >= n_qry) return;
     const uint32_t r0 = blockIdx.y * chunk_refs;
@@ -356,41 +359,42 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
             if ((int)lane >= d) inc += y;
         }
         const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-        // same wave writes and reads these slots: LDS ops of one wave complete in order
-        w_st[wave][lane] = st;
-        w_pre[wave][lane] = inc - cnt;
-        w_tgt[wave][lane] = tgt;
-        __builtin_amdgcn_wave_barrier();
-        // 4 events per lane per pass (ev, ev+64, ev+128, ev+192): their owner searches and
-        // entry loads are independent, so the LDS reads and global loads overlap
-        constexpr int kU = 4;
-        for (uint32_t ev0 = lane; ev0 < total; ev0 += 64 * kU) {
-            uint32_t m[kU];
-#pragma unroll
-            for (int u = 0; u < kU; u++) m[u] = 0;
-#pragma unroll
-            for (uint32_t step = 32; step > 0; step >>= 1) {
+        // same wave writes and reads these slots: LDS ops of one wave complete in order.
+        // Event ev of hash m reads entries[st_m + ev - pre_m] = entries[base_m + ev] (u32
+        // arithmetic wraps consistently).
+        const uint32_t pre = inc - cnt;
+        w_tab[wave][lane] = ((uint64_t)tgt << 32) | (uint32_t)(st - pre);
+        for (uint32_t wb = 0; wb < total; wb += kWin) {
+            // owner map of events [wb, wb + kWin): each lane marks its own hash's events
+            const uint32_t a0 = max(pre, wb), a1 = min(pre + cnt, wb + kWin);
+            for (uint32_t e = a0; e < a1; e++) w_own[wave][e - wb] = (uint8_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t wn = min(kWin, total - wb);
+            // 4 events per lane in flight: owner byte -> (base, fingerprint) -> entry
+            constexpr int kU = 4;
+            for (uint32_t e0 = lane; e0 < wn; e0 += 64 * kU) {
+                uint64_t tab[kU];
 #pragma unroll
                 for (int u = 0; u < kU; u++) {
-                    const uint32_t pv = w_pre[wave][m[u] + step];      // last m with pre <= ev
-                    m[u] = (pv <= ev0 + 64 * u) ? m[u] + step : m[u];
+                    const uint32_t e = e0 + 64 * u;
+                    tab[u] = w_tab[wave][w_own[wave][e < wn ? e : 0]];
+                }
+                uint32_t en[kU];
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const uint32_t e = e0 + 64 * u;
+                    en[u] = e < wn ? entries[(uint32_t)tab[u] + wb + e] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < kU; u++) {
+                    const uint32_t e = e0 + 64 * u;
+                    if (e < wn && (en[u] >> g.rbits) == (uint32_t)(tab[u] >> 32)) {
+                        const uint32_t r = en[u] & rmask;
+                        if (r >= r0 && r < r1c) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+                    }
                 }
             }
-            uint32_t en[kU];
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                const uint32_t ev = ev0 + 64 * u;
-                const uint32_t at = ev < total ? w_st[wave][m[u]] + (ev - w_pre[wave][m[u]]) : 0u;
-                en[u] = ev < total ? entries[at] : 0;
-            }
-#pragma unroll
-            for (int u = 0; u < kU; u++) {
-                const uint32_t ev = ev0 + 64 * u;
-                if (ev < total && (en[u] >> g.rbits) == w_tgt[wave][m[u]]) {
-                    const uint32_t r = en[u] & rmask;
-                    if (r >= r0 && r < r1c) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
-                }
-            }
+            __builtin_amdgcn_wave_barrier();   // before the next window's owner map
         }
         __builtin_amdgcn_wave_barrier();
       }
