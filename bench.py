@@ -35,6 +35,7 @@ import fpmash  # noqa: E402
 from fpmash import datagen  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py,
 # regenerated on the GPU box whenever the kernels change)
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
@@ -296,6 +297,12 @@ def main():
         "unit": "GB/s",
         "frac": achieved / HBM_PEAK_GBS if achieved else None,
         "traffic": traffic.get(dom, {}).get("traffic_bytes"),
+        # integer kernels: the issue side beside the byte roofline (MI355X: 1024 SIMDs x
+        # 2.4 GHz, one wave64 VALU instruction per 2 cycles per SIMD)
+        "valu_issue_frac": (traffic[dom]["sq"]["insts_valu"] /
+                            (ktimes[dom]["avg_ms"] * 1e-3 * VALU_ISSUE_PER_S)
+                            if dom in traffic and "sq" in traffic[dom] else None),
+        "wave_state_frac": traffic.get(dom, {}).get("wave_state_frac"),
         "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if dom in traffic else None,
         "alg_bytes_per_launch": alg.get(dom, (None, ""))[0],
         "alg_bytes_formula": alg.get(dom, (None, ""))[1],

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """tools/pmc_traffic.py — HBM traffic per kernel launch from rocprofv3 PMC counters.
 
-Runs `bench.py` under rocprofv3 twice (FETCH_SIZE and WRITE_SIZE do not fit one pass on
-gfx950), then writes per-kernel bytes per launch to a JSON file that bench.py reads for
-`roofline.traffic`.  Corrections follow MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950
+Runs `bench.py` under rocprofv3 three times (FETCH_SIZE and WRITE_SIZE do not fit one pass
+on gfx950; a third pass takes SQ instruction counts), then writes per-kernel bytes and
+instructions per launch to a JSON file that bench.py reads for `roofline.traffic` and the
+VALU-issue utilisation beside it.  Corrections follow MI355X_MICROARCH.md §HBM: FETCH_SIZE on gfx950
 tallies 128-B requests at 64 B, so it is doubled; WRITE_SIZE is taken as reported; both
 count Infinity-Cache traffic (L2 memory-side requests), so they are an upper bound on
 HBM bytes.  rocprofv3 reports both in KiB.
@@ -48,9 +49,11 @@ def group_of(name: str):
     return None
 
 
-def run_pass(counter: str, outdir: str, bench_args: list[str]) -> dict:
-    cmd = ["rocprofv3", "--pmc", counter, "-d", outdir, "-o", "pmc", "--output-format", "csv",
-           "--", sys.executable, os.path.join(ROOT, "bench.py")] + bench_args
+def run_pass(counter, outdir: str, bench_args: list[str]) -> dict:
+    counters = [counter] if isinstance(counter, str) else list(counter)
+    cmd = ["rocprofv3", "--pmc"] + counters + ["-d", outdir, "-o", "pmc", "--output-format",
+                                               "csv", "--", sys.executable,
+                                               os.path.join(ROOT, "bench.py")] + bench_args
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(outdir + ".log"), "w") as log:
         subprocess.run(cmd, check=True, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
@@ -58,15 +61,15 @@ def run_pass(counter: str, outdir: str, bench_args: list[str]) -> dict:
     files = glob.glob(os.path.join(outdir, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter file under {outdir}")
-    per_disp = collections.defaultdict(float)     # (group, dispatch) -> KiB
+    per_disp = {c: collections.defaultdict(float) for c in counters}   # (group, dispatch) -> v
     for row in csv.DictReader(open(files[0])):
-        if row["Counter_Name"] != counter:
+        if row["Counter_Name"] not in per_disp:
             continue
         g = group_of(row["Kernel_Name"])
         if g is None:
             continue
-        per_disp[(g, row["Dispatch_Id"])] += float(row["Counter_Value"])
-    return per_disp
+        per_disp[row["Counter_Name"]][(g, row["Dispatch_Id"])] += float(row["Counter_Value"])
+    return per_disp[counter] if isinstance(counter, str) else per_disp
 
 
 def per_launch(per_disp: dict, launches: dict) -> dict:
@@ -91,6 +94,10 @@ def main():
     # is several kernels (the index build) is one step's worth of them
     steps = a.steps + a.warmup
     launches = {g: steps for (g, _d) in list(fetch) + list(write)}
+    sq = run_pass(("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
+                   "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"),
+                  os.path.join(a.work, "sq"), bench_args)
+    sqk = {c: per_launch(v, launches) for c, v in sq.items()}
     f = per_launch(fetch, launches)
     w = per_launch(write, launches)
     res = {}
@@ -98,11 +105,19 @@ def main():
         fb = 2.0 * f.get(g, 0.0)          # gfx950: FETCH_SIZE = half the streamed bytes
         wb = w.get(g, 0.0)
         res[g] = {"fetch_bytes": fb, "write_bytes": wb, "traffic_bytes": fb + wb}
+        # SQ counters per launch (per_launch scales by 1024: undo); wave-state split
+        sqg = {c.replace("SQ_", "").lower(): v.get(g, 0.0) / 1024.0 for c, v in sqk.items()}
+        wc = sqg.get("wave_cycles") or 1.0
+        res[g]["sq"] = sqg
+        res[g]["wave_state_frac"] = {"active": sqg.get("active_inst_any", 0) / wc,
+                                     "issue_stall": sqg.get("wait_inst_any", 0) / wc,
+                                     "waiting": sqg.get("wait_any", 0) / wc}
     out = {
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                   f"bench.py --steps {a.steps} --warmup {a.warmup}; bytes per launch = "
                   "2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB x 1024; includes "
-                  "Infinity-Cache traffic",
+                  "Infinity-Cache traffic. A third pass: SQ instruction counts and the "
+                  "wave-state split (active / issue-stall / waiting) per launch",
         "kernels": res,
     }
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
