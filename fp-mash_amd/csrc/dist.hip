@@ -125,7 +125,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *B = qry + (uint64_t)q * qry_stride;
     if (threadIdx.x == 0) s_maxn = 0;
     for (uint32_t t = threadIdx.x; t < lb; t += blockDim.x) Bs[t] = B[t];
-    if (threadIdx.x == 0) Bs[lb] = 0;
+    // sentinel past the end: Bs[lb] >= every A value, so a search that has narrowed to an
+    // empty range (len = 0) reads a value that is not < a and stays put (no len test)
+    if (threadIdx.x == 0) Bs[lb] = ~0ULL;
     __syncthreads();
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
@@ -218,8 +220,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
                 for (int g = 0; g < kGroup; g++) {
                     const uint32_t half = len[g] >> 1;
+                    // len = 0: lo is the lower bound, so Bs[lo] (or the sentinel) >= a
                     const uint64_t bv = Bs[lo[g] + half];
-                    const bool less = (len[g] != 0) & (bv < cur[g]);
+                    const bool less = bv < cur[g];
                     lo[g] = less ? lo[g] + half + 1 : lo[g];
                     len[g] = less ? len[g] - half - 1 : half;
                 }
