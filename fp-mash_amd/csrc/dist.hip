@@ -227,26 +227,34 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                     len[g] = less ? len[g] - half - 1 : half;
                 }
             }
-            bool done = false;
+            // all kGroup equality reads first (j <= lb, Bs[lb] is the sentinel; chunks past
+            // nch have act = 0), then the ballots: one LDS round trip for the group
+            uint64_t bj[kGroup];
+            uint32_t j[kGroup];
 #pragma unroll
             for (int g = 0; g < kGroup; g++) {
-                const uint32_t t = g0 + g;
-                if (t >= nch) break;                      // uniform
-                const uint32_t i = t * 64 + lane;
-                const uint32_t j = act[g] ? lo[g] : lb;
-                const uint64_t bj = Bs[j];
-                const bool eq = act[g] & (j < lb) & (bj == cur[g]);
-                const uint64_t bal = __ballot(eq);
+                j[g] = act[g] ? lo[g] : lb;
+                bj[g] = Bs[j[g]];
+            }
+            uint32_t u_last = 0;
+#pragma unroll
+            for (int g = 0; g < kGroup; g++) {
+                const uint32_t i = (g0 + g) * 64 + lane;
+                const bool eq = act[g] & (j[g] < lb) & (bj[g] == cur[g]);
+                const uint64_t bal = __builtin_amdgcn_ballot_w64(eq);
                 const uint32_t k = shared_below + __builtin_amdgcn_mbcnt_hi(
                                        (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                const uint32_t u = i + j - k;             // union rank of A[i] (valid lanes)
-                cnt += __popcll(__ballot(eq && u < S));
+                const uint32_t u = i + j[g] - k;          // union rank of A[i] (valid lanes)
+                cnt += __popcll(__builtin_amdgcn_ballot_w64(eq & (u < S)));
                 shared_below += __popcll(bal);
-                if (!need_all && g == kGroup - 1) {
-                    // union rank of the group's last valid element; later A elements rank higher
-                    const uint32_t last = min(la - 1 - t * 64, 63u);
-                    if ((uint32_t)__builtin_amdgcn_readlane((int)u, (int)last) >= S) done = true;
-                }
+                if (g == kGroup - 1) u_last = u;
+            }
+            // union rank of the group's last element (the group is full when g0 + kGroup <=
+            // nch); later A elements rank higher
+            bool done = false;
+            if (!need_all && g0 + kGroup <= nch) {
+                const uint32_t last = min(la - 1 - (g0 + kGroup - 1) * 64, 63u);
+                done = (uint32_t)__builtin_amdgcn_readlane((int)u_last, (int)last) >= S;
             }
             if (done) break;
 #pragma unroll
