@@ -277,13 +277,25 @@ def main():
                              "packed sequence bytes read + 8 B per output hash"),
         N[fpmash.K_INDEX]: (n_hash * 8,
                             "reference sketch hashes read once (8 B each)"),
-        N[fpmash.K_PROBE]: (n_hash * 8 + n_pairs * 8,
-                            "query sketch hashes read + numer/denom (8 B/pair) written"),
         N[fpmash.K_COMPARE]: (2 * n_hash * 8,
                               "ref + query sketches read once (8 B per hash)"),
-        N[fpmash.K_FINALIZE]: (n_pairs * (4 + 4 + 8 + 8 + 1),
-                               "numer+denom read, distance+p-value+pass written per pair"),
     }
+    if dstats["sparse"]:
+        # fused sparse dist: the probe writes every cell's final values, the candidate
+        # finalize rewrites the candidate cells (and their mirrors on the symmetric path)
+        n_cand = dstats["candidates"]
+        cells = 2 * n_cand - n if dstats["sparse"] == 2 else n_cand
+        alg[N[fpmash.K_FILL]] = (n_pairs * (4 + 4 + 8 + 8 + 1),
+                                 "numer/denom/distance/p-value/pass (25 B/pair) written")
+        alg[N[fpmash.K_PROBE]] = (n_hash * 8, "query sketch hashes read")
+        alg[N[fpmash.K_FINALIZE]] = (n_cand * (8 + 4 + 4) + cells * (8 + 8 + 1),
+                                     "candidate + its numer/denom read, distance/p-value/pass "
+                                     "written per candidate cell (mirrors included)")
+    else:
+        alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * 8,
+                                  "query sketch hashes read + numer/denom (8 B/pair) written")
+        alg[N[fpmash.K_FINALIZE]] = (n_pairs * (4 + 4 + 8 + 8 + 1),
+                                     "numer+denom read, distance+p-value+pass written per pair")
     traffic = {}
     if os.path.exists(PMC_TRAFFIC):
         traffic = json.load(open(PMC_TRAFFIC)).get("kernels", {})

@@ -107,7 +107,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const uint64_t *__restrict__ qry, const uint32_t *__restrict__ qry_len,
     uint64_t qry_stride, uint32_t S, uint32_t sym, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom)
+    uint32_t *__restrict__ denom, uint32_t *__restrict__ cnum, uint32_t *__restrict__ cden)
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 11 : 12;   // 2 * CAP buckets
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
@@ -263,6 +263,11 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         if (lane == 0) {
             const uint64_t un = (uint64_t)la + lb - shared_below;
             const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
+            if (cnum) {          // compact: the candidate finalize scatters (and mirrors)
+                cnum[base + c] = cnt;
+                cden[base + c] = dn;
+                continue;
+            }
             numer[o] = cnt;
             denom[o] = dn;
             const uint32_t r = (uint32_t)(o - pair_row);
@@ -279,7 +284,8 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
                              uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, hipStream_t st)
+                             uint32_t *d_denom, uint32_t *d_cnum, uint32_t *d_cden,
+                             hipStream_t st)
 {
     if (!n_qry) return hipSuccess;
     const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
@@ -287,11 +293,11 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
     if (cap <= 1024)
         hipLaunchKernelGGL(rank_rows_kernel<1024>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
                            d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
-                           (uint32_t)sym, d_numer, d_denom);
+                           (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else if (cap <= 2048)
         hipLaunchKernelGGL(rank_rows_kernel<2048>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
                            d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
-                           (uint32_t)sym, d_numer, d_denom);
+                           (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -409,6 +415,173 @@ __global__ __launch_bounds__(256) void dist_finalize_kernel(
     dist[o] = dv;
     pval[o] = pv;
     if (pass) pass[o] = ok ? 1 : 0;
+}
+
+// Every cell's no-shared-hash values (PairFill): a pure write stream, 25 B per cell, one
+// workgroup per 1024 cells of one query row (row = blockIdx.x / blocks-per-row, uniform).
+// VEC (n_ref % 4 == 0, so a row starts 4-cell aligned): each lane writes 4 consecutive
+// cells with 16-B stores (1 KiB per wave store; the pass bytes as one dword).
+constexpr uint32_t kFillCells = 1024;
+template <bool VEC>
+__global__ __launch_bounds__(256) void dist_fill_kernel(
+    const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
+    uint32_t nrb, uint32_t ntask, uint32_t S, uint32_t *__restrict__ numer,
+    uint32_t *__restrict__ denom, PairFill fill)
+{
+    const bool keep1 = !(fill.max_dist >= 0 && 1.0 > fill.max_dist);   // distance 0 always kept
+    const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
+    for (uint32_t t = blockIdx.x; t < ntask; t += gridDim.x) {
+    const uint32_t q = t / nrb, rb = t - q * nrb;
+    const uint32_t lq = qry_len[q];
+    const uint64_t row = (uint64_t)q * n_ref;
+    if (VEC) {
+        const uint32_t r = rb * kFillCells + threadIdx.x * 4;
+        if (r >= n_ref) continue;
+        const uint64_t o = row + r;
+        const uint4 rl = *(const uint4 *)(ref_len + r);
+        const uint32_t d[4] = {rl.x + lq, rl.y + lq, rl.z + lq, rl.w + lq};  // <= 2 stride
+        uint32_t dn[4], pa = 0;
+        double dv[4], pv[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const bool ok = d[u] == 0 || keep1;
+            dn[u] = d[u] < S ? d[u] : S;
+            dv[u] = d[u] == 0 ? 0.0 : 1.0;
+            pv[u] = ok ? 1.0 : 0.0;
+            pa |= (ok && pkeep ? 1u : 0u) << (8 * u);
+        }
+        *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
+        *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
+        *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
+        *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
+        *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
+        *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
+        if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+        continue;
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kFillCells / 256; u++) {
+        const uint32_t r = rb * kFillCells + u * 256 + threadIdx.x;
+        if (r >= n_ref) break;
+        const uint64_t o = row + r;
+        const uint32_t d = ref_len[r] + lq;            // both <= stride, no overflow
+        const bool ok = d == 0 || keep1;
+        numer[o] = 0;
+        denom[o] = d < S ? d : S;
+        fill.dist[o] = d == 0 ? 0.0 : 1.0;
+        fill.pval[o] = ok ? 1.0 : 0.0;
+        if (fill.pass) fill.pass[o] = ok && pkeep ? 1 : 0;
+    }
+    }
+}
+
+hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
+                            uint32_t n_qry, uint32_t S, uint32_t *d_numer, uint32_t *d_denom,
+                            const PairFill &fill, hipStream_t st)
+{
+    if (!n_ref || !n_qry) return hipSuccess;
+    const uint32_t nrb = (n_ref + kFillCells - 1) / kFillCells;
+    const uint64_t blocks = (uint64_t)nrb * n_qry;
+    if (blocks >= (1ULL << 31)) return hipErrorInvalidValue;
+    // 16-B stores need 16-B aligned rows of every output (the pass row as 4-B aligned)
+    const auto al = [](const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
+    const bool vec = n_ref % 4 == 0 && al(d_ref_len, 16) && al(d_numer, 16) &&
+                     al(d_denom, 16) && al(fill.dist, 16) && al(fill.pval, 16) &&
+                     al(fill.pass, 4);
+    // the full grid: short workgroups hand their slots back to the candidate compare running
+    // beside; a capped grid-stride fill (256-4096 workgroups) held them and measured slower
+    const uint32_t grid = (uint32_t)blocks;
+    if (vec)
+        hipLaunchKernelGGL(dist_fill_kernel<true>, dim3(grid), dim3(256), 0, st, d_ref_len,
+                           n_ref, d_qry_len, nrb, (uint32_t)blocks, S, d_numer, d_denom, fill);
+    else
+        hipLaunchKernelGGL(dist_fill_kernel<false>, dim3(grid), dim3(256), 0, st, d_ref_len,
+                           n_ref, d_qry_len, nrb, (uint32_t)blocks, S, d_numer, d_denom, fill);
+    return hipGetLastError();
+}
+
+// The same per-pair arithmetic as dist_finalize_kernel, for the candidate cells of the
+// sparse path only (the probe wrote every other cell's final values).  Grid-stride over the
+// device-side candidate count; with `sym` each candidate (q, r), r <= q, also finalizes its
+// mirror (r, q), whose numer / denom the rank kernel wrote.
+__device__ __forceinline__ void finalize_cell(uint64_t o, uint32_t c, uint32_t d, uint64_t len_ref,
+                                              uint64_t len_qry, uint32_t kmer_size,
+                                              double kmer_space, double max_dist,
+                                              double max_pvalue, double *dist, double *pval,
+                                              uint8_t *pass)
+{
+    double dv;
+    if (c == d) dv = 0.0;
+    else if (c == 0) dv = 1.0;
+    else {
+        double jac = (double)c / (double)d;
+        dv = -log(2.0 * jac / (1.0 + jac)) / (double)kmer_size;
+        if (dv > 1.0) dv = 1.0;
+    }
+    bool ok = !(max_dist >= 0 && dv > max_dist);
+    double pv = 0.0;
+    if (ok) {
+        pv = pvalue_dev(c, len_ref, len_qry, kmer_space, d);
+        ok = !(max_pvalue >= 0 && pv > max_pvalue);
+    }
+    dist[o] = dv;
+    pval[o] = pv;
+    if (pass) pass[o] = ok ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
+    const uint64_t *__restrict__ cand, const unsigned long long *__restrict__ n_cand,
+    uint32_t sym, const uint32_t *__restrict__ cnum, const uint32_t *__restrict__ cden,
+    uint32_t *__restrict__ numer, uint32_t *__restrict__ denom,
+    const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
+    uint32_t n_ref, uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
+    double *__restrict__ dist, double *__restrict__ pval, uint8_t *__restrict__ pass)
+{
+    const uint64_t n = *n_cand;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = cand[c];
+        const uint32_t q = (uint32_t)(o / n_ref), r = (uint32_t)(o - (uint64_t)q * n_ref);
+        uint32_t nm, dn;
+        if (cnum) {          // compact results: scatter numer / denom too
+            nm = cnum[c];
+            dn = cden[c];
+            numer[o] = nm;
+            denom[o] = dn;
+        } else {
+            nm = numer[o];
+            dn = denom[o];
+        }
+        finalize_cell(o, nm, dn, ref_length[r], qry_length[q], kmer_size, kmer_space, max_dist,
+                      max_pvalue, dist, pval, pass);
+        if (sym && r != q) {   // cell (r, q): query r against ref q
+            const uint64_t o2 = (uint64_t)r * n_ref + q;
+            if (cnum) {
+                numer[o2] = nm;
+                denom[o2] = dn;
+            }
+            finalize_cell(o2, nm, dn, ref_length[q], qry_length[r], kmer_size, kmer_space,
+                          max_dist, max_pvalue, dist, pval, pass);
+        }
+    }
+}
+
+hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                     uint64_t cap, bool sym, const uint32_t *d_cnum,
+                                     const uint32_t *d_cden, uint32_t *d_numer,
+                                     uint32_t *d_denom, const uint64_t *d_ref_length,
+                                     const uint64_t *d_qry_length, uint32_t n_ref,
+                                     uint32_t kmer_size, double kmer_space, double max_dist,
+                                     double max_pvalue, double *d_dist, double *d_pvalue,
+                                     uint8_t *d_pass, hipStream_t st)
+{
+    if (!cap) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((cap + 255) / 256, 4096);
+    hipLaunchKernelGGL(dist_cand_finalize_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
+                       d_cand, d_n_cand, (uint32_t)sym, d_cnum, d_cden, d_numer, d_denom,
+                       d_ref_length, d_qry_length, n_ref, kmer_size, kmer_space, max_dist,
+                       max_pvalue, d_dist, d_pvalue, d_pass);
+    return hipGetLastError();
 }
 
 // triangle -fp's compareFingerprints (CommandTriangle.cpp:255-302): positional compare of

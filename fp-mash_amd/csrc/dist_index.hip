@@ -302,8 +302,9 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
-    uint32_t *__restrict__ numer, uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
-    unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
+    uint32_t defaults, uint32_t *__restrict__ numer, uint32_t *__restrict__ denom,
+    uint64_t *__restrict__ cand, unsigned long long *__restrict__ n_cand,
+    uint64_t *__restrict__ row_seg)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
@@ -325,12 +326,13 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     const uint32_t lq = qry_len[q];
     const uint64_t rowoff = (uint64_t)q * stride;
     // every pair of the row starts as "no shared value": (0, min(S, la+lb))
-    for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {
-        uint64_t o = (uint64_t)q * n_ref + r;
-        uint64_t d = (uint64_t)ref_len[r] + lq;
-        numer[o] = 0;
-        denom[o] = d < S ? (uint32_t)d : S;
-    }
+    if (defaults)
+        for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {
+            uint64_t o = (uint64_t)q * n_ref + r;
+            uint64_t d = (uint64_t)ref_len[r] + lq;
+            numer[o] = 0;
+            denom[o] = d < S ? (uint32_t)d : S;
+        }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t rmask = (uint32_t)((1ULL << g.rbits) - 1);
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
@@ -477,9 +479,9 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
-                             const uint32_t *d_ref_len, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
-                             uint64_t *row_seg, hipStream_t st)
+                             const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
+                             uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -488,7 +490,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const size_t lds = ((cref + 31) / 32) * 4;
     hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
-                       d_ref_len, S, (uint32_t)sym, d_numer, d_denom, cand, n_cand, row_seg);
+                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, d_numer, d_denom, cand, n_cand,
+                       row_seg);
     return hipGetLastError();
 }
 

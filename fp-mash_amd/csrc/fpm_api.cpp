@@ -65,7 +65,22 @@ struct fpm_ctx {
     int dist_mode = FPM_DIST_AUTO;
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
+    // side stream for the sparse dist's fill (a pure write stream that runs beside the
+    // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
+    hipStream_t aux = nullptr;
+    hipEvent_t ev_in = nullptr, ev_fill = nullptr;
 };
+
+static hipError_t ensure_aux(fpm_ctx *ctx)
+{
+    if (ctx->aux) return hipSuccess;
+    // default priority: a low-priority side stream (or a high-priority main one) measured
+    // slower, the fill then trails the candidate compare instead of sharing its CUs
+    hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming);
+    return e;
+}
 
 // returns a device buffer of at least `bytes` for scratch slot `id`
 static hipError_t scratch(fpm_ctx *ctx, int id, size_t bytes, void **out)
@@ -166,6 +181,9 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
         if (s.p) (void)hipFree(s.p);
     if (ctx->host_counters) (void)hipHostFree(ctx->host_counters);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
+    if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
     delete ctx;
 }
 
@@ -820,13 +838,27 @@ void fpm_fp_text_free(fpm_fptext *j)
 
 }  // extern "C"
 
+// distance / p-value outputs of fpm_dist_dev, handed to compare_impl so the sparse path
+// can finalize in place: the probe writes every cell's no-shared-hash values and a
+// candidate kernel rewrites the candidates (no dense pass re-reading numer / denom)
+struct DistFinal {
+    const uint64_t *ref_length, *qry_length;
+    uint32_t kmer_size;
+    double kmer_space, max_dist, max_pvalue;
+    double *dist, *pval;
+    uint8_t *pass;
+};
+
 // The grid compare: dense walk, or bucket index + probe + candidate kernel (sparse).
+// With `fin`, a sparse run also finalizes and sets *finalized.
 static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
-                        uint32_t *d_denom, void *stream)
+                        uint32_t *d_denom, void *stream, const DistFinal *fin = nullptr,
+                        bool *finalized = nullptr)
 {
+    if (finalized) *finalized = false;
     if (int rc = set_device(ctx)) return rc;
     if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
     hipStream_t st = pick_stream(ctx, stream);
@@ -857,6 +889,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     }
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
+    bool fill_pending = false;
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
@@ -906,21 +939,54 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
             const bool sym = rows_merge && self_set;
+            // with `fin`: every cell's no-shared-hash values, written on the side stream
+            // beside the candidate compare (it needs only the list lengths; beside the
+            // index build or the probe it slowed both, they move as many bytes as it does).
+            // The rank kernel then leaves the grid alone (results per candidate slot), and the
+            // candidate finalize, after the fill, scatters them; the literal walk writes cells
+            // in place, so it waits for the fill instead.
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
-                                          d_ref_len, sketch_size, sym, d_numer, d_denom,
-                                          (uint64_t *)cand, n_cand, (uint64_t *)row_seg, st));
+                                          d_ref_len, sketch_size, sym, fin == nullptr, d_numer,
+                                          d_denom, (uint64_t *)cand, n_cand,
+                                          (uint64_t *)row_seg, st));
                 tl.done();
             }
+            uint32_t *cnum = nullptr, *cden = nullptr;
+            if (fin) {
+                PairFill fill;
+                fill.dist = fin->dist;
+                fill.pval = fin->pval;
+                fill.pass = fin->pass;
+                fill.max_dist = fin->max_dist;
+                fill.max_pvalue = fin->max_pvalue;
+                HIP_TRY(ensure_aux(ctx));
+                HIP_TRY(hipEventRecord(ctx->ev_in, st));
+                HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
+                TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
+                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, d_numer,
+                                         d_denom, fill, ctx->aux));
+                tl.done();
+                HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
+                fill_pending = true;
+                if (rows_merge) {
+                    void *cres;
+                    HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
+                    cnum = (uint32_t *)cres;
+                    cden = cnum + cap;
+                }
+            }
+            if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             {
                 TimedLaunch tl(ctx, FPM_K_COMPARE, st);
                 if (rows_merge)
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
-                                              sketch_size, sym, d_numer, d_denom, st));
+                                              sketch_size, sym, d_numer, d_denom, cnum, cden,
+                                              st));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
@@ -928,12 +994,25 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                    d_denom, st));
                 tl.done();
             }
+            if (fin) {
+                if (cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+                TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
+                HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
+                                                  cden, d_numer, d_denom, fin->ref_length,
+                                                  fin->qry_length,
+                                                  n_ref, fin->kmer_size, fin->kmer_space,
+                                                  fin->max_dist, fin->max_pvalue, fin->dist,
+                                                  fin->pval, fin->pass, st));
+                tl.done();
+                *finalized = true;
+            }
             HIP_TRY(hipMemcpyAsync(ctx->host_counters + 65, n_cand, 8, hipMemcpyDeviceToHost, st));
             ctx->last_sparse = rows_merge ? 2 : 1;
             ctx->last_cand = (uint64_t)-1;   // read lazily by fpm_ctx_last_dist_stats callers after sync
             return FPM_OK;
         }
     }
+    if (fill_pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));   // dense after all
     TimedLaunch tl(ctx, FPM_K_COMPARE, st);
     HIP_TRY(launch_compare_grid(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
                                 n_qry, hash_bytes, sketch_size, d_numer, d_denom, st));
@@ -964,10 +1043,14 @@ int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
 {
     if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
         return fail(FPM_EINVAL, "fpm_dist_dev: lengths, distance and p-value buffers required");
+    const DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
+                        d_dist, d_pvalue, d_pass};
+    bool finalized = false;
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                               qry_stride, n_qry, hash_bytes, sketch_size, d_numer, d_denom,
-                              stream))
+                              stream, &fin, &finalized))
         return rc;
+    if (finalized) return FPM_OK;
     return fpm_dist_finalize_dev(ctx, d_numer, d_denom, d_ref_length, d_qry_length, n_ref, n_qry,
                                  kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue,
                                  d_pass, stream);

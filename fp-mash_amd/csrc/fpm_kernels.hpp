@@ -88,18 +88,35 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                               uint32_t n_qry, uint32_t hash_bytes, IdxGeom g, const uint32_t *dir,
                               unsigned long long *events, uint32_t *unsorted, hipStream_t st);
+// The final values of a pair that shares no hash: (0, min(S, la+lb)), distance 1 (0 when
+// both lists are empty, numer == denom), p-value 1 and the -d / -v filters
+// (CommandDistance.cpp:404-419 at numer = 0).  launch_dist_fill writes them to every cell
+// of the grid; the candidate cells are then rewritten by the candidate compare and
+// launch_dist_cand_finalize.
+struct PairFill {
+    double *dist = nullptr, *pval = nullptr;
+    uint8_t *pass = nullptr;
+    double max_dist = -1, max_pvalue = -1;
+};
+hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
+                            uint32_t n_qry, uint32_t S, uint32_t *d_numer, uint32_t *d_denom,
+                            const PairFill &fill, hipStream_t st);
+// `defaults`: also write (0, min(S, la+lb)) to every numer / denom cell of the row (off
+// when launch_dist_fill already did)
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
-                             const uint32_t *d_ref_len, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, uint64_t *cand, unsigned long long *n_cand,
-                             uint64_t *row_seg, hipStream_t st);
+                             const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
+                             uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st);
 // sorted-distinct candidates: one workgroup per query row, one wave per pair
 hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
                              uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, hipStream_t st);
+                             uint32_t *d_denom, uint32_t *d_cnum, uint32_t *d_cden,
+                             hipStream_t st);
+// (d_cnum, d_cden non-null: results go to candidate slot c instead of the grid cells)
 
 // -fp CFL text: newline index, then one lane per line (fingerprint.hip)
 uint32_t text_blocks(uint64_t len);
@@ -120,6 +137,16 @@ hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
                                   uint32_t *d_numer, uint32_t *d_denom, double *d_dist,
                                   double *d_pvalue, uint8_t *d_pass, hipStream_t st);
 
+// distance / p-value / pass of the candidate cells only (after the candidate compare), and
+// of each mirror cell (r, q) when `sym`; the other cells hold the probe's PairFill values
+hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                     uint64_t cap, bool sym, const uint32_t *d_cnum,
+                                     const uint32_t *d_cden, uint32_t *d_numer,
+                                     uint32_t *d_denom, const uint64_t *d_ref_length,
+                                     const uint64_t *d_qry_length, uint32_t n_ref,
+                                     uint32_t kmer_size, double kmer_space, double max_dist,
+                                     double max_pvalue, double *d_dist, double *d_pvalue,
+                                     uint8_t *d_pass, hipStream_t st);
 hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
                                 const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,

@@ -20,11 +20,12 @@ LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfpmash.so")
 BIN_PATH = os.path.join(PKG_ROOT, "bin", "fpmash")
 
 FPM_OK, FPM_EINVAL, FPM_ENODEV, FPM_EHIP, FPM_ENOMEM = 0, -1, -2, -3, -4
-K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE, K_INDEX, K_PROBE, K_FPTEXT = range(8)
+K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE, K_INDEX, K_PROBE, K_FPTEXT, K_FILL = range(9)
 KERNEL_NAMES = {K_SKETCH: "sketch_tiles_kernel", K_MERGE: "merge_kernel",
                 K_FPHASH: "fp_hash_kernel", K_COMPARE: "candidate compare (rank_rows/walk_cand/compare_grid)",
-                K_FINALIZE: "dist_finalize_kernel", K_INDEX: "dist index build",
-                K_PROBE: "probe_rows_kernel", K_FPTEXT: "fp text parse (nl index + fp_line)"}
+                K_FINALIZE: "dist finalize (dense / candidate cells)", K_INDEX: "dist index build",
+                K_PROBE: "probe_rows_kernel", K_FPTEXT: "fp text parse (nl index + fp_line)",
+                K_FILL: "dist_fill_kernel"}
 DIST_AUTO, DIST_DENSE, DIST_SPARSE = 0, 1, 2
 
 ALPHABET_NUCLEOTIDE = "ACGT"                     # Sketch.h alphabetNucleotide

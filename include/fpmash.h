@@ -86,7 +86,8 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 #define FPM_K_INDEX 5
 #define FPM_K_PROBE 6
 #define FPM_K_FPTEXT 7
-#define FPM_K_COUNT 8
+#define FPM_K_FILL 8
+#define FPM_K_COUNT 9
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */

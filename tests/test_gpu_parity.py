@@ -174,12 +174,23 @@ def test_dist_unsorted_u32_fp(ctx, oracle, dist_mode):
 
 def test_dist_filters(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
-    lengths = [len(x) for x in seqs]
+    # 16 lists (a multiple of 4: the fill kernel's vector path) with an empty one (an empty
+    # pair has distance 0)
+    sk = sk + [np.zeros(0, np.uint64)]
+    lengths = [len(x) for x in seqs] + [100]
     got = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths, max_dist=0.05,
                    max_pvalue=1e-30)
     nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, 1000, 21, 4.0 ** 21)
     exp = (di <= 0.05) & (pv <= 1e-30)
     assert np.array_equal(got["pass"], exp)
+    # a pair dropped by -d keeps p-value 0 (the p-value is not computed for it)
+    np.testing.assert_allclose(got["distance"], di, rtol=RTOL, atol=0)
+    np.testing.assert_allclose(got["pvalue"], np.where(di <= 0.05, pv, 0.0), rtol=RTOL, atol=0)
+    # a -d above 1 keeps every pair; the no-shared-hash cells get p-value 1
+    got = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths, max_dist=1.5,
+                   max_pvalue=0.5)
+    assert np.array_equal(got["pass"], pv <= 0.5)
+    np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
 
 
 def test_dist_sparse_large_grid(ctx, oracle):
@@ -263,6 +274,14 @@ def test_dist_self_symmetric_path(ctx, oracle):
                 assert np.array_equal(a[key], b[key]), key
             nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, S, 21, 4.0 ** 21)
             assert np.array_equal(a["numer"], nu) and np.array_equal(a["denom"], de)
+            np.testing.assert_allclose(a["distance"], di, rtol=RTOL, atol=0)
+            np.testing.assert_allclose(a["pvalue"], pv, rtol=RTOL, atol=0)
+            # filters on the symmetric path: mirror cells get the same decision
+            f = ctx.dist(sk, sk, S, ref_lengths=lengths, qry_lengths=lengths, max_dist=0.1,
+                         max_pvalue=1e-10)
+            assert np.array_equal(f["pass"], (di <= 0.1) & (pv <= 1e-10))
+            np.testing.assert_allclose(f["pvalue"], np.where(di <= 0.1, pv, 0.0), rtol=RTOL,
+                                       atol=0)
     finally:
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 

@@ -33,8 +33,10 @@ GROUPS = [
     ("rank_rows_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
     ("walk_cand_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
     ("compare_grid_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
-    ("dist_finalize_kernel", "dist_finalize_kernel"),
+    ("dist_finalize_kernel", "dist finalize (dense / candidate cells)"),
+    ("dist_cand_finalize_kernel", "dist finalize (dense / candidate cells)"),
     ("probe_rows_kernel", "probe_rows_kernel"),
+    ("dist_fill_kernel", "dist_fill_kernel"),
     ("idx_", "dist index build"),
     ("scan_", "dist index build"),
     ("probe_count_kernel", "dist index build"),
