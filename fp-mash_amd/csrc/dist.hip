@@ -450,6 +450,8 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
             pv[u] = ok ? 1.0 : 0.0;
             pa |= (ok && pkeep ? 1u : 0u) << (8 * u);
         }
+        // plain stores: non-temporal ones (nt) let the candidate compare beside run 15%
+        // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms)
         *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
         *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
         *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
