@@ -49,31 +49,54 @@ __device__ __forceinline__ uint32_t key_fp(uint64_t K, const IdxGeom &g)
     return (uint32_t)(K >> (64 - g.nbits - g.fbits)) & ((1u << g.fbits) - 1);
 }
 
-// ---- 1a. level-1 histogram: one tile = kIdxTile matrix cells, LDS counters per partition
-__global__ __launch_bounds__(256) void idx_part_hist_kernel(
+// Tiles of kIdxTile matrix cells, 1024 threads each (16 cells per thread, 4 loads in
+// flight): 611 tiles at the bench's E = 1e7, ~10 waves per SIMD.  Row of cell e = e / stride
+// by a 64-bit multiply-high with magic = floor((2^64 - 1) / stride) + 1, exact for e < 2^31
+// (the error term e / 2^64 stays below the 1 / stride gap to the next integer).
+constexpr int kIdxThreads = 1024;
+constexpr int kIdxU = 4;
+
+__device__ __forceinline__ uint32_t row_of(uint32_t e, uint32_t stride, uint64_t magic)
+{
+    return stride == 1 ? e : (uint32_t)__umul64hi((uint64_t)e, magic);
+}
+
+// ---- 1a. level-1 histogram: LDS counters per partition; also flags unsorted /
+// duplicate-carrying rows (the next cell's key is the next lane's, lane 63 loads it)
+__global__ __launch_bounds__(kIdxThreads) void idx_part_hist_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
-    uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles, uint32_t *__restrict__ tile_hist,
-    uint32_t *__restrict__ unsorted)
+    uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles,
+    uint32_t *__restrict__ tile_hist, uint32_t *__restrict__ unsorted)
 {
     __shared__ uint32_t hist[kParts];
-    for (uint32_t p = threadIdx.x; p < kParts; p += 256) hist[p] = 0;
+    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) hist[p] = 0;
     __syncthreads();
-    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
+    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
     bool uns = false;
-    for (uint32_t c = threadIdx.x; c < kIdxTile; c += 256) {
-        const uint32_t e = e0 + c;
-        if (e >= n) break;
-        const uint32_t r = e / stride, i = e - r * stride;
-        const uint32_t la = ref_len[r];
-        if (i < la) {
-            const uint64_t key = load_key(ref, hash_bytes, e);
-            atomicAdd(&hist[norm_key(key, hash_bytes) >> (64 - kIdxL1)], 1u);
-            uns |= i + 1 < la && !(key < load_key(ref, hash_bytes, (uint64_t)e + 1));
+    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+        uint64_t key[kIdxU];
+        bool v[kIdxU], nx[kIdxU];
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
+            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+            const uint32_t la = e < n ? ref_len[r] : 0;
+            v[u] = e < n && i < la;
+            nx[u] = v[u] && i + 1 < la;                 // cell e + 1 is in the same list
+            key[u] = v[u] ? load_key(ref, hash_bytes, e) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            uint64_t nk = __shfl_down((unsigned long long)key[u], 1, 64);
+            if (lane == 63 && nx[u])
+                nk = load_key(ref, hash_bytes, (uint64_t)e0 + c0 + u * kIdxThreads + threadIdx.x + 1);
+            uns |= nx[u] && !(key[u] < nk);
+            if (v[u]) atomicAdd(&hist[norm_key(key[u], hash_bytes) >> (64 - kIdxL1)], 1u);
         }
     }
-    if (__any(uns) && (threadIdx.x & 63) == 0) atomicOr(unsorted, 1u);
+    if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < kParts; p += 256)
+    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads)
         tile_hist[(uint64_t)p * ntiles + blockIdx.x] = hist[p];
 }
 
@@ -86,25 +109,34 @@ __device__ __forceinline__ uint64_t pack_l1(uint64_t K, uint32_t r, const IdxGeo
     return (mid << g.rbits) | r;
 }
 
-__global__ __launch_bounds__(256) void idx_part_scatter_kernel(
+__global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
-    uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles, const uint32_t *__restrict__ tile_off,
-    IdxGeom g, uint64_t *__restrict__ tent)
+    uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles,
+    const uint32_t *__restrict__ tile_off, IdxGeom g, uint64_t *__restrict__ tent)
 {
     __shared__ uint32_t cur[kParts];
-    for (uint32_t p = threadIdx.x; p < kParts; p += 256)
+    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads)
         cur[p] = tile_off[(uint64_t)p * ntiles + blockIdx.x];
     __syncthreads();
     const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
-    for (uint32_t c = threadIdx.x; c < kIdxTile; c += 256) {
-        const uint32_t e = e0 + c;
-        if (e >= n) break;
-        const uint32_t r = e / stride, i = e - r * stride;
-        if (i < ref_len[r]) {
-            const uint64_t K = norm_key(load_key(ref, hash_bytes, e), hash_bytes);
-            const uint32_t pos = atomicAdd(&cur[K >> (64 - kIdxL1)], 1u);
-            tent[pos] = pack_l1(K, r, g);
+    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+        uint64_t K[kIdxU];
+        uint32_t rr[kIdxU];
+        bool v[kIdxU];
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
+            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+            v[u] = e < n && i < ref_len[min(r, n_ref - 1)];
+            rr[u] = r;
+            K[u] = v[u] ? norm_key(load_key(ref, hash_bytes, e), hash_bytes) : 0;
         }
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++)
+            if (v[u]) {
+                const uint32_t pos = atomicAdd(&cur[K[u] >> (64 - kIdxL1)], 1u);
+                tent[pos] = pack_l1(K[u], rr[u], g);
+            }
     }
 }
 
@@ -451,14 +483,16 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             unsigned long long *self_events, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
-    hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
-                       (uint32_t)stride, n_ref, hash_bytes, ntiles, tile_hist, unsorted);
+    const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
+    hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
+                       unsorted);
     const uint64_t nh = (uint64_t)kParts * ntiles;
     if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
         return e;
-    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(256), 0, st, d_ref, d_ref_len,
-                       (uint32_t)stride, n_ref, hash_bytes, ntiles, (const uint32_t *)tile_off,
-                       g, tent);
+    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
+                       (const uint32_t *)tile_off, g, tent);
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles, (const uint32_t *)tile_off, g, dir, entries, self_events);
     return hipGetLastError();
