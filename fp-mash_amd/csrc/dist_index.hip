@@ -149,6 +149,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
     __shared__ uint32_t wsum[kBucketThreads / 64];
+    __shared__ unsigned long long wsq[kBucketThreads / 64];
     const uint32_t p = blockIdx.x;
     const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
     const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
@@ -190,14 +191,21 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         acc += c;
         sq += (unsigned long long)c * c;
     }
-    // a set probed against itself does sum_b |b|^2 posting events: no separate count pass
+    // a set probed against itself does sum_b |b|^2 posting events: no separate count pass.
+    // One atomic per workgroup into one of 64 spread counters (sqsum[1..64], summed by
+    // sum64_kernel): 8192 per-wave atomics on one address serialised into a ~0.1 ms tail.
     if (sqsum) {
 #pragma unroll
         for (int d = 32; d > 0; d >>= 1) sq += __shfl_down(sq, d, 64);
-        if (lane == 0 && sq) atomicAdd(sqsum, sq);
+        if (lane == 0) wsq[wave] = sq;
     }
     if (p == kParts - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
     __syncthreads();
+    if (sqsum && threadIdx.x == 0) {
+        unsigned long long t = 0;
+        for (int w = 0; w < kBucketThreads / 64; w++) t += wsq[w];
+        if (t) atomicAdd(&sqsum[1 + (p & 63)], t);
+    }
     for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
         uint64_t K[kU];
 #pragma unroll
@@ -494,7 +502,9 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                        d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
                        (const uint32_t *)tile_off, g, tent);
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
-                       (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles, (const uint32_t *)tile_off, g, dir, entries, self_events);
+                       (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles,
+                       (const uint32_t *)tile_off, g, dir, entries, self_events);
+    if (self_events) hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, self_events);
     return hipGetLastError();
 }
 
