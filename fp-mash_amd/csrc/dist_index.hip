@@ -27,7 +27,10 @@
 
 namespace fpm {
 
-constexpr uint32_t kParts = 1u << kIdxL1;    // level-1 partitions (top 10 key bits)
+constexpr uint32_t kParts = 1u << kIdxL1;
+#ifndef PROBE_KU
+#define PROBE_KU 8
+#endif    // level-1 partitions (top 10 key bits)
 
 __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_bytes, uint64_t idx)
 {
@@ -342,9 +345,9 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
-    uint32_t defaults, uint32_t *__restrict__ numer, uint32_t *__restrict__ denom,
-    uint64_t *__restrict__ cand, unsigned long long *__restrict__ n_cand,
-    uint64_t *__restrict__ row_seg)
+    uint32_t defaults, uint32_t self_set, uint32_t *__restrict__ numer,
+    uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
+    unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
@@ -364,6 +367,11 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) rowbits[w] = 0;
     __syncthreads();
     const uint32_t lq = qry_len[q];
+    // one set against itself: row q's own entry sits in the bucket of each of its hashes,
+    // so a bucket of one entry holds only that entry.  Such buckets (the unique hashes, most
+    // of a sketch) are not read; the pair (q, q) they would mark is set here.
+    if (self_set && threadIdx.x == 0 && lq > 0 && q >= r0 && q < r1c)
+        atomicOr(&rowbits[(q - r0) >> 5], 1u << ((q - r0) & 31));
     const uint64_t rowoff = (uint64_t)q * stride;
     // every pair of the row starts as "no shared value": (0, min(S, la+lb))
     if (defaults)
@@ -387,7 +395,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
             const uint64_t b = K >> (64 - g.nbits);
             const uint32_t d0 = j < lq ? dir[b] : 0u, d1 = j < lq ? dir[b + 1] : 0u;
             st_b[bi] = d0;
-            cnt_b[bi] = d1 - d0;
+            cnt_b[bi] = self_set && d1 - d0 == 1 ? 0u : d1 - d0;
             tgt_b[bi] = key_fp(K, g);
         }
 #pragma unroll
@@ -412,8 +420,8 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
             for (uint32_t e = a0; e < a1; e++) w_own[wave][e - wb] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
             const uint32_t wn = min(kWin, total - wb);
-            // 4 events per lane in flight: owner byte -> (base, fingerprint) -> entry
-            constexpr int kU = 4;
+            // kU events per lane in flight: owner byte -> (base, fingerprint) -> entry
+            constexpr int kU = PROBE_KU;
             for (uint32_t e0 = lane; e0 < wn; e0 += 64 * kU) {
                 uint64_t tab[kU];
 #pragma unroll
@@ -432,7 +440,11 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
                     const uint32_t e = e0 + 64 * u;
                     if (e < wn && (en[u] >> g.rbits) == (uint32_t)(tab[u] >> 32)) {
                         const uint32_t r = en[u] & rmask;
-                        if (r >= r0 && r < r1c) atomicOr(&rowbits[(r - r0) >> 5], 1u << ((r - r0) & 31));
+                        // a read first: lanes of a shared bucket hit the same few words
+                        // (family members have adjacent ids), where an atomic per lane
+                        // serialises; the bits are almost always set already
+                        const uint32_t wi = (r - r0) >> 5, bit = 1u << ((r - r0) & 31);
+                        if (r >= r0 && r < r1c && !(rowbits[wi] & bit)) atomicOr(&rowbits[wi], bit);
                     }
                 }
             }
@@ -524,7 +536,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
-                             uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             bool self_set, uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st)
 {
     if (!n_qry || !n_ref) return hipSuccess;
@@ -534,7 +546,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const size_t lds = ((cref + 31) / 32) * 4;
     hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
-                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, d_numer, d_denom, cand, n_cand,
+                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, (uint32_t)self_set, d_numer,
+                       d_denom, cand, n_cand,
                        row_seg);
     return hipGetLastError();
 }

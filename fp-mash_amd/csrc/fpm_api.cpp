@@ -949,8 +949,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
-                                          d_ref_len, sketch_size, sym, fin == nullptr, d_numer,
-                                          d_denom, (uint64_t *)cand, n_cand,
+                                          d_ref_len, sketch_size, sym, fin == nullptr, self_set,
+                                          d_numer, d_denom, (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, st));
                 tl.done();
             }

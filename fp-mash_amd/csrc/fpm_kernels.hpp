@@ -107,8 +107,10 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
-                             uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             bool self_set, uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st);
+// (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are
+// the row's own hash and are not read)
 // sorted-distinct candidates: one workgroup per query row, one wave per pair
 hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,

@@ -100,6 +100,10 @@ def main():
                    "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"),
                   os.path.join(a.work, "sq"), bench_args)
     sqk = {c: per_launch(v, launches) for c, v in sq.items()}
+    # fourth pass: L2 hit / miss requests and LDS bank-conflict cycles
+    l2 = run_pass(("SQ_LDS_BANK_CONFLICT", "TCC_HIT_sum", "TCC_MISS_sum"),
+                  os.path.join(a.work, "l2"), bench_args)
+    l2k = {c: per_launch(v, launches) for c, v in l2.items()}
     f = per_launch(fetch, launches)
     w = per_launch(write, launches)
     res = {}
@@ -114,12 +118,19 @@ def main():
         res[g]["wave_state_frac"] = {"active": sqg.get("active_inst_any", 0) / wc,
                                      "issue_stall": sqg.get("wait_inst_any", 0) / wc,
                                      "waiting": sqg.get("wait_any", 0) / wc}
+        hit = l2k.get("TCC_HIT_sum", {}).get(g, 0.0) / 1024.0
+        miss = l2k.get("TCC_MISS_sum", {}).get(g, 0.0) / 1024.0
+        res[g]["l2"] = {"hit_req": hit, "miss_req": miss,
+                        "hit_frac": hit / (hit + miss) if hit + miss else None,
+                        "lds_bank_conflict_cycles":
+                            l2k.get("SQ_LDS_BANK_CONFLICT", {}).get(g, 0.0) / 1024.0}
     out = {
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
                   f"bench.py --steps {a.steps} --warmup {a.warmup}; bytes per launch = "
                   "2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB x 1024; includes "
                   "Infinity-Cache traffic. A third pass: SQ instruction counts and the "
-                  "wave-state split (active / issue-stall / waiting) per launch",
+                  "wave-state split (active / issue-stall / waiting) per launch; a fourth: "
+                  "L2 (TCC) hit / miss requests and LDS bank-conflict cycles",
         "kernels": res,
     }
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
