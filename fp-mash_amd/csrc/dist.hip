@@ -451,7 +451,8 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
             pa |= (ok && pkeep ? 1u : 0u) << (8 * u);
         }
         // plain stores: non-temporal ones (nt) let the candidate compare beside run 15%
-        // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms)
+        // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms); 16-B write-through
+        // (sc1) buffer stores slowed it 1.9x (0.9 -> 1.67 ms beside the compare)
         *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
         *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
         *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
