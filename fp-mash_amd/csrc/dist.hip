@@ -453,8 +453,10 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         // plain stores: non-temporal ones (nt) let the candidate compare beside run 15%
         // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms); 16-B write-through
         // (sc1) buffer stores slowed it 1.9x (0.9 -> 1.67 ms beside the compare)
-        *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
-        *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
+        if (numer) {
+            *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
+            *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
+        }
         *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
         *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
         *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
@@ -469,8 +471,10 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         const uint64_t o = row + r;
         const uint32_t d = ref_len[r] + lq;            // both <= stride, no overflow
         const bool ok = d == 0 || keep1;
-        numer[o] = 0;
-        denom[o] = d < S ? d : S;
+        if (numer) {
+            numer[o] = 0;
+            denom[o] = d < S ? d : S;
+        }
         fill.dist[o] = d == 0 ? 0.0 : 1.0;
         fill.pval[o] = ok ? 1.0 : 0.0;
         if (fill.pass) fill.pass[o] = ok && pkeep ? 1 : 0;

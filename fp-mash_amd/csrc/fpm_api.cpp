@@ -949,7 +949,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
-                                          d_ref_len, sketch_size, sym, fin == nullptr, self_set,
+                                          d_ref_len, sketch_size, sym, true, self_set,
                                           d_numer, d_denom, (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, st));
                 tl.done();
@@ -966,8 +966,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
                 HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
                 TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, d_numer,
-                                         d_denom, fill, ctx->aux));
+                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, nullptr,
+                                         nullptr, fill, ctx->aux));
                 tl.done();
                 HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
                 fill_pending = true;
