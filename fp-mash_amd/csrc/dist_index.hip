@@ -345,7 +345,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
-    uint32_t defaults, uint32_t self_set, uint32_t *__restrict__ numer,
+    uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, uint32_t *__restrict__ numer,
     uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
 {
@@ -373,14 +373,6 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     if (self_set && threadIdx.x == 0 && lq > 0 && q >= r0 && q < r1c)
         atomicOr(&rowbits[(q - r0) >> 5], 1u << ((q - r0) & 31));
     const uint64_t rowoff = (uint64_t)q * stride;
-    // every pair of the row starts as "no shared value": (0, min(S, la+lb))
-    if (defaults)
-        for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {
-            uint64_t o = (uint64_t)q * n_ref + r;
-            uint64_t d = (uint64_t)ref_len[r] + lq;
-            numer[o] = 0;
-            denom[o] = d < S ? (uint32_t)d : S;
-        }
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t rmask = (uint32_t)((1ULL << g.rbits) - 1);
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
@@ -481,6 +473,28 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
             cand[pos++] = bit0 + t;
         }
     }
+    // every pair of the row starts as "no shared value": (0, min(S, la+lb)) (the candidate
+    // kernels, later launches, rewrite the candidates).  Last in the kernel: stores count in
+    // the same in-order vmcnt as loads, so stores issued first would hold up every load the
+    // event loop waits on.  16-B stores when the row chunk is 4-cell aligned.
+    if (defaults) {
+        if (vec_defaults) {
+            for (uint32_t r = r0 + threadIdx.x * 4; r < r1; r += 1024) {
+                const uint64_t o = pair_row + r;
+                const uint4 rl = *(const uint4 *)(ref_len + r);
+                const uint32_t d0 = rl.x + lq, d1 = rl.y + lq, d2 = rl.z + lq, d3 = rl.w + lq;
+                *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
+                *(uint4 *)(denom + o) = make_uint4(min(d0, S), min(d1, S), min(d2, S), min(d3, S));
+            }
+        } else {
+            for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {
+                const uint64_t o = pair_row + r;
+                const uint64_t d = (uint64_t)ref_len[r] + lq;
+                numer[o] = 0;
+                denom[o] = d < S ? (uint32_t)d : S;
+            }
+        }
+    }
 }
 
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock + 1; }
@@ -544,9 +558,14 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const uint32_t nchunks = (n_ref + chunk - 1) / chunk;
     const uint32_t cref = nchunks == 1 ? n_ref : chunk;
     const size_t lds = ((cref + 31) / 32) * 4;
+    // 16-B default stores: every row and chunk start 4-cell aligned, buffers 16-B aligned
+    const auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
+    const uint32_t vec_defaults = n_ref % 4 == 0 && cref % 4 == 0 && al(d_ref_len) &&
+                                  al(d_numer) && al(d_denom);
     hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
-                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, (uint32_t)self_set, d_numer,
+                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults, (uint32_t)self_set,
+                       d_numer,
                        d_denom, cand, n_cand,
                        row_seg);
     return hipGetLastError();

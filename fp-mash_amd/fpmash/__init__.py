@@ -16,7 +16,8 @@ import os
 import numpy as np
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libfpmash.so")
+# FPMASH_LIB: another build of the same ABI (A/B timing of kernel variants on one box)
+LIB_PATH = os.environ.get("FPMASH_LIB") or os.path.join(PKG_ROOT, "lib", "libfpmash.so")
 BIN_PATH = os.path.join(PKG_ROOT, "bin", "fpmash")
 
 FPM_OK, FPM_EINVAL, FPM_ENODEV, FPM_EHIP, FPM_ENOMEM = 0, -1, -2, -3, -4
