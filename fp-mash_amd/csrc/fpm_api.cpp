@@ -871,16 +871,17 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
                       (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
     if (E == 0) try_sparse = false;
-    // bucket index geometry: ~1 entry per bucket (2^nbits >= E, at most 2^24 buckets);
+    // bucket index geometry: ~2.4 entries per bucket (2^nbits >= E/4, at most 2^24 buckets);
     // entries are u32 (ref id in rbits, key fingerprint in the other >= 8 bits)
     IdxGeom geom{};
     {
         uint32_t rbits = 1, lg = 1;
         while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
         while (lg < 40 && (1ULL << lg) < E) lg++;
-        // 2^nbits >= E/2 buckets (<= ~1.2 entries per bucket): 8K level-2 counters (32 KiB
-        // of LDS) at the bench's E = 1e7
-        geom.l2 = lg > kIdxL1 + 1 ? std::min<uint32_t>(lg - 1 - kIdxL1, 14) : 1;
+        // 2^nbits >= E/4 buckets (~2.4 entries per bucket): 4K level-2 counters (16 KiB of
+        // LDS) and a 16 MB directory at the bench's E = 1e7.  Same-box A/B: E/2 buckets cost
+        // 0.04 ms more in the bucket pass than the extra probe events saved; E/8 a wash.
+        geom.l2 = lg > kIdxL1 + 2 ? std::min<uint32_t>(lg - 2 - kIdxL1, 14) : 1;
         geom.nbits = kIdxL1 + geom.l2;
         geom.rbits = rbits;
         geom.fbits = 32 - rbits;
