@@ -237,8 +237,6 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.synchronize()
-    ctx.set_timing(True)
-    ctx.reset_timing()
     grp.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -247,9 +245,16 @@ def main():
     ctx.synchronize()
     t1 = time.perf_counter()
     grp.barrier()
-    ctx.set_timing(False)
     elapsed = grp.max(t1 - t0)
 
+    # per-kernel times: HIP events around every launch, in separate steps after the timed
+    # region (the event records add markers between launches, so they stay out of it)
+    ctx.set_timing(True)
+    ctx.reset_timing()
+    for _ in range(max(3, min(args.steps, 10))):
+        step()
+    ctx.synchronize()
+    ctx.set_timing(False)
     dstats = ctx.last_dist_stats()
     ktimes = {}
     for kid, name in fpmash.KERNEL_NAMES.items():
