@@ -55,13 +55,17 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target CPU seconds per baseline leg")
+    ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
+    ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
+    ap.add_argument("--c4-n", type=int, default=50_000)
     return ap.parse_args()
 
 
 def parse_args_for_test(**kw):
     """Defaults of parse() with overrides (tests)."""
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
-                           k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0)
+                           k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
+                           no_c3=True, no_c4=True, c4_n=50_000)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -125,27 +129,33 @@ def cpu_baseline(args, seqs):
     threads = max(1, min(threads, 64))
     P = O.params(k=args.k, s=args.s)
     n = len(seqs)
-    # sketch leg: calibrate on a small slice, then time a slice sized to the budget
+    # sketch leg: calibrate on a small slice, then time whole passes over the batch until
+    # the leg has run about cpu_seconds / 2
     n_cal = min(n, 20 * threads)
     t0 = time.perf_counter()
     O.sketch_batch(P, seqs[:n_cal], threads=threads)
     rate0 = n_cal / max(time.perf_counter() - t0, 1e-6)
-    n_s = int(min(n, max(n_cal, rate0 * args.cpu_seconds)))
+    n_s = int(min(n, max(n_cal, rate0 * args.cpu_seconds / 2)))
+    passes = max(1, int(round(rate0 * args.cpu_seconds / 2 / n_s)))
     t0 = time.perf_counter()
-    sk = O.sketch_batch(P, seqs[:n_s], threads=threads)
+    for _ in range(passes):
+        sk = O.sketch_batch(P, seqs[:n_s], threads=threads)
     t_s = time.perf_counter() - t0
-    sketch_rate = n_s * args.seq_len / t_s
-    # dist leg: a ref-block x query-block of the all-vs-all grid (families included)
+    sketch_rate = passes * n_s * args.seq_len / t_s
+    if n_s < n:
+        sk = O.sketch_batch(P, seqs, threads=threads)
+    # dist leg: a ref-block x all-queries block of the all-vs-all grid (families included),
+    # sized to about cpu_seconds
     lengths = [args.seq_len] * len(sk)
-    n_r = min(len(sk), 1000)
+    n_q = len(sk)
     n_cal = max(1, min(len(sk), 2 * threads))
     t0 = time.perf_counter()
-    O.dist_grid(sk[:n_r], lengths[:n_r], sk[:n_cal], lengths[:n_cal], args.s, args.k,
+    O.dist_grid(sk[:n_cal], lengths[:n_cal], sk, lengths, args.s, args.k,
                 4.0 ** args.k, threads=threads)
-    rate0 = n_r * n_cal / max(time.perf_counter() - t0, 1e-6)
-    n_q = int(min(len(sk), max(n_cal, rate0 * args.cpu_seconds / n_r)))
+    rate0 = n_cal * n_q / max(time.perf_counter() - t0, 1e-6)
+    n_r = int(min(len(sk), max(n_cal, rate0 * args.cpu_seconds / n_q)))
     t0 = time.perf_counter()
-    O.dist_grid(sk[:n_r], lengths[:n_r], sk[:n_q], lengths[:n_q], args.s, args.k,
+    O.dist_grid(sk[:n_r], lengths[:n_r], sk, lengths, args.s, args.k,
                 4.0 ** args.k, threads=threads)
     t_d = time.perf_counter() - t0
     dist_rate = n_r * n_q / t_d
@@ -156,7 +166,7 @@ def cpu_baseline(args, seqs):
         "cores": threads,
         "kind": "port",
         "sample": (f"oracle CPU port on {threads} threads: sketch of {n_s} x {args.seq_len} bp "
-                   f"in {t_s:.1f} s ({sketch_rate / 1e6:.2f} Mbases/s) + dist of a {n_r} x {n_q} "
+                   f"x {passes} pass(es) in {t_s:.1f} s ({sketch_rate / 1e6:.2f} Mbases/s) + dist of a {n_r} x {n_q} "
                    f"pair block in {t_d:.1f} s ({dist_rate / 1e6:.3f} Mpairs/s, with p-values), "
                    f"extrapolated to {n} seqs + {n * n:.3g} pairs"),
         "sketch_bases_per_s": sketch_rate,
@@ -200,6 +210,151 @@ def fp_text_leg(ctx, reps=3):
             "lines_per_s_device": n / dev, "text_GBps_device": len(text) / dev / 1e9,
             "lines_per_s_wall_pcie": n / wall, "wall_ms": wall * 1e3,
             "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap)"}
+
+
+def _group_fp_lines(r, text):
+    """initFromFingerprints' grouping (Sketch.cpp:104-134) of one parsed file: a new
+    reference wherever the line's ID differs from the previous one; length = the first
+    line's value count counted twice + the rest (:117, :134)."""
+    n = len(r["hash"])
+    new = r["new_id"].astype(bool)
+    if n:
+        new[0] = True
+    starts = np.flatnonzero(new)
+    ends = np.append(starts[1:], n)
+    nv = r["n_vals"].astype(np.uint64)
+    csum = np.concatenate([[0], np.cumsum(nv)])
+    lengths = nv[starts] + (csum[ends] - csum[starts])
+    return starts, ends, lengths
+
+
+def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
+    """C3: the -fp path on 5,000 lyn2vec-shaped 2 kb sequences, 1 GPU.
+    `sketch -fp` reads at most 1,000,000 lines per call (Sketch.cpp:37, :82), i.e. 500
+    sequences of 2,000 CFL k-finger lines, so the 5,000 sequences are 10 files of 500, each
+    parsed + hashed on the device (fpm_fp_text_*), grouped into references on the host
+    (ID changes), then `dist -fp` of all 5,000 against all 5,000: unsorted u32 lists, the
+    reference's literal walk capped at s = 1000 (k = 1, k-mer space 10), on the device.
+    Reported beside the metric, not part of `value`."""
+    seqs = datagen.random_dna(n_seqs, 2000, seed=33)
+    ids = datagen.lyn2vec_ids(n_seqs, seed=33)
+    files = [datagen.cfl_text_fast(seqs[i:i + per_file], ids[i:i + per_file])
+             for i in range(0, n_seqs, per_file)]
+    rows, lens, lengths = [], [], []
+    ctx.fp_text(files[0][:100000])                                   # warm
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    t0 = time.perf_counter()
+    n_lines = 0
+    for f in files:
+        r = ctx.fp_text(f, max_lines=1_000_000)
+        n_lines += len(r["hash"])
+        st, en, ln = _group_fp_lines(r, f)
+        h = r["hash"]
+        for a, b in zip(st, en):
+            rows.append(h[a:b])
+        lens.append(en - st)
+        lengths.append(ln)
+    t_parse_wall = time.perf_counter() - t0
+    ctx.set_timing(False)
+    parse_ms, _ = ctx.kernel_time(fpmash.K_FPTEXT)
+    ctx.reset_timing()
+    n = len(rows)
+    w = int(max(len(x) for x in rows))
+    R = np.zeros((n, w), np.uint32)
+    for i, x in enumerate(rows):
+        R[i, :len(x)] = x
+    rl = np.concatenate(lens).astype(np.uint32)
+    rL = np.concatenate(lengths).astype(np.uint64)
+    L = fpmash.lib()
+    d_R = fpmash.DeviceBuffer.from_array(ctx, R)
+    d_rl = fpmash.DeviceBuffer.from_array(ctx, rl)
+    d_rL = fpmash.DeviceBuffer.from_array(ctx, rL)
+    np_ = n * n
+    outs = [fpmash.DeviceBuffer(ctx, np_ * b) for b in (4, 4, 8, 8, 1)]
+
+    def run():
+        fpmash._check(L.fpm_dist_dev(ctx.h, d_R.ptr, d_rl.ptr, d_rL.ptr, w, n, d_R.ptr, d_rl.ptr,
+                                     d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
+                                     *[o.ptr for o in outs], ctx.stream))
+    run()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        run()
+    ctx.synchronize()
+    dist_ms = (time.perf_counter() - t0) / reps * 1e3
+    st = ctx.last_dist_stats()
+    numer = outs[0].to_array(np.uint32, np_)
+    for b in [d_R, d_rl, d_rL] + outs:
+        b.free()
+    return {"config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
+                      f"({n_lines} lines, {sum(map(len, files)) / 1e6:.0f} MB), sketch -fp per file "
+                      f"+ dist -fp {n} x {n} (s={s}, unsorted u32 walk)",
+            "references": n, "lines": n_lines,
+            "parse_device_ms": parse_ms, "parse_wall_ms_pcie": t_parse_wall * 1e3,
+            "lines_per_s_device": n_lines / (parse_ms * 1e-3),
+            "dist_ms": dist_ms, "dist_mpairs_per_s": np_ / (dist_ms * 1e-3) / 1e6,
+            "step_device_ms": parse_ms + dist_ms,
+            "dist_path": ["dense walk", "bucket index + literal walk",
+                          "bucket index + bucketed rank"][int(st["sparse"])],
+            "posting_events": st["events"], "candidate_pairs": st["candidates"],
+            "pairs_sharing_a_hash": int((numer > 0).sum())}
+
+
+def c4_leg(ctx, grp, ws, rank, n=50_000, members=100, s=1000, k=21, steps=3, warmup=1):
+    """C4: one all-vs-all dist of n family-structured sketches, the query
+    rows sharded over the ranks (strong scaling).  Every GPU holds the whole reference set
+    (400 MB at n = 50k: far below one GPU's HBM, so no min-merge / ring exchange is needed,
+    as the north star prescribes); each rank sketches it (standing in for loading
+    all.msh) outside the timed region, and the timed step is its block of query rows
+    against all n references: shared-hash counts, distance, FP64 p-value, pass flags,
+    left in HBM.  The index over the references is rebuilt inside every step.  With one
+    rank the queries are the references (the library's symmetric self path)."""
+    from fpmash.shard import shard_range
+    fams = n // members
+    n = fams * members
+    seqs = datagen.family_dna(fams, members, 2000, sub_rate=(0.01, 0.10), seed=4000)
+    P = fpmash.make_params(k=k, s=s)
+    job = ctx.sketch_job(P, seqs)
+    job.run()
+    d_rows, d_cnt, _ng, stride = job.device_output()
+    del seqs
+    lo, hi = shard_range(n, ws, rank)
+    n_loc = hi - lo
+    L = fpmash.lib()
+    d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, 2000, np.uint64))
+    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (4, 4, 8, 8, 1)]
+    st = ctx.stream
+
+    def run():
+        fpmash._check(L.fpm_dist_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n,
+                                     d_rows + lo * stride * 8, d_cnt + lo * 4, d_len.ptr + lo * 8,
+                                     stride, n_loc, 8, s, k, 4.0 ** k, 1.0, 1.0,
+                                     *[o.ptr for o in outs], st))
+    for _ in range(warmup):
+        run()
+    ctx.synchronize()
+    grp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        run()
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    grp.barrier()
+    el = grp.max(el)
+    dst = ctx.last_dist_stats()
+    cand = grp.sum(dst["candidates"])
+    for b in [d_len] + outs:
+        b.free()
+    job.free()
+    return {"config": f"C4: all-vs-all dist of {n} family-structured 2 kb sketches (k={k}, s={s}), "
+                      f"query rows sharded over {ws} GPU(s), every GPU holding all references",
+            "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
+            "path_rank0": ["dense walk", "bucket index + literal walk",
+                           "bucket index + bucketed rank"][int(dst["sparse"])],
+            "candidates_all_ranks": cand}
 
 
 def main():
@@ -340,6 +495,13 @@ def main():
     di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in di_names) / args.steps
 
     fp_leg = fp_text_leg(ctx) if rank == 0 else None
+    c3 = c3_leg(ctx, s=args.s) if rank == 0 and not args.no_c3 else None
+    c4 = None
+    if not args.no_c4:
+        job.free()                       # the C2 batch's buffers make room for C4's grid
+        for b in (d_numer, d_denom, d_dist, d_pval, d_pass):
+            b.free()
+        c4 = c4_leg(ctx, grp, ws, rank, n=args.c4_n, s=args.s, k=args.k)
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
@@ -376,6 +538,8 @@ def main():
                               "bucket index + bucketed rank"][int(dstats["sparse"])],
                      "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
             "fp_text": fp_leg,
+            "c3_fp": c3,
+            "c4_dist": c4,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,

@@ -95,3 +95,14 @@ def cfl_lines(seq: bytes, gid: str, window=100):
 
 def cfl_text(seqs, ids, window=100):
     return "".join(l for s, i in zip(seqs, ids) for l in cfl_lines(s, "G00000" + i, window)).encode()
+
+
+def cfl_text_fast(seqs, ids, window=100, threads=None):
+    """cfl_text through the C++ generator (bin/cflgen, same bytes): C3-scale inputs
+    (5,000 x 2 kb -> 10 M lines) in seconds instead of minutes."""
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bin", "cflgen")
+    inp = b"".join(i.encode() + b"\t" + s + b"\n" for s, i in zip(seqs, ids))
+    args = [exe, str(window)] + ([str(threads)] if threads else [])
+    return subprocess.run(args, input=inp, stdout=subprocess.PIPE, check=True).stdout

@@ -1,0 +1,56 @@
+"""CPU tests of the bench's host-side helpers: the C++ CFL generator (C3 inputs), the -fp
+line grouping of the C3 leg, and the C4 leg's query-row sharding."""
+import os
+
+import numpy as np
+
+from conftest import GOLDEN
+import seqio
+
+
+def test_cflgen_matches_lyn2vec_fixture():
+    """bin/cflgen reproduces lyn2vec's DNA1-CFL.txt from DNA1.fasta byte for byte."""
+    from fpmash import datagen
+    recs = seqio.read_records(os.path.join(GOLDEN, "DNA1.fasta"))
+    ids = [comment.split()[0].decode()[len("G00000"):] for _name, comment, _seq in recs]
+    out = datagen.cfl_text_fast([seq for _n, _c, seq in recs], ids, threads=3)
+    assert out == open(os.path.join(GOLDEN, "DNA1-CFL.txt"), "rb").read()
+
+
+def test_cflgen_matches_python_generator():
+    """Short records (one window), lowercase, non-ACGT bytes, long records."""
+    from fpmash import datagen
+    seqs = datagen.random_dna(7, 350, seed=9) + [b"acgtNNacg", b"ACGTACGTAC" * 30, b"A", b"tttt" * 40]
+    ids = datagen.lyn2vec_ids(len(seqs), seed=2)
+    assert datagen.cfl_text_fast(seqs, ids) == datagen.cfl_text(seqs, ids)
+    assert datagen.cfl_text_fast(seqs, ids, window=17) == datagen.cfl_text(seqs, ids, window=17)
+
+
+def test_c3_grouping_matches_fixture_lengths(oracle):
+    """bench._group_fp_lines == initFromFingerprints' grouping (Sketch.cpp:104-134): the
+    references, their hash lists and the double-counted first-line length of
+    DNA{1,2,3}-sketch.msh."""
+    import bench
+    for i in (1, 2, 3):
+        text = open(os.path.join(GOLDEN, f"DNA{i}-CFL.txt"), "rb").read()
+        refs, _used, _ = oracle.fp_references(text)
+        ids, vals, _ = oracle.fp_parse(text)
+        r = {"hash": np.array([oracle.get_hash_fp(v, 42, False) for v in vals], np.uint32),
+             "new_id": np.array([1] + [int(a != b) for a, b in zip(ids[1:], ids[:-1])], np.uint8),
+             "n_vals": np.array([len(v) for v in vals], np.uint32)}
+        st, en, ln = bench._group_fp_lines(r, text)
+        assert len(st) == len(refs)
+        for a, b, length, (name, e_len, e_hash) in zip(st, en, ln, refs):
+            assert ids[a] == name and int(length) == e_len
+            assert np.array_equal(r["hash"][a:b], e_hash)
+
+
+def test_c4_row_shards_cover_grid():
+    """The C4 leg's query-row blocks partition [0, n) for every GPU count."""
+    from fpmash.shard import shard_range
+    for n in (1, 7, 50_000):
+        for ws in (1, 2, 3, 4, 8):
+            spans = [shard_range(n, ws, r) for r in range(ws)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
