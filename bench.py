@@ -296,8 +296,7 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
             "lines_per_s_device": n_lines / (parse_ms * 1e-3),
             "dist_ms": dist_ms, "dist_mpairs_per_s": np_ / (dist_ms * 1e-3) / 1e6,
             "step_device_ms": parse_ms + dist_ms,
-            "dist_path": ["dense walk", "bucket index + literal walk",
-                          "bucket index + bucketed rank"][int(st["sparse"])],
+            "dist_path": fpmash.DIST_PATHS[int(st["sparse"])],
             "posting_events": st["events"], "candidate_pairs": st["candidates"],
             "pairs_sharing_a_hash": int((numer > 0).sum())}
 
@@ -352,8 +351,7 @@ def c4_leg(ctx, grp, ws, rank, n=50_000, members=100, s=1000, k=21, steps=3, war
                       f"query rows sharded over {ws} GPU(s), every GPU holding all references",
             "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
-            "path_rank0": ["dense walk", "bucket index + literal walk",
-                           "bucket index + bucketed rank"][int(dst["sparse"])],
+            "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
             "candidates_all_ranks": cand}
 
 
@@ -534,8 +532,7 @@ def main():
             "dist": {"mpairs_per_s": total_pairs / args.steps / (di_ms * 1e-3) / 1e6 if di_ms else None,
                      "device_ms_per_step": di_ms,
                      "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
-                     "path": ["dense walk", "bucket index + literal walk",
-                              "bucket index + bucketed rank"][int(dstats["sparse"])],
+                     "path": fpmash.DIST_PATHS[int(dstats["sparse"])],
                      "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
             "fp_text": fp_leg,
             "c3_fp": c3,

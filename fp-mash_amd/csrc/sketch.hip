@@ -17,6 +17,19 @@ namespace fpm {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 
+// Phase timestamps of the tile kernel for tools/micro/sketch_phases.hip (which defines
+// FPM_SKETCH_PHASES and points g_phase at 8 u64 per workgroup); compiled out of the library.
+#ifdef FPM_SKETCH_PHASES
+__device__ uint64_t *g_phase;
+#define FPM_PHASE_DECL uint64_t ph_[8] = {0, 0, 0, 0, 0, 0, 0, 0}
+#define FPM_PHASE(i) do { if (threadIdx.x == 0) ph_[i] = __builtin_amdgcn_s_memtime(); } while (0)
+#define FPM_PHASE_FLUSH do { if (threadIdx.x == 0) for (int q_ = 0; q_ < 8; q_++) g_phase[blockIdx.x * 8 + q_] = ph_[q_]; } while (0)
+#else
+#define FPM_PHASE_DECL do {} while (0)
+#define FPM_PHASE(i) do {} while (0)
+#define FPM_PHASE_FLUSH do {} while (0)
+#endif
+
 // Block-wide exclusive scan of one u32 per thread; returns the exclusive prefix
 // and writes the block total to *total.  `tmp` holds kWaves+1 dwords of LDS.
 __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *tmp, uint32_t *total)
@@ -61,7 +74,9 @@ __device__ void bitonic_sort(uint64_t *keys)
     }
 }
 
-template <int P>
+// K != 0: the k-mer size as a compile-time constant (the window loads, tail masks and
+// Murmur's block / tail branches fold); K = 0 reads p.k.
+template <int P, int K>
 __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
@@ -78,9 +93,11 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     __shared__ uint32_t bins[P / 2 + 1];
     __shared__ uint32_t big_bucket;
 
+    FPM_PHASE_DECL;
+    FPM_PHASE(0);
     const TileDesc td = tiles[blockIdx.x];
     const uint32_t n = td.n_bytes;
-    const uint32_t k = p.k;
+    const uint32_t k = K ? (uint32_t)K : p.k;
     const int tid = threadIdx.x;
 
     alpha[tid] = p.alphabet[tid];
@@ -91,10 +108,22 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     uint8_t *fb = reinterpret_cast<uint8_t *>(fwd_img);
     uint8_t *rb = reinterpret_cast<uint8_t *>(rc_img);
     constexpr int kImgBytes = kImgWords * 4;
-    for (int b = tid; b < kImgBytes; b += kBlock) {
+    constexpr int kIt = (kImgBytes + kBlock - 1) / kBlock;
+    // every global byte load of the tile issued before the first use (one memory latency
+    // per tile instead of one per pass)
+    uint8_t cb[kIt];
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+        const int b = tid + it * kBlock;
+        cb[it] = (uint32_t)b < n ? seq[td.byte_off + b] : (uint8_t)0;
+    }
+#pragma unroll
+    for (int it = 0; it < kIt; it++) {
+        const int b = tid + it * kBlock;
+        if (b >= kImgBytes) break;
         uint8_t c = 0;
         if ((uint32_t)b < n) {
-            c = seq[td.byte_off + b];
+            c = cb[it];
             if (!p.preserve_case && c > 96 && c < 123) c -= 32;
         }
         fb[b] = c;
@@ -108,6 +137,7 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
         else rb[b] = 0;
     }
     __syncthreads();
+    FPM_PHASE(1);
 
     // ---- hash every window (one k-mer start per thread per pass)
     const uint32_t nk = n >= k ? n - k + 1 : 0;
@@ -163,6 +193,7 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
 
     // ---- long groups: keep only hashes <= the group's bound (the s-th smallest hash of a
     // sample of the group's tiles, an upper bound of the group's own s-th smallest)
+    FPM_PHASE(2);
     uint64_t hmax = p.use64 ? ~0ULL : 0xffffffffULL;
     if (td.thr_slot) {
         hmax = min(hmax, thr[td.thr_slot - 1]);
@@ -187,6 +218,7 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     for (int e = 0; e < E; e++)
         if (vbits >> e & 1) atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
     __syncthreads();
+    FPM_PHASE(3);
     // exclusive scan of the bucket counts: thread t owns buckets [t*per, t*per + per)
     constexpr int per = NB >= kBlock ? NB / kBlock : 1;
     uint32_t run = 0, bmax = 0;
@@ -206,21 +238,48 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     }
     if (bmax > kMaxBucket) big_bucket = 1;
     __syncthreads();
-    // scatter: afterwards bins[b] = end of bucket b, start = bins[b - 1]
+    FPM_PHASE(4);
+    // scatter: afterwards bins[b] = end of bucket b, start = bins[b - 1]; each key keeps
+    // its slot for the in-bucket rank below
+    uint32_t slot[E];
 #pragma unroll
     for (int e = 0; e < E; e++)
-        if (vbits >> e & 1) keys[atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u)] = kr[e];
-    __syncthreads();
-    if (!big_bucket) {
-        for (int b = tid; b < NB; b += kBlock) {
-            const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
-            for (uint32_t i = s0 + 1; i < s1; i++) {
-                const uint64_t x = keys[i];
-                uint32_t j = i;
-                while (j > s0 && keys[j - 1] > x) { keys[j] = keys[j - 1]; j--; }
-                keys[j] = x;
-            }
+        if (vbits >> e & 1) {
+            slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
+            keys[slot[e]] = kr[e];
         }
+    __syncthreads();
+    FPM_PHASE(5);
+    if (!big_bucket) {
+        // in-bucket rank of every key (ties by slot): the bucket's ~2 keys are read with
+        // independent LDS loads, then every key is written to its sorted position (an
+        // insertion sort per bucket was a chain of dependent LDS round trips: 26 % of the
+        // tile's time, tools/micro/sketch_phases.hip)
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if (vbits >> e & 1) {
+                const uint32_t b = (uint32_t)(kr[e] >> bshift);
+                const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
+                const uint32_t mb = s1 - s0;
+                uint32_t r = 0;
+                // 8 speculative reads cover a bucket of <= 8 keys (Poisson(2) buckets: a
+                // longer one is rare) with one LDS round trip
+#pragma unroll
+                for (uint32_t u = 0; u < 8; u++) {
+                    const uint32_t t = s0 + u;
+                    const uint64_t y = keys[t < (uint32_t)P ? t : (uint32_t)P - 1];
+                    r += (u < mb) & ((y < kr[e]) | ((y == kr[e]) & (t < slot[e])));
+                }
+                for (uint32_t t = s0 + 8; t < s1; t++) {
+                    const uint64_t y = keys[t];
+                    r += (y < kr[e]) | ((y == kr[e]) & (t < slot[e]));
+                }
+                slot[e] = s0 + r;
+            }
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; e++)
+            if (vbits >> e & 1) keys[slot[e]] = kr[e];
         __syncthreads();
     } else {
         for (int i = tid; i < P; i += kBlock)
@@ -228,6 +287,7 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
         __syncthreads();
         bitonic_sort<P>(keys);
     }
+    FPM_PHASE(6);
 
     // ---- first s distinct (ties removed: the heap is a set, MinHashHeap.cpp:74)
     const int base = tid * E;
@@ -249,6 +309,8 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
         }
     }
     if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;
+    FPM_PHASE(7);
+    FPM_PHASE_FLUSH;
 }
 
 // Merge of two ascending distinct lists, keeping the first s distinct of the union.
@@ -322,8 +384,12 @@ static hipError_t launch_p(const uint8_t *d_seq, const TileDesc *d_tiles, uint32
                            uint32_t *d_count, hipStream_t st)
 {
     if (n_tiles == 0) return hipSuccess;
-    hipLaunchKernelGGL(sketch_tiles_kernel<P>, dim3(n_tiles), dim3(kBlock), 0, st, d_seq, d_tiles,
-                       p, d_thr, d_out, d_count);
+    if (p.k == 21)      // Mash's default k (sketchParameterSetup, C2/C4/C5)
+        hipLaunchKernelGGL((sketch_tiles_kernel<P, 21>), dim3(n_tiles), dim3(kBlock), 0, st,
+                           d_seq, d_tiles, p, d_thr, d_out, d_count);
+    else
+        hipLaunchKernelGGL((sketch_tiles_kernel<P, 0>), dim3(n_tiles), dim3(kBlock), 0, st,
+                           d_seq, d_tiles, p, d_thr, d_out, d_count);
     return hipGetLastError();
 }
 
@@ -363,9 +429,115 @@ hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, con
     return hipGetLastError();
 }
 
+// The same merge with the searched list staged in LDS (every list holds <= s hashes): B for
+// the A side's lower bounds, then A for the B side's upper bounds.  1024 threads, so a list
+// of s = 10,000 (C5) is 10 chunks per side, each a 14-step binary search in LDS instead of
+// 40 chunks of 14 dependent global loads (C5's final rounds are one merge per genome: ~125
+// workgroups, so per-workgroup latency is the whole round).
+constexpr int kMBlock = 1024;
+constexpr int kMWaves = kMBlock / 64;
+
+__device__ __forceinline__ uint32_t block_exscan_m(uint32_t v, uint32_t *tmp, uint32_t *total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) tmp[wave] = x;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        const uint32_t w = threadIdx.x < kMWaves ? tmp[threadIdx.x] : 0u;
+        uint32_t sc = w;
+#pragma unroll
+        for (int d = 1; d < kMWaves; d <<= 1) {
+            uint32_t y = __shfl_up(sc, d, 64);
+            if ((int)threadIdx.x >= d) sc += y;
+        }
+        if (threadIdx.x < kMWaves) tmp[threadIdx.x] = sc - w;
+        if (threadIdx.x == kMWaves - 1) tmp[kMWaves] = sc;
+    }
+    __syncthreads();
+    const uint32_t ex = tmp[wave] + x - v;
+    *total = tmp[kMWaves];
+    __syncthreads();
+    return ex;
+}
+
+__global__ __launch_bounds__(kMBlock) void merge_lds_kernel(const MergeDesc *__restrict__ descs,
+                                                           uint32_t s)
+{
+    extern __shared__ uint64_t sl[];                 // the list being searched (<= s hashes)
+    __shared__ uint32_t scan_tmp[kMWaves + 1];
+    const MergeDesc md = descs[blockIdx.x];
+    const uint32_t la = *md.alen, lb = md.b ? *md.blen : 0;
+    for (uint32_t j = threadIdx.x; j < lb; j += kMBlock) sl[j] = md.b[j];
+    __syncthreads();
+    // A side: A[i] lands at i + lower_bound(B, A[i]) - #(A elements before i found in B)
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < la; c0 += kMBlock) {
+        const uint32_t i = c0 + threadIdx.x;
+        uint64_t a = 0;
+        uint32_t pos = 0, dup = 0;
+        if (i < la) {
+            a = md.a[i];
+            pos = lower_bound_u64(sl, lb, a);
+            dup = (pos < lb && sl[pos] == a) ? 1u : 0u;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_exscan_m(dup, scan_tmp, &tot);
+        if (i < la) {
+            const uint32_t f = i + pos - (carry + ex);
+            if (f < s) md.c[f] = a;
+        }
+        carry += tot;
+    }
+    const uint32_t dups_total = carry;
+    if (lb) {
+        // B side: A in LDS; B[j] equal to an A element is dropped, the others land at
+        // j + upper_bound(A, B[j]) - #(B elements before j found in A)
+        for (uint32_t i = threadIdx.x; i < la; i += kMBlock) sl[i] = md.a[i];
+        __syncthreads();
+        carry = 0;
+        for (uint32_t c0 = 0; c0 < lb; c0 += kMBlock) {
+            const uint32_t j = c0 + threadIdx.x;
+            uint64_t b = 0;
+            uint32_t pos = 0, dup = 0;
+            if (j < lb) {
+                b = md.b[j];
+                pos = upper_bound_u64(sl, la, b);
+                dup = (pos > 0 && sl[pos - 1] == b) ? 1u : 0u;
+            }
+            uint32_t tot;
+            const uint32_t ex = block_exscan_m(dup, scan_tmp, &tot);
+            if (j < lb && !dup) {
+                const uint32_t f = j + pos - (carry + ex);
+                if (f < s) md.c[f] = b;
+            }
+            carry += tot;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t u = la + lb - dups_total;
+        *md.clen = u < s ? u : s;
+    }
+}
+
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st)
 {
     if (n == 0) return hipSuccess;
+    // up to 128 KiB of staged list (s <= 16,384); beyond, the global-memory searches
+    constexpr size_t kMaxLds = 128 * 1024;
+    const size_t lds = (size_t)s * sizeof(uint64_t);
+    if (lds <= kMaxLds &&
+        hipFuncSetAttribute((const void *)merge_lds_kernel,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds) == hipSuccess) {
+        hipLaunchKernelGGL(merge_lds_kernel, dim3(n), dim3(kMBlock), lds, st, d_desc, s);
+        return hipGetLastError();
+    }
+    (void)hipGetLastError();
     hipLaunchKernelGGL(merge_kernel, dim3(n), dim3(kBlock), 0, st, d_desc, s);
     return hipGetLastError();
 }

@@ -28,6 +28,8 @@ KERNEL_NAMES = {K_SKETCH: "sketch_tiles_kernel", K_MERGE: "merge_kernel",
                 K_PROBE: "probe_rows_kernel", K_FPTEXT: "fp text parse (nl index + fp_line)",
                 K_FILL: "dist_fill_kernel"}
 DIST_AUTO, DIST_DENSE, DIST_SPARSE = 0, 1, 2
+# fpm_ctx_last_dist_stats path codes
+DIST_PATHS = ["dense walk", "bucket index + literal walk", "bucket index + bucketed rank"]
 
 ALPHABET_NUCLEOTIDE = "ACGT"                     # Sketch.h alphabetNucleotide
 ALPHABET_PROTEIN = "ACDEFGHIKLMNPQRSTVWY"         # Sketch.h alphabetProtein

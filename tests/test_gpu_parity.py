@@ -328,7 +328,8 @@ def test_fp_text_parse_matches_oracle(ctx, oracle, use64):
                 prev = idv
 
 
-@pytest.mark.parametrize("k,s", [(21, 1000), (21, 5000), (12, 2000), (21, 50000)])
+@pytest.mark.parametrize("k,s", [(21, 1000), (21, 5000), (12, 2000), (21, 10000), (21, 16384),
+                                 (21, 16385), (21, 50000)])
 def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
     """Groups of >= 32 tiles take the sample pass (every 16th tile sketched first; its s-th
     smallest hash bounds every tile): the sets still equal the reference heap's."""

@@ -146,8 +146,7 @@ def main():
             "mpairs_per_s": n * n / (el / a.steps) / 1e6,
             "bases_per_s": n * a.seq_len / (el / a.steps),
             "phase_ms_rank0": {k_: v / a.steps * 1e3 for k_, v in times.items()},
-            "dist_path": ["dense walk", "bucket index + literal walk",
-                          "bucket index + bucketed rank"][int(st["sparse"])],
+            "dist_path": fpmash.DIST_PATHS[int(st["sparse"])],
             "posting_events_rank0": st["events"], "candidates_rank0": st["candidates"],
             "check_rank0": check}))
     job.free()
