@@ -271,10 +271,10 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
     d_rl = fpmash.DeviceBuffer.from_array(ctx, rl)
     d_rL = fpmash.DeviceBuffer.from_array(ctx, rL)
     np_ = n * n
-    outs = [fpmash.DeviceBuffer(ctx, np_ * b) for b in (4, 4, 8, 8, 1)]
+    outs = [fpmash.DeviceBuffer(ctx, np_ * b) for b in (2, 2, 8, 8, 1)]
 
     def run():
-        fpmash._check(L.fpm_dist_dev(ctx.h, d_R.ptr, d_rl.ptr, d_rL.ptr, w, n, d_R.ptr, d_rl.ptr,
+        fpmash._check(L.fpm_dist_dev16(ctx.h, d_R.ptr, d_rl.ptr, d_rL.ptr, w, n, d_R.ptr, d_rl.ptr,
                                      d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
                                      *[o.ptr for o in outs], ctx.stream))
     run()
@@ -285,7 +285,7 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
     ctx.synchronize()
     dist_ms = (time.perf_counter() - t0) / reps * 1e3
     st = ctx.last_dist_stats()
-    numer = outs[0].to_array(np.uint32, np_)
+    numer = outs[0].to_array(np.uint16, np_)
     for b in [d_R, d_rl, d_rL] + outs:
         b.free()
     return {"config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
@@ -323,11 +323,11 @@ def c4_leg(ctx, grp, ws, rank, n=50_000, members=100, s=1000, k=21, steps=3, war
     n_loc = hi - lo
     L = fpmash.lib()
     d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, 2000, np.uint64))
-    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (4, 4, 8, 8, 1)]
+    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]
     st = ctx.stream
 
     def run():
-        fpmash._check(L.fpm_dist_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n,
+        fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n,
                                      d_rows + lo * stride * 8, d_cnt + lo * 4, d_len.ptr + lo * 8,
                                      stride, n_loc, 8, s, k, 4.0 ** k, 1.0, 1.0,
                                      *[o.ptr for o in outs], st))
@@ -370,8 +370,9 @@ def main():
     d_rows, d_cnt, ng, stride = job.device_output()
     L = fpmash.lib()
     n_pairs = n * n
-    d_numer = fpmash.DeviceBuffer(ctx, n_pairs * 4)
-    d_denom = fpmash.DeviceBuffer(ctx, n_pairs * 4)
+    # u16 numer / denom cells (fpm_dist_dev16: counts <= s = 1000)
+    d_numer = fpmash.DeviceBuffer(ctx, n_pairs * 2)
+    d_denom = fpmash.DeviceBuffer(ctx, n_pairs * 2)
     d_dist = fpmash.DeviceBuffer(ctx, n_pairs * 8)
     d_pval = fpmash.DeviceBuffer(ctx, n_pairs * 8)
     d_pass = fpmash.DeviceBuffer(ctx, n_pairs)
@@ -382,7 +383,7 @@ def main():
     def step():
         job.run(st)
         # compare + distance + p-value + pass in one call
-        fpmash._check(L.fpm_dist_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
+        fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
                                      d_len.ptr, stride, n, 8, args.s, args.k, 4.0 ** args.k,
                                      1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
                                      d_pass.ptr, st))
@@ -419,7 +420,7 @@ def main():
     # sanity: shared-hash counts present (family structure) and no empty sketches
     cnt_host = np.empty(n, dtype=np.uint32)
     fpmash._check(L.fpm_memcpy_d2h(ctx.h, cnt_host.ctypes.data, d_cnt, n * 4))
-    numer_sample = d_numer.to_array(np.uint32, min(n_pairs, 1 << 20))
+    numer_sample = d_numer.to_array(np.uint16, min(n_pairs, 1 << 20))
 
     bases_rank = n * args.seq_len
     total_bases = grp.sum(bases_rank) * args.steps
@@ -443,16 +444,18 @@ def main():
         # finalize rewrites the candidate cells (and their mirrors on the symmetric path)
         n_cand = dstats["candidates"]
         cells = 2 * n_cand - n if dstats["sparse"] == 2 else n_cand
-        alg[N[fpmash.K_FILL]] = (n_pairs * (4 + 4 + 8 + 8 + 1),
-                                 "numer/denom/distance/p-value/pass (25 B/pair) written")
-        alg[N[fpmash.K_PROBE]] = (n_hash * 8, "query sketch hashes read")
-        alg[N[fpmash.K_FINALIZE]] = (n_cand * (8 + 4 + 4) + cells * (8 + 8 + 1),
+        alg[N[fpmash.K_FILL]] = (n_pairs * (8 + 8 + 1),
+                                 "distance/p-value/pass (17 B/pair) written")
+        alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * (2 + 2),
+                                  "query sketch hashes read + u16 numer/denom defaults (4 B/pair) "
+                                  "written")
+        alg[N[fpmash.K_FINALIZE]] = (n_cand * (8 + 4 + 4) + cells * (2 + 2 + 8 + 8 + 1),
                                      "candidate + its numer/denom read, distance/p-value/pass "
                                      "written per candidate cell (mirrors included)")
     else:
-        alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * 8,
-                                  "query sketch hashes read + numer/denom (8 B/pair) written")
-        alg[N[fpmash.K_FINALIZE]] = (n_pairs * (4 + 4 + 8 + 8 + 1),
+        alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * 4,
+                                  "query sketch hashes read + u16 numer/denom (4 B/pair) written")
+        alg[N[fpmash.K_FINALIZE]] = (n_pairs * (2 + 2 + 8 + 8 + 1),
                                      "numer+denom read, distance+p-value+pass written per pair")
     traffic = {}
     if os.path.exists(PMC_TRAFFIC):
@@ -522,7 +525,7 @@ def main():
             "config": {
                 "workload": (f"C2 step: sketch -i k={args.k} s={args.s} of {n} x {args.seq_len} bp "
                              f"+ all-vs-all dist of the {n} sketches ({n_pairs:.3g} pairs, "
-                             "numer/denom + distance + FP64 p-value), per GPU"),
+                             "u16 numer/denom + distance + FP64 p-value + pass), per GPU"),
                 "n_seqs_per_gpu": n, "seq_len": args.seq_len, "k": args.k, "s": args.s,
                 "pairs_per_gpu": n_pairs, "parallelism": f"independent batch per GPU x{ws}",
             },

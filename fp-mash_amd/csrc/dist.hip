@@ -47,12 +47,12 @@ __device__ __forceinline__ void walk_pair(const H *__restrict__ A, uint32_t la,
     denom = d;
 }
 
-template <typename H>
+template <typename H, typename C>
 __global__ __launch_bounds__(256) void compare_grid_kernel(
     const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t n_qry, uint32_t S, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom)
+    uint64_t qry_stride, uint32_t n_qry, uint32_t S, C *__restrict__ numer,
+    C *__restrict__ denom)
 {
     const uint32_t r = blockIdx.x * kTile + (threadIdx.x & (kTile - 1));
     const uint32_t q = blockIdx.y * kTile + (threadIdx.x / kTile);
@@ -61,8 +61,8 @@ __global__ __launch_bounds__(256) void compare_grid_kernel(
     walk_pair(ref + (uint64_t)r * ref_stride, ref_len[r], qry + (uint64_t)q * qry_stride,
               qry_len[q], S, c, d);
     const uint64_t o = (uint64_t)q * n_ref + r;
-    numer[o] = c;
-    denom[o] = d;
+    numer[o] = (C)c;
+    denom[o] = (C)d;
 }
 
 // per lane: bit lane of m ? y : x (one v_cndmask per dword)
@@ -87,12 +87,12 @@ __device__ __forceinline__ uint64_t lane_sel(uint64_t x, uint64_t y, uint64_t m)
 // One wave per SIMD (up to 160 KB of lists per workgroup), one pair per lane: the walk's
 // dependent VALU chain is not hidden by other waves, which bounds it (C3: 5,000 x 5,000 pairs
 // of 2,000 u32 in ~35 ms, against 67 ms for the global-memory walk).
-template <typename H, int BLK>
+template <typename H, int BLK, typename C>
 __global__ __launch_bounds__(256) void compare_grid_lds_kernel(
     const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t n_qry, uint32_t S, uint32_t W, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom)
+    uint64_t qry_stride, uint32_t n_qry, uint32_t S, uint32_t W, C *__restrict__ numer,
+    C *__restrict__ denom)
 {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     H *lds = reinterpret_cast<H *>(smem);
@@ -202,17 +202,17 @@ __global__ __launch_bounds__(256) void compare_grid_lds_kernel(
         d = dd > S ? S : (uint32_t)dd;
     }
     const uint64_t o = (uint64_t)q * n_ref + r;
-    numer[o] = common;
-    denom[o] = d;
+    numer[o] = (C)common;
+    denom[o] = (C)d;
 }
 
 // Walk only the candidate pairs found by the inverted index (dist_index.hip).
-template <typename H>
+template <typename H, typename C>
 __global__ __launch_bounds__(256) void walk_cand_kernel(
     const uint64_t *__restrict__ cand, const unsigned long long *__restrict__ n_cand,
     const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, uint32_t *__restrict__ numer, uint32_t *__restrict__ denom)
+    uint64_t qry_stride, uint32_t S, C *__restrict__ numer, C *__restrict__ denom)
 {
     const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= *n_cand) return;
@@ -221,8 +221,8 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
     uint32_t c, d;
     walk_pair(ref + (uint64_t)r * ref_stride, ref_len[r], qry + (uint64_t)q * qry_stride,
               qry_len[q], S, c, d);
-    numer[o] = c;
-    denom[o] = d;
+    numer[o] = (C)c;
+    denom[o] = (C)d;
 }
 
 // Sorted, distinct lists (every sketch the k-mer path produces): the walk of
@@ -245,13 +245,13 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 // No per-wave LDS image and no merge walk: ~5 LDS reads and ~40 VALU per A element.
 constexpr int kRankWaves = 4;
 
-template <int CAP>
+template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
     const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const uint64_t *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, uint32_t sym, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom, uint32_t *__restrict__ cnum, uint32_t *__restrict__ cden)
+    uint64_t qry_stride, uint32_t S, uint32_t sym, C *__restrict__ numer,
+    C *__restrict__ denom, uint32_t *__restrict__ cnum, uint32_t *__restrict__ cden)
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 11 : 12;   // 2 * CAP buckets
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
@@ -412,39 +412,55 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 cden[base + c] = dn;
                 continue;
             }
-            numer[o] = cnt;
-            denom[o] = dn;
+            numer[o] = (C)cnt;
+            denom[o] = (C)dn;
             const uint32_t r = (uint32_t)(o - pair_row);
             if (sym && r != q) {                          // mirror cell (r, q)
                 const uint64_t o2 = (uint64_t)r * n_ref + q;
-                numer[o2] = cnt;
-                denom[o2] = dn;
+                numer[o2] = (C)cnt;
+                denom[o2] = (C)dn;
             }
         }
     }
 }
 
-hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                             const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                             uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
-                             uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, uint32_t *d_cnum, uint32_t *d_cden,
-                             hipStream_t st)
+template <typename C>
+static hipError_t merge_rows_c(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
+                               const uint64_t *d_ref, const uint32_t *d_ref_len,
+                               uint64_t ref_stride, uint32_t n_ref, const uint64_t *d_qry,
+                               const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t S,
+                               bool sym, C *d_numer, C *d_denom, uint32_t *d_cnum,
+                               uint32_t *d_cden, hipStream_t st)
 {
-    if (!n_qry) return hipSuccess;
     const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
     const uint64_t cap = std::max(ref_stride, qry_stride);
     if (cap <= 1024)
-        hipLaunchKernelGGL(rank_rows_kernel<1024>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
+        hipLaunchKernelGGL((rank_rows_kernel<1024, C>), g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
                            d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
                            (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else if (cap <= 2048)
-        hipLaunchKernelGGL(rank_rows_kernel<2048>, g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
+        hipLaunchKernelGGL((rank_rows_kernel<2048, C>), g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
                            d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
                            (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
+}
+
+hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
+                             const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                             uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
+                             uint64_t qry_stride, uint32_t S, bool sym, Counts cnt,
+                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st)
+{
+    if (!n_qry) return hipSuccess;
+    if (cnt.c16)
+        return merge_rows_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                            d_qry_len, qry_stride, S, sym, (uint16_t *)cnt.numer,
+                            (uint16_t *)cnt.denom, d_cnum, d_cden, st);
+    return merge_rows_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                        d_qry_len, qry_stride, S, sym, (uint32_t *)cnt.numer,
+                        (uint32_t *)cnt.denom, d_cnum, d_cden, st);
 }
 
 // ---- FP64 p-value (same algorithm as the oracle restatement)
@@ -531,8 +547,9 @@ __device__ double pvalue_dev(uint32_t x, uint64_t len_ref, uint64_t len_qry, dou
 
 // distance (CommandDistance.cpp:404-419), p-value and the -d / -v filters, one pair per
 // thread (a candidate's p-value continued fraction stays on its own lane)
+template <typename C>
 __global__ __launch_bounds__(256) void dist_finalize_kernel(
-    const uint32_t *__restrict__ numer, const uint32_t *__restrict__ denom,
+    const C *__restrict__ numer, const C *__restrict__ denom,
     const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
     uint32_t n_ref, uint64_t n_pairs, uint32_t kmer_size, double kmer_space, double max_dist,
     double max_pvalue, double *__restrict__ dist, double *__restrict__ pval,
@@ -566,11 +583,11 @@ __global__ __launch_bounds__(256) void dist_finalize_kernel(
 // VEC (n_ref % 4 == 0, so a row starts 4-cell aligned): each lane writes 4 consecutive
 // cells with 16-B stores (1 KiB per wave store; the pass bytes as one dword).
 constexpr uint32_t kFillCells = 1024;
-template <bool VEC>
+template <bool VEC, typename C>
 __global__ __launch_bounds__(256) void dist_fill_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
-    uint32_t nrb, uint32_t ntask, uint32_t S, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom, PairFill fill)
+    uint32_t nrb, uint32_t ntask, uint32_t S, C *__restrict__ numer,
+    C *__restrict__ denom, PairFill fill)
 {
     const bool keep1 = !(fill.max_dist >= 0 && 1.0 > fill.max_dist);   // distance 0 always kept
     const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
@@ -598,8 +615,8 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms); 16-B write-through
         // (sc1) buffer stores slowed it 1.9x (0.9 -> 1.67 ms beside the compare)
         if (numer) {
-            *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
-            *(uint4 *)(denom + o) = make_uint4(dn[0], dn[1], dn[2], dn[3]);
+            store_counts4(numer + o, 0, 0, 0, 0);
+            store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
         }
         *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
         *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
@@ -617,7 +634,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         const bool ok = d == 0 || keep1;
         if (numer) {
             numer[o] = 0;
-            denom[o] = d < S ? d : S;
+            denom[o] = (C)(d < S ? d : S);
         }
         fill.dist[o] = d == 0 ? 0.0 : 1.0;
         fill.pval[o] = ok ? 1.0 : 0.0;
@@ -627,9 +644,10 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
 }
 
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
-                            uint32_t n_qry, uint32_t S, uint32_t *d_numer, uint32_t *d_denom,
-                            const PairFill &fill, hipStream_t st)
+                            uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
+                            hipStream_t st)
 {
+    void *d_numer = cnt.numer, *d_denom = cnt.denom;
     if (!n_ref || !n_qry) return hipSuccess;
     const uint32_t nrb = (n_ref + kFillCells - 1) / kFillCells;
     const uint64_t blocks = (uint64_t)nrb * n_qry;
@@ -642,12 +660,17 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
     // the full grid: short workgroups hand their slots back to the candidate compare running
     // beside; a capped grid-stride fill (256-4096 workgroups) held them and measured slower
     const uint32_t grid = (uint32_t)blocks;
-    if (vec)
-        hipLaunchKernelGGL(dist_fill_kernel<true>, dim3(grid), dim3(256), 0, st, d_ref_len,
-                           n_ref, d_qry_len, nrb, (uint32_t)blocks, S, d_numer, d_denom, fill);
-    else
-        hipLaunchKernelGGL(dist_fill_kernel<false>, dim3(grid), dim3(256), 0, st, d_ref_len,
-                           n_ref, d_qry_len, nrb, (uint32_t)blocks, S, d_numer, d_denom, fill);
+#define FPM_FILL(V, C)                                                                         \
+    hipLaunchKernelGGL((dist_fill_kernel<V, C>), dim3(grid), dim3(256), 0, st, d_ref_len, n_ref, \
+                       d_qry_len, nrb, (uint32_t)blocks, S, (C *)d_numer, (C *)d_denom, fill)
+    if (cnt.c16) {
+        if (vec) FPM_FILL(true, uint16_t);
+        else FPM_FILL(false, uint16_t);
+    } else {
+        if (vec) FPM_FILL(true, uint32_t);
+        else FPM_FILL(false, uint32_t);
+    }
+#undef FPM_FILL
     return hipGetLastError();
 }
 
@@ -680,10 +703,11 @@ __device__ __forceinline__ void finalize_cell(uint64_t o, uint32_t c, uint32_t d
     if (pass) pass[o] = ok ? 1 : 0;
 }
 
+template <typename C>
 __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
     const uint64_t *__restrict__ cand, const unsigned long long *__restrict__ n_cand,
     uint32_t sym, const uint32_t *__restrict__ cnum, const uint32_t *__restrict__ cden,
-    uint32_t *__restrict__ numer, uint32_t *__restrict__ denom,
+    C *__restrict__ numer, C *__restrict__ denom,
     const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
     uint32_t n_ref, uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
     double *__restrict__ dist, double *__restrict__ pval, uint8_t *__restrict__ pass)
@@ -697,8 +721,8 @@ __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
         if (cnum) {          // compact results: scatter numer / denom too
             nm = cnum[c];
             dn = cden[c];
-            numer[o] = nm;
-            denom[o] = dn;
+            numer[o] = (C)nm;
+            denom[o] = (C)dn;
         } else {
             nm = numer[o];
             dn = denom[o];
@@ -708,8 +732,8 @@ __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
         if (sym && r != q) {   // cell (r, q): query r against ref q
             const uint64_t o2 = (uint64_t)r * n_ref + q;
             if (cnum) {
-                numer[o2] = nm;
-                denom[o2] = dn;
+                numer[o2] = (C)nm;
+                denom[o2] = (C)dn;
             }
             finalize_cell(o2, nm, dn, ref_length[q], qry_length[r], kmer_size, kmer_space,
                           max_dist, max_pvalue, dist, pval, pass);
@@ -719,8 +743,8 @@ __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
 
 hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                      uint64_t cap, bool sym, const uint32_t *d_cnum,
-                                     const uint32_t *d_cden, uint32_t *d_numer,
-                                     uint32_t *d_denom, const uint64_t *d_ref_length,
+                                     const uint32_t *d_cden, Counts cnt,
+                                     const uint64_t *d_ref_length,
                                      const uint64_t *d_qry_length, uint32_t n_ref,
                                      uint32_t kmer_size, double kmer_space, double max_dist,
                                      double max_pvalue, double *d_dist, double *d_pvalue,
@@ -728,10 +752,14 @@ hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long
 {
     if (!cap) return hipSuccess;
     const uint64_t blocks = std::min<uint64_t>((cap + 255) / 256, 4096);
-    hipLaunchKernelGGL(dist_cand_finalize_kernel, dim3((uint32_t)blocks), dim3(256), 0, st,
-                       d_cand, d_n_cand, (uint32_t)sym, d_cnum, d_cden, d_numer, d_denom,
-                       d_ref_length, d_qry_length, n_ref, kmer_size, kmer_space, max_dist,
-                       max_pvalue, d_dist, d_pvalue, d_pass);
+#define FPM_CFIN(C)                                                                          \
+    hipLaunchKernelGGL(dist_cand_finalize_kernel<C>, dim3((uint32_t)blocks), dim3(256), 0, st,  \
+                       d_cand, d_n_cand, (uint32_t)sym, d_cnum, d_cden, (C *)cnt.numer,        \
+                       (C *)cnt.denom, d_ref_length, d_qry_length, n_ref, kmer_size,           \
+                       kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass)
+    if (cnt.c16) FPM_CFIN(uint16_t);
+    else FPM_CFIN(uint32_t);
+#undef FPM_CFIN
     return hipGetLastError();
 }
 
@@ -788,11 +816,11 @@ hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
     return hipGetLastError();
 }
 
-hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                               uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
-                               uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
-                               uint32_t sketch_size, uint32_t *d_numer, uint32_t *d_denom,
-                               hipStream_t st)
+template <typename C>
+static hipError_t compare_grid_c(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                                 uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
+                                 uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
+                                 uint32_t sketch_size, C *d_numer, C *d_denom, hipStream_t st)
 {
     if (n_ref == 0 || n_qry == 0) return hipSuccess;
     dim3 grid((n_ref + kTile - 1) / kTile, (n_qry + kTile - 1) / kTile);
@@ -803,17 +831,17 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
         constexpr int kBlk = FPM_WALK_BLK;
         const size_t lds = (size_t)2 * kTile * ((W + kBlk + 3) & ~3ull) * hash_bytes;
         if (W > 0 && lds <= kMaxLds && (hash_bytes == 4 || hash_bytes == 8)) {
-            const void *fn = hash_bytes == 8 ? (const void *)compare_grid_lds_kernel<uint64_t, kBlk>
-                                             : (const void *)compare_grid_lds_kernel<uint32_t, kBlk>;
+            const void *fn = hash_bytes == 8 ? (const void *)compare_grid_lds_kernel<uint64_t, kBlk, C>
+                                             : (const void *)compare_grid_lds_kernel<uint32_t, kBlk, C>;
             if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds) ==
                 hipSuccess) {
                 if (hash_bytes == 8)
-                    hipLaunchKernelGGL((compare_grid_lds_kernel<uint64_t, kBlk>), grid, dim3(256), lds, st,
+                    hipLaunchKernelGGL((compare_grid_lds_kernel<uint64_t, kBlk, C>), grid, dim3(256), lds, st,
                                        (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                        (const uint64_t *)d_qry, d_qry_len, qry_stride, n_qry,
                                        sketch_size, (uint32_t)W, d_numer, d_denom);
                 else
-                    hipLaunchKernelGGL((compare_grid_lds_kernel<uint32_t, kBlk>), grid, dim3(256), lds, st,
+                    hipLaunchKernelGGL((compare_grid_lds_kernel<uint32_t, kBlk, C>), grid, dim3(256), lds, st,
                                        (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                        (const uint32_t *)d_qry, d_qry_len, qry_stride, n_qry,
                                        sketch_size, (uint32_t)W, d_numer, d_denom);
@@ -823,12 +851,12 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
         }
     }
     if (hash_bytes == 8)
-        hipLaunchKernelGGL(compare_grid_kernel<uint64_t>, grid, dim3(256), 0, st,
+        hipLaunchKernelGGL((compare_grid_kernel<uint64_t, C>), grid, dim3(256), 0, st,
                            (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                            (const uint64_t *)d_qry, d_qry_len, qry_stride, n_qry, sketch_size,
                            d_numer, d_denom);
     else if (hash_bytes == 4)
-        hipLaunchKernelGGL(compare_grid_kernel<uint32_t>, grid, dim3(256), 0, st,
+        hipLaunchKernelGGL((compare_grid_kernel<uint32_t, C>), grid, dim3(256), 0, st,
                            (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
                            (const uint32_t *)d_qry, d_qry_len, qry_stride, n_qry, sketch_size,
                            d_numer, d_denom);
@@ -837,28 +865,57 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
     return hipGetLastError();
 }
 
-hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
-                                  uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
-                                  uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
-                                  const uint32_t *d_qry_len, uint64_t qry_stride,
-                                  uint32_t hash_bytes, uint32_t S, uint32_t *d_numer,
-                                  uint32_t *d_denom, hipStream_t st)
+hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                               uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
+                               uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
+                               uint32_t sketch_size, Counts cnt, hipStream_t st)
 {
-    if (!cap) return hipSuccess;
+    if (cnt.c16)
+        return compare_grid_c(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
+                              n_qry, hash_bytes, sketch_size, (uint16_t *)cnt.numer,
+                              (uint16_t *)cnt.denom, st);
+    return compare_grid_c(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, n_qry,
+                          hash_bytes, sketch_size, (uint32_t *)cnt.numer, (uint32_t *)cnt.denom,
+                          st);
+}
+
+template <typename C>
+static hipError_t walk_candidates_c(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                    uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
+                                    uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                    const uint32_t *d_qry_len, uint64_t qry_stride,
+                                    uint32_t hash_bytes, uint32_t S, C *d_numer, C *d_denom,
+                                    hipStream_t st)
+{
     dim3 grid((uint32_t)((cap + 255) / 256));
     if (hash_bytes == 8)
-        hipLaunchKernelGGL(walk_cand_kernel<uint64_t>, grid, dim3(256), 0, st, d_cand, d_n_cand,
+        hipLaunchKernelGGL((walk_cand_kernel<uint64_t, C>), grid, dim3(256), 0, st, d_cand, d_n_cand,
                            (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                            (const uint64_t *)d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
     else
-        hipLaunchKernelGGL(walk_cand_kernel<uint32_t>, grid, dim3(256), 0, st, d_cand, d_n_cand,
+        hipLaunchKernelGGL((walk_cand_kernel<uint32_t, C>), grid, dim3(256), 0, st, d_cand, d_n_cand,
                            (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
                            (const uint32_t *)d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
     return hipGetLastError();
 }
 
-hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
-                                const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                  uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
+                                  uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                  const uint32_t *d_qry_len, uint64_t qry_stride,
+                                  uint32_t hash_bytes, uint32_t S, Counts cnt, hipStream_t st)
+{
+    if (!cap) return hipSuccess;
+    if (cnt.c16)
+        return walk_candidates_c(d_cand, d_n_cand, cap, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                                 d_qry_len, qry_stride, hash_bytes, S, (uint16_t *)cnt.numer,
+                                 (uint16_t *)cnt.denom, st);
+    return walk_candidates_c(d_cand, d_n_cand, cap, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                             d_qry_len, qry_stride, hash_bytes, S, (uint32_t *)cnt.numer,
+                             (uint32_t *)cnt.denom, st);
+}
+
+hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
                                 double kmer_space, double max_dist, double max_pvalue,
                                 double *d_dist, double *d_pvalue, uint8_t *d_pass,
@@ -867,9 +924,14 @@ hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom
     uint64_t n = (uint64_t)n_ref * n_qry;
     if (n == 0) return hipSuccess;
     const uint64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(dist_finalize_kernel, dim3((uint32_t)blocks), dim3(256), 0, st, d_numer,
-                       d_denom, d_ref_length, d_qry_length, n_ref, n, kmer_size, kmer_space,
-                       max_dist, max_pvalue, d_dist, d_pvalue, d_pass);
+#define FPM_DFIN(C)                                                                          \
+    hipLaunchKernelGGL(dist_finalize_kernel<C>, dim3((uint32_t)blocks), dim3(256), 0, st,       \
+                       (const C *)cnt.numer, (const C *)cnt.denom, d_ref_length, d_qry_length, \
+                       n_ref, n, kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, \
+                       d_pass)
+    if (cnt.c16) FPM_DFIN(uint16_t);
+    else FPM_DFIN(uint32_t);
+#undef FPM_DFIN
     return hipGetLastError();
 }
 

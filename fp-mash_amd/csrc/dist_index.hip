@@ -340,13 +340,14 @@ __global__ void sum64_kernel(unsigned long long *events)
 // a wave scan flattens the 64 buckets into one event range, and the lanes then read
 // consecutive entries of that range (coalesced).  The owner hash of each event comes from
 // a per-wave byte map filled by the lanes for 1024-event windows (one LDS read per event).
+template <typename C>
 __global__ __launch_bounds__(256) void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
-    uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, uint32_t *__restrict__ numer,
-    uint32_t *__restrict__ denom, uint64_t *__restrict__ cand,
+    uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, C *__restrict__ numer,
+    C *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
@@ -483,15 +484,15 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
                 const uint64_t o = pair_row + r;
                 const uint4 rl = *(const uint4 *)(ref_len + r);
                 const uint32_t d0 = rl.x + lq, d1 = rl.y + lq, d2 = rl.z + lq, d3 = rl.w + lq;
-                *(uint4 *)(numer + o) = make_uint4(0, 0, 0, 0);
-                *(uint4 *)(denom + o) = make_uint4(min(d0, S), min(d1, S), min(d2, S), min(d3, S));
+                store_counts4(numer + o, 0, 0, 0, 0);
+                store_counts4(denom + o, min(d0, S), min(d1, S), min(d2, S), min(d3, S));
             }
         } else {
             for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {
                 const uint64_t o = pair_row + r;
                 const uint64_t d = (uint64_t)ref_len[r] + lq;
                 numer[o] = 0;
-                denom[o] = d < S ? (uint32_t)d : S;
+                denom[o] = (C)(d < S ? (uint32_t)d : S);
             }
         }
     }
@@ -550,7 +551,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
-                             bool self_set, uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st)
 {
     if (!n_qry || !n_ref) return hipSuccess;
@@ -558,16 +559,19 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     const uint32_t nchunks = (n_ref + chunk - 1) / chunk;
     const uint32_t cref = nchunks == 1 ? n_ref : chunk;
     const size_t lds = ((cref + 31) / 32) * 4;
-    // 16-B default stores: every row and chunk start 4-cell aligned, buffers 16-B aligned
+    // vector default stores (4 cells): every row and chunk start 4-cell aligned, buffers
+    // 16-B aligned
     const auto al = [](const void *p) { return ((uintptr_t)p & 15) == 0; };
     const uint32_t vec_defaults = n_ref % 4 == 0 && cref % 4 == 0 && al(d_ref_len) &&
-                                  al(d_numer) && al(d_denom);
-    hipLaunchKernelGGL(probe_rows_kernel, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,
-                       d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref,
-                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults, (uint32_t)self_set,
-                       d_numer,
-                       d_denom, cand, n_cand,
-                       row_seg);
+                                  al(cnt.numer) && al(cnt.denom);
+#define FPM_PROBE(C)                                                                            \
+    hipLaunchKernelGGL(probe_rows_kernel<C>, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,  \
+                       d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref, \
+                       d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
+                       (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg)
+    if (cnt.c16) FPM_PROBE(uint16_t);
+    else FPM_PROBE(uint32_t);
+#undef FPM_PROBE
     return hipGetLastError();
 }
 

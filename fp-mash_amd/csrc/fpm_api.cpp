@@ -854,8 +854,8 @@ struct DistFinal {
 static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
-                        uint32_t hash_bytes, uint32_t sketch_size, uint32_t *d_numer,
-                        uint32_t *d_denom, void *stream, const DistFinal *fin = nullptr,
+                        uint32_t hash_bytes, uint32_t sketch_size, Counts cnt,
+                        void *stream, const DistFinal *fin = nullptr,
                         bool *finalized = nullptr)
 {
     if (finalized) *finalized = false;
@@ -951,7 +951,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
                                           d_ref_len, sketch_size, sym, true, self_set,
-                                          d_numer, d_denom, (uint64_t *)cand, n_cand,
+                                          cnt, (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, st));
                 tl.done();
             }
@@ -967,8 +967,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
                 HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
                 TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, nullptr,
-                                         nullptr, fill, ctx->aux));
+                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, Counts{},
+                                         fill, ctx->aux));
                 tl.done();
                 HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
                 fill_pending = true;
@@ -986,20 +986,20 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
-                                              sketch_size, sym, d_numer, d_denom, cnum, cden,
+                                              sketch_size, sym, cnt, cnum, cden,
                                               st));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
-                                                   qry_stride, hash_bytes, sketch_size, d_numer,
-                                                   d_denom, st));
+                                                   qry_stride, hash_bytes, sketch_size, cnt,
+                                                   st));
                 tl.done();
             }
             if (fin) {
                 if (cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
                 HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
-                                                  cden, d_numer, d_denom, fin->ref_length,
+                                                  cden, cnt, fin->ref_length,
                                                   fin->qry_length,
                                                   n_ref, fin->kmer_size, fin->kmer_space,
                                                   fin->max_dist, fin->max_pvalue, fin->dist,
@@ -1016,7 +1016,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (fill_pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));   // dense after all
     TimedLaunch tl(ctx, FPM_K_COMPARE, st);
     HIP_TRY(launch_compare_grid(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
-                                n_qry, hash_bytes, sketch_size, d_numer, d_denom, st));
+                                n_qry, hash_bytes, sketch_size, cnt, st));
     tl.done();
     ctx->last_cand = n_pairs;
     return FPM_OK;
@@ -1031,8 +1031,40 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                          uint32_t *d_denom, void *stream)
 {
     return compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
-                        n_qry, hash_bytes, sketch_size, d_numer, d_denom, stream);
+                        n_qry, hash_bytes, sketch_size, Counts{d_numer, d_denom, false}, stream);
 }
+
+}  // extern "C"
+
+// compare + finalize on device buffers (fpm_dist_dev / fpm_dist_dev16)
+static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                         const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                         const void *d_qry, const uint32_t *d_qry_len,
+                         const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
+                         double kmer_space, double max_dist, double max_pvalue, Counts cnt,
+                         double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream,
+                         const char *who)
+{
+    if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
+        return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
+    const DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
+                        d_dist, d_pvalue, d_pass};
+    bool finalized = false;
+    if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
+                              qry_stride, n_qry, hash_bytes, sketch_size, cnt, stream, &fin,
+                              &finalized))
+        return rc;
+    if (finalized) return FPM_OK;
+    hipStream_t st = pick_stream(ctx, stream);
+    TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
+    HIP_TRY(launch_dist_finalize(cnt, d_ref_length, d_qry_length, n_ref, n_qry, kmer_size,
+                                 kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass, st));
+    tl.done();
+    return FPM_OK;
+}
+
+extern "C" {
 
 int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                  const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
@@ -1042,19 +1074,26 @@ int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                  uint32_t *d_numer, uint32_t *d_denom, double *d_dist, double *d_pvalue,
                  uint8_t *d_pass, void *stream)
 {
-    if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
-        return fail(FPM_EINVAL, "fpm_dist_dev: lengths, distance and p-value buffers required");
-    const DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
-                        d_dist, d_pvalue, d_pass};
-    bool finalized = false;
-    if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
-                              qry_stride, n_qry, hash_bytes, sketch_size, d_numer, d_denom,
-                              stream, &fin, &finalized))
-        return rc;
-    if (finalized) return FPM_OK;
-    return fpm_dist_finalize_dev(ctx, d_numer, d_denom, d_ref_length, d_qry_length, n_ref, n_qry,
-                                 kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue,
-                                 d_pass, stream);
+    return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
+                         d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
+                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, false},
+                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev");
+}
+
+int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                   const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                   const void *d_qry, const uint32_t *d_qry_len, const uint64_t *d_qry_length,
+                   uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes, uint32_t sketch_size,
+                   uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
+                   uint16_t *d_numer, uint16_t *d_denom, double *d_dist, double *d_pvalue,
+                   uint8_t *d_pass, void *stream)
+{
+    if (sketch_size > 65535)
+        return fail(FPM_EINVAL, "fpm_dist_dev16: sketch_size must be <= 65535 (u16 counts)");
+    return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
+                         d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
+                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, true},
+                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev16");
 }
 
 int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,
@@ -1066,9 +1105,9 @@ int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t 
     if (int rc = set_device(ctx)) return rc;
     hipStream_t st = pick_stream(ctx, stream);
     TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
-    HIP_TRY(launch_dist_finalize(d_numer, d_denom, d_ref_length, d_qry_length, n_ref, n_qry,
-                                 kmer_size, kmer_space, max_dist, max_pvalue, d_dist, d_pvalue,
-                                 d_pass, st));
+    HIP_TRY(launch_dist_finalize(Counts{(void *)d_numer, (void *)d_denom, false}, d_ref_length,
+                                 d_qry_length, n_ref, n_qry, kmer_size, kmer_space, max_dist,
+                                 max_pvalue, d_dist, d_pvalue, d_pass, st));
     tl.done();
     return FPM_OK;
 }

@@ -82,6 +82,19 @@ __device__ __forceinline__ uint32_t lds_u32_at(const uint32_t *img, uint32_t byt
     return __builtin_amdgcn_alignbyte(img[q + 1], img[q], r);
 }
 
+// Four consecutive numer / denom cells: one 16-B store (u32 cells, 16-B aligned) or one 8-B
+// store (u16 cells, 8-B aligned).
+__device__ __forceinline__ void store_counts4(uint32_t *p, uint32_t a, uint32_t b, uint32_t c,
+                                              uint32_t d)
+{
+    *(uint4 *)p = make_uint4(a, b, c, d);
+}
+__device__ __forceinline__ void store_counts4(uint16_t *p, uint32_t a, uint32_t b, uint32_t c,
+                                              uint32_t d)
+{
+    *(uint2 *)p = make_uint2(a | (b << 16), c | (d << 16));
+}
+
 // Row-major launches over query rows: workgroups are dealt round-robin over the 8 XCDs, so
 // block b runs on XCD b % 8. Map the blocks of one XCD to a CONTIGUOUS range of rows, so the
 // rows resident on an XCD at once are neighbours (same family / similar sketches) and the

@@ -38,6 +38,13 @@ struct MergeDesc {
     uint64_t *c; uint32_t *clen;
 };
 
+// numer / denom output cells of the dist grid: u32, or u16 (c16) when the sketch size fits
+// (fpm_dist_dev16: counts <= s <= 65535, 4 bytes per pair instead of 8)
+struct Counts {
+    void *numer = nullptr, *denom = nullptr;
+    bool c16 = false;
+};
+
 // Tile capacity classes (k-mer starts per tile).
 constexpr int kTileClasses = 6;
 constexpr uint32_t kTileCap[kTileClasses] = {256, 512, 1024, 2048, 4096, 8192};
@@ -57,15 +64,13 @@ hipError_t launch_fp_hash(const uint64_t *d_vals, const uint64_t *d_line_off, ui
 hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                                uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
                                uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
-                               uint32_t sketch_size, uint32_t *d_numer, uint32_t *d_denom,
-                               hipStream_t st);
+                               uint32_t sketch_size, Counts cnt, hipStream_t st);
 
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                   uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                                   const uint32_t *d_qry_len, uint64_t qry_stride,
-                                  uint32_t hash_bytes, uint32_t S, uint32_t *d_numer,
-                                  uint32_t *d_denom, hipStream_t st);
+                                  uint32_t hash_bytes, uint32_t S, Counts cnt, hipStream_t st);
 
 // bucket index over ref hashes (dist_index.hip)
 constexpr uint32_t kIdxL1 = 10;        // level-1 partition bits
@@ -99,15 +104,15 @@ struct PairFill {
     double max_dist = -1, max_pvalue = -1;
 };
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
-                            uint32_t n_qry, uint32_t S, uint32_t *d_numer, uint32_t *d_denom,
-                            const PairFill &fill, hipStream_t st);
+                            uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
+                            hipStream_t st);
 // `defaults`: also write (0, min(S, la+lb)) to every numer / denom cell of the row (off
 // when launch_dist_fill already did)
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
                              uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
-                             bool self_set, uint32_t *d_numer, uint32_t *d_denom, uint64_t *cand,
+                             bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st);
 // (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are
 // the row's own hash and are not read)
@@ -115,9 +120,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
 hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
-                             uint64_t qry_stride, uint32_t S, bool sym, uint32_t *d_numer,
-                             uint32_t *d_denom, uint32_t *d_cnum, uint32_t *d_cden,
-                             hipStream_t st);
+                             uint64_t qry_stride, uint32_t S, bool sym, Counts cnt,
+                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st);
 // (d_cnum, d_cden non-null: results go to candidate slot c instead of the grid cells)
 
 // -fp CFL text: newline index, then one lane per line (fingerprint.hip)
@@ -143,14 +147,13 @@ hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
 // of each mirror cell (r, q) when `sym`; the other cells hold the probe's PairFill values
 hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                      uint64_t cap, bool sym, const uint32_t *d_cnum,
-                                     const uint32_t *d_cden, uint32_t *d_numer,
-                                     uint32_t *d_denom, const uint64_t *d_ref_length,
+                                     const uint32_t *d_cden, Counts cnt,
+                                     const uint64_t *d_ref_length,
                                      const uint64_t *d_qry_length, uint32_t n_ref,
                                      uint32_t kmer_size, double kmer_space, double max_dist,
                                      double max_pvalue, double *d_dist, double *d_pvalue,
                                      uint8_t *d_pass, hipStream_t st);
-hipError_t launch_dist_finalize(const uint32_t *d_numer, const uint32_t *d_denom,
-                                const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
                                 double kmer_space, double max_dist, double max_pvalue,
                                 double *d_dist, double *d_pvalue, uint8_t *d_pass,

@@ -85,6 +85,9 @@ SYMBOLS = [
     ("fpm_dist_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
                                C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
+    ("fpm_dist_dev16", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
+                                 C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
+                                 C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
     ("fpm_fp_positional_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p,
                                          C.c_uint64, C.c_uint32, C.c_uint32, C.c_double,
                                          C.c_double, u32p, u32p, f64p, f64p, u8p]),
@@ -374,6 +377,43 @@ class Context:
                               _p(pv, f64p), _p(pa, u8p)))
         return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
                 "pass": pa[:n].astype(bool)}
+
+    def dist16(self, ref_lists, qry_lists, sketch_size, use64=True, k=21, kmer_space=None,
+               ref_lengths=None, qry_lengths=None, max_dist=-1.0, max_pvalue=-1.0):
+        """dist() through fpm_dist_dev16 (device buffers, u16 numer / denom cells)."""
+        dt = np.uint64 if use64 else np.uint32
+        w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
+        R, rl = _dense(ref_lists, w, dt)
+        Q, ql = (R, rl) if qry_lists is ref_lists else _dense(qry_lists, w, dt)
+        nr, nq = len(ref_lists), len(qry_lists)
+        n = nr * nq
+        if kmer_space is None:
+            kmer_space = 4.0 ** k
+        bufs = []
+
+        def up(a):
+            b = DeviceBuffer.from_array(self, a)
+            bufs.append(b)
+            return b.ptr
+        try:
+            dR, drl = up(R), up(rl)
+            dQ, dql = (dR, drl) if qry_lists is ref_lists else (up(Q), up(ql))
+            drL = up(np.ascontiguousarray(ref_lengths, dtype=np.uint64))
+            dqL = drL if qry_lists is ref_lists and qry_lengths is ref_lengths else \
+                up(np.ascontiguousarray(qry_lengths, dtype=np.uint64))
+            outs = [DeviceBuffer(self, max(n, 1) * b) for b in (2, 2, 8, 8, 1)]
+            bufs += outs
+            _check(lib().fpm_dist_dev16(self.h, dR, drl, drL, w, nr, dQ, dql, dqL, w, nq,
+                                        8 if use64 else 4, sketch_size, k, kmer_space, max_dist,
+                                        max_pvalue, *[o.ptr for o in outs], None))
+            self.synchronize()
+            res = [o.to_array(t, n) for o, t in zip(outs, (np.uint16, np.uint16, np.float64,
+                                                           np.float64, np.uint8))]
+        finally:
+            for b in bufs:
+                b.free()
+        return {"numer": res[0], "denom": res[1], "distance": res[2], "pvalue": res[3],
+                "pass": res[4].astype(bool)}
 
     def fp_text(self, text, max_lines=1_000_000, seed=42, use64=False):
         """-fp file image -> per line: ID (offset, length), value count, hash, new-ID flag."""

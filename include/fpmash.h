@@ -200,6 +200,16 @@ int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                  uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
                  uint32_t *d_numer, uint32_t *d_denom, double *d_dist, double *d_pvalue,
                  uint8_t *d_pass, void *stream);
+/* fpm_dist_dev with u16 numer / denom cells (every count is <= sketch_size <= 65535): the
+ * same results in 4 bytes per pair instead of 8 (the grid's counts as SURVEY.md §8(b)
+ * sizes them); FPM_EINVAL when sketch_size > 65535. */
+int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                   const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                   const void *d_qry, const uint32_t *d_qry_len, const uint64_t *d_qry_length,
+                   uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes, uint32_t sketch_size,
+                   uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
+                   uint16_t *d_numer, uint16_t *d_denom, double *d_dist, double *d_pvalue,
+                   uint8_t *d_pass, void *stream);
 /* host-buffer convenience: compare + finalize */
 int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
              uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,

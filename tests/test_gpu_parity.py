@@ -286,6 +286,46 @@ def test_dist_self_symmetric_path(ctx, oracle):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 
 
+@pytest.mark.parametrize("mode", ["auto", "dense", "sparse"])
+def test_dist_dev16_matches_u32(ctx, oracle, mode):
+    """fpm_dist_dev16 (u16 numer / denom cells) gives the u32 path's results on the symmetric
+    self path, a query subset, unsorted -fp lists (literal walk) and the dense walk; the
+    counts equal the oracle's; sketch sizes above 65535 are refused."""
+    import fpmash
+    seqs, sk = _family_sketches(oracle, n_fam=6, members=8, seed=23)
+    sk = sk + [sk[0][:10], np.zeros(0, np.uint64), sk[3][:999]]
+    lengths = [len(x) for x in seqs] + [2000, 100, 2000]
+    ctx.set_dist_mode({"auto": fpmash.DIST_AUTO, "dense": fpmash.DIST_DENSE,
+                       "sparse": fpmash.DIST_SPARSE}[mode])
+    try:
+        for S in (1000, 300):
+            for qry, ql in ((sk, lengths), (sk[5:19], lengths[5:19])):
+                a = ctx.dist(sk, qry, S, ref_lengths=lengths, qry_lengths=ql)
+                b = ctx.dist16(sk, qry, S, ref_lengths=lengths, qry_lengths=ql)
+                for key in ("numer", "denom", "distance", "pvalue", "pass"):
+                    assert np.array_equal(a[key].astype(np.float64) if key in ("numer", "denom")
+                                          else a[key],
+                                          b[key].astype(np.float64) if key in ("numer", "denom")
+                                          else b[key]), (S, key)
+                nu, de, _di, _pv = oracle.dist_grid(sk, lengths, list(qry), list(ql), S, 21,
+                                                    4.0 ** 21)
+                assert np.array_equal(b["numer"], nu) and np.array_equal(b["denom"], de)
+        rng = np.random.default_rng(4)
+        base = rng.integers(0, 2 ** 32, size=800, dtype=np.uint64).astype(np.uint32)
+        lists = [base[rng.integers(0, 800, size=int(rng.integers(0, 1500)))] for _ in range(24)]
+        fl = [int(rng.integers(1, 9000)) for _ in lists]
+        a = ctx.dist(lists, lists, 1000, use64=False, k=1, kmer_space=10.0, ref_lengths=fl,
+                     qry_lengths=fl)
+        b = ctx.dist16(lists, lists, 1000, use64=False, k=1, kmer_space=10.0, ref_lengths=fl,
+                       qry_lengths=fl)
+        assert np.array_equal(a["numer"], b["numer"]) and np.array_equal(a["denom"], b["denom"])
+        np.testing.assert_array_equal(a["pvalue"], b["pvalue"])
+        with pytest.raises(fpmash.FpmError):
+            ctx.dist16(sk, sk, 70000, ref_lengths=lengths, qry_lengths=lengths)
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
 def _fp_texts():
     rng = np.random.default_rng(31)
     import fpmash.datagen as D
