@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=8.0,
                     help="target CPU seconds per baseline leg")
+    ap.add_argument("--no-fp-text", action="store_true", help="skip the -fp text parse leg")
     ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
@@ -65,7 +66,7 @@ def parse_args_for_test(**kw):
     """Defaults of parse() with overrides (tests)."""
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
-                           no_c3=True, no_c4=True, c4_n=50_000)
+                           no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -495,7 +496,7 @@ def main():
     sk_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in sk_names) / args.steps
     di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in di_names) / args.steps
 
-    fp_leg = fp_text_leg(ctx) if rank == 0 else None
+    fp_leg = fp_text_leg(ctx) if rank == 0 and not args.no_fp_text else None
     c3 = c3_leg(ctx, s=args.s) if rank == 0 and not args.no_c3 else None
     c4 = None
     if not args.no_c4:

@@ -64,6 +64,7 @@ def run_pass(counter, outdir: str, bench_args: list[str]) -> dict:
     if not files:
         raise SystemExit(f"no counter file under {outdir}")
     per_disp = {c: collections.defaultdict(float) for c in counters}   # (group, dispatch) -> v
+    disp = collections.defaultdict(set)                                 # (group, kernel) -> ids
     for row in csv.DictReader(open(files[0])):
         if row["Counter_Name"] not in per_disp:
             continue
@@ -71,7 +72,17 @@ def run_pass(counter, outdir: str, bench_args: list[str]) -> dict:
         if g is None:
             continue
         per_disp[row["Counter_Name"]][(g, row["Dispatch_Id"])] += float(row["Counter_Value"])
+        disp[(g, row["Kernel_Name"])].add(row["Dispatch_Id"])
+    # launches of a group = dispatches of its most frequent kernel (each of a group's
+    # kernels runs once per bench step: the index build's hist / scans / scatter / buckets)
+    launches = collections.defaultdict(int)
+    for (g, _k), ids in disp.items():
+        launches[g] = max(launches[g], len(ids))
+    LAUNCHES.update(launches)
     return per_disp[counter] if isinstance(counter, str) else per_disp
+
+
+LAUNCHES: dict = {}
 
 
 def per_launch(per_disp: dict, launches: dict) -> dict:
@@ -89,13 +100,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     a = ap.parse_args()
     os.makedirs(a.work, exist_ok=True)
-    bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline"]
+    # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
+    bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline",
+                  "--no-fp-text", "--no-c3", "--no-c4"]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.work, "fetch"), bench_args)
     write = run_pass("WRITE_SIZE", os.path.join(a.work, "write"), bench_args)
-    # every group runs once per bench step (warmup included): one "launch" of a group that
-    # is several kernels (the index build) is one step's worth of them
-    steps = a.steps + a.warmup
-    launches = {g: steps for (g, _d) in list(fetch) + list(write)}
+    # one "launch" of a group that is several kernels (the index build) is one step's worth
+    launches = dict(LAUNCHES)
     sq = run_pass(("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES",
                    "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"),
                   os.path.join(a.work, "sq"), bench_args)
