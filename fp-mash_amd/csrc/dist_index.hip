@@ -7,11 +7,12 @@
 // share at least one hash ("candidates") need the walk.  The candidates come from
 // an index over the reference lists:
 //   1. bucket index: every ref hash becomes one packed u32 entry (key fingerprint << rbits
-//      | ref id) in a bucket array grouped by the key's top `nbits` bits, with a
-//      directory dir[b] = first entry of bucket b.  Hashes are uniform (MurmurHash3), so
-//      this is a two-level counting sort with no global atomics: per-tile LDS histograms
-//      of the top 10 bits + one exclusive scan place every entry in its partition, then
-//      one workgroup per partition counting-sorts it by the next l2 bits in LDS and
+//      | ref id) in a bucket array grouped by the key's bucket (its value scaled to the
+//      indexed range [0, kmax]: bottom-s sketches only use the low part of the hash range),
+//      with a directory dir[b] = first entry of bucket b.  Hashes are uniform (MurmurHash3),
+//      so this is a two-level counting sort with no global atomics: per-tile LDS histograms
+//      of the top 10 bucket bits + one exclusive scan place every entry in its partition,
+//      then one workgroup per partition counting-sorts it by the next l2 bits in LDS and
 //      writes its slice of the directory;
 //   2. one workgroup per query row looks up the bucket of each of its hashes; each wave
 //      flattens the buckets of 64 hashes into one event range and reads it coalesced,
@@ -24,6 +25,8 @@
 // host falls back to walking every pair.
 #include "fpm_device.hpp"
 #include "fpm_kernels.hpp"
+
+#include <algorithm>
 
 namespace fpm {
 
@@ -44,12 +47,30 @@ __device__ __forceinline__ uint64_t norm_key(uint64_t h, uint32_t hash_bytes)
     return hash_bytes == 8 ? h : (h << 32);
 }
 
-// u32 entry = fingerprint << rbits | ref id, fingerprint = the fbits key bits just below the
-// bucket bits.  A fingerprint collision only adds a candidate pair that shares no hash; the
-// exact candidate kernels then produce the same (0, min(S, la+lb)) the probe already wrote.
-__device__ __forceinline__ uint32_t key_fp(uint64_t K, const IdxGeom &g)
+// Bucket of a (normalized) key: floor(K * NB / (kmax + 1)) with kmax = the largest indexed
+// key (from the rows' last entries, idx_kmax_kernel), clamped to NB - 1.  Bottom-s sketches
+// only hold values up to about s / (distinct k-mers) of the hash range (C2: 0.54 * 2^64), so
+// plain top bits would leave half the buckets empty and double the others (8 % more posting
+// events, and the fused level 1's fixed partition slabs would overflow).  mult = NB * 2^64 /
+// (kmax + 1) is computed by every kernel from the same kmax with the same double ops.
+__device__ __forceinline__ uint64_t idx_mult(const IdxGeom &g)
 {
-    return (uint32_t)(K >> (64 - g.nbits - g.fbits)) & ((1u << g.fbits) - 1);
+    const double q = ldexp(1.0, 64 + (int)g.nbits) / ((double)*g.kmax + 1.0);
+    return q >= 18446744073709551615.0 ? ~0ULL : (uint64_t)q;
+}
+__device__ __forceinline__ uint32_t bucket_of(uint64_t K, const IdxGeom &g, uint64_t mult)
+{
+    const uint64_t b = __umul64hi(K, mult);
+    const uint64_t top = (1ULL << g.nbits) - 1;
+    return (uint32_t)(b < top ? b : top);
+}
+// u32 entry = fingerprint << rbits | ref id, fingerprint = the top fbits of the low half of
+// K * mult (for a power-of-two range: the key bits just below the bucket bits).  A fingerprint
+// collision only adds a candidate pair that shares no hash; the exact candidate kernels then
+// produce the same (0, min(S, la+lb)) the probe already wrote.
+__device__ __forceinline__ uint32_t key_fp(uint64_t K, const IdxGeom &g, uint64_t mult)
+{
+    return (uint32_t)((K * mult) >> (64 - g.fbits));
 }
 
 // Tiles of kIdxTile matrix cells, 1024 threads each (16 cells per thread, 4 loads in
@@ -64,14 +85,31 @@ __device__ __forceinline__ uint32_t row_of(uint32_t e, uint32_t stride, uint64_t
     return stride == 1 ? e : (uint32_t)__umul64hi((uint64_t)e, magic);
 }
 
+// ---- 0. the largest normalized key among the rows' last entries (the maximum for sorted
+// rows; unsorted rows may hold larger keys, which bucket_of clamps into the last bucket)
+__global__ __launch_bounds__(256) void idx_kmax_kernel(
+    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
+    uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax)
+{
+    uint64_t mx = 0;
+    for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < n_ref; r += gridDim.x * 256) {
+        const uint32_t l = ref_len[r];
+        if (l) mx = max(mx, norm_key(load_key(ref, hash_bytes, (uint64_t)r * stride + l - 1), hash_bytes));
+    }
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor((unsigned long long)mx, d, 64));
+    if ((threadIdx.x & 63) == 0 && mx) atomicMax(kmax, (unsigned long long)mx);
+}
+
 // ---- 1a. level-1 histogram: LDS counters per partition; also flags unsorted /
 // duplicate-carrying rows (the next cell's key is the next lane's, lane 63 loads it)
 __global__ __launch_bounds__(kIdxThreads) void idx_part_hist_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
     uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles,
-    uint32_t *__restrict__ tile_hist, uint32_t *__restrict__ unsorted)
+    uint32_t *__restrict__ tile_hist, uint32_t *__restrict__ unsorted, IdxGeom g)
 {
     __shared__ uint32_t hist[kParts];
+    const uint64_t mult = idx_mult(g);
     for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) hist[p] = 0;
     __syncthreads();
     const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
@@ -94,7 +132,7 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_hist_kernel(
             if (lane == 63 && nx[u])
                 nk = load_key(ref, hash_bytes, (uint64_t)e0 + c0 + u * kIdxThreads + threadIdx.x + 1);
             uns |= nx[u] && !(key[u] < nk);
-            if (v[u]) atomicAdd(&hist[norm_key(key[u], hash_bytes) >> (64 - kIdxL1)], 1u);
+            if (v[u]) atomicAdd(&hist[bucket_of(norm_key(key[u], hash_bytes), g, mult) >> g.l2], 1u);
         }
     }
     if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
@@ -106,10 +144,10 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_hist_kernel(
 // ---- 1b. level-1 scatter into partitions.  One u64 per entry: the key bits below the
 // partition bits that level 2 needs (l2 sub-bucket bits, then the fbits fingerprint) over
 // the ref id, i.e. (sub << 32) | final u32 entry, since fbits + rbits = 32.
-__device__ __forceinline__ uint64_t pack_l1(uint64_t K, uint32_t r, const IdxGeom &g)
+__device__ __forceinline__ uint64_t pack_l1(uint64_t K, uint32_t r, const IdxGeom &g, uint64_t mult)
 {
-    const uint64_t mid = (K << kIdxL1) >> (64 - (g.l2 + g.fbits));
-    return (mid << g.rbits) | r;
+    const uint32_t sub = bucket_of(K, g, mult) & ((1u << g.l2) - 1);
+    return ((uint64_t)sub << 32) | ((uint64_t)key_fp(K, g, mult) << g.rbits) | r;
 }
 
 __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
@@ -118,6 +156,7 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint64_t *__restrict__ tent)
 {
     __shared__ uint32_t cur[kParts];
+    const uint64_t mult = idx_mult(g);
     for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads)
         cur[p] = tile_off[(uint64_t)p * ntiles + blockIdx.x];
     __syncthreads();
@@ -137,25 +176,107 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
 #pragma unroll
         for (int u = 0; u < kIdxU; u++)
             if (v[u]) {
-                const uint32_t pos = atomicAdd(&cur[K[u] >> (64 - kIdxL1)], 1u);
-                tent[pos] = pack_l1(K[u], rr[u], g);
+                const uint32_t pos = atomicAdd(&cur[bucket_of(K[u], g, mult) >> g.l2], 1u);
+                tent[pos] = pack_l1(K[u], rr[u], g, mult);
             }
     }
 }
 
+// ---- 1ab fused. level 1 in one pass: each tile keeps its 16 keys per thread in registers,
+// builds the LDS histogram of their top 10 bits, reserves its run in every partition with
+// one global atomic per non-empty partition (partition p owns the fixed slab
+// tent[p * cap, (p + 1) * cap): uniform hashes fill each to E / 1024 +- a few sigma, cap
+// leaves 25 % + 256), then scatters the keys into their runs.  No separate histogram read
+// of the reference matrix and no exclusive scan.  A partition that would overflow its slab
+// (skewed 32-bit values) raises *overflow and the host rebuilds with the exact two-pass
+// scatter (idx_part_hist + exscan + idx_part_scatter).
+__global__ __launch_bounds__(kIdxThreads) void idx_part_fused_kernel(
+    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
+    uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t cap,
+    uint32_t *__restrict__ part_cnt, uint64_t *__restrict__ tent, uint32_t *__restrict__ unsorted,
+    uint32_t *__restrict__ overflow)
+{
+    __shared__ uint32_t hist[kParts];
+    const uint64_t mult = idx_mult(g);
+    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) hist[p] = 0;
+    __syncthreads();
+    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
+    constexpr int kR = kIdxTile / kIdxThreads;            // 16 cells per thread, all in flight
+    uint64_t K[kR];
+    uint32_t rr[kR];
+    bool v[kR], nx[kR];
+#pragma unroll
+    for (int u = 0; u < kR; u++) {
+        const uint32_t e = e0 + u * kIdxThreads + threadIdx.x;
+        const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+        const uint32_t la = e < n ? ref_len[r] : 0;
+        v[u] = e < n && i < la;
+        nx[u] = v[u] && i + 1 < la;
+        rr[u] = r;
+        K[u] = v[u] ? load_key(ref, hash_bytes, e) : 0;
+    }
+    bool uns = false;
+#pragma unroll
+    for (int u = 0; u < kR; u++) {
+        uint64_t nk = __shfl_down((unsigned long long)K[u], 1, 64);
+        if (lane == 63 && nx[u])
+            nk = load_key(ref, hash_bytes, (uint64_t)e0 + u * kIdxThreads + threadIdx.x + 1);
+        uns |= nx[u] && !(K[u] < nk);
+        K[u] = norm_key(K[u], hash_bytes);
+        if (v[u]) atomicAdd(&hist[bucket_of(K[u], g, mult) >> g.l2], 1u);
+    }
+    if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) {
+        const uint32_t c = hist[p];
+        const uint32_t base = c ? atomicAdd(&part_cnt[p], c) : 0u;
+        if (base + c > cap) atomicOr(overflow, 1u);
+        hist[p] = base;                                   // becomes the tile's cursor
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kR; u++)
+        if (v[u]) {
+            const uint32_t p = bucket_of(K[u], g, mult) >> g.l2;
+            const uint32_t pos = atomicAdd(&hist[p], 1u);
+            if (pos < cap) tent[(uint64_t)p * cap + pos] = pack_l1(K[u], rr[u], g, mult);
+        }
+}
+
 // ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits
 constexpr int kBucketThreads = 512;
+// Partition p's entries: tent[s0, s1) of the exact two-pass layout (tile_off), or, with
+// part_cnt (the fused level 1), the first part_cnt[p] entries of the slab tent[p * cap, ...),
+// written to entries[base + ...] with base = the sum of the earlier partitions' counts.
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tent, uint32_t ntiles,
-    const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
+    const uint32_t *__restrict__ tile_off, const uint32_t *__restrict__ part_cnt, uint32_t cap,
+    IdxGeom g, uint32_t *__restrict__ dir,
     uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
     __shared__ uint32_t wsum[kBucketThreads / 64];
     __shared__ unsigned long long wsq[kBucketThreads / 64];
+    __shared__ uint32_t s_base;
     const uint32_t p = blockIdx.x;
-    const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
-    const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
+    uint32_t s0, s1;
+    int64_t shift = 0;                           // tent index = entry index + shift
+    if (part_cnt) {
+        uint32_t part = 0;
+        for (uint32_t q = threadIdx.x; q < p; q += kBucketThreads) part += part_cnt[q];
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) part += __shfl_down(part, d, 64);
+        if (threadIdx.x == 0) s_base = 0;
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0 && part) atomicAdd(&s_base, part);
+        __syncthreads();
+        s0 = s_base;
+        s1 = s0 + part_cnt[p];
+        shift = (int64_t)p * cap - (int64_t)s0;
+    } else {
+        s0 = tile_off[(uint64_t)p * ntiles];
+        s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
+    }
     const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
@@ -166,7 +287,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tent[e] : 0;
+            K[u] = e < s1 ? tent[(uint64_t)((int64_t)e + shift)] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
@@ -214,7 +335,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tent[e] : 0;
+            K[u] = e < s1 ? tent[(uint64_t)((int64_t)e + shift)] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
@@ -312,7 +433,7 @@ __global__ __launch_bounds__(256) void probe_count_kernel(
         const uint32_t lq = qry_len[q];
         if (j < lq) {
             const uint64_t key = load_key(qry, hash_bytes, e);
-            const uint64_t b = norm_key(key, hash_bytes) >> (64 - g.nbits);
+            const uint64_t b = bucket_of(norm_key(key, hash_bytes), g, idx_mult(g));
             ev = dir[b + 1] - dir[b];
             if (j + 1 < lq && !(key < load_key(qry, hash_bytes, e + 1))) uns = 1;
         }
@@ -360,6 +481,7 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     __shared__ uint8_t w_own[4][kWin];
     const uint32_t q = xcd_row(blockIdx.x, n_qry);   // XCD-contiguous rows: shared buckets in L2
     if (q >= n_qry) return;
+    const uint64_t mult = idx_mult(g);
     const uint32_t r0 = blockIdx.y * chunk_refs;
     const uint32_t r1 = min(n_ref, r0 + chunk_refs);
     // symmetric self-comparison: only refs r <= q become candidates of row q
@@ -385,11 +507,11 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
         for (int bi = 0; bi < kB; bi++) {
             const uint32_t j = jb + 256 * bi + lane;
             const uint64_t K = j < lq ? norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes) : 0;
-            const uint64_t b = K >> (64 - g.nbits);
+            const uint64_t b = bucket_of(K, g, mult);
             const uint32_t d0 = j < lq ? dir[b] : 0u, d1 = j < lq ? dir[b + 1] : 0u;
             st_b[bi] = d0;
             cnt_b[bi] = self_set && d1 - d0 == 1 ? 0u : d1 - d0;
-            tgt_b[bi] = key_fp(K, g);
+            tgt_b[bi] = key_fp(K, g, mult);
         }
 #pragma unroll
       for (int bi = 0; bi < kB; bi++) {
@@ -511,26 +633,47 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
     return hipGetLastError();
 }
 
+uint32_t idx_slab_cap(uint64_t E)
+{
+    // the scaled buckets spread uniform keys evenly; clumps of equal hashes (a family's
+    // shared k-mers) add a few hundred per partition at the bench's E = 1e7
+    const uint64_t mean = (E + kParts - 1) / kParts;
+    return (uint32_t)std::min<uint64_t>(mean + mean * 2 / 5 + 1024, 0xFFFFFFFFull);
+}
+
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
-                            unsigned long long *self_events, hipStream_t st)
+                            unsigned long long *self_events, uint32_t *part_cnt, uint32_t cap,
+                            uint32_t *overflow, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
-    hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
-                       unsorted);
-    const uint64_t nh = (uint64_t)kParts * ntiles;
-    if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
-        return e;
-    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
-                       (const uint32_t *)tile_off, g, tent);
+    // *g.kmax zeroed by the caller
+    hipLaunchKernelGGL(idx_kmax_kernel, dim3(std::min<uint32_t>((n_ref + 255) / 256, 256)),
+                       dim3(256), 0, st, d_ref, d_ref_len, stride, n_ref, hash_bytes,
+                       (unsigned long long *)g.kmax);
+    if (part_cnt) {
+        // fused level 1 into fixed partition slabs (part_cnt and *overflow zeroed by the caller)
+        hipLaunchKernelGGL(idx_part_fused_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, g, cap,
+                           part_cnt, tent, unsorted, overflow);
+    } else {
+        hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
+                           tile_hist, unsorted, g);
+        const uint64_t nh = (uint64_t)kParts * ntiles;
+        if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
+            return e;
+        hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
+                           (const uint32_t *)tile_off, g, tent);
+    }
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles,
-                       (const uint32_t *)tile_off, g, dir, entries, self_events);
+                       (const uint32_t *)tile_off, (const uint32_t *)part_cnt, cap, g, dir,
+                       entries, self_events);
     if (self_events) hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, self_events);
     return hipGetLastError();
 }
