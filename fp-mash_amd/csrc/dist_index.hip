@@ -51,8 +51,8 @@ __device__ __forceinline__ uint64_t norm_key(uint64_t h, uint32_t hash_bytes)
 // key (from the rows' last entries, idx_kmax_kernel), clamped to NB - 1.  Bottom-s sketches
 // only hold values up to about s / (distinct k-mers) of the hash range (C2: 0.54 * 2^64), so
 // plain top bits would leave half the buckets empty and double the others (8 % more posting
-// events, and the fused level 1's fixed partition slabs would overflow).  mult = NB * 2^64 /
-// (kmax + 1) is computed by every kernel from the same kmax with the same double ops.
+// events).  mult = NB * 2^64 / (kmax + 1) is computed by every kernel from the same kmax with
+// the same double ops.
 __device__ __forceinline__ uint64_t idx_mult(const IdxGeom &g)
 {
     const double q = ldexp(1.0, 64 + (int)g.nbits) / ((double)*g.kmax + 1.0);
@@ -182,101 +182,19 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     }
 }
 
-// ---- 1ab fused. level 1 in one pass: each tile keeps its 16 keys per thread in registers,
-// builds the LDS histogram of their top 10 bits, reserves its run in every partition with
-// one global atomic per non-empty partition (partition p owns the fixed slab
-// tent[p * cap, (p + 1) * cap): uniform hashes fill each to E / 1024 +- a few sigma, cap
-// leaves 25 % + 256), then scatters the keys into their runs.  No separate histogram read
-// of the reference matrix and no exclusive scan.  A partition that would overflow its slab
-// (skewed 32-bit values) raises *overflow and the host rebuilds with the exact two-pass
-// scatter (idx_part_hist + exscan + idx_part_scatter).
-__global__ __launch_bounds__(kIdxThreads) void idx_part_fused_kernel(
-    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
-    uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t cap,
-    uint32_t *__restrict__ part_cnt, uint64_t *__restrict__ tent, uint32_t *__restrict__ unsorted,
-    uint32_t *__restrict__ overflow)
-{
-    __shared__ uint32_t hist[kParts];
-    const uint64_t mult = idx_mult(g);
-    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) hist[p] = 0;
-    __syncthreads();
-    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
-    constexpr int kR = kIdxTile / kIdxThreads;            // 16 cells per thread, all in flight
-    uint64_t K[kR];
-    uint32_t rr[kR];
-    bool v[kR], nx[kR];
-#pragma unroll
-    for (int u = 0; u < kR; u++) {
-        const uint32_t e = e0 + u * kIdxThreads + threadIdx.x;
-        const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
-        const uint32_t la = e < n ? ref_len[r] : 0;
-        v[u] = e < n && i < la;
-        nx[u] = v[u] && i + 1 < la;
-        rr[u] = r;
-        K[u] = v[u] ? load_key(ref, hash_bytes, e) : 0;
-    }
-    bool uns = false;
-#pragma unroll
-    for (int u = 0; u < kR; u++) {
-        uint64_t nk = __shfl_down((unsigned long long)K[u], 1, 64);
-        if (lane == 63 && nx[u])
-            nk = load_key(ref, hash_bytes, (uint64_t)e0 + u * kIdxThreads + threadIdx.x + 1);
-        uns |= nx[u] && !(K[u] < nk);
-        K[u] = norm_key(K[u], hash_bytes);
-        if (v[u]) atomicAdd(&hist[bucket_of(K[u], g, mult) >> g.l2], 1u);
-    }
-    if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
-    __syncthreads();
-    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) {
-        const uint32_t c = hist[p];
-        const uint32_t base = c ? atomicAdd(&part_cnt[p], c) : 0u;
-        if (base + c > cap) atomicOr(overflow, 1u);
-        hist[p] = base;                                   // becomes the tile's cursor
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kR; u++)
-        if (v[u]) {
-            const uint32_t p = bucket_of(K[u], g, mult) >> g.l2;
-            const uint32_t pos = atomicAdd(&hist[p], 1u);
-            if (pos < cap) tent[(uint64_t)p * cap + pos] = pack_l1(K[u], rr[u], g, mult);
-        }
-}
-
 // ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits
 constexpr int kBucketThreads = 512;
-// Partition p's entries: tent[s0, s1) of the exact two-pass layout (tile_off), or, with
-// part_cnt (the fused level 1), the first part_cnt[p] entries of the slab tent[p * cap, ...),
-// written to entries[base + ...] with base = the sum of the earlier partitions' counts.
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tent, uint32_t ntiles,
-    const uint32_t *__restrict__ tile_off, const uint32_t *__restrict__ part_cnt, uint32_t cap,
-    IdxGeom g, uint32_t *__restrict__ dir,
+    const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
     uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
     __shared__ uint32_t wsum[kBucketThreads / 64];
     __shared__ unsigned long long wsq[kBucketThreads / 64];
-    __shared__ uint32_t s_base;
     const uint32_t p = blockIdx.x;
-    uint32_t s0, s1;
-    int64_t shift = 0;                           // tent index = entry index + shift
-    if (part_cnt) {
-        uint32_t part = 0;
-        for (uint32_t q = threadIdx.x; q < p; q += kBucketThreads) part += part_cnt[q];
-#pragma unroll
-        for (int d = 32; d > 0; d >>= 1) part += __shfl_down(part, d, 64);
-        if (threadIdx.x == 0) s_base = 0;
-        __syncthreads();
-        if ((threadIdx.x & 63) == 0 && part) atomicAdd(&s_base, part);
-        __syncthreads();
-        s0 = s_base;
-        s1 = s0 + part_cnt[p];
-        shift = (int64_t)p * cap - (int64_t)s0;
-    } else {
-        s0 = tile_off[(uint64_t)p * ntiles];
-        s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
-    }
+    const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
+    const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
     const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
@@ -287,7 +205,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tent[(uint64_t)((int64_t)e + shift)] : 0;
+            K[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
@@ -335,7 +253,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tent[(uint64_t)((int64_t)e + shift)] : 0;
+            K[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
@@ -633,20 +551,11 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
     return hipGetLastError();
 }
 
-uint32_t idx_slab_cap(uint64_t E)
-{
-    // the scaled buckets spread uniform keys evenly; clumps of equal hashes (a family's
-    // shared k-mers) add a few hundred per partition at the bench's E = 1e7
-    const uint64_t mean = (E + kParts - 1) / kParts;
-    return (uint32_t)std::min<uint64_t>(mean + mean * 2 / 5 + 1024, 0xFFFFFFFFull);
-}
-
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
-                            unsigned long long *self_events, uint32_t *part_cnt, uint32_t cap,
-                            uint32_t *overflow, hipStream_t st)
+                            unsigned long long *self_events, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
@@ -654,26 +563,18 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     hipLaunchKernelGGL(idx_kmax_kernel, dim3(std::min<uint32_t>((n_ref + 255) / 256, 256)),
                        dim3(256), 0, st, d_ref, d_ref_len, stride, n_ref, hash_bytes,
                        (unsigned long long *)g.kmax);
-    if (part_cnt) {
-        // fused level 1 into fixed partition slabs (part_cnt and *overflow zeroed by the caller)
-        hipLaunchKernelGGL(idx_part_fused_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, g, cap,
-                           part_cnt, tent, unsorted, overflow);
-    } else {
-        hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
-                           tile_hist, unsorted, g);
-        const uint64_t nh = (uint64_t)kParts * ntiles;
-        if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
-            return e;
-        hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                           d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
-                           (const uint32_t *)tile_off, g, tent);
-    }
+    hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
+                       unsorted, g);
+    const uint64_t nh = (uint64_t)kParts * ntiles;
+    if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
+        return e;
+    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
+                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
+                       (const uint32_t *)tile_off, g, tent);
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles,
-                       (const uint32_t *)tile_off, (const uint32_t *)part_cnt, cap, g, dir,
-                       entries, self_events);
+                       (const uint32_t *)tile_off, g, dir, entries, self_events);
     if (self_events) hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, self_events);
     return hipGetLastError();
 }

@@ -838,14 +838,6 @@ void fpm_fp_text_free(fpm_fptext *j)
 
 }  // extern "C"
 
-// the one-pass level 1 (global atomics reserving every tile's run in fixed partition slabs)
-// measured slower than histogram + scan + scatter: 147 us against 106 us at E = 1e7 (611
-// atomics per partition counter serialise); kept behind this switch for other shapes
-#ifndef FPM_IDX_FUSED
-#define FPM_IDX_FUSED 0
-#endif
-constexpr int kIdxExactFirst = FPM_IDX_FUSED ? 0 : 1;
-
 // distance / p-value outputs of fpm_dist_dev, handed to compare_impl so the sparse path
 // can finalize in place: the probe writes every cell's no-shared-hash values and a
 // candidate kernel rewrites the candidates (no dense pass re-reading numer / denom)
@@ -905,44 +897,34 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         void *tile_hist, *tile_off, *tent, *dir, *entries, *scan_s, *ctr;
         HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
         HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
-        const uint32_t slab = idx_slab_cap(E);
-        HIP_TRY(scratch(ctx, 2, std::max<uint64_t>(E, (uint64_t)slab << kIdxL1) * 8, &tent));
+        HIP_TRY(scratch(ctx, 2, E * 8, &tent));
         HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir));
         HIP_TRY(scratch(ctx, 5, E * 4, &entries));
         HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
-        constexpr size_t kCtr = 72 * 8 + (4u << kIdxL1);
-        HIP_TRY(scratch(ctx, 7, kCtr, &ctr));
+        HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
         if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
         // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
-        // [67] slab overflow flag, [68] largest indexed key; then the fused level 1's 1024
-        // partition counts
+        // [68] the largest indexed key (the bucket scale)
         unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
-        uint32_t *unsorted = (uint32_t *)(events + 66), *overflow = (uint32_t *)(events + 67);
-        uint32_t *part_cnt = (uint32_t *)(events + 72);
-        geom.kmax = events + 68;                         // [68] the largest indexed key
-        // the fused one-pass level 1 (fixed partition slabs) first; a slab overflow (skewed
-        // 32-bit values) rebuilds with the exact two-pass scatter
-        for (int exact = kIdxExactFirst; exact < 2; exact++) {
-            {
-                TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                HIP_TRY(hipMemsetAsync(ctr, 0, kCtr, st));
-                // one set against itself: the query side is the ref side, so its sortedness
-                // is the ref flag and its posting events are sum_b |b|^2 from the bucket pass
-                HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
-                                         (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                         (uint32_t *)scan_s, (uint64_t *)tent,
-                                         (uint32_t *)dir, (uint32_t *)entries, unsorted,
-                                         self_set ? events : nullptr,
-                                         exact ? nullptr : part_cnt, slab, overflow, st));
-                if (!self_set)
-                    HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                               geom, (const uint32_t *)dir, events, unsorted, st));
-                tl.done();
-            }
-            HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 68 * 8, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
-            if (((const uint32_t *)(ctx->host_counters + 67))[0] == 0) break;
+        uint32_t *unsorted = (uint32_t *)(events + 66);
+        geom.kmax = events + 68;
+        {
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+            // one set against itself: the query side is the ref side, so its sortedness is
+            // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
+            HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
+                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                     (uint32_t *)scan_s, (uint64_t *)tent,
+                                     (uint32_t *)dir, (uint32_t *)entries, unsorted,
+                                     self_set ? events : nullptr, st));
+            if (!self_set)
+                HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
+                                           (const uint32_t *)dir, events, unsorted, st));
+            tl.done();
         }
+        HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
         const uint64_t ev = ctx->host_counters[0];
         const bool all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
         ctx->last_events = ev;

@@ -89,11 +89,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
-                            unsigned long long *self_events, uint32_t *part_cnt, uint32_t cap,
-                            uint32_t *overflow, hipStream_t st);
-// part_cnt != nullptr: the fused level 1 (one pass, fixed slabs of `cap` entries per
-// partition, tent sized kParts * cap); *overflow = 1 if a partition outgrew its slab
-uint32_t idx_slab_cap(uint64_t E);
+                            unsigned long long *self_events, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
