@@ -287,6 +287,16 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
     dist_ms = (time.perf_counter() - t0) / reps * 1e3
     st = ctx.last_dist_stats()
     numer = outs[0].to_array(np.uint16, np_)
+    denom = outs[1].to_array(np.uint16, np_)
+    # full-size parity of the index path: the same grid by the dense literal walk of every pair
+    same_as_dense = None
+    if st["sparse"]:
+        ctx.set_dist_mode(fpmash.DIST_DENSE)
+        run()
+        ctx.synchronize()
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+        same_as_dense = bool(np.array_equal(numer, outs[0].to_array(np.uint16, np_)) and
+                             np.array_equal(denom, outs[1].to_array(np.uint16, np_)))
     for b in [d_R, d_rl, d_rL] + outs:
         b.free()
     return {"config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
@@ -299,7 +309,8 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
             "step_device_ms": parse_ms + dist_ms,
             "dist_path": fpmash.DIST_PATHS[int(st["sparse"])],
             "posting_events": st["events"], "candidate_pairs": st["candidates"],
-            "pairs_sharing_a_hash": int((numer > 0).sum())}
+            "pairs_sharing_a_hash": int((numer > 0).sum()),
+            "counts_equal_dense_walk": same_as_dense}
 
 
 def c4_leg(ctx, grp, ws, rank, n=50_000, members=100, s=1000, k=21, steps=3, warmup=1):

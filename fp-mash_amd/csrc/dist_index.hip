@@ -387,7 +387,8 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
     uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, C *__restrict__ numer,
     C *__restrict__ denom, uint64_t *__restrict__ cand,
-    unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg)
+    unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg,
+    const uint32_t *__restrict__ qry_it_len)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
@@ -407,7 +408,10 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     const uint32_t nwords = (r1 - r0 + 31) / 32;
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) rowbits[w] = 0;
     __syncthreads();
+    // lq: the row's list length (the defaults); lit: the hashes probed, which differ from lq
+    // when the probed rows are the deduplicated copies of unsorted lists (dedup_rows_kernel)
     const uint32_t lq = qry_len[q];
+    const uint32_t lit = qry_it_len ? qry_it_len[q] : lq;
     // one set against itself: row q's own entry sits in the bucket of each of its hashes,
     // so a bucket of one entry holds only that entry.  Such buckets (the unique hashes, most
     // of a sketch) are not read; the pair (q, q) they would mark is set here.
@@ -419,21 +423,21 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
     // loaded together (their global loads overlap) before the batches are expanded
     constexpr int kB = 4;
-    for (uint32_t jb = wave * 64; jb < lq; jb += 256 * kB) {
+    for (uint32_t jb = wave * 64; jb < lit; jb += 256 * kB) {
         uint32_t st_b[kB], cnt_b[kB], tgt_b[kB];
 #pragma unroll
         for (int bi = 0; bi < kB; bi++) {
             const uint32_t j = jb + 256 * bi + lane;
-            const uint64_t K = j < lq ? norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes) : 0;
+            const uint64_t K = j < lit ? norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes) : 0;
             const uint64_t b = bucket_of(K, g, mult);
-            const uint32_t d0 = j < lq ? dir[b] : 0u, d1 = j < lq ? dir[b + 1] : 0u;
+            const uint32_t d0 = j < lit ? dir[b] : 0u, d1 = j < lit ? dir[b + 1] : 0u;
             st_b[bi] = d0;
             cnt_b[bi] = self_set && d1 - d0 == 1 ? 0u : d1 - d0;
             tgt_b[bi] = key_fp(K, g, mult);
         }
 #pragma unroll
       for (int bi = 0; bi < kB; bi++) {
-        if (jb + 256 * bi >= lq) break;                   // wave-uniform
+        if (jb + 256 * bi >= lit) break;                  // wave-uniform
         const uint32_t st = st_b[bi], cnt = cnt_b[bi], tgt = tgt_b[bi];
         uint32_t inc = cnt;
 #pragma unroll
@@ -538,6 +542,93 @@ __global__ __launch_bounds__(256) void probe_rows_kernel(
     }
 }
 
+// ---- unsorted (-fp) lists: the posting events of the raw lists are sum_v n_v^2 over
+// occurrences, and CFL k-finger lists repeat a few values hundreds of times per list (the
+// line "100" is ~1 % of all lines: C3 gives 2.9e10 events, more than walking every pair).
+// Whether a pair shares a value does not depend on order or multiplicity, and the literal
+// walk (CommandDistance.cpp:376-400) only ever reads A[i] with i < min(la, S) (i <= steps <
+// S), so the index and the probe run on each row's first min(len, S) entries sorted and
+// deduplicated; the candidates they find are then walked on the original lists.
+// One workgroup per row: bitonic sort of NP (pow2 >= the row cap) keys in LDS, pads = ~0
+// (a real ~0 sorts among the pads, but only positions < m are read), then a block scan
+// of the first-of-run flags compacts the distinct values into out[row * out_stride ...].
+template <typename H, int NP>
+__global__ __launch_bounds__(256) void dedup_rows_kernel(
+    const H *__restrict__ in, const uint32_t *__restrict__ in_len, uint64_t in_stride,
+    uint32_t S, H *__restrict__ out, uint32_t *__restrict__ out_len, uint64_t out_stride)
+{
+    __shared__ H key[NP];
+    __shared__ uint32_t wsum[4];
+    constexpr int PT = NP / 256;          // elements per thread in the compaction
+    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    const uint32_t m = min(min(in_len[row], S), (uint32_t)out_stride);
+    const H *src = in + (uint64_t)row * in_stride;
+    for (uint32_t i = t; i < NP; i += 256) key[i] = i < m ? src[i] : (H)~(H)0;
+    __syncthreads();
+    for (uint32_t k = 2; k <= NP; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < NP; i += 256) {
+                const uint32_t x = i ^ j;
+                if (x > i) {
+                    const H a = key[i], b = key[x];
+                    if ((a > b) == ((i & k) == 0)) { key[i] = b; key[x] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    H v[PT];
+    uint32_t f = 0, cnt = 0;
+#pragma unroll
+    for (int u = 0; u < PT; u++) {
+        const uint32_t i = t * PT + u;
+        v[u] = key[i];
+        const bool first = i < m && (i == 0 || key[i - 1] != v[u]);
+        f |= (first ? 1u : 0u) << u;
+        cnt += first ? 1u : 0u;
+    }
+    const uint32_t lane = t & 63, wave = t >> 6;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t pos = x - cnt, tot = 0;
+    for (uint32_t w = 0; w < 4; w++) { if (w < wave) pos += wsum[w]; tot += wsum[w]; }
+    H *dst = out + (uint64_t)row * out_stride;
+#pragma unroll
+    for (int u = 0; u < PT; u++)
+        if (f >> u & 1u) dst[pos++] = v[u];
+    if (t == 0) out_len[row] = tot;
+}
+
+template <typename H>
+static hipError_t dedup_rows_h(const void *in, const uint32_t *in_len, uint64_t in_stride,
+                               uint32_t n, uint32_t S, void *out, uint32_t *out_len,
+                               uint64_t out_stride, hipStream_t st)
+{
+#define FPM_DEDUP(NP)                                                                         \
+    hipLaunchKernelGGL((dedup_rows_kernel<H, NP>), dim3(n), dim3(256), 0, st, (const H *)in,  \
+                       in_len, in_stride, S, (H *)out, out_len, out_stride)
+    if (out_stride <= 256) FPM_DEDUP(256);
+    else if (out_stride <= 512) FPM_DEDUP(512);
+    else if (out_stride <= 1024) FPM_DEDUP(1024);
+    else if (out_stride <= 2048) FPM_DEDUP(2048);
+    else FPM_DEDUP(4096);
+#undef FPM_DEDUP
+    return hipGetLastError();
+}
+
+hipError_t launch_dedup_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
+                             uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
+                             uint32_t *out_len, uint64_t out_stride, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    if (out_stride > kDedupMax) return hipErrorInvalidValue;
+    return hash_bytes == 8
+               ? dedup_rows_h<uint64_t>(in, in_len, in_stride, n, S, out, out_len, out_stride, st)
+               : dedup_rows_h<uint32_t>(in, in_len, in_stride, n, S, out, out_len, out_stride, st);
+}
+
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock + 1; }
 
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
@@ -596,7 +687,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
                              bool self_set, Counts cnt, uint64_t *cand,
-                             unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st)
+                             unsigned long long *n_cand, uint64_t *row_seg,
+                             const uint32_t *d_qry_it_len, hipStream_t st)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -612,7 +704,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
     hipLaunchKernelGGL(probe_rows_kernel<C>, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,  \
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref, \
                        d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
-                       (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg)
+                       (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg, \
+                       d_qry_it_len)
     if (cnt.c16) FPM_PROBE(uint16_t);
     else FPM_PROBE(uint32_t);
 #undef FPM_PROBE

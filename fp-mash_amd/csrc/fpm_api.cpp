@@ -60,7 +60,7 @@ struct fpm_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
     // grow-only device scratch, one buffer per named slot (no allocation in steady state)
     struct Slot { void *p = nullptr; size_t bytes = 0; };
-    Slot scratch[12];
+    Slot scratch[16];
     unsigned long long *host_counters = nullptr;   // pinned, for the events read-back
     int dist_mode = FPM_DIST_AUTO;
     int last_sparse = 0;
@@ -873,8 +873,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (E == 0) try_sparse = false;
     // bucket index geometry: ~2.4 entries per bucket (2^nbits >= E/4, at most 2^24 buckets);
     // entries are u32 (ref id in rbits, key fingerprint in the other >= 8 bits)
-    IdxGeom geom{};
-    {
+    // bucket index geometry for E entries over n_ref rows
+    const auto make_geom = [n_ref](uint64_t E) {
+        IdxGeom geom{};
         uint32_t rbits = 1, lg = 1;
         while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
         while (lg < 40 && (1ULL << lg) < E) lg++;
@@ -886,8 +887,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         geom.rbits = rbits;
         geom.fbits = 32 - rbits;
         geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
-        if (rbits > 24 || E >= (1ULL << 31)) try_sparse = false;
-    }
+        return geom;
+    };
+    IdxGeom geom = make_geom(E);
+    if (geom.rbits > 24 || E >= (1ULL << 31)) try_sparse = false;
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
     bool fill_pending = false;
@@ -925,11 +928,58 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         }
         HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-        const uint64_t ev = ctx->host_counters[0];
+        uint64_t ev = ctx->host_counters[0];
         const bool all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
+        // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
+        // deduplicated (launch_dedup_rows); repeated values no longer square the posting
+        // events.  The candidates are walked on the original lists.
+        const void *p_qry = d_qry;                  // the rows the probe reads
+        const uint32_t *p_qry_it = nullptr;         // and their lengths (null: d_qry_len)
+        uint64_t p_qry_stride = qry_stride;
+        const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
+        const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
+        if (!all_sorted && mr <= kDedupMax && mq <= kDedupMax && ev > 0) {
+            void *dref, *dref_len, *dqry = nullptr, *dqry_len = nullptr;
+            HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
+            HIP_TRY(scratch(ctx, 11, (size_t)n_ref * 4, &dref_len));
+            if (!self_set) {
+                HIP_TRY(scratch(ctx, 12, (size_t)n_qry * mq * hash_bytes, &dqry));
+                HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
+            }
+            geom = make_geom((uint64_t)n_ref * mr);
+            geom.kmax = events + 68;
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+            HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, sketch_size,
+                                      dref, (uint32_t *)dref_len, mr, st));
+            if (!self_set)
+                HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                          sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
+            HIP_TRY(launch_idx_build(dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes, geom,
+                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                     (uint32_t *)scan_s, (uint64_t *)tent,
+                                     (uint32_t *)dir, (uint32_t *)entries, unsorted,
+                                     self_set ? events : nullptr, st));
+            p_qry = self_set ? dref : dqry;
+            p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
+            p_qry_stride = self_set ? mr : mq;
+            if (!self_set)
+                HIP_TRY(launch_probe_count(p_qry, p_qry_it, p_qry_stride, n_qry, hash_bytes, geom,
+                                           (const uint32_t *)dir, events, unsorted, st));
+            tl.done();
+            HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            ev = ctx->host_counters[0];
+        }
         ctx->last_events = ev;
+        // Unsorted lists: a candidate costs a literal walk of ~S steps from global memory,
+        // and whether the walk ever meets a shared value depends on the order, so a pair
+        // sharing values rarely shares a counted one (C3: every pair shares the frequent
+        // k-fingers, 4 % have numer > 0).  Take the index path only when the events say
+        // most pairs share nothing (fewer events than half the pairs).
         const bool sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
-                            (long double)ev * 4.0L <= (long double)n_pairs * sketch_size;
+                            ((long double)ev * 4.0L <= (long double)n_pairs * sketch_size &&
+                             (all_sorted || 2 * ev <= n_pairs));
         if (sparse) {
             const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(ev, n_pairs));
             void *cand, *row_seg;
@@ -950,11 +1000,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // in place, so it waits for the fill instead.
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
-                HIP_TRY(launch_probe_rows(d_qry, d_qry_len, qry_stride, n_qry, n_ref, hash_bytes,
+                HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, (const uint32_t *)dir, (const uint32_t *)entries,
                                           d_ref_len, sketch_size, sym, true, self_set,
                                           cnt, (uint64_t *)cand, n_cand,
-                                          (uint64_t *)row_seg, st));
+                                          (uint64_t *)row_seg, p_qry_it, st));
                 tl.done();
             }
             uint32_t *cnum = nullptr, *cden = nullptr;

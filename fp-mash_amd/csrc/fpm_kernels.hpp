@@ -91,6 +91,12 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, hipStream_t st);
 uint64_t scan_scratch_words(uint64_t n);
+// each row's first min(len, S, out_stride) entries sorted and deduplicated (dist_index.hip),
+// the index / probe input for unsorted lists; out_stride <= kDedupMax
+constexpr uint32_t kDedupMax = 4096;
+hipError_t launch_dedup_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
+                             uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
+                             uint32_t *out_len, uint64_t out_stride, hipStream_t st);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
@@ -116,7 +122,10 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              const uint32_t *dir, const uint32_t *entries,
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
                              bool self_set, Counts cnt, uint64_t *cand,
-                             unsigned long long *n_cand, uint64_t *row_seg, hipStream_t st);
+                             unsigned long long *n_cand, uint64_t *row_seg,
+                             const uint32_t *d_qry_it_len, hipStream_t st);
+// (d_qry_it_len non-null: the probed query rows are launch_dedup_rows copies of length
+// d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)
 // (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are
 // the row's own hash and are not read)
 // sorted-distinct candidates: one workgroup per query row, one wave per pair

@@ -172,6 +172,54 @@ def test_dist_unsorted_u32_fp(ctx, oracle, dist_mode):
         np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
 
 
+def _skewed_fp_lists(rng, base, n, heavy=4, max_len=2100):
+    """CFL-like -fp lists: a few values repeated hundreds of times in most lists (the
+    "100" k-finger), the rest drawn from a large vocabulary, in file order."""
+    hv = base[:heavy]
+    lists = []
+    for i in range(n):
+        m = int(rng.integers(0, max_len))
+        fam = int(rng.integers(0, 40))
+        pool = base[heavy + fam * 400: heavy + fam * 400 + 400]
+        x = np.where(rng.random(m) < 0.3, hv[rng.integers(0, heavy, size=m)],
+                     pool[rng.integers(0, len(pool), size=m)])
+        if i % 7 == 0:          # some lists without the heavy values
+            x = pool[rng.integers(0, len(pool), size=m)]
+        lists.append(x.astype(np.uint32))
+    return lists
+
+
+@pytest.mark.parametrize("mode", ["auto", "sparse"])
+def test_dist_unsorted_dedup_index(ctx, oracle, mode):
+    """Unsorted lists with heavily repeated values: the index is rebuilt over each row's
+    sorted, deduplicated first min(len, S) entries and the candidates are walked on the
+    original lists.  Self set and a separate query set, against the literal-walk oracle."""
+    import fpmash
+    rng = np.random.default_rng(77)
+    base = rng.integers(0, 2 ** 32, size=20000, dtype=np.uint64).astype(np.uint32)
+    refs = _skewed_fp_lists(rng, base, 90)
+    qrys = _skewed_fp_lists(rng, base, 70)
+    rl = [int(rng.integers(1, 20000)) for _ in refs]
+    ql = [int(rng.integers(1, 20000)) for _ in qrys]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE if mode == "sparse" else fpmash.DIST_AUTO)
+    try:
+        for S in (1000, 2000, 64):
+            for (a, al), (b, bl) in (((refs, rl), (refs, rl)), ((refs, rl), (qrys, ql))):
+                got = ctx.dist(a, b, S, use64=False, k=1, kmer_space=10.0, ref_lengths=al,
+                               qry_lengths=bl)
+                st = ctx.last_dist_stats()
+                nu, de, di, pv = oracle.dist_grid(a, al, b, bl, S, 1, 10.0, use64=False)
+                assert np.array_equal(got["numer"], nu), S
+                assert np.array_equal(got["denom"], de), S
+                np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+                assert (nu > 0).any() and (nu == 0).any()
+                if mode == "sparse":
+                    assert st["sparse"] == 1, st          # index + literal walk
+                    assert st["candidates"] < len(a) * len(b)
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
 def test_dist_filters(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
     # 16 lists (a multiple of 4: the fill kernel's vector path) with an empty one (an empty
