@@ -879,6 +879,395 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
                           st);
 }
 
+// ---- Dense walk of u32 lists on 16-bit rank images (the -fp shape: C3).
+// The walk only compares values (<, ==, >).  For a block of 32 query lists with U = the
+// sorted distinct union of their first W entries, f(x) = 2 * #{u in U : u < x} + [x in U]
+// preserves every comparison between a value x of ANY list and a value b of the block
+// (f(b) = 2 rank(b) + 1; x < b => f(x) <= 2 rank(b) < f(b); x == b => equal;
+// x > b => f(x) >= 2 rank(b) + 2), and |U| <= 32 W <= 32736 keeps f below 2^16.
+// Half-width images double the lists an LDS tile holds: 32 x 32 pairs per workgroup
+// (64 lists of W u16) instead of 16 x 16 (32 lists of W u32), i.e. 4 waves per SIMD
+// instead of one, which hides the walk's dependent compare/select chain.
+// qblock_union_kernel (once per query block): U and the block's u16 images.
+// compare_grid_img_kernel (per tile): U staged in LDS, the 32 ref lists' values mapped by
+// a fixed-step lower bound, then both images in LDS and the literal walk of 1,024 pairs.
+constexpr int kImgTile = 32;
+#ifndef FPM_IMG_BLK
+#define FPM_IMG_BLK 3     // walk steps per LDS window (4 merged into unaligned ds_read_b64: 27 vs 15 ms on C3)
+#endif
+constexpr uint32_t kImgMaxW = 1023;          // 2 * 32 * W + 1 < 2^16
+constexpr uint32_t kImgNP = 32768;           // pow2 >= 32 * kImgMaxW
+constexpr uint32_t kInfA = 0xFFFF, kInfB = 0xFFFE;
+// U of a query block is followed by a directory over its values' top 12 bits (dir[v >> 20] =
+// lower bound of v's bucket, 4097 entries): ~8 values per bucket, so a lower bound is one
+// directory read + a few in-bucket steps instead of 15 steps over the whole U
+constexpr uint32_t kDirBits = 12, kDir = 1u << kDirBits;
+constexpr uint32_t kImgBlk = kImgNP + kDir + 4;   // u32 per query block in ublk (16-B multiple)   // padded-walk sentinels (> 2 * 32736 + 1)
+
+// x + (bit lane of m): one v_addc with the mask as carry-in
+__device__ __forceinline__ uint32_t add_mask(uint32_t x, uint64_t m)
+{
+    uint32_t r;
+    uint64_t c;
+    asm("v_addc_co_u32_e64 %0, %1, %2, 0, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
+__global__ __launch_bounds__(1024) void qblock_union_kernel(
+    const uint32_t *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t qry_stride,
+    uint32_t n_qry, uint32_t W, uint32_t Wimg, uint32_t *__restrict__ ublk,
+    uint32_t *__restrict__ usize, uint16_t *__restrict__ bimg)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t key[];   // kImgNP + kDir + 1
+    __shared__ uint32_t wsum[16];
+    const uint32_t b = blockIdx.x, q0 = b * kImgTile, t = threadIdx.x;
+    const uint32_t nv = kImgTile * W;
+    for (uint32_t x = t; x < kImgNP; x += 1024) {
+        uint32_t v = 0xFFFFFFFFu;
+        if (x < nv) {
+            const uint32_t l = x / W, e = x - l * W, row = q0 + l;
+            if (row < n_qry && e < min(qry_len[row], W)) v = qry[(uint64_t)row * qry_stride + e];
+        }
+        key[x] = v;
+    }
+    uint32_t n_valid = 0;
+    for (uint32_t l = 0; l < (uint32_t)kImgTile; l++)
+        if (q0 + l < n_qry) n_valid += min(qry_len[q0 + l], W);
+    __syncthreads();
+    for (uint32_t k = 2; k <= kImgNP; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = t; i < kImgNP; i += 1024) {
+                const uint32_t x = i ^ j;
+                if (x > i) {
+                    const uint32_t a = key[i], c = key[x];
+                    if ((a > c) == ((i & k) == 0)) { key[i] = c; key[x] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    // distinct values among the n_valid smallest (pads sort last; a real 0xFFFFFFFF is
+    // kept because only positions < n_valid are read)
+    constexpr int PT = kImgNP / 1024;
+    uint32_t v[PT], f = 0, cnt = 0;
+#pragma unroll
+    for (int u = 0; u < PT; u++) {
+        const uint32_t i = t * PT + u;
+        v[u] = key[i];
+        const bool first = i < n_valid && (i == 0 || key[i - 1] != v[u]);
+        f |= (first ? 1u : 0u) << u;
+        cnt += first ? 1u : 0u;
+    }
+    const uint32_t lane = t & 63, wave = t >> 6;
+    uint32_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { const uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t pos = x - cnt, tot = 0;
+    for (uint32_t w = 0; w < 16; w++) { if (w < wave) pos += wsum[w]; tot += wsum[w]; }
+#pragma unroll
+    for (int u = 0; u < PT; u++)
+        if (f >> u & 1u) { key[pos] = v[u]; ublk[(uint64_t)b * kImgBlk + pos] = v[u]; pos++; }
+    __syncthreads();
+    uint32_t P = 1;
+    while (P <= tot) P <<= 1;
+    // directory: dir[k] = #{U < k << 20}, dir[kDir] = |U|; and the largest bucket
+    uint32_t *dir = key + kImgNP;
+    __shared__ uint32_t maxb;
+    if (t == 0) maxb = 0;
+    for (uint32_t k = t; k <= kDir; k += 1024) {
+        uint32_t lo = 0;
+        if (k < kDir) {
+            const uint32_t a = k << (32 - kDirBits);
+            for (uint32_t st = P >> 1; st >= 1; st >>= 1)
+                if (lo + st <= tot && key[lo + st - 1] < a) lo += st;
+        } else {
+            lo = tot;
+        }
+        dir[k] = lo;
+        ublk[(uint64_t)b * kImgBlk + kImgNP + k] = lo;
+    }
+    __syncthreads();
+    for (uint32_t k = t; k < kDir; k += 1024) atomicMax(&maxb, dir[k + 1] - dir[k]);
+    __syncthreads();
+    if (t == 0) { usize[2 * b] = tot; usize[2 * b + 1] = maxb; }
+    for (uint32_t y = t; y < nv; y += 1024) {
+        const uint32_t l = y / W, e = y - l * W, row = q0 + l;
+        if (row >= n_qry) continue;
+        uint32_t img = 0;
+        if (e < min(qry_len[row], W)) {
+            const uint32_t a = qry[(uint64_t)row * qry_stride + e];
+            uint32_t lo = 0;
+            for (uint32_t st = P >> 1; st >= 1; st >>= 1)
+                if (lo + st <= tot && key[lo + st - 1] < a) lo += st;
+            img = 2 * lo + 1;                       // a is in U
+        }
+        bimg[(uint64_t)row * Wimg + e] = (uint16_t)img;
+    }
+}
+
+// LDS image row in u16: an odd number of dwords, so the 32 ref rows that lanes 0-31 (and
+// 32-63) of a wave read at similar offsets fall in 32 different banks of ds_read_u16's
+// (a/4) mod 32 banking (an even stride such as 504 dwords put them in 4 banks)
+__host__ __device__ __forceinline__ uint32_t img_row_u16(uint32_t W, uint32_t blk)
+{
+    return 2 * (((W + blk + 1) / 2) | 1u);
+}
+
+#ifdef FPM_IMG_PHASES
+// timing experiment: per-phase s_memtime deltas of thread 0, summed over workgroups
+__device__ unsigned long long g_img_ph[8];
+#define IMG_STAMP(k)                                                                   \
+    if (t == 0) {                                                                      \
+        const uint64_t now = __builtin_amdgcn_s_memtime();                             \
+        if (k) atomicAdd(&g_img_ph[k - 1], (unsigned long long)(now - ph_last));       \
+        ph_last = now;                                                                 \
+    }
+extern "C" int fpm_debug_img_phases(unsigned long long *out)
+{
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_img_ph), sizeof(g_img_ph));
+}
+#else
+#define IMG_STAMP(k)
+#endif
+
+template <int BLK, typename C>
+__global__ __launch_bounds__(1024) void compare_grid_img_kernel(
+    const uint32_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
+    uint32_t n_ref, const uint32_t *__restrict__ qry_len, uint32_t n_qry,
+    const uint32_t *__restrict__ ublk, const uint32_t *__restrict__ usize,
+    const uint16_t *__restrict__ bimg, uint32_t Wimg, uint32_t S, uint32_t W,
+    C *__restrict__ numer, C *__restrict__ denom)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
+    uint16_t *img = reinterpret_cast<uint16_t *>(lds32);
+    constexpr int kPer = (kImgTile * kImgMaxW + 1023) / 1024;   // ref values per thread (<= 32)
+    const uint32_t Wp = img_row_u16(W, BLK);
+    const uint32_t t = threadIdx.x, r0 = blockIdx.x * kImgTile, qb = blockIdx.y,
+                   q0 = qb * kImgTile;
+#ifdef FPM_IMG_PHASES
+    uint64_t ph_last = 0;
+#endif
+    const uint32_t us = usize[2 * qb], maxb = usize[2 * qb + 1];
+    const uint32_t nv = kImgTile * W;
+    uint32_t *dirL = lds32 + kImgNP;
+    IMG_STAMP(0);
+    {   // U: every thread's 16-B loads in flight before its LDS stores
+        constexpr int kUV = kImgNP / 4096;
+        const uint32_t *src = ublk + (uint64_t)qb * kImgBlk;
+        for (uint32_t k = t; k <= kDir; k += 1024) dirL[k] = src[kImgNP + k];
+        uint4 buf[kUV];
+#pragma unroll
+        for (int v = 0; v < kUV; v++) {
+            const uint32_t x = t * 4 + 4096u * v;
+            buf[v] = x + 4 <= us ? *(const uint4 *)(src + x) : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int v = 0; v < kUV; v++) {
+            const uint32_t x = t * 4 + 4096u * v;
+            if (x + 4 <= us) *(uint4 *)(lds32 + x) = buf[v];
+            else if (x < us) for (uint32_t y = x; y < us; y++) lds32[y] = src[y];
+        }
+    }
+    __syncthreads();
+    IMG_STAMP(1);
+    uint32_t P = 1;
+    while (P <= maxb) P <<= 1;
+    // the 32 ref lists' first W values: entry t + 1024 k.  Groups of 8, the next group's
+    // global loads issued before the current group's lower bounds in U (branch-free, every
+    // step's 8 LDS reads in flight); results packed two u16 per register
+    auto load_group = [&](int k0, uint32_t *val, uint32_t &okg) {
+        okg = 0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t y = t + 1024u * (k0 + u);
+            const uint32_t l = y / W, e = y - l * W, row = r0 + l;
+            const bool ok = y < nv && row < n_ref && e < min(ref_len[min(row, n_ref - 1)], W);
+            val[u] = ok ? ref[(uint64_t)row * ref_stride + e] : 0u;
+            okg |= (ok ? 1u : 0u) << u;
+        }
+    };
+    uint32_t res[kPer / 2];
+    uint32_t cur[8], nxt[8], okc, okn = 0;
+    load_group(0, cur, okc);
+#pragma unroll
+    for (int k0 = 0; k0 < kPer; k0 += 8) {
+        if (k0 + 8 < kPer) load_group(k0 + 8, nxt, okn);
+        uint32_t lo[8], hi[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const uint32_t bk = cur[u] >> (32 - kDirBits);
+            lo[u] = dirL[bk];
+            hi[u] = dirL[bk + 1];
+        }
+        for (uint32_t st = P >> 1; st >= 1; st >>= 1) {
+            uint32_t v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const uint32_t x = lo[u] + st - 1;
+                v[u] = lds32[x < hi[u] ? x : 0u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                lo[u] += (lo[u] + st <= hi[u]) & (v[u] < cur[u]) ? st : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u += 2) {
+            uint32_t mm[2];
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                const uint32_t e = lds32[lo[u + h] < us ? lo[u + h] : 0u];
+                mm[h] = (okc >> (u + h) & 1u)
+                            ? 2 * lo[u + h] + ((lo[u + h] < us) & (e == cur[u + h]) ? 1u : 0u)
+                            : kInfA;
+            }
+            res[(k0 + u) / 2] = mm[0] | (mm[1] << 16);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) cur[u] = nxt[u];
+        okc = okn;
+    }
+    __syncthreads();
+    IMG_STAMP(2);
+    // images: ref lists 0..31, query lists 32..63, rows of Wp u16
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+        const uint32_t y = t + 1024u * k;
+        if (y < nv) {
+            const uint32_t l = y / W, e = y - l * W;
+            img[l * Wp + e] = (uint16_t)(res[k / 2] >> (16 * (k & 1)));
+        }
+    }
+    for (uint32_t y = t; y < nv; y += 1024) {
+        const uint32_t l = y / W, e = y - l * W, row = q0 + l;
+        img[(kImgTile + l) * Wp + e] =
+            row < n_qry && e < min(qry_len[row], W) ? bimg[(uint64_t)row * Wimg + e] : (uint16_t)kInfB;
+    }
+    {   // the rows' tails [W, Wp): sentinels
+        const uint32_t tw = Wp - W;
+        for (uint32_t y = t; y < 2 * kImgTile * tw; y += 1024) {
+            const uint32_t l = y / tw;
+            img[l * Wp + W + (y - l * tw)] = (uint16_t)(l < (uint32_t)kImgTile ? kInfA : kInfB);
+        }
+    }
+    __syncthreads();
+    IMG_STAMP(3);
+    const uint32_t lane = t & 63;
+    const uint32_t r = r0 + (t & (kImgTile - 1)), q = q0 + t / kImgTile;
+    if (r >= n_ref || q >= n_qry) return;
+    const uint32_t la = ref_len[r], lb = qry_len[q];
+    const uint16_t *A = img + (t & (kImgTile - 1)) * Wp;
+    const uint16_t *B = img + (kImgTile + t / kImgTile) * Wp;
+    (void)lane;
+    // Padded walk: past its first min(len, W) entries each image row holds a sentinel,
+    // kInfA (ref) > kInfB (query) > every image value, so the walk needs no end-of-list
+    // tests: it runs S steps (S <= W here), an exhausted list is never advanced again
+    // while the other one is real, the sentinels never compare equal, and with
+    // i* = min(i, la), j* = min(j, lb) the reference's denom (steps + remainders, capped
+    // at S: CommandDistance.cpp:376-415) is min(S, i* + j* - common).  Per step: two
+    // compares into lane masks, three masked increments, the window shifts.
+    uint32_t i = 0, j = 0, common = 0;
+#ifdef FPM_IMG_NOWALK
+    const uint32_t Swalk = 0;   // timing experiment: prologue only
+#else
+    const uint32_t Swalk = S;
+#endif
+    for (uint32_t d0 = 0; d0 < Swalk; d0 += BLK) {
+        if (!__any((i < la) | (j < lb))) break;
+        uint32_t a[BLK], b[BLK];
+#pragma unroll
+        for (int u = 0; u < BLK; u++) {
+            a[u] = A[i + u];
+            b[u] = B[j + u];
+        }
+#pragma unroll
+        for (int u = 0; u < BLK; u++) {
+            if (d0 + u >= S) break;                    // uniform
+            const uint64_t mlt = __builtin_amdgcn_ballot_w64(a[0] < b[0]);
+            const uint64_t mgt = __builtin_amdgcn_ballot_w64(b[0] < a[0]);
+            const uint64_t ma = ~mgt, mb = ~mlt, meq = ~(mlt | mgt);
+            common = add_mask(common, meq);
+            i = add_mask(i, ma);
+            j = add_mask(j, mb);
+#pragma unroll
+            for (int v = 0; v + 1 < BLK - u; v++) {
+                a[v] = lane_sel(a[v], a[v + 1], ma);
+                b[v] = lane_sel(b[v], b[v + 1], mb);
+            }
+        }
+    }
+    IMG_STAMP(4);
+    const uint32_t is = min(i, la), js = min(j, lb);
+    const uint32_t d = min(S, is + js - common);
+    const uint64_t o = (uint64_t)q * n_ref + r;
+    numer[o] = (C)common;
+    denom[o] = (C)d;
+}
+
+bool compare_grid_img_ok(uint32_t hash_bytes, uint32_t sketch_size, uint64_t ref_stride,
+                         uint64_t qry_stride)
+{
+    const uint64_t W = std::min<uint64_t>(sketch_size, std::max(ref_stride, qry_stride));
+    // the padded walk runs S steps inside rows of W + BLK entries: S <= W
+    return hash_bytes == 4 && W >= 64 && W <= kImgMaxW && sketch_size <= W;
+}
+
+void compare_grid_img_scratch(uint32_t n_qry, uint32_t sketch_size, uint64_t ref_stride,
+                              uint64_t qry_stride, size_t *ublk_bytes, size_t *bimg_bytes)
+{
+    const uint64_t W = std::min<uint64_t>(sketch_size, std::max(ref_stride, qry_stride));
+    const uint64_t nqb = (n_qry + kImgTile - 1) / kImgTile;
+    const uint64_t Wimg = (W + 7) & ~7ull;
+    *ublk_bytes = nqb * kImgBlk * 4 + nqb * 8 + 64;
+    *bimg_bytes = (uint64_t)n_qry * Wimg * 2 + 64;
+}
+
+template <typename C>
+static hipError_t compare_grid_img_c(const uint32_t *ref, const uint32_t *ref_len,
+                                     uint64_t ref_stride, uint32_t n_ref, const uint32_t *qry,
+                                     const uint32_t *qry_len, uint64_t qry_stride, uint32_t n_qry,
+                                     uint32_t S, void *ublk_p, void *bimg_p, C *numer, C *denom,
+                                     hipStream_t st)
+{
+    constexpr int kBlk = FPM_IMG_BLK;
+    const uint32_t W = (uint32_t)std::min<uint64_t>(S, std::max(ref_stride, qry_stride));
+    const uint32_t nqb = (n_qry + kImgTile - 1) / kImgTile, nrb = (n_ref + kImgTile - 1) / kImgTile;
+    const uint32_t Wimg = (W + 7) & ~7u, Wp = img_row_u16(W, kBlk);
+    uint32_t *ublk = (uint32_t *)ublk_p, *usize = ublk + (size_t)nqb * kImgBlk;
+    uint16_t *bimg = (uint16_t *)bimg_p;
+    const size_t lds_u = (size_t)(kImgNP + kDir + 1) * 4;
+    const size_t lds_t = std::max<size_t>((size_t)(kImgNP + kDir + 1) * 4, (size_t)2 * kImgTile * Wp * 2);
+    if (hipError_t e = hipFuncSetAttribute((const void *)qblock_union_kernel,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_u))
+        return e;
+    const void *fn = (const void *)compare_grid_img_kernel<kBlk, C>;
+    if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_t))
+        return e;
+    hipLaunchKernelGGL(qblock_union_kernel, dim3(nqb), dim3(1024), lds_u, st, qry, qry_len,
+                       qry_stride, n_qry, W, Wimg, ublk, usize, bimg);
+    hipLaunchKernelGGL((compare_grid_img_kernel<kBlk, C>), dim3(nrb, nqb), dim3(1024), lds_t, st,
+                       ref, ref_len, ref_stride, n_ref, qry_len, n_qry, (const uint32_t *)ublk,
+                       (const uint32_t *)usize, (const uint16_t *)bimg, Wimg, S, W, numer, denom);
+    return hipGetLastError();
+}
+
+hipError_t launch_compare_grid_img(const void *d_ref, const uint32_t *d_ref_len,
+                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                   const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                                   uint32_t sketch_size, void *ublk, void *bimg, Counts cnt,
+                                   hipStream_t st)
+{
+    if (n_ref == 0 || n_qry == 0) return hipSuccess;
+    if (cnt.c16)
+        return compare_grid_img_c((const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                                  (const uint32_t *)d_qry, d_qry_len, qry_stride, n_qry,
+                                  sketch_size, ublk, bimg, (uint16_t *)cnt.numer,
+                                  (uint16_t *)cnt.denom, st);
+    return compare_grid_img_c((const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                              (const uint32_t *)d_qry, d_qry_len, qry_stride, n_qry, sketch_size,
+                              ublk, bimg, (uint32_t *)cnt.numer, (uint32_t *)cnt.denom, st);
+}
+
 template <typename C>
 static hipError_t walk_candidates_c(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                     uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <memory>
 #include <cstdio>
 #include <cstring>
@@ -63,6 +64,8 @@ struct fpm_ctx {
     Slot scratch[16];
     unsigned long long *host_counters = nullptr;   // pinned, for the events read-back
     int dist_mode = FPM_DIST_AUTO;
+    // dense walk of u32 lists on 16-bit rank images (FPM_DENSE_IMG=0 turns it off, A/B)
+    bool dense_img = true;
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
     // side stream for the sparse dist's fill (a pure write stream that runs beside the
@@ -162,6 +165,7 @@ int fpm_ctx_create(int device, fpm_ctx **out)
                                     ", fpmash kernels are built for gfx950 only");
     fpm_ctx *ctx = new fpm_ctx();
     ctx->device = device;
+    if (const char *v = getenv("FPM_DENSE_IMG")) ctx->dense_img = atoi(v) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1066,6 +1070,19 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         }
     }
     if (fill_pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));   // dense after all
+    if (ctx->dense_img && compare_grid_img_ok(hash_bytes, sketch_size, ref_stride, qry_stride)) {
+        size_t ub, bb;
+        compare_grid_img_scratch(n_qry, sketch_size, ref_stride, qry_stride, &ub, &bb);
+        void *ublk, *bimg;
+        HIP_TRY(scratch(ctx, 14, ub, &ublk));
+        HIP_TRY(scratch(ctx, 15, bb, &bimg));
+        TimedLaunch tl(ctx, FPM_K_COMPARE, st);
+        HIP_TRY(launch_compare_grid_img(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
+                                        qry_stride, n_qry, sketch_size, ublk, bimg, cnt, st));
+        tl.done();
+        ctx->last_cand = n_pairs;
+        return FPM_OK;
+    }
     TimedLaunch tl(ctx, FPM_K_COMPARE, st);
     HIP_TRY(launch_compare_grid(d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
                                 n_qry, hash_bytes, sketch_size, cnt, st));

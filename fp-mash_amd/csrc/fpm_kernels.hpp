@@ -66,6 +66,17 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
                                uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
                                uint32_t sketch_size, Counts cnt, hipStream_t st);
 
+// dense walk of u32 lists on 16-bit rank images (dist.hip), for 64 <= min(S, stride) <= 1023;
+// scratch from compare_grid_img_scratch
+bool compare_grid_img_ok(uint32_t hash_bytes, uint32_t sketch_size, uint64_t ref_stride,
+                         uint64_t qry_stride);
+void compare_grid_img_scratch(uint32_t n_qry, uint32_t sketch_size, uint64_t ref_stride,
+                              uint64_t qry_stride, size_t *ublk_bytes, size_t *bimg_bytes);
+hipError_t launch_compare_grid_img(const void *d_ref, const uint32_t *d_ref_len,
+                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
+                                   const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
+                                   uint32_t sketch_size, void *ublk, void *bimg, Counts cnt,
+                                   hipStream_t st);
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                   uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
