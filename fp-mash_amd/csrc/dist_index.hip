@@ -366,9 +366,10 @@ __global__ __launch_bounds__(256) void probe_count_kernel(
     }
 }
 
+// events[1..64] -> events[0].  (A last-workgroup sum inside the bucket pass instead
+// measured 0.1 ms slower: its done counter is one address taking an atomic per workgroup.)
 __global__ void sum64_kernel(unsigned long long *events)
 {
-    // events[1..64] -> events[0]
     unsigned long long v = events[1 + threadIdx.x];
     for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d, 64);
     if (threadIdx.x == 0) events[0] = v;

@@ -68,6 +68,8 @@ struct fpm_ctx {
     bool dense_img = true;
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
+    const unsigned long long *last_cand_dev = nullptr;   // the last sparse call's counter
+    hipStream_t last_cand_stream = nullptr;
     // side stream for the sparse dist's fill (a pure write stream that runs beside the
     // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
@@ -260,8 +262,10 @@ int fpm_ctx_last_dist_stats(fpm_ctx *ctx, int *sparse, uint64_t *events, uint64_
     if (events) *events = ctx->last_events;
     if (ctx->last_cand == (uint64_t)-1) {
         if (int rc = set_device(ctx)) return rc;
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
-        ctx->last_cand = ctx->host_counters[65];
+        HIP_TRY(hipStreamSynchronize(ctx->last_cand_stream));
+        unsigned long long v = 0;
+        HIP_TRY(hipMemcpy(&v, ctx->last_cand_dev, 8, hipMemcpyDeviceToHost));
+        ctx->last_cand = v;
     }
     if (candidates) *candidates = ctx->last_cand;
     return FPM_OK;
@@ -540,6 +544,9 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     alloc((void **)&job->d_tiles, by_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_rows, (size_t)n_rows * s * sizeof(uint64_t));
     alloc((void **)&job->d_count, (size_t)n_rows * sizeof(uint32_t));
+    // groups without any k-mer keep count 0: zeroed once here (every run rewrites the count
+    // of each group that has tiles: the tile kernel or the last merge of its group)
+    if (e == hipSuccess) e = hipMemset(job->d_count, 0, (size_t)n_rows * sizeof(uint32_t));
     alloc((void **)&job->d_merge, mplan.size() * sizeof(MergeDesc));
     alloc((void **)&job->d_stiles, sby_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_smerge, splan.size() * sizeof(MergeDesc));
@@ -591,8 +598,6 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     fpm_ctx *ctx = job->ctx;
     if (int rc = set_device(ctx)) return rc;
     hipStream_t st = pick_stream(ctx, stream);
-    // groups without any k-mer keep count 0
-    HIP_TRY(hipMemsetAsync(job->d_count, 0, (size_t)job->n_groups * sizeof(uint32_t), st));
     auto tiles_pass = [&](const TileDesc *d_t, const uint32_t *begin) -> int {
         for (int c = 0; c < kTileClasses; c++) {
             uint32_t b = begin[c], n = begin[c + 1] - b;
@@ -1063,9 +1068,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 tl.done();
                 *finalized = true;
             }
-            HIP_TRY(hipMemcpyAsync(ctx->host_counters + 65, n_cand, 8, hipMemcpyDeviceToHost, st));
             ctx->last_sparse = rows_merge ? 2 : 1;
-            ctx->last_cand = (uint64_t)-1;   // read lazily by fpm_ctx_last_dist_stats callers after sync
+            ctx->last_cand = (uint64_t)-1;   // read by fpm_ctx_last_dist_stats (sync + copy)
+            ctx->last_cand_dev = n_cand;
+            ctx->last_cand_stream = st;
             return FPM_OK;
         }
     }
