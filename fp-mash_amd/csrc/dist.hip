@@ -243,7 +243,10 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
 // No per-wave LDS image and no merge walk: ~5 LDS reads and ~40 VALU per A element.
-constexpr int kRankWaves = 4;
+#ifndef FPM_RANK_WAVES
+#define FPM_RANK_WAVES 4
+#endif
+constexpr int kRankWaves = FPM_RANK_WAVES;
 
 template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
@@ -300,7 +303,10 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // ranked), `nxt` (this candidate's next group, issued before `cur` is ranked) and `pf`
     // (the next candidate's first group, issued when a candidate starts): 24 VGPRs of row
     // data, and the groups after an early exit are never loaded.
-    constexpr int kGroup = 4;
+#ifndef FPM_RANK_GROUP
+#define FPM_RANK_GROUP 4
+#endif
+    constexpr int kGroup = FPM_RANK_GROUP;
     struct Row { __amdgpu_buffer_rsrc_t rsrc; uint32_t la; uint64_t o; };
     auto open_row = [&](uint64_t o) -> Row {
         const uint32_t rr = __builtin_amdgcn_readfirstlane((uint32_t)(o - pair_row));
