@@ -54,6 +54,13 @@ int tile_class(uint32_t nstarts)
 
 }  // namespace
 
+// merge rounds whose estimated input lists are at most merge_small_cap() long use
+// merge_small_kernel; FPM_MERGE_SMALL=0 turns it off (A/B)
+static const bool g_merge_small_off = [] {
+    const char *v = getenv("FPM_MERGE_SMALL");
+    return v && atoi(v) == 0;
+}();
+
 struct fpm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -331,6 +338,7 @@ struct fpm_sketch_job {
     MergeDesc *d_merge = nullptr;
     uint32_t class_begin[kTileClasses + 1] = {0};
     std::vector<uint32_t> round_begin;
+    std::vector<uint8_t> round_small, sround_small;   // per round: merge_small_kernel
     // long groups: a 1-in-kSampleEvery sample of their tiles is sketched first; its s-th
     // smallest hash bounds what every tile of the group keeps
     uint32_t n_slots = 0;
@@ -467,13 +475,29 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
         }
         for (size_t t = 0; t < tiles.size(); t++) tiles[t].thr_slot = slot_of[tile_group[t]];
     }
+    // list-length estimate per row (steers merge_small_kernel only; results do not depend
+    // on it): a tile keeps at most its k-mers and s; a tile of a sampled (thresholded) group
+    // keeps ~kSampleEvery * s / tiles of the group's hashes (2x margin)
+    std::vector<uint64_t> est(n_rows, s);
+    for (size_t t = 0; t < tiles.size(); t++) {
+        const uint32_t g = tile_group[t];
+        uint64_t e = std::min<uint64_t>(s, tiles[t].n_bytes >= k ? tiles[t].n_bytes - k + 1 : 0);
+        if (slot_of[g]) e = std::min<uint64_t>(e, 2ULL * kSampleEvery * s / ntile_of[g] + 64);
+        if (tiles[t].out_row < est.size()) est[tiles[t].out_row] = e;
+    }
+    for (auto &st : stiles)
+        if (st.out_row < est.size())
+            est[st.out_row] = std::min<uint64_t>(s, st.n_bytes >= k ? st.n_bytes - k + 1 : 0);
     struct Plan { uint32_t a, b, c; };
     // pairwise merge rounds of each group's lists; the last merge writes final_row(g)
     auto plan_rounds = [&](std::vector<std::vector<uint32_t>> &L_of, auto final_row,
-                           std::vector<Plan> &plan, std::vector<uint32_t> &rounds) {
+                           std::vector<Plan> &plan, std::vector<uint32_t> &rounds,
+                           std::vector<uint8_t> &small) {
         rounds.assign(1, 0);
+        small.clear();
         for (;;) {
             bool any = false;
+            uint64_t round_max = 0;
             for (uint32_t g = 0; g < n_groups; g++) {
                 auto &L = L_of[g];
                 if (L.size() < 2) continue;
@@ -483,6 +507,10 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
                     uint32_t c = (L.size() == 2) ? final_row(g) : n_rows++;
                     plan.push_back({L[i], L[i + 1], c});
                     next.push_back(c);
+                    if (est.size() <= c) est.resize(c + 1, s);
+                    const uint64_t ea = est[L[i]], eb = est[L[i + 1]];
+                    est[c] = std::min<uint64_t>(s, ea + eb);
+                    round_max = std::max(round_max, std::max(ea, eb));
                 }
                 if (L.size() % 2) next.push_back(L.back());
                 if (next.size() == 1) next.clear();   // reached the final row
@@ -490,18 +518,20 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
             }
             if (!any) break;
             rounds.push_back((uint32_t)plan.size());
+            small.push_back(round_max <= merge_small_cap() ? 1 : 0);
         }
     };
     std::vector<Plan> splan, mplan;
     std::vector<uint32_t> srb, rb;
+    std::vector<uint8_t> ssmall, msmall;
     for (uint32_t g = 0; g < n_groups; g++)
         if (slot_of[g]) srow[slot_of[g] - 1] = slists[g].size() == 1 ? slists[g][0] : 0;
     plan_rounds(slists, [&](uint32_t g) {
         const uint32_t r = n_rows++;
         srow[slot_of[g] - 1] = r;
         return r;
-    }, splan, srb);
-    plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb);
+    }, splan, srb, ssmall);
+    plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb, msmall);
 
     // tiles ordered by capacity class
     auto order_by_class = [&](const std::vector<TileDesc> &in, std::vector<TileDesc> &out,
@@ -534,6 +564,8 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     memcpy(job->sclass_begin, sclass_begin, sizeof(sclass_begin));
     job->round_begin = rb;
     job->sround_begin = srb;
+    job->round_small = msmall;
+    job->sround_small = ssmall;
     job->n_slots = (uint32_t)srow.size();
 
     hipError_t e = hipSuccess;
@@ -609,23 +641,25 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         }
         return FPM_OK;
     };
-    auto merge_pass = [&](const MergeDesc *d_m, const std::vector<uint32_t> &rounds) -> int {
+    auto merge_pass = [&](const MergeDesc *d_m, const std::vector<uint32_t> &rounds,
+                          const std::vector<uint8_t> &small) -> int {
         for (size_t r = 0; r + 1 < rounds.size(); r++) {
             uint32_t b = rounds[r], n = rounds[r + 1] - b;
             TimedLaunch tl(ctx, FPM_K_MERGE, st);
-            HIP_TRY(launch_merge(d_m + b, n, job->kp.s, st));
+            HIP_TRY(launch_merge(d_m + b, n, job->kp.s, r < small.size() && small[r] && !g_merge_small_off,
+                                 st));
             tl.done();
         }
         return FPM_OK;
     };
     if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
         if (int rc = tiles_pass(job->d_stiles, job->sclass_begin)) return rc;
-        if (int rc = merge_pass(job->d_smerge, job->sround_begin)) return rc;
+        if (int rc = merge_pass(job->d_smerge, job->sround_begin, job->sround_small)) return rc;
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
                                         job->kp.s, job->d_thr, st));
     }
     if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
-    return merge_pass(job->d_merge, job->round_begin);
+    return merge_pass(job->d_merge, job->round_begin, job->round_small);
 }
 
 int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,

@@ -56,7 +56,10 @@ hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_
 hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
                                    const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                    hipStream_t st);
-hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st);
+uint32_t merge_small_cap();   // list length merge_small_kernel stages in LDS
+// small: the round's lists are estimated short (merge_small_kernel; exact for any length)
+hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,
+                        hipStream_t st);
 
 hipError_t launch_fp_hash(const uint64_t *d_vals, const uint64_t *d_line_off, uint64_t n_lines,
                           uint32_t seed, uint32_t use64, void *d_out, hipStream_t st);

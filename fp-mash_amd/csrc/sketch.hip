@@ -525,9 +525,112 @@ __global__ __launch_bounds__(kMBlock) void merge_lds_kernel(const MergeDesc *__r
     }
 }
 
-hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, hipStream_t st)
+
+// Merge rounds whose lists are known to be short (the threshold-bounded tile lists of long
+// groups: ~2 * 16 * s / tiles hashes each in C5's first rounds): 256 threads per merge and a
+// fixed 16 KiB of LDS instead of 1,024 threads and s * 8 bytes (80 KiB at s = 10,000, two
+// merges per CU), so ~5 merges share a CU.  A list longer than kSCap is searched in global
+// memory instead (same results; the host's size estimate only steers speed).
+#ifndef FPM_SBLOCK
+#define FPM_SBLOCK 256
+#endif
+#ifndef FPM_SCAP
+#define FPM_SCAP 2048
+#endif
+constexpr int kSBlock = FPM_SBLOCK, kSWaves = kSBlock / 64;
+constexpr uint32_t kSCap = FPM_SCAP;
+uint32_t merge_small_cap() { return kSCap; }
+
+__device__ __forceinline__ uint32_t block_exscan_s(uint32_t v, uint32_t *tmp, uint32_t *total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) tmp[wave] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kSWaves; w++) { const uint32_t t = tmp[w]; pre += w < wave ? t : 0u; tot += t; }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+__global__ __launch_bounds__(kSBlock) void merge_small_kernel(const MergeDesc *__restrict__ descs,
+                                                              uint32_t s)
+{
+    __shared__ uint64_t sl[kSCap];
+    __shared__ uint32_t scan_tmp[kSWaves];
+    const MergeDesc md = descs[blockIdx.x];
+    const uint32_t la = *md.alen, lb = md.b ? *md.blen : 0;
+    const bool bfit = lb <= kSCap;
+    if (bfit)
+        for (uint32_t j = threadIdx.x; j < lb; j += kSBlock) sl[j] = md.b[j];
+    __syncthreads();
+    const uint64_t *Bv = bfit ? sl : md.b;
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < la; c0 += kSBlock) {
+        const uint32_t i = c0 + threadIdx.x;
+        uint64_t a = 0;
+        uint32_t pos = 0, dup = 0;
+        if (i < la) {
+            a = md.a[i];
+            pos = lower_bound_u64(Bv, lb, a);
+            dup = (pos < lb && Bv[pos] == a) ? 1u : 0u;
+        }
+        uint32_t tot;
+        const uint32_t ex = block_exscan_s(dup, scan_tmp, &tot);
+        if (i < la) {
+            const uint32_t f = i + pos - (carry + ex);
+            if (f < s) md.c[f] = a;
+        }
+        carry += tot;
+    }
+    const uint32_t dups_total = carry;
+    if (lb) {
+        const bool afit = la <= kSCap;
+        __syncthreads();                               // every search of sl is done
+        if (afit)
+            for (uint32_t i = threadIdx.x; i < la; i += kSBlock) sl[i] = md.a[i];
+        __syncthreads();
+        const uint64_t *Av = afit ? sl : md.a;
+        carry = 0;
+        for (uint32_t c0 = 0; c0 < lb; c0 += kSBlock) {
+            const uint32_t j = c0 + threadIdx.x;
+            uint64_t b = 0;
+            uint32_t pos = 0, dup = 0;
+            if (j < lb) {
+                b = md.b[j];
+                pos = upper_bound_u64(Av, la, b);
+                dup = (pos > 0 && Av[pos - 1] == b) ? 1u : 0u;
+            }
+            uint32_t tot;
+            const uint32_t ex = block_exscan_s(dup, scan_tmp, &tot);
+            if (j < lb && !dup) {
+                const uint32_t f = j + pos - (carry + ex);
+                if (f < s) md.c[f] = b;
+            }
+            carry += tot;
+        }
+    }
+    if (threadIdx.x == 0) {
+        const uint32_t u = la + lb - dups_total;
+        *md.clen = u < s ? u : s;
+    }
+}
+
+hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,
+                        hipStream_t st)
 {
     if (n == 0) return hipSuccess;
+    if (small) {
+        hipLaunchKernelGGL(merge_small_kernel, dim3(n), dim3(kSBlock), 0, st, d_desc, s);
+        return hipGetLastError();
+    }
     // up to 128 KiB of staged list (s <= 16,384); beyond, the global-memory searches
     constexpr size_t kMaxLds = 128 * 1024;
     const size_t lds = (size_t)s * sizeof(uint64_t);
