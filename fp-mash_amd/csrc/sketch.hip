@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kMBlock) void merge_lds_kernel(const MergeDesc *__r
 // Merge rounds whose lists are known to be short (the threshold-bounded tile lists of long
 // groups: ~2 * 16 * s / tiles hashes each in C5's first rounds): 256 threads per merge and a
 // fixed 16 KiB of LDS instead of 1,024 threads and s * 8 bytes (80 KiB at s = 10,000, two
-// merges per CU), so ~5 merges share a CU.  A list longer than kSCap is searched in global
+// merges per CU), so up to 8 merges share a CU.  A list longer than kSCap is searched in global
 // memory instead (same results; the host's size estimate only steers speed).
 #ifndef FPM_SBLOCK
 #define FPM_SBLOCK 256
