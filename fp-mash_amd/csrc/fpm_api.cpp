@@ -55,10 +55,11 @@ int tile_class(uint32_t nstarts)
 }  // namespace
 
 // merge rounds whose estimated input lists are at most merge_small_cap() long use
-// merge_small_kernel; FPM_MERGE_SMALL=0 turns it off (A/B)
-static const bool g_merge_small_off = [] {
+// merge_small_kernel; FPM_MERGE_SMALL=0 turns it off (A/B), =2 uses it for every round
+// (tests: its global-memory search past the LDS cap)
+static const int g_merge_small_env = [] {
     const char *v = getenv("FPM_MERGE_SMALL");
-    return v && atoi(v) == 0;
+    return v ? atoi(v) : 1;
 }();
 
 struct fpm_ctx {
@@ -646,8 +647,9 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         for (size_t r = 0; r + 1 < rounds.size(); r++) {
             uint32_t b = rounds[r], n = rounds[r + 1] - b;
             TimedLaunch tl(ctx, FPM_K_MERGE, st);
-            HIP_TRY(launch_merge(d_m + b, n, job->kp.s, r < small.size() && small[r] && !g_merge_small_off,
-                                 st));
+            const bool sm = g_merge_small_env == 2 ||
+                            (g_merge_small_env != 0 && r < small.size() && small[r]);
+            HIP_TRY(launch_merge(d_m + b, n, job->kp.s, sm, st));
             tl.done();
         }
         return FPM_OK;

@@ -433,3 +433,15 @@ def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
     got = ctx.sketch(P, recs, groups=groups, n_groups=4)
     exp = oracle.sketch_batch(oracle.params(k=k, s=s), recs, groups=groups, n_groups=4)
     check_sketches(got, exp)
+
+
+def test_merge_small_kernel_forced():
+    """Every merge round on merge_small_kernel (FPM_MERGE_SMALL=2, in a child process: the
+    switch is read when the library loads), including lists longer than its LDS cap that
+    it searches in global memory: sketches equal the oracle's."""
+    import subprocess
+    import sys
+    env = dict(os.environ, FPM_MERGE_SMALL="2")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "_merge_small_worker.py")],
+                       env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
