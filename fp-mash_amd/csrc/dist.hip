@@ -1115,7 +1115,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
             }
 #pragma unroll
             for (int u = 0; u < 8; u++)
-                lo[u] += (lo[u] + st <= hi[u]) & (v[u] < cur[u]) ? st : 0u;
+                lo[u] += ((lo[u] + st <= hi[u]) & (v[u] < cur[u])) ? st : 0u;
         }
 #pragma unroll
         for (int u = 0; u < 8; u += 2) {
@@ -1124,7 +1124,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
             for (int h = 0; h < 2; h++) {
                 const uint32_t e = lds32[lo[u + h] < us ? lo[u + h] : 0u];
                 mm[h] = (okc >> (u + h) & 1u)
-                            ? 2 * lo[u + h] + ((lo[u + h] < us) & (e == cur[u + h]) ? 1u : 0u)
+                            ? 2 * lo[u + h] + (((lo[u + h] < us) & (e == cur[u + h])) ? 1u : 0u)
                             : kInfA;
             }
             res[(k0 + u) / 2] = mm[0] | (mm[1] << 16);
