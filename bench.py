@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
+    ap.add_argument("--no-parity", action="store_true",
+                    help="skip the oracle checks of the C2 / C3 / C4 results")
     return ap.parse_args()
 
 
@@ -66,10 +68,23 @@ def parse_args_for_test(**kw):
     """Defaults of parse() with overrides (tests)."""
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
-                           no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000)
+                           no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
+                           no_parity=True)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
+
+
+def timing_steps(steps):
+    """Steps run with per-launch HIP events after the timed region (the event records add
+    marker packets between launches, so they stay out of the timed steps)."""
+    return max(3, min(steps, 10))
+
+
+def per_step_ms(ktimes, names, n_timed):
+    """Device milliseconds per step of the named kernels: their event totals over the
+    n_timed event-timed steps (not over --steps: those ran without events)."""
+    return sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in names) / n_timed
 
 
 def dist_env():
@@ -83,14 +98,21 @@ class Group:
     """Barrier + max over ranks.  gloo (host-side) keeps the timing collective off
     the device; the data path itself has no collective (independent batches)."""
 
-    def __init__(self, ws):
+    def __init__(self, ws, local=0, nccl=False):
         self.ws = ws
-        self.pg = None
+        self.nccl = None
         if ws > 1:
+            import datetime
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
             self.dist = dist
+            if nccl:
+                # RCCL (backend "nccl") for the C4 leg's sketch-row all-gather over xGMI
+                import torch
+                torch.cuda.set_device(local)
+                self.nccl = dist.new_group(backend="nccl",
+                                           timeout=datetime.timedelta(seconds=300))
 
     def barrier(self):
         if self.ws > 1:
@@ -229,7 +251,88 @@ def _group_fp_lines(r, text):
     return starts, ends, lengths
 
 
-def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
+
+# ---- parity (the CPU leg's checker: oracle/ restatement, outside every timed region) ----
+
+def _threads():
+    t = int(os.environ.get("OMP_NUM_THREADS", "0")) or len(os.sched_getaffinity(0))
+    return max(1, min(t, 64))
+
+
+def fetch_rows(buf, dtype, n_cols, rows):
+    """rows [r] of a device matrix [.][n_cols] (query-major dist outputs) -> host [len(rows), n_cols]"""
+    isz = np.dtype(dtype).itemsize
+    out = np.empty((len(rows), n_cols), dtype=dtype)
+    L = fpmash.lib()
+    for i, r in enumerate(rows):
+        fpmash._check(L.fpm_memcpy_d2h(buf.ctx.h, out[i].ctypes.data,
+                                       buf.ptr + int(r) * n_cols * isz, n_cols * isz))
+    return out
+
+
+def sample_rows(n, m, salt=0):
+    """m query rows spread over [0, n) (every family of the family-structured batches)"""
+    m = min(m, n)
+    rng = np.random.default_rng(12345 + salt)
+    return np.sort(rng.choice(n, size=m, replace=False)) if m else np.zeros(0, np.int64)
+
+
+def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
+    """device (numer u16, denom u16, distance, p-value, pass) rows vs the oracle's grid of the
+    same query rows: counts and pass flags exact, distance and p-value within rtol 1e-12
+    (the north-star tolerance)"""
+    nu_o, de_o, di_o, pv_o = (x.reshape(len(rows), n_ref) for x in exp)
+    nu = fetch_rows(outs[0], np.uint16, n_ref, rows)
+    de = fetch_rows(outs[1], np.uint16, n_ref, rows)
+    di = fetch_rows(outs[2], np.float64, n_ref, rows)
+    pv = fetch_rows(outs[3], np.float64, n_ref, rows)
+    pa = fetch_rows(outs[4], np.uint8, n_ref, rows)
+    exp_pass = (di_o <= max_dist) & (pv_o <= max_pvalue)
+    counts_ok = bool(np.array_equal(nu, nu_o) and np.array_equal(de, de_o))
+    dist_ok = bool(np.allclose(di, di_o, rtol=1e-12, atol=0))
+    pv_ok = bool(np.allclose(pv, pv_o, rtol=1e-12, atol=0))
+    pass_ok = bool(np.array_equal(pa.astype(bool), exp_pass))
+    return {"rows": len(rows), "pairs": int(len(rows) * n_ref),
+            "pairs_sharing": int((nu_o > 0).sum()),
+            "counts_exact": counts_ok, "distance_rtol_1e-12": dist_ok,
+            "pvalue_rtol_1e-12": pv_ok, "pass_exact": pass_ok,
+            "max_pvalue_rel_err": float(np.max(np.abs(pv - pv_o) / np.maximum(np.abs(pv_o), 1e-300)))
+            if pv.size else 0.0,
+            "ok": counts_ok and dist_ok and pv_ok and pass_ok}
+
+
+def parity_summary(c2, c3, c4):
+    """the line's `parity` object: every oracle check of this run and whether all passed"""
+    parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
+             "c4": c4.get("parity") if c4 else None}
+    done = [v["ok"] for v in parts.values() if v]
+    parts["all_ok"] = all(done) if done else None
+    parts["checker"] = ("oracle/ CPU restatement (pinned to the reference's fixtures), "
+                        "outside the timed regions")
+    return parts
+
+
+def c2_parity(job, seqs, outs, args, n_rows=200):
+    """C2 at full size: all sketches of the batch vs the oracle's CPU port (bit-exact rows
+    and counts), and a 200-query-row x all-refs block of the all-vs-all dist."""
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    th = _threads()
+    rows_d, cnt_d = job.fetch()
+    exp = O.sketch_batch(O.params(k=args.k, s=args.s), seqs, threads=th)
+    sk_ok = all(int(cnt_d[i]) == len(e) and np.array_equal(rows_d[i, :len(e)], e)
+                for i, e in enumerate(exp))
+    n = len(seqs)
+    rows = sample_rows(n, n_rows)
+    lengths = [args.seq_len] * n
+    g = O.dist_grid(exp, lengths, [exp[int(r)] for r in rows], [lengths[int(r)] for r in rows],
+                    args.s, args.k, 4.0 ** args.k, threads=th)
+    d = check_grid_rows(outs, n, rows, g)
+    return {"sketches": n, "sketch_rows_exact": bool(sk_ok), "dist": d,
+            "ok": bool(sk_ok) and d["ok"], "check_s": time.perf_counter() - t0}
+
+
+def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
     """C3: the -fp path on 5,000 lyn2vec-shaped 2 kb sequences, 1 GPU.
     `sketch -fp` reads at most 1,000,000 lines per call (Sketch.cpp:37, :82), i.e. 500
     sequences of 2,000 CFL k-finger lines, so the 5,000 sequences are 10 files of 500, each
@@ -297,6 +400,30 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
         same_as_dense = bool(np.array_equal(numer, outs[0].to_array(np.uint16, np_)) and
                              np.array_equal(denom, outs[1].to_array(np.uint16, np_)))
+    par = None
+    if parity:
+        # the CPU leg's checker: 200 query rows x all 5,000 references by the oracle's
+        # literal walk, `.txt` mode (whole lists, walk capped at s) and `.msh` mode (lists
+        # truncated to s as loadCapnp does, Sketch.cpp:1117-1120)
+        from oracle import oracle as O
+        t0 = time.perf_counter()
+        th = _threads()
+        qrows = sample_rows(n, 200, salt=3)
+        par = {}
+        for mode, cut in (("txt", None), ("msh", s)):
+            lists = [x if cut is None else x[:cut] for x in rows]
+            if cut is not None:
+                d_rl2 = fpmash.DeviceBuffer.from_array(ctx, np.minimum(rl, cut).astype(np.uint32))
+                fpmash._check(L.fpm_dist_dev16(ctx.h, d_R.ptr, d_rl2.ptr, d_rL.ptr, w, n, d_R.ptr,
+                                             d_rl2.ptr, d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
+                                             *[o.ptr for o in outs], ctx.stream))
+                ctx.synchronize()
+                d_rl2.free()
+            g = O.dist_grid(lists, list(rL), [lists[int(q)] for q in qrows],
+                            [rL[int(q)] for q in qrows], s, 1, 10.0, use64=False, threads=th)
+            par[mode] = check_grid_rows(outs, n, qrows, g)
+        par["ok"] = par["txt"]["ok"] and par["msh"]["ok"]
+        par["check_s"] = time.perf_counter() - t0
     for b in [d_R, d_rl, d_rL] + outs:
         b.free()
     return {"config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
@@ -310,67 +437,150 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3):
             "dist_path": fpmash.DIST_PATHS[int(st["sparse"])],
             "posting_events": st["events"], "candidate_pairs": st["candidates"],
             "pairs_sharing_a_hash": int((numer > 0).sum()),
-            "counts_equal_dense_walk": same_as_dense}
+            "counts_equal_dense_walk": same_as_dense, "parity": par}
 
 
-def c4_leg(ctx, grp, ws, rank, n=50_000, members=100, s=1000, k=21, steps=3, warmup=1):
-    """C4: one all-vs-all dist of n family-structured sketches, the query
-    rows sharded over the ranks (strong scaling).  Every GPU holds the whole reference set
-    (400 MB at n = 50k: far below one GPU's HBM, so no min-merge / ring exchange is needed,
-    as the north star prescribes); each rank sketches it (standing in for loading
-    all.msh) outside the timed region, and the timed step is its block of query rows
-    against all n references: shared-hash counts, distance, FP64 p-value, pass flags,
-    left in HBM.  The index over the references is rebuilt inside every step.  With one
-    rank the queries are the references (the library's symmetric self path)."""
-    from fpmash.shard import shard_range
+def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
+           steps=3, warmup=1, parity=True):
+    """C4: one all-vs-all dist of n family-structured sketches, sharded over
+    the ranks (strong scaling).  A timed step is the whole job on every rank:
+      1. sketch its contiguous shard of families (each family generated from its own seed,
+         so the data does not depend on the GPU count);
+      2. all-gather the sketch rows, counts and lengths (RCCL over xGMI, the "nccl" backend,
+         N x s x 8 B = 400 MB at n = 50k) -- the job's only exchange: the reference set fits
+         every GPU's HBM many times over, so no min-merge / ring rotation is needed;
+      3. dist of its query rows against all n references: shared-hash counts, distance,
+         FP64 p-value, pass flags, left in HBM (the index over the references is built
+         inside the step).
+    With one rank there is no gather and the queries are the references (the library's
+    symmetric self path)."""
+    from fpmash.shard import all_gather_rows, shard_range
     fams = n // members
     n = fams * members
-    seqs = datagen.family_dna(fams, members, 2000, sub_rate=(0.01, 0.10), seed=4000)
+    f_lo, f_hi = shard_range(fams, ws, rank)
+    lo, hi = f_lo * members, f_hi * members
+    n_loc = hi - lo
+    seqs = []
+    for f in range(f_lo, f_hi):
+        seqs += datagen.family_dna(1, members, seq_len, sub_rate=(0.01, 0.10), seed=4000 + f)
     P = fpmash.make_params(k=k, s=s)
     job = ctx.sketch_job(P, seqs)
-    job.run()
     d_rows, d_cnt, _ng, stride = job.device_output()
-    del seqs
-    lo, hi = shard_range(n, ws, rank)
-    n_loc = hi - lo
     L = fpmash.lib()
-    d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, 2000, np.uint64))
-    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]
     st = ctx.stream
+    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]
+    g = {}
+    if ws > 1:
+        import torch
+        # RCCL gathers device tensors over xGMI; without an nccl group (the 2-rank GPU test
+        # on one card) the same rows go through gloo on host tensors and back to the device
+        on_dev = grp.nccl is not None
+        dev = torch.device(f"cuda:{local}") if on_dev else torch.device("cpu")
+        loc_rows = torch.empty((n_loc, stride), dtype=torch.int64, device=dev)
+        loc_cnt = torch.empty((n_loc, 1), dtype=torch.int32, device=dev)
+        loc_len = torch.full((n_loc, 1), seq_len, dtype=torch.int64, device=dev)
+        g["len"] = all_gather_rows(loc_len, n, ws, group=grp.nccl)
+        if not on_dev:
+            g["d_rows"] = fpmash.DeviceBuffer(ctx, n * stride * 8)
+            g["d_cnt"] = fpmash.DeviceBuffer(ctx, n * 4)
+            g["d_len"] = fpmash.DeviceBuffer.from_array(ctx, g["len"].numpy())
+    else:
+        d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, seq_len, np.uint64))
+    phase = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
 
-    def run():
-        fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n,
-                                     d_rows + lo * stride * 8, d_cnt + lo * 4, d_len.ptr + lo * 8,
-                                     stride, n_loc, 8, s, k, 4.0 ** k, 1.0, 1.0,
-                                     *[o.ptr for o in outs], st))
+    def run(timed):
+        t0 = time.perf_counter()
+        job.run(st)
+        if timed:
+            ctx.synchronize()
+        if ws > 1:
+            if on_dev:
+                fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_rows.data_ptr(), d_rows,
+                                               n_loc * stride * 8))
+                fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
+            else:
+                fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_rows.data_ptr(), d_rows,
+                                               n_loc * stride * 8))
+                fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
+            ctx.synchronize()
+            t1 = time.perf_counter()
+            g["rows"] = all_gather_rows(loc_rows, n, ws, group=grp.nccl)
+            g["cnt"] = all_gather_rows(loc_cnt, n, ws, group=grp.nccl)
+            if on_dev:
+                torch.cuda.synchronize(dev)
+                R, C_, Ln = g["rows"].data_ptr(), g["cnt"].data_ptr(), g["len"].data_ptr()
+            else:
+                fpmash._check(L.fpm_memcpy_h2d(ctx.h, g["d_rows"].ptr, g["rows"].data_ptr(),
+                                               n * stride * 8))
+                fpmash._check(L.fpm_memcpy_h2d(ctx.h, g["d_cnt"].ptr, g["cnt"].data_ptr(), n * 4))
+                R, C_, Ln = g["d_rows"].ptr, g["d_cnt"].ptr, g["d_len"].ptr
+        else:
+            t1 = time.perf_counter()
+            R, C_, Ln = d_rows, d_cnt, d_len.ptr
+        t2 = time.perf_counter()
+        fpmash._check(L.fpm_dist_dev16(ctx.h, R, C_, Ln, stride, n, R + lo * stride * 8,
+                                     C_ + lo * 4, Ln + lo * 8, stride, n_loc, 8, s, k, 4.0 ** k,
+                                     1.0, 1.0, *[o.ptr for o in outs], st))
+        if timed:
+            ctx.synchronize()
+            t3 = time.perf_counter()
+            phase["sketch"] += t1 - t0
+            phase["gather"] += t2 - t1
+            phase["dist"] += t3 - t2
     for _ in range(warmup):
-        run()
+        run(False)
     ctx.synchronize()
     grp.barrier()
     t0 = time.perf_counter()
     for _ in range(steps):
-        run()
+        run(False)
     ctx.synchronize()
     el = time.perf_counter() - t0
     grp.barrier()
     el = grp.max(el)
     dst = ctx.last_dist_stats()
     cand = grp.sum(dst["candidates"])
-    for b in [d_len] + outs:
+    run(True)                                   # one more step, phase-timed (not in el)
+    par = None
+    if parity and (rank == 0 or parity == "all"):
+        # the CPU leg's checker: 50 of this rank's query rows x all n references
+        from oracle import oracle as O
+        t_c = time.perf_counter()
+        if ws > 1:
+            rows_h = g["rows"].cpu().numpy().view(np.uint64)
+            cnt_h = g["cnt"].cpu().numpy()[:, 0]
+        else:
+            rows_h, cnt_h = job.fetch()
+        refs = [rows_h[i, :cnt_h[i]] for i in range(n)]
+        lens = [seq_len] * n
+        q = sample_rows(n_loc, 50, salt=4)
+        gr = O.dist_grid(refs, lens, [refs[lo + int(x)] for x in q], [seq_len] * len(q), s, k,
+                         4.0 ** k, threads=_threads())
+        par = check_grid_rows(outs, n, q, gr)
+        par["check_s"] = time.perf_counter() - t_c
+    for b in outs:
         b.free()
+    if ws == 1:
+        d_len.free()
+    for key in ("d_rows", "d_cnt", "d_len"):
+        if key in g:
+            g[key].free()
     job.free()
-    return {"config": f"C4: all-vs-all dist of {n} family-structured 2 kb sketches (k={k}, s={s}), "
-                      f"query rows sharded over {ws} GPU(s), every GPU holding all references",
+    return {"config": f"C4: all-vs-all dist of {n} family-structured {seq_len} bp sketches "
+                      f"(k={k}, s={s}); a step = sketch own shard + all-gather of the sketch "
+                      f"rows (RCCL) + dist of own query rows vs all, {ws} GPU(s)",
             "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
+            "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
+            "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
             "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
-            "candidates_all_ranks": cand}
+            "candidates_all_ranks": cand, "parity": par}
 
 
 def main():
     args = parse()
     ws, rank, local = dist_env()
-    grp = Group(ws)
+    grp = Group(ws, local, nccl=not args.no_c4)
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
     n = len(seqs)
@@ -415,9 +625,10 @@ def main():
 
     # per-kernel times: HIP events around every launch, in separate steps after the timed
     # region (the event records add markers between launches, so they stay out of it)
+    n_timed = timing_steps(args.steps)
     ctx.set_timing(True)
     ctx.reset_timing()
-    for _ in range(max(3, min(args.steps, 10))):
+    for _ in range(n_timed):
         step()
     ctx.synchronize()
     ctx.set_timing(False)
@@ -433,10 +644,12 @@ def main():
     cnt_host = np.empty(n, dtype=np.uint32)
     fpmash._check(L.fpm_memcpy_d2h(ctx.h, cnt_host.ctypes.data, d_cnt, n * 4))
     numer_sample = d_numer.to_array(np.uint16, min(n_pairs, 1 << 20))
+    c2par = None
+    if rank == 0 and not args.no_parity:
+        c2par = c2_parity(job, seqs, (d_numer, d_denom, d_dist, d_pval, d_pass), args)
 
     bases_rank = n * args.seq_len
     total_bases = grp.sum(bases_rank) * args.steps
-    total_pairs = grp.sum(n_pairs) * args.steps
     value = total_bases / elapsed
 
     # roofline of the dominant kernel (algorithmic bytes per launch / avg launch time)
@@ -504,17 +717,20 @@ def main():
     sk_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_SKETCH, fpmash.K_MERGE)]
     di_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_INDEX, fpmash.K_PROBE,
                                                   fpmash.K_COMPARE, fpmash.K_FINALIZE)]
-    sk_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in sk_names) / args.steps
-    di_ms = sum(ktimes.get(x, {}).get("total_ms", 0.0) for x in di_names) / args.steps
+    sk_ms = per_step_ms(ktimes, sk_names, n_timed)
+    di_ms = per_step_ms(ktimes, di_names, n_timed)
+    bases_step = grp.sum(bases_rank)
+    pairs_step = grp.sum(n_pairs)
 
     fp_leg = fp_text_leg(ctx) if rank == 0 and not args.no_fp_text else None
-    c3 = c3_leg(ctx, s=args.s) if rank == 0 and not args.no_c3 else None
+    c3 = c3_leg(ctx, s=args.s, parity=not args.no_parity) if rank == 0 and not args.no_c3 else None
     c4 = None
     if not args.no_c4:
         job.free()                       # the C2 batch's buffers make room for C4's grid
         for b in (d_numer, d_denom, d_dist, d_pval, d_pass):
             b.free()
-        c4 = c4_leg(ctx, grp, ws, rank, n=args.c4_n, s=args.s, k=args.k)
+        c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
+                    parity=not args.no_parity)
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
@@ -541,10 +757,11 @@ def main():
                 "n_seqs_per_gpu": n, "seq_len": args.seq_len, "k": args.k, "s": args.s,
                 "pairs_per_gpu": n_pairs, "parallelism": f"independent batch per GPU x{ws}",
             },
-            "sketch": {"bases_per_s": total_bases / args.steps / (sk_ms * 1e-3) if sk_ms else None,
+            "kernel_timing_steps": n_timed,
+            "sketch": {"bases_per_s": bases_step / (sk_ms * 1e-3) if sk_ms else None,
                        "device_ms_per_step": sk_ms, "tiles": info["n_tiles"],
                        "kmers": info["n_kmers"]},
-            "dist": {"mpairs_per_s": total_pairs / args.steps / (di_ms * 1e-3) / 1e6 if di_ms else None,
+            "dist": {"mpairs_per_s": pairs_step / (di_ms * 1e-3) / 1e6 if di_ms else None,
                      "device_ms_per_step": di_ms,
                      "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
                      "path": fpmash.DIST_PATHS[int(dstats["sparse"])],
@@ -556,6 +773,7 @@ def main():
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
+            "parity": parity_summary(c2par, c3, c4),
         }
         print(json.dumps(line))
     job.free()

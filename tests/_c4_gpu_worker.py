@@ -1,0 +1,32 @@
+"""Worker for test_multirank.test_c4_leg_two_ranks_one_gpu (-m gpu): bench.c4_leg, the C4
+job (sketch own shard -> all-gather of the sketch rows -> dist of own query rows vs all),
+on two ranks that share the one visible GPU through libfpmash, with the rows gathered over
+gloo.  Every rank checks 50 of its query rows against the oracle; rank 0 also checks the
+gathered reference set against a single-process sketch of all sequences."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "fp-mash_amd")):
+    sys.path.insert(0, p)
+
+import bench  # noqa: E402
+import fpmash  # noqa: E402
+
+
+def main():
+    ws, rank, _local = bench.dist_env()
+    grp = bench.Group(ws)                       # gloo only: both ranks use device 0
+    ctx = fpmash.Context(0)
+    r = bench.c4_leg(ctx, grp, ws, rank, 0, n=3000, members=100, s=1000, k=21, steps=1,
+                     warmup=1, parity="all")
+    out = {"rank": rank, "parity": r["parity"], "pairs": r["pairs"],
+           "candidates_all_ranks": r["candidates_all_ranks"], "path": r["path_rank0"]}
+    print("C4RANK " + json.dumps(out), flush=True)
+    grp.barrier()
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -186,3 +186,124 @@ def read_msh(path_or_bytes):
         })
     hdr["references"] = out
     return hdr
+
+
+# ---------------------------------------------------------------------------
+# writer (test support: builds the EXPECTED .msh bytes from oracle sketches, so
+# the product's host/Msh.cpp writer is checked against an independent encoder)
+# ---------------------------------------------------------------------------
+
+class _Arena:
+    """capnp MallocMessageBuilder's allocation model (Sketch.cpp:546 uses the default
+    builder): the first segment holds max(need, 1024) words; every later segment holds
+    max(need, words allocated so far); an object goes into its pointer's segment when it
+    fits there, else into the newest segment with room, behind a far pointer + landing pad."""
+
+    FIRST = 1024
+
+    def __init__(self):
+        self.segs = []        # [bytearray of used words, capacity in words]
+        self.grow = self.FIRST
+        self.newest = None
+
+    def _try(self, s, n):
+        seg = self.segs[s]
+        used = len(seg[0]) // 8
+        if used + n > seg[1]:
+            return None
+        seg[0].extend(b"\0" * (8 * n))
+        return used
+
+    def _arena(self, n):
+        if self.newest is not None:
+            o = self._try(self.newest, n)
+            if o is not None:
+                return self.newest, o
+        size = max(n, self.grow)
+        self.grow = size if not self.segs else self.grow + size
+        self.segs.append([bytearray(), size])
+        self.newest = len(self.segs) - 1
+        return self.newest, self._try(self.newest, n)
+
+    def put(self, s, w, v):
+        struct.pack_into("<Q", self.segs[s][0], 8 * w, v & 0xFFFFFFFFFFFFFFFF)
+
+    def get(self, s, w):
+        return struct.unpack_from("<Q", self.segs[s][0], 8 * w)[0]
+
+    def obj(self, s, w, n, kind, upper):
+        """allocate n words for an object whose pointer lives at (s, w)"""
+        o = self._try(s, n)
+        if o is not None:
+            self.put(s, w, kind | (((o - (w + 1)) & 0x3FFFFFFF) << 2) | (upper << 32))
+            return s, o
+        ts, to = self._arena(n + 1)
+        self.put(s, w, 2 | (to << 3) | (ts << 32))
+        self.put(ts, to, kind | (upper << 32))
+        return ts, to + 1
+
+    def data(self):
+        n = len(self.segs)
+        tab = [n - 1] + [len(sg[0]) // 8 for sg in self.segs]
+        if len(tab) % 2:
+            tab.append(0)
+        return struct.pack(f"<{len(tab)}I", *tab) + b"".join(bytes(sg[0]) for sg in self.segs)
+
+
+def _text(A, s, w, t: bytes):
+    n = len(t) + 1
+    ts, to = A.obj(s, w, (n + 7) // 8, 1, 2 | (n << 3))
+    A.segs[ts][0][8 * to: 8 * to + len(t)] = t
+
+
+def write_msh(hdr, refs, use64=True, counts=False) -> bytes:
+    """Serialize a MinHash message the way Sketch::writeToCapnp (Sketch.cpp:536-642)
+    builds it: root, reference list (referenceListOld when the seed is 42, :549), per
+    reference name, comment, length64, hashes64/hashes32 (+ counts32), the empty locus
+    list, then the scalar fields and the alphabet.  refs: dicts with name, comment,
+    length, hashes (ascending), optional counts."""
+    A = _Arena()
+    A._arena(1)                                   # root pointer
+    rs, rw = A.obj(0, 0, 7, 0, 3 | (4 << 16))     # MinHash: 3 data words, 4 pointers
+    rp = rw + 3
+    seed = hdr.get("seed", 42)
+    ls, lw = A.obj(rs, rp + (0 if seed == 42 else 3), 1, 0, 0 | (1 << 16))
+    n = len(refs)
+    es, ew = A.obj(ls, lw, 1 + 9 * n, 1, 7 | ((9 * n) << 3))
+    A.put(es, ew, (n << 2) | ((2 | (7 << 16)) << 32))
+    for i, r in enumerate(refs):
+        dw = ew + 1 + 9 * i
+        pw = dw + 2
+        _text(A, es, pw + 2, bytes(r["name"]))
+        _text(A, es, pw + 3, bytes(r["comment"]))
+        A.put(es, dw + 1, int(r["length"]))
+        h = np.asarray(r["hashes"], dtype=np.uint64)
+        if len(h):
+            m = len(h)
+            if use64:
+                ts, to = A.obj(es, pw + 5, m, 1, 5 | (m << 3))
+                A.segs[ts][0][8 * to: 8 * (to + m)] = h.astype("<u8").tobytes()
+            else:
+                ts, to = A.obj(es, pw + 4, (m + 1) // 2, 1, 4 | (m << 3))
+                A.segs[ts][0][8 * to: 8 * to + 4 * m] = h.astype("<u4").tobytes()
+            c = r.get("counts")
+            if counts and c is not None and len(c):
+                c = np.asarray(c, dtype="<u4")
+                ts, to = A.obj(es, pw + 6, (len(c) + 1) // 2, 1, 4 | (len(c) << 3))
+                A.segs[ts][0][8 * to: 8 * to + 4 * len(c)] = c.tobytes()
+                A.put(es, dw, A.get(es, dw) | (1 << 32))
+    # locusList with an empty composite loci list (Sketch.cpp:606-621)
+    cs, cw = A.obj(rs, rp + 1, 1, 0, 0 | (1 << 16))
+    ts, to = A.obj(cs, cw, 1, 1, 7 | (0 << 3))
+    A.put(ts, to, (3 << 32))
+    # scalars (Sketch.cpp:623-630): kmer u32@0, windowSize @4, minHashesPerWindow @8,
+    # error f32 @16, hashSeed @20 (xor 42), bits 96-98
+    w0 = int(hdr["kmer"]) | (int(hdr.get("windowSize", 0)) << 32)
+    w1 = int(hdr["sketchSize"]) | (int(hdr.get("concatenated", False)) << 32) | \
+        (int(hdr.get("noncanonical", False)) << 33) | (int(hdr.get("preserveCase", False)) << 34)
+    err = struct.unpack("<I", struct.pack("<f", float(hdr.get("error", 0.0))))[0]
+    w2 = err | ((seed ^ 42) << 32)
+    for j, v in enumerate((w0, w1, w2)):
+        A.put(rs, rw + j, v)
+    _text(A, rs, rp + 2, bytes(hdr["alphabet"]))
+    return A.data()

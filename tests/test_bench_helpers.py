@@ -54,3 +54,23 @@ def test_c4_row_shards_cover_grid():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def test_sub_rates_divide_by_event_timed_steps():
+    """bench's sketch / dist sub-rates: kernel totals come from the event-timed steps run
+    after the timed region, so per-step device time divides by their count."""
+    import bench
+    for steps, n in ((1, 3), (5, 5), (20, 10), (100, 10)):
+        assert bench.timing_steps(steps) == n
+    kt = {"a": {"total_ms": 1.8, "launches": 10, "avg_ms": 0.18},
+          "b": {"total_ms": 0.2, "launches": 10, "avg_ms": 0.02}}
+    ms = bench.per_step_ms(kt, ["a", "b", "missing"], bench.timing_steps(20))
+    assert abs(ms - 0.2) < 1e-12          # = avg launch time summed over the kernels
+
+
+def test_parity_summary():
+    import bench
+    p = bench.parity_summary({"ok": True}, {"parity": {"ok": True}}, None)
+    assert p["all_ok"] is True and p["c4"] is None
+    p = bench.parity_summary({"ok": True}, {"parity": {"ok": False}}, {"parity": None})
+    assert p["all_ok"] is False

@@ -36,6 +36,22 @@ def test_msh_writer_byte_identical_roundtrip(name):
     assert p.returncode == 0 and p.stdout.startswith("same"), p.stdout + p.stderr
 
 
+@pytest.mark.parametrize("name", REF_MSH)
+def test_python_msh_writer_pinned_to_fixtures(name):
+    """The test-side encoder (mshfmt.write_msh, independent of host/Msh.cpp) rebuilds
+    every fixture .msh byte for byte from its decoded content: it is the expected-bytes
+    oracle of the full-size .msh tests below."""
+    data = open(os.path.join(GOLDEN, name), "rb").read()
+    h = mshfmt.read_msh(data)
+    use64 = h["references"][0]["hashes64"] is not None
+    refs = [dict(name=r["name"], comment=r["comment"], length=r["length"],
+                 hashes=r["hashes64"] if use64 else r["hashes32"], counts=r["counts"])
+            for r in h["references"]]
+    out = mshfmt.write_msh(h, refs, use64=use64,
+                           counts=any(r["countsSorted"] for r in h["references"]))
+    assert out == data
+
+
 def test_info_json_matches_fork_dump():
     out = run(["info", "-d", os.path.join(GOLDEN, "DNA1-sketch.msh")]).stdout
     assert out == open(os.path.join(GOLDEN, "DNA1-sketch.json"), "rb").read()
@@ -123,6 +139,34 @@ def test_sketch_individual_matches_oracle(tmp_path, oracle):
         h = r["hashes64"] if r["hashes64"] is not None else np.zeros(0, np.uint64)
         assert np.array_equal(h, e)
     assert not got["concatenated"]
+
+
+def c2_fasta(n=10000, seed=1000):
+    """Config C2's input: n x 2 kb family-structured lyn2vec-shaped records (the bench batch
+    of rank 0) as one FASTA file."""
+    from fpmash import datagen
+    seqs = datagen.family_dna(100, n // 100, 2000, sub_rate=(0.01, 0.10), seed=seed)[:n]
+    ids = datagen.lyn2vec_ids(len(seqs))
+    return seqs, ids, datagen.fasta_bytes(seqs, ids)
+
+
+@pytest.mark.gpu
+def test_sketch_c2_10k_msh_byte_identical(tmp_path, oracle):
+    """North star "bit-identical .msh" at config C2's full size: `sketch -i -k 21 -s 1000`
+    of 10,000 x 2 kb records through the drop-in CLI == the .msh the oracle's sketches
+    encode to (mshfmt.write_msh, pinned to every fixture), byte for byte."""
+    seqs, ids, fa = c2_fasta()
+    (tmp_path / "c2.fa").write_bytes(fa)
+    run(["sketch", "-i", "-k", "21", "-s", "1000", "-o", "c2", "c2.fa"], cwd=tmp_path)
+    got = (tmp_path / "c2.msh").read_bytes()
+    exp_h = oracle.sketch_batch(oracle.params(k=21, s=1000), seqs, threads=8)
+    refs = [dict(name=b"T00000" + i.encode(), comment=b"G00000" + i.encode(), length=len(s),
+                 hashes=h) for s, i, h in zip(seqs, ids, exp_h)]
+    hdr = dict(kmer=21, windowSize=0, sketchSize=1000, concatenated=False, noncanonical=False,
+               preserveCase=False, error=0.0, seed=42, alphabet=b"ACGT")
+    exp = mshfmt.write_msh(hdr, refs)
+    assert len(got) == len(exp)
+    assert got == exp
 
 
 @pytest.mark.gpu

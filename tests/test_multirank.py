@@ -6,6 +6,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -40,3 +42,19 @@ def test_shard_gather_two_ranks():
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-2000:]
     assert "shard-ok" in p.stdout
+
+
+@pytest.mark.gpu
+def test_c4_leg_two_ranks_one_gpu():
+    """bench.c4_leg at world size 2 through libfpmash (both ranks on the one visible GPU,
+    rows gathered over gloo): each rank's dist rows of the sharded job match the oracle."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "_c4_gpu_worker.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines() if l.startswith("C4RANK ")]
+    assert sorted(r["rank"] for r in res) == [0, 1]
+    for r in res:
+        assert r["parity"]["ok"], r
+        assert r["parity"]["pairs_sharing"] > 0
