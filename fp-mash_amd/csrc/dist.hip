@@ -232,21 +232,76 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 // For A[i] = c with j = #{B < c} and k = #{shared values below c}: U(c) = i + j - k.
 //
 // Rank kernel, one workgroup per query row B, one wave per candidate ref row A:
-//  * B is staged once in LDS together with a bucket table over its value range
-//    (bucket = value >> shift, 2 buckets per B slot, so <= 1 B element per bucket);
-//    bucket b holds the B positions [lo, hi) whose values fall in it.
+//  * B is staged once in LDS with a bucket directory over its value range (bucket = value
+//    >> shift, ~8 buckets per B element for CAP 1024): Bkt[b] = #{B < b << shift}, u16.
 //  * lane l takes A[64t + l] (coalesced 512-byte buffer loads, prefetched one candidate
-//    ahead into registers); j comes from a fixed-length binary search inside the bucket
-//    (the row's largest bucket sets the step count, typically 2-3), equality from B[j].
+//    ahead into registers).  j = #{B < a} and the equality test come from NP independent
+//    LDS reads Bs[lo .. lo + NP) at lo = Bkt[a >> shift]: NP = the row's largest bucket
+//    (2-4 for hash values), so every element of a's bucket is read; positions past the
+//    bucket hold larger values (later buckets, or the ~0 sentinels past the end), so
+//    j = lo + #{reads < a} and eq = any(read == a) need no bucket-end test.  No dependent
+//    search chain: one directory read, then NP reads in flight together.  Rows with a
+//    bucket past kRankProbeMax (or a ~0 value, which equals the sentinel) take a bounded
+//    binary search inside the bucket instead.
 //  * k is a running ballot count: popc of this chunk's shared lanes below l + earlier chunks.
 //  * when max(|A|, |B|) >= S, denom is S whatever #shared is, and no A element after the
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
-// No per-wave LDS image and no merge walk: ~5 LDS reads and ~40 VALU per A element.
 #ifndef FPM_RANK_WAVES
 #define FPM_RANK_WAVES 4
 #endif
 constexpr int kRankWaves = FPM_RANK_WAVES;
+constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest unrolled probe
+#ifndef FPM_RANK_EXP
+#define FPM_RANK_EXP 0               // measurement builds: 1 = A loads only, 2 = row setup only
+#endif
+#ifndef FPM_RANK_LOGB
+#define FPM_RANK_LOGB 12             // log2 buckets for CAP 1024 (CAP 2048: one more)
+#endif
+
+// One chunk of 64 A elements against B (one per lane): j = #{B < a} and the lanes whose a
+// is in B (a wave mask).
+// NP > 0 (the fast path): B's values have distinct 32-bit keys K32 = the top 32 bits of the
+// row's value window (v >> max(bits - 32, 0)), which order them exactly, and the bucket of
+// a value is the top kLogB bits of its key.  The NP reads K32[lo .. lo + NP) at lo =
+// Bkt[bucket(a)] cover a's whole bucket (NP >= the row's largest bucket); later positions
+// hold larger keys (next buckets, or the 0xFFFFFFFF sentinels past the end), so
+// p = lo + #{keys < key(a)} is the first position whose value is not below a on the key,
+// and one 64-bit read of Bs[p] settles the rest: j = p + (Bs[p] < a), eq = (Bs[p] == a).
+// A value past the last B value's bucket `top` clamps to bucket top + 1 (lo = lb, the
+// sentinels): j = lb.
+// NP = 0 (any row): 64-bit reads over the row's largest bucket (maxn), every position
+// clamped to the sentinel and tested against lb.
+template <int NP>
+__device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_t *K32,
+                                               const uint16_t *Bkt, uint32_t shift,
+                                               uint32_t kshift, uint32_t top, uint32_t lb,
+                                               uint32_t maxn, uint64_t a, uint32_t &j)
+{
+    const uint64_t t = a >> shift;
+    const bool over = t > (uint64_t)top;
+    const uint32_t lo = Bkt[over ? top + 1 : (uint32_t)t];
+    if constexpr (NP > 0) {
+        const uint32_t ka = (uint32_t)(a >> kshift);
+        uint32_t p = lo;
+#pragma unroll
+        for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
+        const uint64_t v = Bs[p];
+        j = p + (v < a ? 1u : 0u);
+        return __builtin_amdgcn_ballot_w64(v == a) & ~__builtin_amdgcn_ballot_w64(over);
+    } else {
+        uint32_t jj = lo;
+        uint64_t eqm = 0;
+        for (uint32_t q = 0; q < maxn; q++) {
+            const uint32_t p = min(lo + q, lb);
+            const uint64_t v = Bs[p];
+            jj += ((v < a) & (p < lb)) ? 1u : 0u;
+            eqm |= __builtin_amdgcn_ballot_w64((v == a) & (p < lb));
+        }
+        j = jj;
+        return eqm;
+    }
+}
 
 template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
@@ -256,11 +311,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     uint64_t qry_stride, uint32_t S, uint32_t sym, C *__restrict__ numer,
     C *__restrict__ denom, uint32_t *__restrict__ cnum, uint32_t *__restrict__ cden)
 {
-    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? 11 : 12;   // 2 * CAP buckets
+    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? FPM_RANK_LOGB : FPM_RANK_LOGB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
-    __shared__ uint64_t Bs[CAP + 1];
-    __shared__ uint32_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
-    __shared__ uint32_t s_maxn;
+    __shared__ uint64_t Bs[CAP + kRankProbeMax];
+    __shared__ uint32_t K32[CAP + kRankProbeMax];      // 32-bit keys of B (rank_chunk)
+    __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
+    __shared__ uint32_t s_maxn, s_keydup;
     const uint32_t q = xcd_row(blockIdx.x, n_qry);
     if (q >= n_qry) return;
     const uint64_t seg = row_seg[q];
@@ -270,43 +326,86 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
     const uint64_t *B = qry + (uint64_t)q * qry_stride;
-    if (threadIdx.x == 0) s_maxn = 0;
-    for (uint32_t t = threadIdx.x; t < lb; t += blockDim.x) Bs[t] = B[t];
-    // sentinel past the end: Bs[lb] >= every A value, so a search that has narrowed to an
-    // empty range (len = 0) reads a value that is not < a and stays put (no len test)
-    if (threadIdx.x == 0) Bs[lb] = ~0ULL;
+    if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; }
+    {
+        // stage B: every load of the row issued before the first LDS store (4 in flight per
+        // thread: CAP / 256 with CAP 1024; a serial load-store loop paid the global latency
+        // once per value)
+        constexpr int kStage = (CAP + 64 * kRankWaves - 1) / (64 * kRankWaves);
+        uint64_t v[kStage];
+#pragma unroll
+        for (int u = 0; u < kStage; u++) {
+            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
+            v[u] = t < lb ? B[t] : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kStage; u++) {
+            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
+            if (t < lb) Bs[t] = v[u];
+        }
+    }
+    // sentinels past the end: no A value is below them
+    if (threadIdx.x < kRankProbeMax) {
+        Bs[lb + threadIdx.x] = ~0ULL;
+        K32[lb + threadIdx.x] = 0xFFFFFFFFu;
+    }
     __syncthreads();
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
     const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
-    // bucket b = values [b << shift, (b + 1) << shift) = B positions [Bkt[b], Bkt[b + 1]).
-    // Bkt[b] = #{B < b << shift}: element j owns the buckets after its predecessor's bucket
-    // up to its own, so each thread fills one gap (O(lb + buckets) writes, no searches).
+    const uint32_t kshift = bits > 32 ? bits - 32 : 0;
+    // top = the last B value's bucket; the directory stops at Bkt[top + 1] = lb (filling
+    // every bucket up to kBuckets cost one thread up to kBuckets / 2 serial stores)
+    const uint32_t top = (uint32_t)(bmax >> shift);
+    // keys (distinct and below the sentinel for the fast path, else the row takes NP = 0)
+    // and the bucket directory: bucket b = values [b << shift, (b + 1) << shift) = B
+    // positions [Bkt[b], Bkt[b + 1]).  Element j owns the buckets after its predecessor's
+    // bucket up to its own, so each thread fills one gap.
+    uint32_t dup = 0;
     for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
-        const uint32_t bj = j < lb ? (uint32_t)(Bs[j] >> shift) : kBuckets;
-        const uint32_t bp = j > 0 ? (uint32_t)(Bs[j - 1] >> shift) + 1 : 0;
-        for (uint32_t b = bp; b <= bj; b++) Bkt[b] = j;
+        const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
+        if (j < lb) {
+            const uint32_t k = (uint32_t)(v >> kshift);
+            K32[j] = k;
+            dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
+        }
+        const uint32_t bj = j < lb ? (uint32_t)(v >> shift) : top + 1;
+        const uint32_t bp = j > 0 ? (uint32_t)(vp >> shift) + 1 : 0;
+        for (uint32_t b = bp; b <= bj; b++) Bkt[b] = (uint16_t)j;
     }
+    if (dup) s_keydup = 1;
     __syncthreads();
+    // the largest bucket: element j is the (j - Bkt[bucket(j)] + 1)-th of its bucket
     uint32_t mx = 0;
-    for (uint32_t b = threadIdx.x; b < kBuckets; b += blockDim.x) mx = max(mx, Bkt[b + 1] - Bkt[b]);
+    for (uint32_t j = threadIdx.x; j < lb; j += blockDim.x)
+        mx = max(mx, j + 1 - (uint32_t)Bkt[(uint32_t)(Bs[j] >> shift)]);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-    if (lane == 0) atomicMax(&s_maxn, mx);
+    if (lane == 0 && mx) atomicMax(&s_maxn, mx);
     __syncthreads();
-    const uint32_t steps = 32 - __clz(s_maxn);          // lower_bound steps for the largest bucket
+    const uint32_t maxn = s_maxn;
+#if FPM_RANK_EXP == 2
+    if (maxn < 1000000) return;      // measurement: the per-row setup only
+#endif
+    // probe width (row-uniform): unrolled reads for buckets of up to 2 / 3 / 4 / 8 values;
+    // 0 = the clamped loop (a crowded bucket, or keys that do not order the row)
+    const uint32_t np = s_keydup ? 0u
+                      : maxn <= 2 ? 2u : maxn <= 3 ? 3u : maxn <= 4 ? 4u
+                      : maxn <= (uint32_t)kRankProbeMax ? (uint32_t)kRankProbeMax : 0u;
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
-    // A rows are read in groups of kGroup chunks (64 x u64 each) through a bounds-checked
-    // buffer descriptor (reads past ld return 0).  Three register groups: `cur` (being
-    // ranked), `nxt` (this candidate's next group, issued before `cur` is ranked) and `pf`
-    // (the next candidate's first group, issued when a candidate starts): 24 VGPRs of row
-    // data, and the groups after an early exit are never loaded.
+    // A rows are read in chunks of 128 values, 16 B per lane (lane l holds A[i0 + 2l] and
+    // A[i0 + 2l + 1]: 16-B loads run at about twice the rate of 8-B ones), in groups of
+    // kGroup chunks through a bounds-checked buffer descriptor (reads past ld return 0).
+    // Three register groups: `cur` (being ranked), `nxt` (this candidate's next group,
+    // issued before `cur` is ranked) and `pf` (the next candidate's first group, issued when
+    // a candidate starts); the groups after an early exit are never loaded.
 #ifndef FPM_RANK_GROUP
-#define FPM_RANK_GROUP 4
+#define FPM_RANK_GROUP 1
 #endif
     constexpr int kGroup = FPM_RANK_GROUP;
+    constexpr uint32_t kChunk = 128;
     struct Row { __amdgpu_buffer_rsrc_t rsrc; uint32_t la; uint64_t o; };
     auto open_row = [&](uint64_t o) -> Row {
         const uint32_t rr = __builtin_amdgcn_readfirstlane((uint32_t)(o - pair_row));
@@ -321,113 +420,127 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         R.o = o;
         return R;
     };
-    auto load_group = [&](const Row &R, uint32_t gi, uint64_t (&dst)[kGroup]) {
+    struct Pair { uint64_t e0, e1; };
+    auto load_group = [&](const Row &R, uint32_t gi, Pair (&dst)[kGroup]) {
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * 64 + lane) * 8u, 0, 0);
-            dst[u] = ((uint64_t)v[1] << 32) | v[0];
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(R.rsrc, (t * kChunk + 2 * lane) * 8u,
+                                                                 0, 0);
+            dst[u].e0 = ((uint64_t)v[1] << 32) | v[0];
+            dst[u].e1 = ((uint64_t)v[3] << 32) | v[2];
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
         return cand[base + __builtin_amdgcn_readfirstlane(cc)];
     };
-    uint64_t cur[kGroup], nxt[kGroup], pf[kGroup];
-    Row Rc{};
-    if (wave < n) { Rc = open_row(cand_at(wave)); load_group(Rc, 0, pf); }
-    for (uint32_t c = wave; c < n; c += kRankWaves) {
-        const Row R = Rc;
+    // one group of kGroup chunks: shared-hash count below the union rank S (cnt), shared
+    // values so far (shared_below); returns the union rank of the last valid element of the
+    // group's last chunk
+    auto rank_group = [&](auto probe, uint32_t g0, uint32_t la, const Pair (&cur)[kGroup],
+                          uint32_t &shared_below, uint32_t &cnt) -> uint32_t {
+        uint32_t j0[kGroup], j1[kGroup];
+        uint64_t m0[kGroup], m1[kGroup];
+#if FPM_RANK_EXP == 1
+        // measurement: loads only (no LDS probes)
 #pragma unroll
-        for (int u = 0; u < kGroup; u++) cur[u] = pf[u];
-        if (c + kRankWaves < n) { Rc = open_row(cand_at(c + kRankWaves)); load_group(Rc, 0, pf); }
-        const uint32_t la = R.la;
-        const uint64_t o = R.o;
-        const bool need_all = la < S && lb < S;           // denom depends on #shared
-        const uint32_t nch = (la + 63) / 64;
-        const uint32_t ngr = (nch + kGroup - 1) / kGroup;
-        uint32_t shared_below = 0, cnt = 0;
-        for (uint32_t gi = 0; gi < ngr; gi++) {
-            if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
-            const uint32_t g0 = gi * kGroup;
-            // bucket reads and search steps of the group's chunks are independent, so each
-            // LDS round trip carries kGroup reads
-            uint32_t lo[kGroup], len[kGroup];
-            bool act[kGroup];
+        for (int g = 0; g < kGroup; g++) {
+            m0[g] = __builtin_amdgcn_ballot_w64(cur[g].e0 & 1); j0[g] = (uint32_t)cur[g].e0 & 7;
+            m1[g] = __builtin_amdgcn_ballot_w64(cur[g].e1 & 1); j1[g] = (uint32_t)cur[g].e1 & 7;
+        }
+#else
 #pragma unroll
-            for (int g = 0; g < kGroup; g++) {
-                const uint32_t i = (g0 + g) * 64 + lane;
-                const uint64_t a = cur[g];
-                act[g] = i < la && lb && a <= bmax;
-                // every index below stays inside the LDS arrays (bk < kBuckets, lo + half
-                // <= lb <= CAP), so the reads are unconditional and the tests bitwise: a
-                // short-circuit && would become a branch with its own lgkmcnt(0) wait
-                const uint32_t bk = act[g] ? (uint32_t)(a >> shift) : 0;
-                const uint32_t b0 = Bkt[bk], b1 = Bkt[bk + 1];
-                lo[g] = b0;
-                len[g] = act[g] ? b1 - b0 : 0;
+        for (int g = 0; g < kGroup; g++) {
+            m0[g] = probe(cur[g].e0, j0[g]);
+            m1[g] = probe(cur[g].e1, j1[g]);
+        }
+#endif
+        uint32_t u_last = 0;
+#pragma unroll
+        for (int g = 0; g < kGroup; g++) {
+            const uint32_t i0 = (g0 + g) * kChunk;
+            // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
+            const int rem = (int)la - (int)i0;
+            const int r0 = (rem + 1) >> 1, r1 = rem >> 1;   // lanes whose e0 / e1 are valid
+            const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
+            const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
+            const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u)) +
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(a1 >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
+            const uint32_t k0 = shared_below + below;
+            const uint32_t k1 = k0 + (uint32_t)((a0 >> lane) & 1);
+            const uint32_t i = i0 + 2 * lane;
+            const uint32_t u0 = i + j0[g] - k0, u1 = i + 1 + j1[g] - k1;   // union ranks
+            cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
+                   __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
+            shared_below += __popcll(a0) + __popcll(a1);
+            if (g == kGroup - 1) {
+                const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
+                u_last = (uint32_t)__builtin_amdgcn_readlane((int)((e & 1) ? u1 : u0), (int)(e >> 1));
             }
-            for (uint32_t st = 0; st < steps; st++) {
+        }
+        return u_last;
+    };
+    auto run = [&](auto probe) {
+        Pair cur[kGroup], nxt[kGroup], pf[kGroup];
+        Row Rc{};
+        if (wave < n) { Rc = open_row(cand_at(wave)); load_group(Rc, 0, pf); }
+        for (uint32_t c = wave; c < n; c += kRankWaves) {
+            const Row R = Rc;
 #pragma unroll
-                for (int g = 0; g < kGroup; g++) {
-                    const uint32_t half = len[g] >> 1;
-                    // len = 0: lo is the lower bound, so Bs[lo] (or the sentinel) >= a
-                    const uint64_t bv = Bs[lo[g] + half];
-                    const bool less = bv < cur[g];
-                    lo[g] = less ? lo[g] + half + 1 : lo[g];
-                    len[g] = less ? len[g] - half - 1 : half;
+            for (int u = 0; u < kGroup; u++) cur[u] = pf[u];
+            if (c + kRankWaves < n) { Rc = open_row(cand_at(c + kRankWaves)); load_group(Rc, 0, pf); }
+            const uint32_t la = R.la;
+            const uint64_t o = R.o;
+            const bool need_all = la < S && lb < S;       // denom depends on #shared
+            const uint32_t nch = (la + kChunk - 1) / kChunk;
+            const uint32_t ngr = (nch + kGroup - 1) / kGroup;
+            uint32_t shared_below = 0, cnt = 0;
+            for (uint32_t gi = 0; gi < ngr; gi++) {
+                if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
+                const uint32_t g0 = gi * kGroup;
+                const uint32_t u_last = rank_group(probe, g0, la, cur, shared_below, cnt);
+                // union rank of the group's last element (the group is full when g0 + kGroup
+                // <= nch); later A elements rank higher
+                if (!need_all && g0 + kGroup <= nch && u_last >= S) break;
+#pragma unroll
+                for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
+            }
+            if (lane == 0) {
+                const uint64_t un = (uint64_t)la + lb - shared_below;
+                const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
+                if (cnum) {      // compact: the candidate finalize scatters (and mirrors)
+                    cnum[base + c] = cnt;
+                    cden[base + c] = dn;
+                    continue;
+                }
+                numer[o] = (C)cnt;
+                denom[o] = (C)dn;
+                const uint32_t r = (uint32_t)(o - pair_row);
+                if (sym && r != q) {                      // mirror cell (r, q)
+                    const uint64_t o2 = (uint64_t)r * n_ref + q;
+                    numer[o2] = (C)cnt;
+                    denom[o2] = (C)dn;
                 }
             }
-            // all kGroup equality reads first (j <= lb, Bs[lb] is the sentinel; chunks past
-            // nch have act = 0), then the ballots: one LDS round trip for the group
-            uint64_t bj[kGroup];
-            uint32_t j[kGroup];
-#pragma unroll
-            for (int g = 0; g < kGroup; g++) {
-                j[g] = act[g] ? lo[g] : lb;
-                bj[g] = Bs[j[g]];
-            }
-            uint32_t u_last = 0;
-#pragma unroll
-            for (int g = 0; g < kGroup; g++) {
-                const uint32_t i = (g0 + g) * 64 + lane;
-                const bool eq = act[g] & (j[g] < lb) & (bj[g] == cur[g]);
-                const uint64_t bal = __builtin_amdgcn_ballot_w64(eq);
-                const uint32_t k = shared_below + __builtin_amdgcn_mbcnt_hi(
-                                       (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                const uint32_t u = i + j[g] - k;          // union rank of A[i] (valid lanes)
-                cnt += __popcll(__builtin_amdgcn_ballot_w64(eq & (u < S)));
-                shared_below += __popcll(bal);
-                if (g == kGroup - 1) u_last = u;
-            }
-            // union rank of the group's last element (the group is full when g0 + kGroup <=
-            // nch); later A elements rank higher
-            bool done = false;
-            if (!need_all && g0 + kGroup <= nch) {
-                const uint32_t last = min(la - 1 - (g0 + kGroup - 1) * 64, 63u);
-                done = (uint32_t)__builtin_amdgcn_readlane((int)u_last, (int)last) >= S;
-            }
-            if (done) break;
-#pragma unroll
-            for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
         }
-        if (lane == 0) {
-            const uint64_t un = (uint64_t)la + lb - shared_below;
-            const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
-            if (cnum) {          // compact: the candidate finalize scatters (and mirrors)
-                cnum[base + c] = cnt;
-                cden[base + c] = dn;
-                continue;
-            }
-            numer[o] = (C)cnt;
-            denom[o] = (C)dn;
-            const uint32_t r = (uint32_t)(o - pair_row);
-            if (sym && r != q) {                          // mirror cell (r, q)
-                const uint64_t o2 = (uint64_t)r * n_ref + q;
-                numer[o2] = (C)cnt;
-                denom[o2] = (C)dn;
-            }
-        }
+    };
+    const uint16_t *bk_ = Bkt;
+    const uint64_t *bs_ = Bs;
+    const uint32_t *k_ = K32;
+#define FPM_RANK_NP(NP_) \
+    run([&](uint64_t a, uint32_t &j) { \
+        return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+    switch (np) {
+    case 2: FPM_RANK_NP(2); break;
+    case 3: FPM_RANK_NP(3); break;
+    case 4: FPM_RANK_NP(4); break;
+    case kRankProbeMax: FPM_RANK_NP(kRankProbeMax); break;
+    default: FPM_RANK_NP(0); break;
     }
+#undef FPM_RANK_NP
 }
 
 template <typename C>

@@ -74,6 +74,9 @@ struct fpm_ctx {
     int dist_mode = FPM_DIST_AUTO;
     // dense walk of u32 lists on 16-bit rank images (FPM_DENSE_IMG=0 turns it off, A/B)
     bool dense_img = true;
+    // FPM_FILL_SERIAL=1 runs the sparse dist's fill before the candidate compare instead of
+    // beside it (measurement only: per-kernel times without the overlap)
+    bool fill_serial = false;
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
     const unsigned long long *last_cand_dev = nullptr;   // the last sparse call's counter
@@ -176,6 +179,7 @@ int fpm_ctx_create(int device, fpm_ctx **out)
     fpm_ctx *ctx = new fpm_ctx();
     ctx->device = device;
     if (const char *v = getenv("FPM_DENSE_IMG")) ctx->dense_img = atoi(v) != 0;
+    if (const char *v = getenv("FPM_FILL_SERIAL")) ctx->fill_serial = atoi(v) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1076,7 +1080,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     cden = cnum + cap;
                 }
             }
-            if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+            if (fill_pending && (!cnum || ctx->fill_serial))
+                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             {
                 TimedLaunch tl(ctx, FPM_K_COMPARE, st);
                 if (rows_merge)

@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for i in $(seq 1 "$N"); do
   for L in A B; do
     lib=$A; [ "$L" = B ] && lib=$B
-    FPMASH_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline \
+    FPMASH_LIB=$lib timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-parity \
       > gpurun_out/ab_$L$i.json 2>&1 || exit 1
     python3 -c "
 import json,sys; d=json.loads(open('gpurun_out/ab_$L$i.json').read().strip().splitlines()[-1])
