@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 RefSeq-scale sketch leg")
+    ap.add_argument("--c5-genomes", type=int, default=1000)
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
     return ap.parse_args()
@@ -69,7 +71,7 @@ def parse_args_for_test(**kw):
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
-                           no_parity=True)
+                           no_parity=True, no_c5=True, c5_genomes=1000)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -301,10 +303,11 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4):
+def parity_summary(c2, c3, c4, c5=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
-             "c4": c4.get("parity") if c4 else None}
+             "c4": c4.get("parity") if c4 else None,
+             "c5": c5.get("parity") if c5 else None}
     done = [v["ok"] for v in parts.values() if v]
     parts["all_ok"] = all(done) if done else None
     parts["checker"] = ("oracle/ CPU restatement (pinned to the reference's fixtures), "
@@ -577,6 +580,129 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "candidates_all_ranks": cand, "parity": par}
 
 
+_ACGT_LUT = None
+
+
+def c5_genome(g, length):
+    """Synthetic C5 genome g: uniform ACGT from its own seed (the data does not depend on the
+    GPU count), 2 bits of a random byte per base."""
+    global _ACGT_LUT
+    if _ACGT_LUT is None:
+        acgt = np.frombuffer(b"ACGT", np.uint8)
+        b = np.arange(256)
+        _ACGT_LUT = np.stack([acgt[(b >> 6) & 3], acgt[(b >> 4) & 3], acgt[(b >> 2) & 3],
+                              acgt[b & 3]], axis=1).astype(np.uint8)
+    rng = np.random.default_rng(5000 + g)
+    r = rng.integers(0, 256, size=(length + 3) // 4, dtype=np.uint8)
+    return _ACGT_LUT[r].reshape(-1)[:length].tobytes()
+
+
+def balanced_file_shards(lengths, ws):
+    """Contiguous file ranges per rank balanced by bases: rank r takes the files
+    whose base-count prefix midpoint falls in [r, r + 1) / ws of the total."""
+    tot = float(sum(lengths)) or 1.0
+    bounds = [0] * (ws + 1)
+    acc = 0
+    r = 1
+    for i, L in enumerate(lengths):
+        mid = (acc + L / 2.0) / tot
+        while r < ws and mid >= r / ws:
+            bounds[r] = i
+            r += 1
+        acc += L
+    for rr in range(r, ws + 1):
+        bounds[rr] = len(lengths)
+    return [(bounds[i], bounds[i + 1]) for i in range(ws)]
+
+
+def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21, steps=2,
+           warmup=1, parity=True):
+    """C5: RefSeq-scale sketch of n_genomes x length bp, k=21, s=10,000, default
+    (per-file, concatenated) mode: one sketch per genome.  Files are sharded over the ranks
+    as contiguous ranges balanced by bases; each rank stages its genomes in HBM once and the
+    timed step is its sketch kernels (tile hashing + bottom-s, then each genome's merge
+    rounds).  After the timed steps the per-genome sketches are gathered to rank 0 in file
+    order (the ordered reassembly); rank 0 checks the first and the last genome against the
+    oracle."""
+    from concurrent.futures import ThreadPoolExecutor
+    lengths = [length] * n_genomes
+    lo, hi = balanced_file_shards(lengths, ws)[rank]
+    with ThreadPoolExecutor(max_workers=min(16, _threads())) as ex:
+        seqs = list(ex.map(lambda g: c5_genome(g, length), range(lo, hi)))
+    n_loc = hi - lo
+    P = fpmash.make_params(k=k, s=s)
+    job = ctx.sketch_job(P, seqs, groups=list(range(n_loc)), n_groups=n_loc)
+    info = job.info()
+    del seqs
+    st = ctx.stream
+    for _ in range(warmup):
+        job.run(st)
+    ctx.synchronize()
+    grp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        job.run(st)
+    ctx.synchronize()
+    el = time.perf_counter() - t0
+    grp.barrier()
+    el_max = grp.max(el)
+    # kernel times of this rank (HIP events, extra runs outside the timed ones)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    job.run(st)
+    ctx.synchronize()
+    ctx.set_timing(False)
+    kt = {}
+    dev_ms = 0.0
+    for kid in (fpmash.K_SKETCH, fpmash.K_MERGE):
+        tot, cnt = ctx.kernel_time(kid)
+        kt[fpmash.KERNEL_NAMES[kid]] = {"ms": tot, "launches": cnt}
+        dev_ms += tot
+    ctx.reset_timing()
+    rows, cnt = job.fetch()
+    job.free()
+    # ordered reassembly on rank 0 (host rows over gloo: 80 KB per genome)
+    if ws > 1:
+        import torch
+        from fpmash.shard import all_gather_rows
+        m = max(h - l for l, h in balanced_file_shards(lengths, ws))
+        buf = np.zeros((m, s + 1), np.int64)
+        buf[:n_loc, :s] = rows.view(np.int64)
+        buf[:n_loc, s] = cnt
+        parts = [torch.empty((m, s + 1), dtype=torch.int64) for _ in range(ws)]
+        grp.dist.all_gather(parts, torch.from_numpy(buf))
+        spans = balanced_file_shards(lengths, ws)
+        allr = np.concatenate([parts[r].numpy()[: h - l] for r, (l, h) in enumerate(spans)])
+        rows_all, cnt_all = allr[:, :s].view(np.uint64), allr[:, s].astype(np.uint32)
+    else:
+        rows_all, cnt_all = rows, cnt
+    bases_loc = n_loc * length
+    alg = info["seq_bytes"] + int(cnt.astype(np.uint64).sum()) * 8
+    out = {"config": f"C5: {n_genomes} x {length} bp genomes, k={k}, s={s}, one sketch per "
+                     f"genome, files sharded over {ws} GPU(s) (contiguous, balanced by bases)",
+           "n_gpus": ws, "genomes": n_genomes, "bases": n_genomes * length, "steps": steps,
+           "ms_per_step": el_max / steps * 1e3,
+           "bases_per_s": n_genomes * length / (el_max / steps), "scaling": "strong",
+           "rank0": {"genomes": n_loc, "bases": bases_loc, "device_ms": dev_ms,
+                     "bases_per_s_device": bases_loc / (dev_ms * 1e-3) if dev_ms else None,
+                     "alg_bytes": alg,
+                     "alg_GBps": alg / (dev_ms * 1e-3) / 1e9 if dev_ms else None,
+                     "frac_hbm": alg / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if dev_ms else None,
+                     "tiles": info["n_tiles"], "kernels": kt},
+           "reassembled_genomes": int(len(rows_all)) if rank == 0 else None}
+    if parity and rank == 0:
+        from oracle import oracle as O
+        t_c = time.perf_counter()
+        idx = sorted({0, n_genomes - 1})
+        exp = O.sketch_batch(O.params(k=k, s=s), [c5_genome(g, length) for g in idx],
+                             threads=2)
+        ok = [bool(int(cnt_all[g]) == len(e) and np.array_equal(rows_all[g, :len(e)], e))
+              for g, e in zip(idx, exp)]
+        out["parity"] = {"genomes_checked": idx, "sketch_exact": ok, "ok": all(ok),
+                         "check_s": time.perf_counter() - t_c}
+    return out
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -732,6 +858,10 @@ def main():
         c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
                     parity=not args.no_parity)
 
+    c5 = None
+    if not args.no_c5:
+        c5 = c5_leg(ctx, grp, ws, rank, n_genomes=args.c5_genomes, parity=not args.no_parity)
+
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seqs)
@@ -769,11 +899,12 @@ def main():
             "fp_text": fp_leg,
             "c3_fp": c3,
             "c4_dist": c4,
+            "c5_sketch": c5,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4),
+            "parity": parity_summary(c2par, c3, c4, c5),
         }
         print(json.dumps(line))
     job.free()

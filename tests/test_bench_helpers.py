@@ -74,3 +74,25 @@ def test_parity_summary():
     assert p["all_ok"] is True and p["c4"] is None
     p = bench.parity_summary({"ok": True}, {"parity": {"ok": False}}, {"parity": None})
     assert p["all_ok"] is False
+
+
+def test_c5_file_shards_balanced_by_bases():
+    """bench.balanced_file_shards: contiguous file ranges covering every file once, in
+    order, each rank's bases within one file of the even share."""
+    import bench
+    rng = np.random.default_rng(3)
+    for ws in (1, 2, 3, 4, 8):
+        for lengths in ([5] * 1000, list(rng.integers(1, 100, size=37)), [10, 1, 1, 1, 1, 10]):
+            spans = bench.balanced_file_shards(lengths, ws)
+            assert spans[0][0] == 0 and spans[-1][1] == len(lengths)
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            share = sum(lengths) / ws
+            for lo, hi in spans:
+                assert abs(sum(lengths[lo:hi]) - share) <= max(lengths)
+
+
+def test_c5_genome_deterministic():
+    import bench
+    a = bench.c5_genome(7, 1001)
+    assert a == bench.c5_genome(7, 1001) and a != bench.c5_genome(8, 1001)
+    assert len(a) == 1001 and set(a) <= set(b"ACGT")
