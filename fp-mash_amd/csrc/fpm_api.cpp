@@ -898,14 +898,135 @@ struct DistFinal {
     uint8_t *pass;
 };
 
+// bucket index geometry for E entries over n_ref rows: ~2.4 entries per bucket (2^nbits >=
+// E/4, at most 2^24 buckets); entries are u32 (ref id in rbits, key fingerprint in the other
+// >= 8 bits).  4K level-2 counters (16 KiB of LDS) and a 16 MB directory at the bench's
+// E = 1e7.  Same-box A/B: E/2 buckets cost 0.04 ms more in the bucket pass than the extra
+// probe events saved; E/8 a wash.
+static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
+{
+    IdxGeom geom{};
+    uint32_t rbits = 1, lg = 1;
+    while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
+    while (lg < 40 && (1ULL << lg) < E) lg++;
+    geom.l2 = lg > kIdxL1 + 2 ? std::min<uint32_t>(lg - 2 - kIdxL1, 14) : 1;
+    geom.nbits = kIdxL1 + geom.l2;
+    geom.rbits = rbits;
+    geom.fbits = 32 - rbits;
+    geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
+    return geom;
+}
+
+// A reference set resident on the device with its bucket index built once (fpm_refset_*):
+// query blocks probe it without re-uploading the references or rebuilding the index.
+struct fpm_refset {
+    fpm_ctx *ctx = nullptr;
+    // reference rows (owned when uploaded from host buffers)
+    const void *ref = nullptr;
+    const uint32_t *ref_len = nullptr;
+    const uint64_t *ref_length = nullptr;
+    uint64_t ref_stride = 0;
+    uint32_t n_ref = 0, hash_bytes = 0, sketch_size = 0;
+    void *own[3] = {nullptr, nullptr, nullptr};
+    // index buffers (slot ids as in compare_impl), the largest indexed key, host state
+    fpm_ctx::Slot slot[16];
+    unsigned long long *kmax = nullptr;
+    IdxGeom geom{};
+    bool sparse_ok = false;       // the index exists (the sparse path is possible)
+    bool ref_unsorted = false;    // some reference row is unsorted / carries duplicates
+    bool deduped = false;         // the index holds launch_dedup_rows copies (slots 10, 11)
+    uint64_t mr = 0;              // their row stride
+    // per-query-block host buffers (fpm_refset_dist): pinned staging + device copies
+    void *h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    fpm_ctx::Slot qslot[10];
+};
+
+static hipError_t slot_buf(fpm_ctx::Slot &s, size_t bytes, void **out)
+{
+    if (s.bytes < bytes) {
+        if (s.p) { hipError_t e = hipFree(s.p); if (e != hipSuccess) return e; }
+        s.p = nullptr;
+        s.bytes = 0;
+        size_t b = bytes + bytes / 8 + 256;
+        hipError_t e = hipMalloc(&s.p, b);
+        if (e != hipSuccess) return e;
+        s.bytes = b;
+    }
+    *out = s.p;
+    return hipSuccess;
+}
+
+// Build the reference index of a resident set (once): over the raw rows, or, when a row is
+// unsorted / carries duplicates (-fp lists) and min(stride, S) <= kDedupMax, over their
+// sorted distinct copies (the probe then sees each value once per list).
+static int refset_build_index(fpm_refset *rs, hipStream_t st)
+{
+    fpm_ctx *ctx = rs->ctx;
+    const uint64_t E = (uint64_t)rs->n_ref * rs->ref_stride;
+    IdxGeom geom = make_geom(rs->n_ref, E);
+    rs->sparse_ok = E > 0 && geom.rbits <= 24 && E < (1ULL << 31);
+    if (!rs->sparse_ok) return FPM_OK;
+    void *ctr;
+    HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
+    if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
+    if (!rs->kmax) HIP_TRY(hipMalloc((void **)&rs->kmax, 8));
+    uint32_t *unsorted = (uint32_t *)((unsigned long long *)ctr + 66);
+    auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom g) -> int {
+        const uint64_t nh = (uint64_t)(1u << kIdxL1) * g.ntiles;
+        const uint64_t En = (uint64_t)rs->n_ref * stride;
+        void *tile_hist, *tile_off, *tent, *dir, *entries, *scan_s;
+        HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
+        HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
+        HIP_TRY(scratch(ctx, 2, En * 8, &tent));
+        HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
+        HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
+        HIP_TRY(slot_buf(rs->slot[5], En * 4, &entries));
+        HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+        HIP_TRY(hipMemsetAsync(rs->kmax, 0, 8, st));
+        TimedLaunch tl(ctx, FPM_K_INDEX, st);
+        HIP_TRY(launch_idx_build(rows, len, stride, rs->n_ref, rs->hash_bytes, g,
+                                 (uint32_t *)tile_hist, (uint32_t *)tile_off, (uint32_t *)scan_s,
+                                 (uint64_t *)tent, (uint32_t *)dir, (uint32_t *)entries,
+                                 unsorted, nullptr, st));
+        tl.done();
+        return FPM_OK;
+    };
+    geom.kmax = rs->kmax;
+    if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom)) return rc;
+    HIP_TRY(hipMemcpyAsync(ctx->host_counters, ctr, 67 * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
+    rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
+    rs->deduped = rs->ref_unsorted && rs->mr <= kDedupMax;
+    if (rs->deduped) {
+        void *dref, *dref_len;
+        HIP_TRY(slot_buf(rs->slot[10], (size_t)rs->n_ref * rs->mr * rs->hash_bytes, &dref));
+        HIP_TRY(slot_buf(rs->slot[11], (size_t)rs->n_ref * 4, &dref_len));
+        {
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(launch_dedup_rows(rs->ref, rs->ref_len, rs->ref_stride, rs->n_ref,
+                                      rs->hash_bytes, rs->sketch_size, dref,
+                                      (uint32_t *)dref_len, rs->mr, st));
+            tl.done();
+        }
+        geom = make_geom(rs->n_ref, (uint64_t)rs->n_ref * rs->mr);
+        geom.kmax = rs->kmax;
+        if (int rc = build(dref, (const uint32_t *)dref_len, rs->mr, geom)) return rc;
+    }
+    rs->geom = geom;
+    return FPM_OK;
+}
+
 // The grid compare: dense walk, or bucket index + probe + candidate kernel (sparse).
-// With `fin`, a sparse run also finalizes and sets *finalized.
+// With `fin`, a sparse run also finalizes and sets *finalized.  With `rs`, the references
+// are that resident set and its index is reused (not rebuilt).
 static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
                         uint32_t hash_bytes, uint32_t sketch_size, Counts cnt,
                         void *stream, const DistFinal *fin = nullptr,
-                        bool *finalized = nullptr)
+                        bool *finalized = nullptr, fpm_refset *rs = nullptr)
 {
     if (finalized) *finalized = false;
     if (int rc = set_device(ctx)) return rc;
@@ -920,105 +1041,124 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
                       (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
     if (E == 0) try_sparse = false;
-    // bucket index geometry: ~2.4 entries per bucket (2^nbits >= E/4, at most 2^24 buckets);
-    // entries are u32 (ref id in rbits, key fingerprint in the other >= 8 bits)
-    // bucket index geometry for E entries over n_ref rows
-    const auto make_geom = [n_ref](uint64_t E) {
-        IdxGeom geom{};
-        uint32_t rbits = 1, lg = 1;
-        while (rbits < 32 && (1ULL << rbits) < n_ref) rbits++;
-        while (lg < 40 && (1ULL << lg) < E) lg++;
-        // 2^nbits >= E/4 buckets (~2.4 entries per bucket): 4K level-2 counters (16 KiB of
-        // LDS) and a 16 MB directory at the bench's E = 1e7.  Same-box A/B: E/2 buckets cost
-        // 0.04 ms more in the bucket pass than the extra probe events saved; E/8 a wash.
-        geom.l2 = lg > kIdxL1 + 2 ? std::min<uint32_t>(lg - 2 - kIdxL1, 14) : 1;
-        geom.nbits = kIdxL1 + geom.l2;
-        geom.rbits = rbits;
-        geom.fbits = 32 - rbits;
-        geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
-        return geom;
-    };
-    IdxGeom geom = make_geom(E);
+    IdxGeom geom = make_geom(n_ref, E);
     if (geom.rbits > 24 || E >= (1ULL << 31)) try_sparse = false;
+    if (rs && !rs->sparse_ok) try_sparse = false;
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
     bool fill_pending = false;
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
-        void *tile_hist, *tile_off, *tent, *dir, *entries, *scan_s, *ctr;
-        HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
-        HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
-        HIP_TRY(scratch(ctx, 2, E * 8, &tent));
-        HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir));
-        HIP_TRY(scratch(ctx, 5, E * 4, &entries));
-        HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
+        void *ctr;
         HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
         if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
         // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
         // [68] the largest indexed key (the bucket scale)
         unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
         uint32_t *unsorted = (uint32_t *)(events + 66);
-        geom.kmax = events + 68;
-        {
-            TimedLaunch tl(ctx, FPM_K_INDEX, st);
-            HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
-            // one set against itself: the query side is the ref side, so its sortedness is
-            // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
-            HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
-                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                     (uint32_t *)scan_s, (uint64_t *)tent,
-                                     (uint32_t *)dir, (uint32_t *)entries, unsorted,
-                                     self_set ? events : nullptr, st));
-            if (!self_set)
-                HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
-                                           (const uint32_t *)dir, events, unsorted, st));
-            tl.done();
-        }
-        HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        uint64_t ev = ctx->host_counters[0];
-        const bool all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
-        // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
-        // deduplicated (launch_dedup_rows); repeated values no longer square the posting
-        // events.  The candidates are walked on the original lists.
         const void *p_qry = d_qry;                  // the rows the probe reads
         const uint32_t *p_qry_it = nullptr;         // and their lengths (null: d_qry_len)
         uint64_t p_qry_stride = qry_stride;
-        const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
-        const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
-        if (!all_sorted && mr <= kDedupMax && mq <= kDedupMax && ev > 0) {
-            void *dref, *dref_len, *dqry = nullptr, *dqry_len = nullptr;
-            HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
-            HIP_TRY(scratch(ctx, 11, (size_t)n_ref * 4, &dref_len));
-            if (!self_set) {
+        const uint32_t *dir = nullptr, *entries = nullptr;
+        uint64_t ev = 0;
+        bool all_sorted = true;
+        if (rs) {
+            // resident index: count this block's posting events (and its sortedness)
+            geom = rs->geom;
+            dir = (const uint32_t *)rs->slot[4].p;
+            entries = (const uint32_t *)rs->slot[5].p;
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(hipMemsetAsync(ctr, 0, 67 * 8, st));
+            if (rs->deduped) {
+                const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
+                void *dqry, *dqry_len;
                 HIP_TRY(scratch(ctx, 12, (size_t)n_qry * mq * hash_bytes, &dqry));
                 HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
-            }
-            geom = make_geom((uint64_t)n_ref * mr);
-            geom.kmax = events + 68;
-            TimedLaunch tl(ctx, FPM_K_INDEX, st);
-            HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
-            HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, sketch_size,
-                                      dref, (uint32_t *)dref_len, mr, st));
-            if (!self_set)
                 HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
                                           sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
-            HIP_TRY(launch_idx_build(dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes, geom,
-                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                     (uint32_t *)scan_s, (uint64_t *)tent,
-                                     (uint32_t *)dir, (uint32_t *)entries, unsorted,
-                                     self_set ? events : nullptr, st));
-            p_qry = self_set ? dref : dqry;
-            p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
-            p_qry_stride = self_set ? mr : mq;
-            if (!self_set)
-                HIP_TRY(launch_probe_count(p_qry, p_qry_it, p_qry_stride, n_qry, hash_bytes, geom,
-                                           (const uint32_t *)dir, events, unsorted, st));
+                p_qry = dqry;
+                p_qry_it = (const uint32_t *)dqry_len;
+                p_qry_stride = mq;
+            }
+            HIP_TRY(launch_probe_count(p_qry, p_qry_it ? p_qry_it : d_qry_len, p_qry_stride, n_qry,
+                                       hash_bytes, geom, dir, events, unsorted, st));
             tl.done();
             HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
             HIP_TRY(hipStreamSynchronize(st));
             ev = ctx->host_counters[0];
+            const bool q_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
+            // deduplicated probe rows are sorted by construction: the query's own order is
+            // what the walk needs, so test the originals when the index is deduplicated
+            all_sorted = !rs->ref_unsorted && (rs->deduped ? false : !q_unsorted);
+        } else {
+            void *tile_hist, *tile_off, *tent, *dir_, *entries_, *scan_s;
+            HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
+            HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
+            HIP_TRY(scratch(ctx, 2, E * 8, &tent));
+            HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir_));
+            HIP_TRY(scratch(ctx, 5, E * 4, &entries_));
+            HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
+            geom.kmax = events + 68;
+            {
+                TimedLaunch tl(ctx, FPM_K_INDEX, st);
+                HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+                // one set against itself: the query side is the ref side, so its sortedness is
+                // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
+                HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
+                                         (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                         (uint32_t *)scan_s, (uint64_t *)tent,
+                                         (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
+                                         self_set ? events : nullptr, st));
+                if (!self_set)
+                    HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
+                                               (const uint32_t *)dir_, events, unsorted, st));
+                tl.done();
+            }
+            dir = (const uint32_t *)dir_;
+            entries = (const uint32_t *)entries_;
+            HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            ev = ctx->host_counters[0];
+            all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
+            // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
+            // deduplicated (launch_dedup_rows); repeated values no longer square the posting
+            // events.  The candidates are walked on the original lists.
+            const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
+            const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
+            if (!all_sorted && mr <= kDedupMax && mq <= kDedupMax && ev > 0) {
+                void *dref, *dref_len, *dqry = nullptr, *dqry_len = nullptr;
+                HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
+                HIP_TRY(scratch(ctx, 11, (size_t)n_ref * 4, &dref_len));
+                if (!self_set) {
+                    HIP_TRY(scratch(ctx, 12, (size_t)n_qry * mq * hash_bytes, &dqry));
+                    HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
+                }
+                geom = make_geom(n_ref, (uint64_t)n_ref * mr);
+                geom.kmax = events + 68;
+                TimedLaunch tl(ctx, FPM_K_INDEX, st);
+                HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
+                HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, sketch_size,
+                                          dref, (uint32_t *)dref_len, mr, st));
+                if (!self_set)
+                    HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                              sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
+                HIP_TRY(launch_idx_build(dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes, geom,
+                                         (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                         (uint32_t *)scan_s, (uint64_t *)tent,
+                                         (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
+                                         self_set ? events : nullptr, st));
+                p_qry = self_set ? dref : dqry;
+                p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
+                p_qry_stride = self_set ? mr : mq;
+                if (!self_set)
+                    HIP_TRY(launch_probe_count(p_qry, p_qry_it, p_qry_stride, n_qry, hash_bytes, geom,
+                                               (const uint32_t *)dir_, events, unsorted, st));
+                tl.done();
+                HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                ev = ctx->host_counters[0];
+            }
         }
         ctx->last_events = ev;
         // Unsorted lists: a candidate costs a literal walk of ~S steps from global memory,
@@ -1050,9 +1190,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
-                                          geom, (const uint32_t *)dir, (const uint32_t *)entries,
-                                          d_ref_len, sketch_size, sym, true, self_set,
-                                          cnt, (uint64_t *)cand, n_cand,
+                                          geom, dir, entries, d_ref_len, sketch_size, sym, true,
+                                          self_set, cnt, (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, p_qry_it, st));
                 tl.done();
             }
@@ -1160,7 +1299,7 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                          uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
                          double kmer_space, double max_dist, double max_pvalue, Counts cnt,
                          double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream,
-                         const char *who)
+                         const char *who, fpm_refset *rs = nullptr)
 {
     if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
         return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
@@ -1169,7 +1308,7 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     bool finalized = false;
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                               qry_stride, n_qry, hash_bytes, sketch_size, cnt, stream, &fin,
-                              &finalized))
+                              &finalized, rs))
         return rc;
     if (finalized) return FPM_OK;
     hipStream_t st = pick_stream(ctx, stream);
@@ -1293,6 +1432,169 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
     if (out_pvalue) HIP_TRY(hipMemcpy(out_pvalue, pv.p, np * 8, hipMemcpyDeviceToHost));
     if (out_pass) HIP_TRY(hipMemcpy(out_pass, pa.p, np, hipMemcpyDeviceToHost));
     return FPM_OK;
+}
+
+// ---- resident reference set ----------------------------------------------------------
+
+int fpm_host_alloc(fpm_ctx *ctx, void **p, size_t bytes)
+{
+    if (!p) return fail(FPM_EINVAL, "host_alloc: null output");
+    *p = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    if (hipHostMalloc(p, bytes ? bytes : 16) != hipSuccess)
+        return fail(FPM_ENOMEM, "host_alloc: pinned allocation failed");
+    return FPM_OK;
+}
+
+int fpm_host_free(fpm_ctx *ctx, void *p)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (p) HIP_TRY(hipHostFree(p));
+    return FPM_OK;
+}
+
+static int refset_init(fpm_refset *rs)
+{
+    hipStream_t st = rs->ctx->stream;
+    if (int rc = refset_build_index(rs, st)) return rc;
+    HIP_TRY(hipStreamSynchronize(st));
+    return FPM_OK;
+}
+
+int fpm_refset_create_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                          const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                          uint32_t hash_bytes, uint32_t sketch_size, fpm_refset **out)
+{
+    if (!out) return fail(FPM_EINVAL, "refset_create: null output");
+    *out = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
+    std::unique_ptr<fpm_refset, void (*)(fpm_refset *)> rs(new fpm_refset, fpm_refset_free);
+    rs->ctx = ctx;
+    rs->ref = d_ref;
+    rs->ref_len = d_ref_len;
+    rs->ref_length = d_ref_length;
+    rs->ref_stride = ref_stride;
+    rs->n_ref = n_ref;
+    rs->hash_bytes = hash_bytes;
+    rs->sketch_size = sketch_size;
+    if (int rc = refset_init(rs.get())) return rc;
+    *out = rs.release();
+    return FPM_OK;
+}
+
+int fpm_refset_create(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                      const uint64_t *ref_length, uint64_t ref_stride, uint32_t n_ref,
+                      uint32_t hash_bytes, uint32_t sketch_size, fpm_refset **out)
+{
+    if (!out) return fail(FPM_EINVAL, "refset_create: null output");
+    *out = nullptr;
+    if (int rc = set_device(ctx)) return rc;
+    if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
+    std::unique_ptr<fpm_refset, void (*)(fpm_refset *)> rs(new fpm_refset, fpm_refset_free);
+    rs->ctx = ctx;
+    const size_t mb = std::max<size_t>(16, (size_t)n_ref * ref_stride * hash_bytes);
+    HIP_TRY(hipMalloc(&rs->own[0], mb));
+    HIP_TRY(hipMalloc(&rs->own[1], std::max<size_t>(16, (size_t)n_ref * 4)));
+    HIP_TRY(hipMalloc(&rs->own[2], std::max<size_t>(16, (size_t)n_ref * 8)));
+    hipStream_t st = ctx->stream;
+    if ((size_t)n_ref * ref_stride)
+        HIP_TRY(hipMemcpyAsync(rs->own[0], ref, (size_t)n_ref * ref_stride * hash_bytes,
+                               hipMemcpyHostToDevice, st));
+    if (n_ref) {
+        HIP_TRY(hipMemcpyAsync(rs->own[1], ref_len, (size_t)n_ref * 4, hipMemcpyHostToDevice, st));
+        if (ref_length)
+            HIP_TRY(hipMemcpyAsync(rs->own[2], ref_length, (size_t)n_ref * 8, hipMemcpyHostToDevice,
+                                   st));
+    }
+    rs->ref = rs->own[0];
+    rs->ref_len = (const uint32_t *)rs->own[1];
+    rs->ref_length = (const uint64_t *)rs->own[2];
+    rs->ref_stride = ref_stride;
+    rs->n_ref = n_ref;
+    rs->hash_bytes = hash_bytes;
+    rs->sketch_size = sketch_size;
+    if (int rc = refset_init(rs.get())) return rc;
+    *out = rs.release();
+    return FPM_OK;
+}
+
+int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                        const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                        uint32_t sketch_size, uint32_t count_bytes, uint32_t kmer_size,
+                        double kmer_space, double max_dist, double max_pvalue, void *d_numer,
+                        void *d_denom, double *d_dist, double *d_pvalue, uint8_t *d_pass,
+                        void *stream)
+{
+    if (!rs) return fail(FPM_EINVAL, "refset_dist: null set");
+    if (sketch_size != rs->sketch_size)
+        return fail(FPM_EINVAL, "refset_dist: sketch_size differs from the set's");
+    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
+    if (count_bytes == 2 && sketch_size > 65535)
+        return fail(FPM_EINVAL, "refset_dist: u16 counts need sketch_size <= 65535");
+    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
+                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
+                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue,
+                         Counts{d_numer, d_denom, count_bytes == 2}, d_dist, d_pvalue, d_pass,
+                         stream, "fpm_refset_dist_dev", rs);
+}
+
+int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
+                    const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+                    uint32_t sketch_size, uint32_t kmer_size, double kmer_space, double max_dist,
+                    double max_pvalue, uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
+                    double *out_pvalue, uint8_t *out_pass)
+{
+    if (!rs) return fail(FPM_EINVAL, "refset_dist: null set");
+    fpm_ctx *ctx = rs->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    const uint64_t np = (uint64_t)rs->n_ref * n_qry;
+    if (np == 0) return FPM_OK;
+    hipStream_t st = ctx->stream;
+    void *q, *ql, *qL, *nu, *de, *di, *pv, *pa;
+    const size_t qb = std::max<size_t>(16, (size_t)n_qry * qry_stride * rs->hash_bytes);
+    HIP_TRY(slot_buf(rs->qslot[0], qb, &q));
+    HIP_TRY(slot_buf(rs->qslot[1], (size_t)n_qry * 4, &ql));
+    HIP_TRY(slot_buf(rs->qslot[2], (size_t)n_qry * 8, &qL));
+    HIP_TRY(slot_buf(rs->qslot[3], np * 4, &nu));
+    HIP_TRY(slot_buf(rs->qslot[4], np * 4, &de));
+    HIP_TRY(slot_buf(rs->qslot[5], np * 8, &di));
+    HIP_TRY(slot_buf(rs->qslot[6], np * 8, &pv));
+    HIP_TRY(slot_buf(rs->qslot[7], np, &pa));
+    HIP_TRY(hipMemcpyAsync(q, qry, (size_t)n_qry * qry_stride * rs->hash_bytes,
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(ql, qry_len, (size_t)n_qry * 4, hipMemcpyHostToDevice, st));
+    if (qry_length)
+        HIP_TRY(hipMemcpyAsync(qL, qry_length, (size_t)n_qry * 8, hipMemcpyHostToDevice, st));
+    else
+        HIP_TRY(hipMemsetAsync(qL, 0, (size_t)n_qry * 8, st));
+    if (int rc = fpm_refset_dist_dev(rs, q, (const uint32_t *)ql, (const uint64_t *)qL, qry_stride,
+                                     n_qry, sketch_size, 4, kmer_size, kmer_space, max_dist,
+                                     max_pvalue, nu, de, (double *)di, (double *)pv,
+                                     (uint8_t *)pa, st))
+        return rc;
+    // results: caller memory (pinned from fpm_host_alloc copies at full PCIe rate)
+    if (out_numer) HIP_TRY(hipMemcpyAsync(out_numer, nu, np * 4, hipMemcpyDeviceToHost, st));
+    if (out_denom) HIP_TRY(hipMemcpyAsync(out_denom, de, np * 4, hipMemcpyDeviceToHost, st));
+    if (out_dist) HIP_TRY(hipMemcpyAsync(out_dist, di, np * 8, hipMemcpyDeviceToHost, st));
+    if (out_pvalue) HIP_TRY(hipMemcpyAsync(out_pvalue, pv, np * 8, hipMemcpyDeviceToHost, st));
+    if (out_pass) HIP_TRY(hipMemcpyAsync(out_pass, pa, np, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    return FPM_OK;
+}
+
+void fpm_refset_free(fpm_refset *rs)
+{
+    if (!rs) return;
+    if (rs->ctx) (void)hipSetDevice(rs->ctx->device);
+    for (auto &sl : rs->slot)
+        if (sl.p) (void)hipFree(sl.p);
+    for (auto &sl : rs->qslot)
+        if (sl.p) (void)hipFree(sl.p);
+    for (void *o : rs->own)
+        if (o) (void)hipFree(o);
+    if (rs->kmax) (void)hipFree(rs->kmax);
+    delete rs;
 }
 
 int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,

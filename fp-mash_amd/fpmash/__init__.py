@@ -94,6 +94,19 @@ SYMBOLS = [
     ("fpm_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, vp, u32p, u64p,
                            C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                            C.c_double, C.c_double, C.c_double, u32p, u32p, f64p, f64p, u8p]),
+    ("fpm_refset_create", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                    C.c_uint32, C.POINTER(vp)]),
+    ("fpm_refset_create_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32,
+                                        C.c_uint32, C.POINTER(vp)]),
+    ("fpm_refset_dist_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32,
+                                      C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_double,
+                                      vp, vp, vp, vp, vp, vp]),
+    ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                  C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
+                                  f64p, f64p, u8p]),
+    ("fpm_refset_free", None, [vp]),
+    ("fpm_host_alloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
+    ("fpm_host_free", C.c_int, [vp, vp]),
 ]
 
 
@@ -415,6 +428,10 @@ class Context:
         return {"numer": res[0], "denom": res[1], "distance": res[2], "pvalue": res[3],
                 "pass": res[4].astype(bool)}
 
+    def refset(self, ref_lists, sketch_size, use64=True, ref_lengths=None, width=None):
+        """A resident reference set (fpm_refset_create): rows uploaded and indexed once."""
+        return RefSet(self, ref_lists, sketch_size, use64, ref_lengths, width)
+
     def fp_text(self, text, max_lines=1_000_000, seed=42, use64=False):
         """-fp file image -> per line: ID (offset, length), value count, hash, new-ID flag."""
         job, n = vp(), C.c_uint64()
@@ -452,6 +469,56 @@ class Context:
                                             _p(de, u32p), _p(di, f64p), _p(pv, f64p), _p(pa, u8p)))
         return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
                 "pass": pa[:n].astype(bool)}
+
+
+class RefSet:
+    """fpm_refset_*: the reference rows stay on the device with their bucket index built
+    once; dist() runs one query block against them (results as Context.dist)."""
+
+    def __init__(self, ctx, ref_lists, sketch_size, use64=True, ref_lengths=None, width=None):
+        self.ctx, self.use64, self.S = ctx, use64, int(sketch_size)
+        self.dt = np.uint64 if use64 else np.uint32
+        self.w = int(width or max([len(x) for x in ref_lists] + [1]))
+        R, rl = _dense(ref_lists, self.w, self.dt)
+        self.n = len(ref_lists)
+        rL = np.ascontiguousarray(ref_lengths if ref_lengths is not None else
+                                  [0] * self.n, dtype=np.uint64)
+        h = vp()
+        _check(lib().fpm_refset_create(ctx.h, R.ctypes.data, _p(rl, u32p), _p(rL, u64p), self.w,
+                                       self.n, 8 if use64 else 4, self.S, C.byref(h)))
+        self.h = h.value
+
+    def dist(self, qry_lists, k=21, kmer_space=None, qry_lengths=None, max_dist=-1.0,
+             max_pvalue=-1.0):
+        Q, ql = _dense(qry_lists, self.w, self.dt)
+        nq = len(qry_lists)
+        n = self.n * nq
+        qL = np.ascontiguousarray(qry_lengths if qry_lengths is not None else [0] * nq,
+                                  dtype=np.uint64)
+        if kmer_space is None:
+            kmer_space = 4.0 ** k
+        nu = np.zeros(max(n, 1), np.uint32)
+        de = np.zeros(max(n, 1), np.uint32)
+        di = np.zeros(max(n, 1), np.float64)
+        pv = np.zeros(max(n, 1), np.float64)
+        pa = np.zeros(max(n, 1), np.uint8)
+        _check(lib().fpm_refset_dist(self.h, Q.ctypes.data, _p(ql, u32p), _p(qL, u64p), self.w,
+                                     nq, self.S, k, kmer_space, max_dist, max_pvalue,
+                                     _p(nu, u32p), _p(de, u32p), _p(di, f64p), _p(pv, f64p),
+                                     _p(pa, u8p)))
+        return {"numer": nu[:n], "denom": de[:n], "distance": di[:n], "pvalue": pv[:n],
+                "pass": pa[:n].astype(bool)}
+
+    def free(self):
+        if self.h:
+            lib().fpm_refset_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
 
 
 def _dense(lists, width, dtype):

@@ -7,9 +7,17 @@
 #include "Sketch.h"
 
 #include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <deque>
+#include <functional>
 #include <iostream>
+#include <mutex>
+#include <thread>
 
 namespace fpmhost {
 
@@ -53,11 +61,14 @@ namespace {
 
 struct Out {
     std::string buf;
+    bool autoflush = true;            // false: a formatter piece, written later in order
     void flush() { fwrite(buf.data(), 1, buf.size(), stdout); buf.clear(); }
-    void put(const std::string &s) { buf += s; if (buf.size() > (1 << 22)) flush(); }
+    void put(const std::string &s) { buf += s; if (autoflush && buf.size() > (1 << 22)) flush(); }
     void put(char c) { buf.push_back(c); }
     void num(double x)   // ostream default: %g, precision 6
     {
+        if (x == 1.0) { buf.push_back('1'); return; }     // most cells: no shared hash
+        if (x == 0.0 && !std::signbit(x)) { buf.push_back('0'); return; }
         char t[64];
         int n = snprintf(t, sizeof t, "%g", x);
         buf.append(t, n);
@@ -191,51 +202,173 @@ int CommandDistance::run() const
     pack(sketchRef, R, rl, rL, width);
     pack(sketchQuery, Q, ql, qL, width);
 
-    // query blocks bound the host buffers (~64 M pairs per block)
-    const uint64_t block = nR ? std::max<uint64_t>(1, (64ULL << 20) / nR) : 1;
-    std::vector<uint32_t> nu, de;
-    std::vector<double> di, pv;
-    std::vector<uint8_t> pa;
-    for (uint64_t q0 = 0; q0 < nQ && nR; q0 += block) {
-        const uint64_t nq = std::min(block, nQ - q0);
-        const uint64_t np = nq * nR;
-        nu.resize(np); de.resize(np); di.resize(np); pv.resize(np); pa.resize(np);
-        check(fpm_dist(device(), R.data(), rl.data(), rL.data(), width, (uint32_t)nR,
-                       Q.data() + q0 * width * hb, ql.data() + q0, qL.data() + q0, width,
-                       (uint32_t)nq, hb, (uint32_t)sketchSize, (uint32_t)sketchRef.getKmerSize(),
-                       sketchRef.getKmerSpace(), distanceMax, pValueMax, nu.data(), de.data(),
-                       di.data(), pv.data(), pa.data()),
-              "dist");
-        // writeOutput (CommandDistance.cpp:276-333), query-major
-        for (uint64_t qi = 0; qi < nq; qi++) {
+    // The grid in query blocks (CommandDistance.cpp:224-261 chunks it for the pool): every
+    // device holds the reference set with its index built once (fpm_refset_create) and takes
+    // blocks in turn; results land in pinned buffers; formatter threads (-p) turn each block
+    // into text pieces, which this thread writes strictly in block order (writeOutput,
+    // :276-333, consumes the pool's outputs in order).
+    const int nDev = nR && nQ ? deviceCount() : 0;
+    std::vector<fpm_refset *> sets(nDev, nullptr);
+    for (int d = 0; d < nDev; d++)
+        check(fpm_refset_create(device(d), R.data(), rl.data(), rL.data(), width, (uint32_t)nR,
+                                hb, (uint32_t)sketchSize, &sets[d]),
+              "dist reference set");
+    uint64_t blockPairs = 16ULL << 20;
+    if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
+    const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
+    const uint64_t nBlocks = nR ? (nQ + block - 1) / block : 0;
+    const int nSlots = std::max(2, 2 * nDev + 1);
+    const int nFmt = std::max(1, std::min(parameters.parallelism > 1 ? parameters.parallelism
+                                          : (int)std::thread::hardware_concurrency(), 64));
+    struct Slot {
+        uint32_t *nu = nullptr, *de = nullptr;
+        double *di = nullptr, *pv = nullptr;
+        uint8_t *pa = nullptr;
+        int dev = 0;
+        uint64_t b = ~0ULL;                 // block held
+        std::vector<std::string> text;      // formatted pieces
+        int pending = 0;                    // pieces still being formatted
+        bool ready = false;
+    };
+    std::vector<Slot> slots(nSlots);
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t written = 0;                   // blocks already written out
+    std::deque<std::function<void()>> tasks;
+    bool stop = false;
+    for (int i = 0; i < nSlots && nBlocks; i++) {
+        // pinned buffers of one block on the context of the device that fills them
+        Slot &sl = slots[i];
+        const uint64_t np = block * nR;
+        fpm_ctx *c = device(0);
+        check(fpm_host_alloc(c, (void **)&sl.nu, np * 4), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.de, np * 4), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.di, np * 8), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
+    }
+    auto format = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, std::string &dst) {
+        Out o;
+        o.autoflush = false;
+        for (uint64_t qi = qa; qi < qb; qi++) {
             const Reference &qr = sketchQuery.getReference(q0 + qi);
-            if (table) out.put(qr.name);
+            if (table) o.put(qr.name);
+            std::string qtail;              // "\t<query>[:comment]\t"
+            if (!table) {
+                qtail.push_back('\t');
+                qtail += qr.name;
+                if (comment) { qtail.push_back(':'); qtail += qr.comment; }
+                qtail.push_back('\t');
+            }
             for (uint64_t j = 0; j < nR; j++) {
                 const uint64_t k = qi * nR + j;
                 if (table) {
-                    out.put('\t');
-                    if (pa[k]) out.num(di[k]);
-                } else if (pa[k]) {
+                    o.put('\t');
+                    if (sl.pa[k]) o.num(sl.di[k]);
+                } else if (sl.pa[k]) {
                     const Reference &rr = sketchRef.getReference(j);
-                    out.put(rr.name);
-                    if (comment) { out.put(':'); out.put(rr.comment); }
-                    out.put('\t');
-                    out.put(qr.name);
-                    if (comment) { out.put(':'); out.put(qr.comment); }
-                    out.put('\t');
-                    out.num(di[k]);
-                    out.put('\t');
-                    out.num(pv[k]);
-                    out.put('\t');
-                    out.u(nu[k]);
-                    out.put('/');
-                    out.u(de[k]);
-                    out.put('\n');
+                    o.put(rr.name);
+                    if (comment) { o.put(':'); o.put(rr.comment); }
+                    o.put(qtail);
+                    o.num(sl.di[k]);
+                    o.put('\t');
+                    o.num(sl.pv[k]);
+                    o.put('\t');
+                    o.u(sl.nu[k]);
+                    o.put('/');
+                    o.u(sl.de[k]);
+                    o.put('\n');
                 }
             }
-            if (table) out.put('\n');
+            if (table) o.put('\n');
         }
+        dst.swap(o.buf);
+    };
+    std::vector<std::thread> fmt;
+    for (int t = 0; t < nFmt; t++)
+        fmt.emplace_back([&] {
+            for (;;) {
+                std::function<void()> job;
+                {
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return stop || !tasks.empty(); });
+                    if (tasks.empty()) return;
+                    job = std::move(tasks.front());
+                    tasks.pop_front();
+                }
+                job();
+            }
+        });
+    std::atomic<uint64_t> next{0};
+    std::vector<std::thread> gpu;
+    for (int d = 0; d < nDev; d++)
+        gpu.emplace_back([&, d] {
+            for (;;) {
+                const uint64_t b = next.fetch_add(1);
+                if (b >= nBlocks) return;
+                Slot &sl = slots[b % nSlots];
+                {
+                    // the slot's previous block must be written out first
+                    std::unique_lock<std::mutex> lk(mu);
+                    cv.wait(lk, [&] { return written + nSlots > b; });
+                }
+                const uint64_t q0 = b * block, nq = std::min(block, nQ - q0);
+                check(fpm_refset_dist(sets[d], Q.data() + q0 * width * hb, ql.data() + q0,
+                                      qL.data() + q0, width, (uint32_t)nq, (uint32_t)sketchSize,
+                                      (uint32_t)sketchRef.getKmerSize(), sketchRef.getKmerSpace(),
+                                      distanceMax, pValueMax, sl.nu, sl.de, sl.di, sl.pv, sl.pa),
+                      "dist");
+                // pieces of ~1 M pairs (at least one query row) for the formatter threads
+                const uint64_t per = std::max<uint64_t>(1, (1ULL << 20) / nR);
+                const uint64_t parts = (nq + per - 1) / per;
+                std::lock_guard<std::mutex> lk(mu);
+                sl.b = b;
+                sl.dev = d;
+                sl.text.assign(parts, std::string());
+                sl.pending = (int)parts;
+                sl.ready = false;
+                for (uint64_t p = 0; p < parts; p++) {
+                    const uint64_t qa = p * per, qb = std::min(nq, qa + per);
+                    tasks.emplace_back([&, q0, qa, qb, p, bslot = &sl] {
+                        std::string t;
+                        format(*bslot, q0, qa, qb, t);
+                        std::lock_guard<std::mutex> lk2(mu);
+                        bslot->text[p].swap(t);
+                        if (--bslot->pending == 0) bslot->ready = true;
+                        cv.notify_all();
+                    });
+                }
+                cv.notify_all();
+            }
+        });
+    for (uint64_t b = 0; b < nBlocks; b++) {
+        Slot &sl = slots[b % nSlots];
+        std::vector<std::string> pieces;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return sl.b == b && sl.ready; });
+            pieces.swap(sl.text);
+        }
+        out.flush();
+        for (auto &t : pieces) fwrite(t.data(), 1, t.size(), stdout);
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            written = b + 1;
+        }
+        cv.notify_all();
     }
+    for (auto &t : gpu) t.join();
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = true;
+    }
+    cv.notify_all();
+    for (auto &t : fmt) t.join();
+    for (auto &sl : slots)
+        for (void *ptr : {(void *)sl.nu, (void *)sl.de, (void *)sl.di, (void *)sl.pv,
+                          (void *)sl.pa})
+            if (ptr) fpm_host_free(device(0), ptr);
+    for (auto *rs : sets) fpm_refset_free(rs);
     out.flush();
     fflush(stdout);
     if (warningCount > 0 && !parameters.reads)

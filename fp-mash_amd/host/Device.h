@@ -1,13 +1,19 @@
-// Device.h — the host's single gfx950 context.  Every call goes through the C ABI
+// Device.h — the host's gfx950 contexts.  Every call goes through the C ABI
 // (include/fpmash.h); a non-zero status prints "ERROR: ..." and exit(1)s, the
 // reference's failure convention on this path (Sketch.cpp:75-76, 1446-1463).
+//
+// Devices used: FPMASH_DEVICE=i pins one device; otherwise every visible device (at most
+// FPMASH_DEVICES=n of them).  device(0) is the default context; the dist and sketch
+// commands spread query blocks / sketch groups over device(0..deviceCount()-1), the way
+// the reference spreads them over its -p threads (CommandDistance.cpp:191, Sketch.cpp:253).
 #pragma once
 
 #include "fpmash.h"
 
 namespace fpmhost {
 
-fpm_ctx *device();
+int deviceCount();
+fpm_ctx *device(int i = 0);
 void check(int rc, const char *what);
 
 }  // namespace fpmhost

@@ -218,6 +218,41 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
              double max_dist, double max_pvalue, uint32_t *out_numer, uint32_t *out_denom,
              double *out_dist, double *out_pvalue, uint8_t *out_pass);
 
+/* ---- resident reference set -------------------------------------------------------
+ * CommandDistance::run compares every query against the same reference sketch
+ * (CommandDistance.cpp:191-261: the pool's CompareInput holds `const Sketch & sketchRef`
+ * for all query chunks).  A refset keeps the reference rows on the device and builds their
+ * bucket index ONCE; each query block then only uploads its own rows, probes the resident
+ * index and runs the exact candidate compare + distance / p-value (the same results as
+ * fpm_dist_dev).  sketch_size (min of the two sketches' s, :342-344) is fixed per set.
+ * _create copies host rows to the device (owned); _create_dev borrows device rows, which
+ * must outlive the set.  count_bytes selects u16 (2, sketch_size <= 65535) or u32 (4)
+ * numer / denom cells.  fpm_refset_dist takes host query rows and host outputs (pinned
+ * buffers from fpm_host_alloc copy at full PCIe rate). */
+typedef struct fpm_refset fpm_refset;
+int fpm_refset_create(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
+                      const uint64_t *ref_length, uint64_t ref_stride, uint32_t n_ref,
+                      uint32_t hash_bytes, uint32_t sketch_size, fpm_refset **out);
+int fpm_refset_create_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                          const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                          uint32_t hash_bytes, uint32_t sketch_size, fpm_refset **out);
+int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                        const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                        uint32_t sketch_size, uint32_t count_bytes, uint32_t kmer_size,
+                        double kmer_space, double max_dist, double max_pvalue, void *d_numer,
+                        void *d_denom, double *d_dist, double *d_pvalue, uint8_t *d_pass,
+                        void *stream);
+int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
+                    const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+                    uint32_t sketch_size, uint32_t kmer_size, double kmer_space, double max_dist,
+                    double max_pvalue, uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
+                    double *out_pvalue, uint8_t *out_pass);
+void fpm_refset_free(fpm_refset *rs);
+
+/* pinned (page-locked) host memory for staging buffers of the host-buffer calls */
+int fpm_host_alloc(fpm_ctx *ctx, void **p, size_t bytes);
+int fpm_host_free(fpm_ctx *ctx, void *p);
+
 /* ---- triangle -fp ---------------------------------------------------------------
  * Replaces compareFingerprints (CommandTriangle.cpp:255-302): positional compare of
  * two lists over min(len) entries, matches = equal values at the same position (the

@@ -334,3 +334,43 @@ def test_positional_grid_abi(ctx, oracle):
                 assert np.isnan(got["distance"][k])
             assert got["pvalue"][k] == pytest.approx(pv, rel=1e-12)
             assert got["pass"][k] == (dv <= 0.9 and pv <= 0.5)
+
+
+def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
+    """writeOutput's lines (CommandDistance.cpp:276-333) from the oracle's grid."""
+    nu, de, di, pv = oracle.dist_grid([r["hashes64"] for r in refs], [r["length"] for r in refs],
+                                      [q["hashes64"] for q in qrys], [q["length"] for q in qrys],
+                                      S, k, space)
+    out = []
+    n = len(refs)
+    for qi, q in enumerate(qrys):
+        qn = q["name"].decode() + (":" + q["comment"].decode() if comment else "")
+        for ri, r in enumerate(refs):
+            x = qi * n + ri
+            rn = r["name"].decode() + (":" + r["comment"].decode() if comment else "")
+            out.append(f"{rn}\t{qn}\t{di[x]:g}\t{pv[x]:g}\t{nu[x]}/{de[x]}")
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block_pairs", [None, "50000"])
+def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs):
+    """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
+    blocks of 50,000 pairs (FPMASH_DIST_BLOCK_PAIRS) written by the formatter threads in
+    order: every line equals the oracle's, in the reference's query-major order."""
+    from fpmash import datagen
+    seqs = datagen.family_dna(12, 100, 2000, sub_rate=(0.01, 0.10), seed=23)
+    ids = datagen.lyn2vec_ids(len(seqs), seed=23)
+    (tmp_path / "all.fa").write_bytes(datagen.fasta_bytes(seqs, ids))
+    run(["sketch", "-i", "-o", "all", "all.fa"], cwd=tmp_path)
+    env = dict(os.environ)
+    if block_pairs:
+        env["FPMASH_DIST_BLOCK_PAIRS"] = block_pairs
+    p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
+                       capture_output=True, env=env)
+    assert p.returncode == 0, p.stderr.decode()
+    refs = mshfmt.read_msh(str(tmp_path / "all.msh"))["references"]
+    exp = _oracle_dist_lines(oracle, refs, refs, 1000, 21, 4.0 ** 21)
+    got = p.stdout.decode().splitlines()
+    assert len(got) == len(exp) == len(refs) ** 2
+    assert got == exp

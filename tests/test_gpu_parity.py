@@ -445,3 +445,42 @@ def test_merge_small_kernel_forced():
     r = subprocess.run([sys.executable, os.path.join(os.path.dirname(__file__), "_merge_small_worker.py")],
                        env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("use64,mode", [(True, "sorted"), (False, "fp"), (True, "dense")])
+def test_refset_blocks_match_grid(ctx, oracle, use64, mode):
+    """fpm_refset_*: references uploaded and indexed once, several query blocks probed
+    against the resident index == the one-shot grid (and the oracle), for sorted u64
+    sketches (index + rank), unsorted -fp u32 lists (deduplicated index + literal walk) and
+    near-identical sets (events past the sparse threshold: dense walk)."""
+    import fpmash
+    from fpmash import datagen
+    rng = np.random.default_rng(11)
+    if mode == "fp":
+        lists = [rng.integers(0, 40, size=int(rng.integers(1, 300))).astype(np.uint32)
+                 for _ in range(60)]
+        S, k, space = 200, 1, 10.0
+    else:
+        seqs = datagen.family_dna(6, 10, 1500, sub_rate=(0.0, 0.02 if mode == "dense" else 0.1),
+                                  seed=17)
+        lists = oracle.sketch_batch(oracle.params(k=21, s=300), seqs)
+        S, k, space = 300, 21, 4.0 ** 21
+    lengths = [int(len(x)) * 7 + 1000 for x in lists]
+    refs, qrys = lists[:45], lists[15:]
+    rl, ql = lengths[:45], lengths[15:]
+    rs = ctx.refset(refs, S, use64=use64, ref_lengths=rl,
+                    width=max(len(x) for x in lists))
+    try:
+        # no distance filter: the reference computes the p-value only for pairs that pass
+        # it (CommandDistance.cpp:416-423); here every p-value is compared
+        got = [rs.dist(qrys[i:i + 13], k=k, kmer_space=space, qry_lengths=ql[i:i + 13],
+                       max_dist=-1.0, max_pvalue=0.5) for i in range(0, len(qrys), 13)]
+    finally:
+        rs.free()
+    cat = {key: np.concatenate([g[key] for g in got]) for key in got[0]}
+    nu, de, di, pv = oracle.dist_grid(refs, rl, qrys, ql, S, k, space, use64=use64)
+    assert np.array_equal(cat["numer"], nu) and np.array_equal(cat["denom"], de)
+    assert np.allclose(cat["distance"], di, rtol=1e-12, atol=0)
+    assert np.allclose(cat["pvalue"], pv, rtol=1e-12, atol=0)
+    assert np.array_equal(cat["pass"], pv <= 0.5)
