@@ -60,6 +60,8 @@ def parse():
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 RefSeq-scale sketch leg")
+    ap.add_argument("--no-cli", action="store_true",
+                    help="skip the end-to-end CLI leg (fpmash sketch + dist, 1e8 text lines)")
     ap.add_argument("--c5-genomes", type=int, default=1000)
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
@@ -71,7 +73,7 @@ def parse_args_for_test(**kw):
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
-                           no_parity=True, no_c5=True, c5_genomes=1000)
+                           no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -303,11 +305,12 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4, c5=None):
+def parity_summary(c2, c3, c4, c5=None, cli=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
              "c4": c4.get("parity") if c4 else None,
-             "c5": c5.get("parity") if c5 else None}
+             "c5": c5.get("parity") if c5 else None,
+             "cli": cli.get("parity") if cli else None}
     done = [v["ok"] for v in parts.values() if v]
     parts["all_ok"] = all(done) if done else None
     parts["checker"] = ("oracle/ CPU restatement (pinned to the reference's fixtures), "
@@ -578,6 +581,87 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
             "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
             "candidates_all_ranks": cand, "parity": par}
+
+
+def cli_leg(args, seqs, cpu=None, check=True):
+    """The drop-in CLI end to end (CPU wall / GPU wall of the same command), on
+    config C2's batch written as one lyn2vec-style FASTA:
+      fpmash sketch -i -k 21 -s 1000 c2.fa -o c2     (parse + sketch + .msh write)
+      fpmash dist c2.msh c2.msh > out                 (1e8 lines: resident reference set,
+                                                       pipelined blocks, ordered text)
+    Outside the timed commands: the .msh is byte-compared with the .msh the oracle's
+    sketches encode to (tests/mshfmt.write_msh), and the first and last 20 query rows of the
+    text with the oracle's lines."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "fp-mash_amd", "bin", "fpmash")
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    tmp = tempfile.mkdtemp(prefix="fpm_cli_", dir=base)
+    try:
+        ids = datagen.lyn2vec_ids(len(seqs))
+        fa = os.path.join(tmp, "c2.fa")
+        with open(fa, "wb") as f:
+            f.write(datagen.fasta_bytes(seqs, ids))
+        env = dict(os.environ)
+        t0 = time.perf_counter()
+        subprocess.run([exe, "sketch", "-i", "-k", str(args.k), "-s", str(args.s), "-o", "c2",
+                        "c2.fa"], cwd=tmp, check=True, capture_output=True, env=env)
+        t_sketch = time.perf_counter() - t0
+        out_path = os.path.join(tmp, "out.tsv")
+        t0 = time.perf_counter()
+        with open(out_path, "wb") as f:
+            subprocess.run([exe, "dist", "-p", str(_threads()), "c2.msh", "c2.msh"], cwd=tmp,
+                           check=True, stdout=f, stderr=subprocess.PIPE, env=env)
+        t_dist = time.perf_counter() - t0
+        out_bytes = os.path.getsize(out_path)
+        n = len(seqs)
+        res = {"command_sketch": f"fpmash sketch -i -k {args.k} -s {args.s} -o c2 c2.fa",
+               "command_dist": "fpmash dist c2.msh c2.msh > out",
+               "fasta_bytes": os.path.getsize(fa), "cli_sketch_wall_s": t_sketch,
+               "cli_dist_wall_s": t_dist, "dist_lines": n * n, "dist_text_bytes": out_bytes,
+               "dist_lines_per_s": n * n / t_dist, "output_dir": base or tempfile.gettempdir()}
+        if cpu:
+            # the CPU port's wall for the same work, from the cpu_baseline leg's rates (its
+            # sketch and dist with p-values; text formatting not included)
+            res["cpu_port_sketch_s"] = n * args.seq_len / cpu["sketch_bases_per_s"]
+            res["cpu_port_dist_s"] = n * n / cpu["dist_pairs_per_s"]
+            res["speedup_sketch"] = res["cpu_port_sketch_s"] / t_sketch
+            res["speedup_dist"] = res["cpu_port_dist_s"] / t_dist
+        if check:
+            from oracle import oracle as O
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import mshfmt
+            t_c = time.perf_counter()
+            exp = O.sketch_batch(O.params(k=args.k, s=args.s), seqs, threads=_threads())
+            refs = [dict(name=b"T00000" + i.encode(), comment=b"G00000" + i.encode(),
+                         length=len(q), hashes=h) for q, i, h in zip(seqs, ids, exp)]
+            hdr = dict(kmer=args.k, windowSize=0, sketchSize=args.s, concatenated=False,
+                       noncanonical=False, preserveCase=False, error=0.0, seed=42,
+                       alphabet=b"ACGT")
+            msh_ok = open(os.path.join(tmp, "c2.msh"), "rb").read() == mshfmt.write_msh(hdr, refs)
+            rows = list(range(20)) + list(range(n - 20, n))
+            nu, de, di, pv = O.dist_grid(exp, [len(q) for q in seqs], [exp[r] for r in rows],
+                                         [len(seqs[r]) for r in rows], args.s, args.k,
+                                         4.0 ** args.k, threads=_threads())
+            names = [b"T00000" + i.encode() for i in ids]
+            want = []
+            for x, qr in enumerate(rows):
+                for r in range(n):
+                    c = x * n + r
+                    want.append(b"%s\t%s\t%s\t%s\t%d/%d" % (
+                        names[r], names[qr], (b"%g" % di[c]), (b"%g" % pv[c]), nu[c], de[c]))
+            with open(out_path, "rb") as f:
+                head = [f.readline().rstrip(b"\n") for _ in range(20 * n)]
+                f.seek(max(0, out_bytes - 20 * n * 200))
+                tail = f.read().split(b"\n")[:-1][-20 * n:]
+            text_ok = head == want[:20 * n] and tail == want[20 * n:]
+            res["parity"] = {"msh_byte_identical": bool(msh_ok),
+                             "dist_text_rows_checked": len(rows), "dist_text_exact": bool(text_ok),
+                             "ok": bool(msh_ok and text_ok), "check_s": time.perf_counter() - t_c}
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 _ACGT_LUT = None
@@ -866,6 +950,10 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seqs)
 
+    cli = None
+    if rank == 0 and ws == 1 and not args.no_cli:
+        cli = cli_leg(args, seqs, cpu, check=not args.no_parity)
+
     if rank == 0:
         line = {
             "metric": METRIC,
@@ -900,11 +988,12 @@ def main():
             "c3_fp": c3,
             "c4_dist": c4,
             "c5_sketch": c5,
+            "cli": cli,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4, c5),
+            "parity": parity_summary(c2par, c3, c4, c5, cli),
         }
         print(json.dumps(line))
     job.free()
