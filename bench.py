@@ -38,7 +38,14 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
 # per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py,
 # regenerated on the GPU box whenever the kernels change)
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+def _latest_pmc():
+    """profiles/rNN/pmc_traffic.json of the newest round that has one."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_traffic.json")))
+    return found[-1] if found else os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+
+
+PMC_TRAFFIC = _latest_pmc()
 METRIC = "bases/s sketched + Mpairs/s dist, k=21 s=1000, 1/2/4/8 MI355X; %HBM roofline"
 
 

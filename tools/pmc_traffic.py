@@ -10,7 +10,7 @@ count Infinity-Cache traffic (L2 memory-side requests), so they are an upper bou
 HBM bytes.  rocprofv3 reports both in KiB.
 
 Run it on the GPU box (this process never touches the GPU itself):
-    python3 tools/pmc_traffic.py --out profiles/r01/pmc_traffic.json
+    python3 tools/pmc_traffic.py --out profiles/r02/pmc_traffic.json
 """
 from __future__ import annotations
 
@@ -94,7 +94,7 @@ def per_launch(per_disp: dict, launches: dict) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"))
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -102,7 +102,7 @@ def main():
     os.makedirs(a.work, exist_ok=True)
     # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
     bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline",
-                  "--no-fp-text", "--no-c3", "--no-c4"]
+                  "--no-fp-text", "--no-c3", "--no-c4", "--no-c5", "--no-cli", "--no-parity"]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.work, "fetch"), bench_args)
     write = run_pass("WRITE_SIZE", os.path.join(a.work, "write"), bench_args)
     # one "launch" of a group that is several kernels (the index build) is one step's worth
