@@ -85,7 +85,85 @@ struct fpm_ctx {
     // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
+    // pinned staging ring for host -> device copies of pageable caller memory
+    static constexpr int kRing = 4;
+    static constexpr size_t kRingBytes = 8u << 20;
+    void *ring[kRing] = {};
+    hipEvent_t ring_ev[kRing] = {};
+    hipStream_t copy = nullptr;
 };
+
+static hipError_t ensure_ring(fpm_ctx *ctx)
+{
+    hipError_t e = hipSuccess;
+    if (ctx->copy) return e;
+    for (int i = 0; e == hipSuccess && i < fpm_ctx::kRing; i++) {
+        e = hipHostMalloc(&ctx->ring[i], fpm_ctx::kRingBytes, hipHostMallocDefault);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ring_ev[i], hipEventDisableTiming);
+    }
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking);
+    return e;
+}
+
+// Host -> device copy of pageable memory through the context's pinned ring: the caller's
+// thread memcpy's piece i into a pinned buffer while the DMA engine moves piece i - 1
+// (hipMemcpy from pageable memory stages through the runtime's own buffers one piece at a
+// time: ~3.8 GB/s measured on the -fp text).  Synchronous on return.
+static hipError_t h2d_staged(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!bytes) return hipSuccess;
+    if (bytes < (1u << 20)) return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    hipError_t e = ensure_ring(ctx);
+    if (e != hipSuccess) return e;
+    const char *s = static_cast<const char *>(src);
+    char *d = static_cast<char *>(dst);
+    bool used[fpm_ctx::kRing] = {};
+    for (size_t off = 0, i = 0; off < bytes; off += fpm_ctx::kRingBytes, i++) {
+        const int slot = (int)(i % fpm_ctx::kRing);
+        const size_t n = std::min(fpm_ctx::kRingBytes, bytes - off);
+        if (used[slot] && (e = hipEventSynchronize(ctx->ring_ev[slot])) != hipSuccess) return e;
+        memcpy(ctx->ring[slot], s + off, n);
+        if ((e = hipMemcpyAsync(d + off, ctx->ring[slot], n, hipMemcpyHostToDevice, ctx->copy)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipEventRecord(ctx->ring_ev[slot], ctx->copy)) != hipSuccess) return e;
+        used[slot] = true;
+    }
+    return hipStreamSynchronize(ctx->copy);
+}
+
+static hipError_t ensure_ring(fpm_ctx *ctx);
+
+// Device -> host copy into pageable caller memory through the same pinned ring: the DMA of
+// piece i overlaps the caller thread's memcpy of piece i - 1 out of the ring.
+static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!bytes) return hipSuccess;
+    if (bytes < (64u << 10)) return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    hipError_t e = ensure_ring(ctx);
+    if (e != hipSuccess) return e;
+    const char *s = static_cast<const char *>(src);
+    char *d = static_cast<char *>(dst);
+    const size_t R = fpm_ctx::kRingBytes;
+    const size_t n_pieces = (bytes + R - 1) / R;
+    auto issue = [&](size_t i) -> hipError_t {
+        const int slot = (int)(i % fpm_ctx::kRing);
+        const size_t off = i * R, n = std::min(R, bytes - off);
+        hipError_t x = hipMemcpyAsync(ctx->ring[slot], s + off, n, hipMemcpyDeviceToHost, ctx->copy);
+        if (x == hipSuccess) x = hipEventRecord(ctx->ring_ev[slot], ctx->copy);
+        return x;
+    };
+    for (size_t i = 0; i < std::min<size_t>(n_pieces, fpm_ctx::kRing); i++)
+        if ((e = issue(i)) != hipSuccess) return e;
+    for (size_t i = 0; i < n_pieces; i++) {
+        const int slot = (int)(i % fpm_ctx::kRing);
+        const size_t off = i * R, n = std::min(R, bytes - off);
+        if ((e = hipEventSynchronize(ctx->ring_ev[slot])) != hipSuccess) return e;
+        memcpy(d + off, ctx->ring[slot], n);
+        if (i + fpm_ctx::kRing < n_pieces && (e = issue(i + fpm_ctx::kRing)) != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 static hipError_t ensure_aux(fpm_ctx *ctx)
 {
@@ -202,6 +280,11 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
+    for (int i = 0; i < fpm_ctx::kRing; i++) {
+        if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
+        if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
+    }
+    if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     delete ctx;
 }
 
@@ -233,7 +316,8 @@ int fpm_free(fpm_ctx *ctx, void *dptr)
 int fpm_memcpy_h2d(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (int rc = set_device(ctx)) return rc;
-    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));   // earlier work on dst is ordered before
+    if (bytes) HIP_TRY(h2d_staged(ctx, dst, src, bytes));
     return FPM_OK;
 }
 
@@ -367,23 +451,69 @@ static void job_release(fpm_sketch_job *j)
 
 extern "C" {
 
+}  // extern "C"
+
+// Records to sketch, in the order their groups stream them: `rec_len(r)` bytes at `rec_pos(r)`
+// of the device sequence buffer.  Host path: fpm_sketch_stage packs the records itself
+// (host_packed); device path: fpm_sketch_stage_seq adopts the buffer seqparse.hip packed.
+struct StageRecords {
+    std::vector<uint32_t> order;        // records in group order (records of no group left out)
+    std::vector<uint64_t> pos, len;     // per record (indexed by record id)
+    std::vector<uint32_t> group;        // per record
+    uint32_t n_groups = 0;
+    const char *host_seq = nullptr;     // host path: record r is host_seq[pos..pos+len)
+    uint8_t *d_seq = nullptr;           // device path: packed buffer (ownership moves to the job)
+    uint64_t d_seq_bytes = 0;
+};
+
+static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
+                      fpm_sketch_job **job_out);
+
+extern "C" {
+
 int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
                      const uint64_t *rec_off, uint32_t n_rec, const uint32_t *group_of_rec,
                      uint32_t n_groups, fpm_sketch_job **job_out)
 {
     if (int rc = set_device(ctx)) return rc;
     if (!p || !job_out || (n_rec && (!seq || !rec_off))) return fail(FPM_EINVAL, "null argument");
-    if (p->kmer_size < 1 || p->kmer_size > 32) return fail(FPM_EINVAL, "kmer_size must be 1..32");
-    if (p->sketch_size < 1) return fail(FPM_EINVAL, "sketch_size must be >= 1");
     *job_out = nullptr;
-    const uint32_t k = p->kmer_size, s = p->sketch_size;
     if (!group_of_rec) n_groups = n_rec;
     for (uint32_t r = 0; r < n_rec; r++)
         if (rec_off[r + 1] < rec_off[r]) return fail(FPM_EINVAL, "record offsets must be non-decreasing");
     if (group_of_rec)
         for (uint32_t r = 0; r < n_rec; r++)
             if (group_of_rec[r] >= n_groups) return fail(FPM_EINVAL, "group id out of range");
+    StageRecords R;
+    R.n_groups = n_groups;
+    R.host_seq = seq;
+    R.pos.resize(n_rec);
+    R.len.resize(n_rec);
+    R.group.resize(n_rec);
+    R.order.resize(n_rec);
+    for (uint32_t r = 0; r < n_rec; r++) {
+        R.pos[r] = rec_off[r];
+        R.len[r] = rec_off[r + 1] - rec_off[r];
+        R.group[r] = group_of_rec ? group_of_rec[r] : r;
+        R.order[r] = r;
+    }
+    // records of a group in stream order, groups ascending
+    if (group_of_rec)
+        std::stable_sort(R.order.begin(), R.order.end(),
+                         [&](uint32_t a, uint32_t b) { return R.group[a] < R.group[b]; });
+    return stage_core(ctx, p, R, job_out);
+}
 
+}  // extern "C"
+
+static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
+                      fpm_sketch_job **job_out)
+{
+    if (p->kmer_size < 1 || p->kmer_size > 32) return fail(FPM_EINVAL, "kmer_size must be 1..32");
+    if (p->sketch_size < 1) return fail(FPM_EINVAL, "sketch_size must be >= 1");
+    const uint32_t k = p->kmer_size, s = p->sketch_size;
+    const uint32_t n_groups = R.n_groups;
+    const std::vector<uint32_t> &order = R.order;
     SketchKParams kp{};
     kp.k = k; kp.s = s; kp.seed = p->seed; kp.use64 = p->use64 ? 1 : 0;
     kp.canonical = p->noncanonical ? 0 : 1; kp.preserve_case = p->preserve_case ? 1 : 0;
@@ -393,21 +523,25 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     }
     kp.alphabet[0] = 0;   // the separator byte is never a k-mer byte
 
-    // records of a group in stream order, groups ascending
-    std::vector<uint32_t> order(n_rec);
-    for (uint32_t r = 0; r < n_rec; r++) order[r] = r;
-    if (group_of_rec)
-        std::stable_sort(order.begin(), order.end(),
-                         [&](uint32_t a, uint32_t b) { return group_of_rec[a] < group_of_rec[b]; });
-
-    // pack records >= k (each followed by 0x00) and cut tiles
-    uint64_t total = 0;
-    for (uint32_t r : order) {
-        uint64_t l = rec_off[r + 1] - rec_off[r];
-        if (l >= k) total += l + 1;
-    }
+    // host path: pack records >= k (each followed by 0x00) in group order
     std::vector<uint8_t> packed;
-    packed.reserve(total + 64);
+    if (R.host_seq) {
+        uint64_t total = 0;
+        for (uint32_t r : order)
+            if (R.len[r] >= k) total += R.len[r] + 1;
+        packed.resize(total);
+        uint64_t at = 0;
+        for (uint32_t r : order) {
+            if (R.len[r] < k) continue;
+            memcpy(packed.data() + at, R.host_seq + R.pos[r], R.len[r]);
+            packed[at + R.len[r]] = 0;
+            R.pos[r] = at;                      // now the packed offset
+            at += R.len[r] + 1;
+        }
+    }
+    // cut tiles: a tile covers [byte_off, byte_off + n_bytes) of the packed buffer, records of
+    // one group only; short records share a tile while its k-mer starts fit (bytes between
+    // them, separators or records shorter than k, hold no valid window)
     std::vector<TileDesc> tiles;
     std::vector<uint32_t> tile_group;
     uint64_t n_kmers = 0;
@@ -418,13 +552,11 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
         if (open) { tiles.push_back(cur); tile_group.push_back(cur_group); open = false; }
     };
     for (uint32_t r : order) {
-        const uint64_t l = rec_off[r + 1] - rec_off[r];
-        const uint32_t g = group_of_rec ? group_of_rec[r] : r;
+        const uint64_t l = R.len[r];
+        const uint32_t g = R.group[r];
         if (g != cur_group) { close(); cur_group = g; }
         if (l < k) continue;
-        const uint64_t poff = packed.size();
-        packed.insert(packed.end(), seq + rec_off[r], seq + rec_off[r] + l);
-        packed.push_back(0);
+        const uint64_t poff = R.pos[r];
         const uint64_t nk = l - k + 1;
         n_kmers += nk;
         if (nk > kPackKmers) {
@@ -434,8 +566,9 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
                 tiles.push_back(TileDesc{poff + c0, (uint32_t)(cn + k - 1), 0});
                 tile_group.push_back(g);
             }
-        } else if (open && (uint64_t)cur.n_bytes + 1 + l - k + 1 <= kPackKmers) {
-            cur.n_bytes += (uint32_t)(1 + l);   // separator + this record
+        } else if (open && poff > cur.byte_off + cur.n_bytes &&
+                   poff + l - cur.byte_off - k + 1 <= kPackKmers) {
+            cur.n_bytes = (uint32_t)(poff + l - cur.byte_off);   // through this record
         } else {
             close();
             cur = TileDesc{poff, (uint32_t)l, 0};
@@ -562,7 +695,7 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     job->kp = kp;
     job->n_groups = n_groups;
     job->n_rows = n_rows;
-    job->seq_bytes = packed.size();
+    job->seq_bytes = R.host_seq ? packed.size() : R.d_seq_bytes;
     job->n_kmers = n_kmers;
     job->n_tiles = tiles.size();
     memcpy(job->class_begin, class_begin, sizeof(class_begin));
@@ -577,7 +710,8 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     auto alloc = [&](void **ptr, size_t bytes) {
         if (e == hipSuccess) e = hipMalloc(ptr, bytes ? bytes : 16);
     };
-    alloc((void **)&job->d_seq, packed.size() + 64);
+    if (R.host_seq) alloc((void **)&job->d_seq, packed.size() + 64);
+    else { job->d_seq = R.d_seq; R.d_seq = nullptr; }   // the parse's packed records
     alloc((void **)&job->d_tiles, by_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_rows, (size_t)n_rows * s * sizeof(uint64_t));
     alloc((void **)&job->d_count, (size_t)n_rows * sizeof(uint32_t));
@@ -607,7 +741,7 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
         return md;
     };
     const std::vector<MergeDesc> md = descs(mplan), smd = descs(splan);
-    if (!packed.empty()) e = hipMemcpy(job->d_seq, packed.data(), packed.size(), hipMemcpyHostToDevice);
+    if (!packed.empty()) e = h2d_staged(ctx, job->d_seq, packed.data(), packed.size());
     if (e == hipSuccess && !by_class.empty())
         e = hipMemcpy(job->d_tiles, by_class.data(), by_class.size() * sizeof(TileDesc),
                       hipMemcpyHostToDevice);
@@ -628,6 +762,8 @@ int fpm_sketch_stage(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,
     *job_out = job;
     return FPM_OK;
 }
+
+extern "C" {
 
 int fpm_sketch_run(fpm_sketch_job *job, void *stream)
 {
@@ -687,8 +823,8 @@ int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_co
     HIP_TRY(hipStreamSynchronize(ctx->stream));
     HIP_TRY(hipDeviceSynchronize());
     if (out_hashes && job->n_groups)
-        HIP_TRY(hipMemcpy(out_hashes, job->d_rows, (size_t)job->n_groups * job->kp.s * sizeof(uint64_t),
-                          hipMemcpyDeviceToHost));
+        HIP_TRY(d2h_staged(ctx, out_hashes, job->d_rows,
+                           (size_t)job->n_groups * job->kp.s * sizeof(uint64_t)));
     if (out_count && job->n_groups)
         HIP_TRY(hipMemcpy(out_count, job->d_count, (size_t)job->n_groups * sizeof(uint32_t),
                           hipMemcpyDeviceToHost));
@@ -815,7 +951,7 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
     const uint64_t scan_w = scan_scratch_words(nb ? nb : 1);
     HIP_TRY(hipMalloc(&j->d_text, text_len + 16));
     HIP_TRY(hipMalloc(&j->d_blk, ((size_t)2 * nb + 2 + scan_w) * 4));
-    if (text_len) HIP_TRY(hipMemcpyAsync(j->d_text, text, text_len, hipMemcpyHostToDevice, st));
+    if (text_len) HIP_TRY(h2d_staged(ctx, j->d_text, text, text_len));
     uint32_t *blk_cnt = j->d_blk, *blk_off = j->d_blk + nb, *scan_s = j->d_blk + 2 * nb + 2;
     // newline count first: it sizes the line index
     uint64_t n_nl = 0;
@@ -880,6 +1016,168 @@ void fpm_fp_text_free(fpm_fptext *j)
     fptext_release(j);
     delete j;
 }
+
+}  // extern "C"
+
+// ----------------------------------------------------------------------------
+// FASTA text -> packed records on the device (seqparse.hip)
+// ----------------------------------------------------------------------------
+
+struct fpm_seqtext {
+    fpm_ctx *ctx = nullptr;
+    std::vector<uint64_t> seg_off, seg_len;     // each file's offset in the device text
+    uint64_t n_rec = 0, total_kept = 0;
+    uint8_t *d_text = nullptr, *d_reset = nullptr, *d_out = nullptr;
+    void *d_xf = nullptr, *d_cin = nullptr;
+    uint64_t *d_rec = nullptr;                  // hdr_pos | hdr_end | kept_at | seq_off | seq_len
+    uint64_t *d_totals = nullptr;
+};
+
+static void seqtext_release(fpm_seqtext *j)
+{
+    if (!j) return;
+    (void)hipSetDevice(j->ctx->device);
+    for (void *p : {(void *)j->d_text, (void *)j->d_reset, (void *)j->d_out, j->d_xf, j->d_cin,
+                    (void *)j->d_rec, (void *)j->d_totals})
+        if (p) (void)hipFree(p);
+}
+
+extern "C" {
+
+int fpm_seq_parse(fpm_ctx *ctx, const char *const *seg_text, const uint64_t *seg_len,
+                  uint32_t n_seg, fpm_seqtext **job, uint64_t *n_records, int *quality_lines)
+{
+    if (!job || !n_records || (n_seg && (!seg_text || !seg_len)))
+        return fail(FPM_EINVAL, "seq_parse: null argument");
+    *job = nullptr;
+    *n_records = 0;
+    if (quality_lines) *quality_lines = 0;
+    if (int rc = set_device(ctx)) return rc;
+    std::unique_ptr<fpm_seqtext, void (*)(fpm_seqtext *)> j(new fpm_seqtext,
+        [](fpm_seqtext *p) { seqtext_release(p); delete p; });
+    j->ctx = ctx;
+    // each file from a chunk boundary, at least one '\n' after it
+    uint64_t at = 0;
+    for (uint32_t i = 0; i < n_seg; i++) {
+        j->seg_off.push_back(at);
+        j->seg_len.push_back(seg_len[i]);
+        at = (at + seg_len[i] + 1 + kSpChunk - 1) / kSpChunk * kSpChunk;
+    }
+    const uint64_t text_bytes = at;
+    const uint64_t n_chunks64 = text_bytes / kSpChunk;
+    if (n_chunks64 > 0xFFFFFFFFull) return fail(FPM_EINVAL, "seq_parse: input too large");
+    const uint32_t n_chunks = (uint32_t)n_chunks64;
+    hipStream_t st = ctx->stream;
+    HIP_TRY(hipMalloc(&j->d_text, text_bytes ? text_bytes : 16));
+    HIP_TRY(hipMalloc(&j->d_reset, n_chunks ? n_chunks : 1));
+    HIP_TRY(hipMalloc(&j->d_xf, (size_t)(n_chunks ? n_chunks : 1) * seq_xf_bytes()));
+    HIP_TRY(hipMalloc(&j->d_cin, (size_t)(n_chunks ? n_chunks : 1) * seq_cin_bytes()));
+    HIP_TRY(hipMalloc(&j->d_totals, 3 * sizeof(uint64_t)));
+    std::vector<uint8_t> reset(n_chunks ? n_chunks : 1, 0);
+    for (uint32_t i = 0; i < n_seg; i++)
+        if (j->seg_off[i] / kSpChunk < n_chunks) reset[j->seg_off[i] / kSpChunk] = 1;
+    HIP_TRY(hipMemsetAsync(j->d_text, '\n', text_bytes, st));
+    HIP_TRY(hipMemcpyAsync(j->d_reset, reset.data(), n_chunks, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < n_seg; i++)
+        HIP_TRY(h2d_staged(ctx, j->d_text + j->seg_off[i], seg_text[i], seg_len[i]));
+    uint64_t tot[3] = {0, 0, 0};
+    if (n_chunks) {
+        TimedLaunch tl(ctx, FPM_K_SEQPARSE, st);
+        HIP_TRY(launch_seq_scan(j->d_text, j->d_reset, n_chunks, j->d_xf, j->d_cin, j->d_totals, st));
+        tl.done();
+        HIP_TRY(hipMemcpyAsync(tot, j->d_totals, sizeof(tot), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    j->n_rec = tot[0];
+    j->total_kept = tot[1];
+    if (quality_lines) *quality_lines = tot[2] ? 1 : 0;
+    HIP_TRY(hipMalloc(&j->d_out, j->total_kept + j->n_rec + 64));
+    HIP_TRY(hipMalloc(&j->d_rec, (size_t)(j->n_rec ? j->n_rec : 1) * 5 * sizeof(uint64_t)));
+    if (n_chunks) {
+        const uint64_t n = j->n_rec ? j->n_rec : 1;
+        TimedLaunch tl(ctx, FPM_K_SEQPARSE, st);
+        HIP_TRY(launch_seq_emit(j->d_text, n_chunks, j->d_cin, j->n_rec, j->total_kept, j->d_rec,
+                                j->d_rec + n, j->d_rec + 2 * n, j->d_rec + 3 * n, j->d_rec + 4 * n,
+                                j->d_out, st));
+        tl.done();
+    }
+    // the text image and scan scratch are not needed past this point
+    HIP_TRY(hipStreamSynchronize(st));
+    for (void **p : {(void **)&j->d_text, (void **)&j->d_xf, (void **)&j->d_cin})
+        if (*p) { (void)hipFree(*p); *p = nullptr; }
+    *n_records = j->n_rec;
+    *job = j.release();
+    return FPM_OK;
+}
+
+int fpm_seq_records(fpm_seqtext *j, uint32_t *seg_of_rec, uint64_t *hdr_off, uint64_t *hdr_len,
+                    uint64_t *seq_len)
+{
+    if (!j) return fail(FPM_EINVAL, "seq_records: null job");
+    if (int rc = set_device(j->ctx)) return rc;
+    const uint64_t n = j->n_rec;
+    if (!n) return FPM_OK;
+    std::vector<uint64_t> rec((size_t)n * 5);
+    HIP_TRY(d2h_staged(j->ctx, rec.data(), j->d_rec, rec.size() * 8));
+    const uint64_t *pos = rec.data(), *end = pos + n, *len = pos + 4 * n;
+    for (uint64_t r = 0; r < n; r++) {
+        // the file holding the header: the last segment starting at or before it
+        const uint32_t sg = (uint32_t)(std::upper_bound(j->seg_off.begin(), j->seg_off.end(), pos[r]) -
+                                       j->seg_off.begin()) - 1;
+        const uint64_t o = pos[r] - j->seg_off[sg];
+        // the header's '\n', or the end of its file (the '\n' bytes after a file are padding)
+        const uint64_t e = std::min(end[r] - j->seg_off[sg], j->seg_len[sg]);
+        if (seg_of_rec) seg_of_rec[r] = sg;
+        if (hdr_off) hdr_off[r] = o;
+        if (hdr_len) hdr_len[r] = e - o;
+        if (seq_len) seq_len[r] = len[r];
+    }
+    return FPM_OK;
+}
+
+void fpm_seq_free(fpm_seqtext *j)
+{
+    seqtext_release(j);
+    delete j;
+}
+
+int fpm_sketch_stage_seq(fpm_ctx *ctx, const fpm_sketch_params *p, fpm_seqtext *seq,
+                         const uint32_t *group_of_rec, uint32_t n_groups, fpm_sketch_job **job_out)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!p || !seq || !job_out || (seq->n_rec && !group_of_rec))
+        return fail(FPM_EINVAL, "sketch_stage_seq: null argument");
+    if (seq->ctx != ctx) return fail(FPM_EINVAL, "sketch_stage_seq: records parsed on another context");
+    if (!seq->d_out) return fail(FPM_EINVAL, "sketch_stage_seq: records already staged");
+    *job_out = nullptr;
+    const uint64_t n = seq->n_rec;
+    if (n > 0xFFFFFFFFull) return fail(FPM_EINVAL, "sketch_stage_seq: too many records");
+    StageRecords R;
+    R.n_groups = n_groups;
+    R.pos.resize(n);
+    R.len.resize(n);
+    R.group.assign(group_of_rec, group_of_rec + n);
+    const uint64_t nn = n ? n : 1;
+    HIP_TRY(d2h_staged(ctx, R.pos.data(), seq->d_rec + 3 * nn, n * 8));
+    HIP_TRY(d2h_staged(ctx, R.len.data(), seq->d_rec + 4 * nn, n * 8));
+    for (uint64_t r = 0; r < n; r++) {
+        if (group_of_rec[r] == FPM_NO_GROUP) continue;
+        if (group_of_rec[r] >= n_groups) return fail(FPM_EINVAL, "group id out of range");
+        R.order.push_back((uint32_t)r);
+    }
+    std::stable_sort(R.order.begin(), R.order.end(),
+                     [&](uint32_t a, uint32_t b) { return R.group[a] < R.group[b]; });
+    R.d_seq = seq->d_out;
+    R.d_seq_bytes = seq->total_kept + seq->n_rec;
+    const int rc = stage_core(ctx, p, R, job_out);
+    if (!R.d_seq) seq->d_out = nullptr;   // the job owns the packed records now
+    return rc;
+}
+
+}  // extern "C"
+
+extern "C" {
 
 // ----------------------------------------------------------------------------
 // dist

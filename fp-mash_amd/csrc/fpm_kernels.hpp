@@ -161,6 +161,21 @@ hipError_t launch_fp_lines(const uint8_t *d_text, uint64_t len, const uint64_t *
                            uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals, void *hash,
                            uint8_t *new_id, hipStream_t st);
 
+// FASTA text -> packed records (seqparse.hip).  The text buffer holds each file from a
+// kSpChunk-aligned offset, '\n' bytes after it; reset[c] = 1 on a file's first chunk.
+constexpr uint32_t kSpChunk = 4096;
+size_t seq_xf_bytes();    // per-chunk summary
+size_t seq_cin_bytes();   // per-chunk input state / counts
+// summaries + chunk scan; d_totals = {records, sequence bytes, '+' in sequence text}
+hipError_t launch_seq_scan(const uint8_t *d_text, const uint8_t *d_reset, uint32_t n_chunks,
+                           void *d_xf, void *d_cin, uint64_t *d_totals, hipStream_t st);
+// record table (header '>' position, header '\n' position, packed offset, length) and the
+// packed records (sequence bytes + 0x00 each) in d_out
+hipError_t launch_seq_emit(const uint8_t *d_text, uint32_t n_chunks, const void *d_cin,
+                           uint64_t n_rec, uint64_t total_kept, uint64_t *d_hdr_pos,
+                           uint64_t *d_hdr_end, uint64_t *d_kept_at, uint64_t *d_seq_off,
+                           uint64_t *d_seq_len, uint8_t *d_out, hipStream_t st);
+
 // triangle -fp positional compare (dist.hip)
 hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,

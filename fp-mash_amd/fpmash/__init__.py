@@ -21,12 +21,14 @@ LIB_PATH = os.environ.get("FPMASH_LIB") or os.path.join(PKG_ROOT, "lib", "libfpm
 BIN_PATH = os.path.join(PKG_ROOT, "bin", "fpmash")
 
 FPM_OK, FPM_EINVAL, FPM_ENODEV, FPM_EHIP, FPM_ENOMEM = 0, -1, -2, -3, -4
-K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE, K_INDEX, K_PROBE, K_FPTEXT, K_FILL = range(9)
+(K_SKETCH, K_MERGE, K_FPHASH, K_COMPARE, K_FINALIZE, K_INDEX, K_PROBE, K_FPTEXT, K_FILL,
+ K_SEQPARSE) = range(10)
+NO_GROUP = 0xFFFFFFFF
 KERNEL_NAMES = {K_SKETCH: "sketch_tiles_kernel", K_MERGE: "merge_kernel",
                 K_FPHASH: "fp_hash_kernel", K_COMPARE: "candidate compare (rank_rows/walk_cand/compare_grid)",
                 K_FINALIZE: "dist finalize (dense / candidate cells)", K_INDEX: "dist index build",
                 K_PROBE: "probe_rows_kernel", K_FPTEXT: "fp text parse (nl index + fp_line)",
-                K_FILL: "dist_fill_kernel"}
+                K_FILL: "dist_fill_kernel", K_SEQPARSE: "FASTA parse (seq chunk scan + emit)"}
 DIST_AUTO, DIST_DENSE, DIST_SPARSE = 0, 1, 2
 # fpm_ctx_last_dist_stats path codes
 DIST_PATHS = ["dense walk", "bucket index + literal walk", "bucket index + bucketed rank"]
@@ -105,6 +107,11 @@ SYMBOLS = [
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),
     ("fpm_refset_free", None, [vp]),
+    ("fpm_seq_parse", C.c_int, [vp, C.POINTER(C.c_char_p), u64p, C.c_uint32, C.POINTER(vp),
+                                u64p, C.POINTER(C.c_int)]),
+    ("fpm_seq_records", C.c_int, [vp, u32p, u64p, u64p, u64p]),
+    ("fpm_sketch_stage_seq", C.c_int, [vp, vp, vp, u32p, C.c_uint32, C.POINTER(vp)]),
+    ("fpm_seq_free", None, [vp]),
     ("fpm_host_alloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
     ("fpm_host_free", C.c_int, [vp, vp]),
 ]
@@ -335,6 +342,50 @@ class Context:
 
     def sketch_job(self, params, seqs, groups=None, n_groups=None):
         return SketchJob(self, params, seqs, groups, n_groups)
+
+    # --- FASTA text on the device -------------------------------------------------
+    def seq_parse(self, files):
+        """fpm_seq_parse over file images -> (handle, records dict, quality_lines flag).
+        records: seg, hdr_off, hdr_len, seq_len per record (kseq record rules)."""
+        n_seg = len(files)
+        ptrs = (C.c_char_p * max(n_seg, 1))(*files)
+        lens = np.array([len(f) for f in files] + [0], dtype=np.uint64)
+        job, n, q = vp(), C.c_uint64(), C.c_int()
+        _check(lib().fpm_seq_parse(self.h, ptrs, _p(lens, u64p), n_seg, C.byref(job),
+                                   C.byref(n), C.byref(q)))
+        n = n.value
+        seg = np.zeros(max(n, 1), np.uint32)
+        ho, hl, sl = (np.zeros(max(n, 1), np.uint64) for _ in range(3))
+        try:
+            _check(lib().fpm_seq_records(job, _p(seg, u32p), _p(ho, u64p), _p(hl, u64p),
+                                         _p(sl, u64p)))
+        except Exception:
+            lib().fpm_seq_free(job)
+            raise
+        return job.value, {"seg": seg[:n], "hdr_off": ho[:n], "hdr_len": hl[:n],
+                           "seq_len": sl[:n]}, bool(q.value)
+
+    def sketch_seq(self, params, seq_job, groups, n_groups):
+        """fpm_sketch_stage_seq + run + fetch over parsed records (the job takes the packed
+        records; free the parse handle with seq_free afterwards)."""
+        g = np.ascontiguousarray(groups, dtype=np.uint32)
+        if g.size == 0:
+            g = np.zeros(1, np.uint32)
+        h = vp()
+        _check(lib().fpm_sketch_stage_seq(self.h, C.byref(params), seq_job, _p(g, u32p),
+                                          n_groups, C.byref(h)))
+        job = SketchJob.__new__(SketchJob)
+        job.ctx, job.params, job.n_groups, job.h, job._keep = self, params, n_groups, h.value, None
+        try:
+            job.run()
+            rows, cnt = job.fetch()
+        finally:
+            job.free()
+        return [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+
+    @staticmethod
+    def seq_free(seq_job):
+        lib().fpm_seq_free(seq_job)
 
     # --- -fp ----------------------------------------------------------------
     def fp_hash_lines(self, values_per_line, seed=42, use64=False):

@@ -5,8 +5,10 @@
 #include "Command.h"
 #include "Device.h"
 #include "Sketch.h"
+#include "Timing.h"
 
 #include <algorithm>
+#include <chrono>
 #include <atomic>
 #include <cmath>
 #include <condition_variable>
@@ -18,6 +20,10 @@
 #include <iostream>
 #include <mutex>
 #include <thread>
+
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
 namespace fpmhost {
 
@@ -75,9 +81,10 @@ struct Out {
     }
     void u(uint64_t x)
     {
-        char t[32];
-        int n = snprintf(t, sizeof t, "%llu", (unsigned long long)x);
-        buf.append(t, n);
+        char t[24];
+        int n = 0;
+        do { t[23 - n++] = (char)('0' + x % 10); x /= 10; } while (x);
+        buf.append(t + 24 - n, n);
     }
 };
 
@@ -89,6 +96,7 @@ int CommandDistance::run() const
         print();
         return 0;
     }
+    warmDevices();
     const bool list = options.at("list").active;
     const bool table = options.at("table").active;
     const bool comment = options.at("comment").active;
@@ -124,6 +132,7 @@ int CommandDistance::run() const
     else if (fingerprint && tagTXT) sketchRef.initFromFingerprints(refArg, parameters);
     else sketchRef.initFromFiles(refArg, parameters);
 
+    phaseMark("reference sketch loaded");
     const double lengthThreshold =
         (parameters.warning * sketchRef.getKmerSpace()) / (1. - parameters.warning);
     if (isSketch) {
@@ -171,6 +180,7 @@ int CommandDistance::run() const
     else if (fingerprint && tagTXT) sketchQuery.initFromFingerprints(queryFiles, parameters);
     else sketchQuery.initFromFiles(queryFiles, parameters, 0, true);
 
+    phaseMark("query sketch loaded");
     const uint64_t nR = sketchRef.getReferenceCount(), nQ = sketchQuery.getReferenceCount();
     const uint64_t sketchSize = (uint64_t)std::min(sketchQuery.getMinHashesPerWindow(),
                                                    sketchRef.getMinHashesPerWindow());
@@ -187,33 +197,21 @@ int CommandDistance::run() const
             const Reference &r = sk.getReference(i);
             len[i] = (uint32_t)r.hashes.size();
             L[i] = r.length;
-            for (uint64_t j = 0; j < r.hashes.size(); j++) {
-                if (use64) memcpy(&m[(i * width + j) * 8], &r.hashes[j], 8);
-                else { uint32_t v = (uint32_t)r.hashes[j]; memcpy(&m[(i * width + j) * 4], &v, 4); }
+            if (use64) {
+                memcpy(&m[i * width * 8], r.hashes.data(), r.hashes.size() * 8);
+            } else {
+                uint32_t *row = reinterpret_cast<uint32_t *>(&m[i * width * 4]);
+                for (uint64_t j = 0; j < r.hashes.size(); j++) row[j] = (uint32_t)r.hashes[j];
             }
         }
     };
     uint64_t width = 1;
     for (uint64_t i = 0; i < nR; i++) width = std::max<uint64_t>(width, sketchRef.getReference(i).hashes.size());
     for (uint64_t i = 0; i < nQ; i++) width = std::max<uint64_t>(width, sketchQuery.getReference(i).hashes.size());
-    std::vector<uint8_t> R, Q;
-    std::vector<uint32_t> rl, ql;
-    std::vector<uint64_t> rL, qL;
-    pack(sketchRef, R, rl, rL, width);
-    pack(sketchQuery, Q, ql, qL, width);
-
-    // The grid in query blocks (CommandDistance.cpp:224-261 chunks it for the pool): every
-    // device holds the reference set with its index built once (fpm_refset_create) and takes
-    // blocks in turn; results land in pinned buffers; formatter threads (-p) turn each block
-    // into text pieces, which this thread writes strictly in block order (writeOutput,
-    // :276-333, consumes the pool's outputs in order).
     const int nDev = nR && nQ ? deviceCount() : 0;
-    std::vector<fpm_refset *> sets(nDev, nullptr);
-    for (int d = 0; d < nDev; d++)
-        check(fpm_refset_create(device(d), R.data(), rl.data(), rL.data(), width, (uint32_t)nR,
-                                hb, (uint32_t)sketchSize, &sets[d]),
-              "dist reference set");
-    uint64_t blockPairs = 16ULL << 20;
+    // 2 M pairs per block: 58 MB of pinned results per slot (16 M-pair slots made pinning and
+    // unpinning ~1.4 GB cost ~0.6 s of the C2 command)
+    uint64_t blockPairs = 2ULL << 20;
     if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
     const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
     const uint64_t nBlocks = nR ? (nQ + block - 1) / block : 0;
@@ -236,20 +234,43 @@ int CommandDistance::run() const
     uint64_t written = 0;                   // blocks already written out
     std::deque<std::function<void()>> tasks;
     bool stop = false;
-    for (int i = 0; i < nSlots && nBlocks; i++) {
-        // pinned buffers of one block on the context of the device that fills them
-        Slot &sl = slots[i];
-        const uint64_t np = block * nR;
-        fpm_ctx *c = device(0);
-        check(fpm_host_alloc(c, (void **)&sl.nu, np * 4), "pinned buffers");
-        check(fpm_host_alloc(c, (void **)&sl.de, np * 4), "pinned buffers");
-        check(fpm_host_alloc(c, (void **)&sl.di, np * 8), "pinned buffers");
-        check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
-        check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
-    }
+    // pinned result buffers (page locking costs ~0.6 ms per MB): one thread per slot, beside
+    // the row packing and the reference sets
+    std::vector<std::thread> pinner;
+    for (int i = 0; i < nSlots && nBlocks; i++)
+        pinner.emplace_back([&, i] {
+            Slot &sl = slots[i];
+            const uint64_t np = block * nR;
+            fpm_ctx *c = device(0);
+            check(fpm_host_alloc(c, (void **)&sl.nu, np * 4), "pinned buffers");
+            check(fpm_host_alloc(c, (void **)&sl.de, np * 4), "pinned buffers");
+            check(fpm_host_alloc(c, (void **)&sl.di, np * 8), "pinned buffers");
+            check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
+            check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
+        });
+    std::vector<uint8_t> R, Q;
+    std::vector<uint32_t> rl, ql;
+    std::vector<uint64_t> rL, qL;
+    pack(sketchRef, R, rl, rL, width);
+    pack(sketchQuery, Q, ql, qL, width);
+
+    // The grid in query blocks (CommandDistance.cpp:224-261 chunks it for the pool): every
+    // device holds the reference set with its index built once (fpm_refset_create) and takes
+    // blocks in turn; results land in pinned buffers; formatter threads (-p) turn each block
+    // into text pieces, which this thread writes strictly in block order (writeOutput,
+    // :276-333, consumes the pool's outputs in order).
+    std::vector<fpm_refset *> sets(nDev, nullptr);
+    for (int d = 0; d < nDev; d++)
+        check(fpm_refset_create(device(d), R.data(), rl.data(), rL.data(), width, (uint32_t)nR,
+                                hb, (uint32_t)sketchSize, &sets[d]),
+              "dist reference set");
+    for (auto &t : pinner) t.join();
+    phaseMark("rows packed + reference sets on the devices");
     auto format = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, std::string &dst) {
         Out o;
         o.autoflush = false;
+        o.buf.swap(dst);                    // the piece's buffer from earlier blocks (no regrowth)
+        o.buf.clear();
         for (uint64_t qi = qa; qi < qb; qi++) {
             const Reference &qr = sketchQuery.getReference(q0 + qi);
             if (table) o.put(qr.name);
@@ -324,13 +345,17 @@ int CommandDistance::run() const
                 std::lock_guard<std::mutex> lk(mu);
                 sl.b = b;
                 sl.dev = d;
-                sl.text.assign(parts, std::string());
+                sl.text.resize(parts);
                 sl.pending = (int)parts;
                 sl.ready = false;
                 for (uint64_t p = 0; p < parts; p++) {
                     const uint64_t qa = p * per, qb = std::min(nq, qa + per);
                     tasks.emplace_back([&, q0, qa, qb, p, bslot = &sl] {
                         std::string t;
+                        {
+                            std::lock_guard<std::mutex> lk2(mu);
+                            t.swap(bslot->text[p]);
+                        }
                         format(*bslot, q0, qa, qb, t);
                         std::lock_guard<std::mutex> lk2(mu);
                         bslot->text[p].swap(t);
@@ -341,22 +366,74 @@ int CommandDistance::run() const
                 cv.notify_all();
             }
         });
+    // stdout a regular file (not O_APPEND): the pieces of a block go out as pwrite()s at their
+    // offsets from the formatter threads; otherwise (pipes, terminals) this thread writes them
+    out.flush();
+    fflush(stdout);
+    const int ofd = fileno(stdout);
+    struct stat ost {};
+    const int ofl = fcntl(ofd, F_GETFL);
+    off_t opos = -1;
+    const bool direct = nBlocks && fstat(ofd, &ost) == 0 && S_ISREG(ost.st_mode) && ofl >= 0 &&
+                        !(ofl & O_APPEND) && (opos = lseek(ofd, 0, SEEK_CUR)) >= 0;
+    std::atomic<bool> writeFailed{false};
+    double waitMs = 0, writeMs = 0;
     for (uint64_t b = 0; b < nBlocks; b++) {
         Slot &sl = slots[b % nSlots];
         std::vector<std::string> pieces;
+        auto t0 = std::chrono::steady_clock::now();
         {
             std::unique_lock<std::mutex> lk(mu);
             cv.wait(lk, [&] { return sl.b == b && sl.ready; });
             pieces.swap(sl.text);
         }
-        out.flush();
-        for (auto &t : pieces) fwrite(t.data(), 1, t.size(), stdout);
+        auto t1 = std::chrono::steady_clock::now();
+        if (direct) {
+            int left = (int)pieces.size();
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                for (auto &t : pieces) {
+                    const off_t at = opos;
+                    opos += (off_t)t.size();
+                    tasks.emplace_front([&, at, piece = &t] {
+                        for (size_t q = 0; q < piece->size();) {
+                            const ssize_t w = pwrite(ofd, piece->data() + q, piece->size() - q, at + (off_t)q);
+                            if (w <= 0) { writeFailed = true; break; }
+                            q += (size_t)w;
+                        }
+                        std::lock_guard<std::mutex> lk2(mu);
+                        --left;
+                        cv.notify_all();
+                    });
+                }
+            }
+            cv.notify_all();
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return left == 0; });
+        } else {
+            for (auto &t : pieces) fwrite(t.data(), 1, t.size(), stdout);
+        }
+        auto t2 = std::chrono::steady_clock::now();
+        waitMs += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        writeMs += std::chrono::duration<double, std::milli>(t2 - t1).count();
         {
+            // the piece buffers go back to the slot for its next block: allocating and
+            // unmapping ~40 MB strings per piece cost ~0.4 s of page faults and munmap
             std::lock_guard<std::mutex> lk(mu);
+            pieces.swap(sl.text);
             written = b + 1;
         }
         cv.notify_all();
     }
+    if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
+    if (writeFailed) {
+        std::cerr << "ERROR: writing the distance output failed." << std::endl;
+        exit(1);
+    }
+    if (timingOn())
+        fprintf(stderr, "[fpmash] writer: waited %.1f ms for blocks, wrote for %.1f ms\n", waitMs,
+                writeMs);
+    phaseMark("blocks computed, formatted and written");
     for (auto &t : gpu) t.join();
     {
         std::lock_guard<std::mutex> lk(mu);

@@ -1,6 +1,7 @@
 // CommandSketch.cpp — `fpmash sketch` (CommandSketch.cpp:19-122): same options,
 // messages and .msh output; sketching runs on the MI355X.
 #include "Command.h"
+#include "Device.h"
 #include "Sketch.h"
 
 #include <iostream>
@@ -40,6 +41,7 @@ int CommandSketch::run() const
         print();
         return 0;
     }
+    warmDevices();
     const int verbosity = 1;
     const bool list = options.at("list").active;
     const bool fingerprint = options.at("fingerprint").active;

@@ -65,6 +65,7 @@ int CommandTriangle::run() const
         print();
         return 0;
     }
+    warmDevices();
     const bool list = options.at("list").active;
     const bool comment = options.at("comment").active;
     bool edge = options.at("edge").active;

@@ -3,6 +3,7 @@
 #include <cstdlib>
 #include <iostream>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 namespace fpmhost {
@@ -12,12 +13,33 @@ std::vector<fpm_ctx *> g_ctx;
 std::vector<int> g_ids;
 std::once_flag g_once;
 std::mutex g_mu;
+std::thread g_warm;
+std::once_flag g_warm_join;
+
+void join_warm()
+{
+    if (g_warm.joinable()) g_warm.join();
+}
 
 void release()
 {
     for (auto *c : g_ctx)
         if (c) fpm_ctx_destroy(c);
     g_ctx.clear();
+}
+
+std::once_flag g_exit_once;
+
+void shutdown()
+{
+    join_warm();
+    release();
+}
+
+// one exit handler, registered on the main thread before any context exists
+void ensure_exit_handler()
+{
+    std::call_once(g_exit_once, [] { atexit(shutdown); });
 }
 
 void init_ids()
@@ -32,7 +54,7 @@ void init_ids()
         if (g_ids.empty()) g_ids.push_back(0);   // fpm_ctx_create reports the missing device
     }
     g_ctx.assign(g_ids.size(), nullptr);
-    atexit(release);
+    ensure_exit_handler();
 }
 }  // namespace
 
@@ -46,12 +68,31 @@ void check(int rc, const char *what)
 
 int deviceCount()
 {
+    std::call_once(g_warm_join, join_warm);
     std::call_once(g_once, init_ids);
     return (int)g_ids.size();
 }
 
+void warmDevices()
+{
+    ensure_exit_handler();
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_warm.joinable()) return;
+    // HIP runtime start-up (device enumeration + context streams: ~0.1-0.25 s) runs beside
+    // the caller's input reading; a context that fails to come up is reported by the first
+    // device() call on the main thread
+    g_warm = std::thread([] {
+        std::call_once(g_once, init_ids);
+        for (size_t i = 0; i < g_ids.size(); i++) {
+            std::lock_guard<std::mutex> lk2(g_mu);
+            if (!g_ctx[i] && fpm_ctx_create(g_ids[i], &g_ctx[i]) != FPM_OK) g_ctx[i] = nullptr;
+        }
+    });
+}
+
 fpm_ctx *device(int i)
 {
+    std::call_once(g_warm_join, join_warm);
     std::call_once(g_once, init_ids);
     std::lock_guard<std::mutex> lk(g_mu);
     if (!g_ctx[i]) check(fpm_ctx_create(g_ids[i], &g_ctx[i]), "MI355X device");

@@ -13,6 +13,8 @@
 namespace fpmhost {
 
 int deviceCount();
+// start creating every context on a background thread (the first device() call joins it)
+void warmDevices();
 fpm_ctx *device(int i = 0);
 void check(int rc, const char *what);
 

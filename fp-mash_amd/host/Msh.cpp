@@ -12,7 +12,12 @@
 #include "Msh.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
+
+#include <fcntl.h>
+#include <unistd.h>
 
 namespace fpmhost {
 
@@ -21,47 +26,127 @@ namespace {
 enum : uint64_t { kStruct = 0, kList = 1, kFar = 2 };
 enum : uint64_t { kByte = 2, kFour = 4, kEight = 5, kComposite = 7 };
 
-// capnp MallocMessageBuilder + BuilderArena allocation model
+// capnp MallocMessageBuilder + BuilderArena allocation model.  A segment is a run of
+// pieces: words the builder owns, or an external block (a reference's hash list, read in
+// place when the message is written: the 8 B/hash bulk of a .msh is never copied).
 class Builder {
 public:
+    struct Piece {
+        uint64_t off, n;                 // word range in the segment
+        std::vector<uint64_t> own;       // owned words (empty for an external block)
+        const void *ext = nullptr;
+    };
     struct Seg {
-        std::vector<uint64_t> w;   // used words
-        uint64_t cap;
+        std::vector<Piece> pieces;
+        uint64_t used = 0, cap = 0;
     };
     std::vector<Seg> segs;
 
     // allocate the root pointer (first allocation creates segment 0)
-    void allocRootPointer() { arenaAlloc(1); }
+    void allocRootPointer() { arenaAlloc(1, nullptr); }
 
     // WireHelpers::allocate: an object of n words referenced from (rs, ro).
     // Returns the object's (segment, offset); writes the pointer (or far pointer +
-    // landing pad) with the given kind and upper 32 bits.
-    std::pair<int, uint64_t> alloc(int rs, uint64_t ro, uint64_t n, uint64_t kind, uint64_t upper)
+    // landing pad) with the given kind and upper 32 bits.  ext != nullptr: the object's
+    // words are n words at ext (written as they are).
+    std::pair<int, uint64_t> alloc(int rs, uint64_t ro, uint64_t n, uint64_t kind, uint64_t upper,
+                                   const void *ext = nullptr)
     {
         uint64_t off = 0;
-        if (tryAlloc(rs, n, off)) {
-            segs[rs].w[ro] = pointer(kind, (int64_t)off - (int64_t)(ro + 1), upper);
+        if (tryAlloc(rs, n, off, ext)) {
+            word(rs, ro) = pointer(kind, (int64_t)off - (int64_t)(ro + 1), upper);
             return {rs, off};
         }
-        auto a = arenaAlloc(n + 1);   // landing pad + object
-        segs[rs].w[ro] = kFar | (a.second << 3) | ((uint64_t)a.first << 32);
-        segs[a.first].w[a.second] = pointer(kind, 0, upper);
+        auto a = arenaAlloc(n + 1, ext);              // landing pad, then the object
+        word(rs, ro) = kFar | (a.second << 3) | ((uint64_t)a.first << 32);
+        word(a.first, a.second) = pointer(kind, 0, upper);
         return {a.first, a.second + 1};
     }
 
-    uint64_t &word(int s, uint64_t o) { return segs[s].w[o]; }
-
-    std::string serialize() const
+    uint64_t &word(int s, uint64_t o)
     {
-        std::string out;
+        auto &P = segs[s].pieces;
+        // the piece holding word o (pieces are in offset order; most accesses hit the last)
+        size_t lo = 0, hi = P.size();
+        if (o >= P.back().off) lo = P.size() - 1;
+        else
+            while (hi - lo > 1) {
+                const size_t m = (lo + hi) / 2;
+                if (P[m].off <= o) lo = m; else hi = m;
+            }
+        return P[lo].own[o - P[lo].off];
+    }
+
+    std::vector<uint32_t> segmentTable() const
+    {
         const uint32_t n = (uint32_t)segs.size();
         std::vector<uint32_t> table;
         table.push_back(n - 1);
-        for (auto &s : segs) table.push_back((uint32_t)s.w.size());
+        for (auto &s : segs) table.push_back((uint32_t)s.used);
         if (table.size() % 2) table.push_back(0);
-        out.append(reinterpret_cast<const char *>(table.data()), table.size() * 4);
-        for (auto &s : segs) out.append(reinterpret_cast<const char *>(s.w.data()), s.w.size() * 8);
+        return table;
+    }
+
+    // the message as (pointer, bytes) blocks in file order
+    std::vector<std::pair<const char *, size_t>> blocks(const std::vector<uint32_t> &table) const
+    {
+        std::vector<std::pair<const char *, size_t>> v;
+        v.push_back({reinterpret_cast<const char *>(table.data()), table.size() * 4});
+        for (auto &s : segs)
+            for (auto &p : s.pieces)
+                if (p.n)
+                    v.push_back({p.ext ? static_cast<const char *>(p.ext)
+                                       : reinterpret_cast<const char *>(p.own.data()),
+                                 p.n * 8});
+        return v;
+    }
+
+    std::string serialize() const
+    {
+        const std::vector<uint32_t> table = segmentTable();
+        std::string out;
+        for (auto &b : blocks(table)) out.append(b.first, b.second);
         return out;
+    }
+
+    // the same bytes as serialize() into a file: sized first, then written by up to 8
+    // threads with pwrite over disjoint byte ranges (80 MB of a C2 .msh: page allocation of
+    // the output file dominated a single-threaded write)
+    bool write(const std::string &path) const
+    {
+        const std::vector<uint32_t> table = segmentTable();
+        const auto B = blocks(table);
+        std::vector<uint64_t> at(B.size() + 1, 0);
+        for (size_t i = 0; i < B.size(); i++) at[i + 1] = at[i] + B[i].second;
+        const uint64_t total = at.back();
+        const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+        if (fd < 0) return false;
+        bool ok = ftruncate(fd, (off_t)total) == 0;
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        const unsigned nt = total < (8u << 20) ? 1u : std::min(8u, hw);
+        std::atomic<bool> good{ok};
+        auto part = [&](unsigned t) {
+            const uint64_t a = total * t / nt, e = total * (t + 1) / nt;
+            size_t i = std::upper_bound(at.begin(), at.end(), a) - at.begin() - 1;
+            for (uint64_t pos = a; pos < e && i < B.size(); i++) {
+                const uint64_t b0 = std::max(pos, at[i]), b1 = std::min(e, at[i + 1]);
+                for (uint64_t q = b0; q < b1;) {
+                    const ssize_t w = pwrite(fd, B[i].first + (q - at[i]), (size_t)(b1 - q), (off_t)q);
+                    if (w <= 0) { good = false; return; }
+                    q += (uint64_t)w;
+                }
+                pos = b1;
+            }
+        };
+        if (ok) {
+            std::vector<std::thread> th;
+            for (unsigned t = 1; t < nt; t++) th.emplace_back(part, t);
+            part(0);
+            for (auto &x : th) x.join();
+        }
+        ok = good.load();
+        if (close(fd) != 0) ok = false;
+        return ok;
     }
 
 private:
@@ -73,25 +158,41 @@ private:
         return kind | (((uint64_t)offset & 0x3FFFFFFFULL) << 2) | (upper << 32);
     }
 
-    bool tryAlloc(int s, uint64_t n, uint64_t &off)
+    bool tryAlloc(int s, uint64_t n, uint64_t &off, const void *ext)
     {
         Seg &g = segs[s];
-        if (g.w.size() + n > g.cap) return false;
-        off = g.w.size();
-        g.w.resize(g.w.size() + n, 0);
+        if (g.used + n > g.cap) return false;
+        off = g.used;
+        if (ext) {
+            g.pieces.push_back(Piece{off, n, {}, ext});
+        } else {
+            if (g.pieces.empty() || g.pieces.back().ext) g.pieces.push_back(Piece{off, 0, {}, nullptr});
+            Piece &p = g.pieces.back();
+            p.own.resize(p.own.size() + n, 0);
+            p.n += n;
+        }
+        g.used += n;
         return true;
     }
 
-    std::pair<int, uint64_t> arenaAlloc(uint64_t n)
+    // n words in the newest segment with room, else a new one; ext != nullptr: a far
+    // pointer's landing pad (1 owned word) followed by the n - 1 external words
+    std::pair<int, uint64_t> arenaAlloc(uint64_t n, const void *ext)
     {
+        auto place = [&](int sg, uint64_t &off) {
+            if (segs[sg].used + n > segs[sg].cap) return false;
+            if (!ext) return tryAlloc(sg, n, off, nullptr);
+            uint64_t o2 = 0;
+            return tryAlloc(sg, 1, off, nullptr) && tryAlloc(sg, n - 1, o2, ext);
+        };
         uint64_t off = 0;
-        if (withSpace >= 0 && tryAlloc(withSpace, n, off)) return {withSpace, off};
+        if (withSpace >= 0 && place(withSpace, off)) return {withSpace, off};
         uint64_t size = std::max(n, nextSize);
         if (segs.empty()) nextSize = size;   // after the first segment: total so far
         else nextSize += size;
-        segs.push_back(Seg{{}, size});
+        segs.push_back(Seg{{}, 0, size});
         withSpace = (int)segs.size() - 1;
-        tryAlloc(withSpace, n, off);
+        place(withSpace, off);
         return {withSpace, off};
     }
 };
@@ -123,10 +224,11 @@ void setBit(Builder &b, int s, uint64_t w, int bit, bool v)
 
 }  // namespace
 
-std::string mshSerialize(const MshHeader &h, const std::vector<MshReference> &refs, bool use64,
-                         bool writeCounts)
+namespace {
+
+void build(Builder &b, const MshHeader &h, const MshRefView *refs, uint64_t n, bool use64,
+           bool writeCounts)
 {
-    Builder b;
     b.allocRootPointer();
     // root struct: 3 data + 4 pointer words, referenced from segment 0 word 0
     auto root = b.alloc(0, 0, 7, kStruct, structUpper(3, 4));
@@ -136,32 +238,29 @@ std::string mshSerialize(const MshHeader &h, const std::vector<MshReference> &re
     // referenceListOld when the seed is the schema default (Sketch.cpp:549)
     const uint64_t listSlot = h.hashSeed == 42 ? rp + 0 : rp + 3;
     auto rl = b.alloc(rs, listSlot, 1, kStruct, structUpper(0, 1));
-    const uint64_t n = refs.size();
     auto lst = b.alloc(rl.first, rl.second, 1 + 9 * n, kList, listUpper(kComposite, 9 * n));
     b.word(lst.first, lst.second) = kStruct | ((n & 0x3FFFFFFFULL) << 2) | (structUpper(2, 7) << 32);
     for (uint64_t i = 0; i < n; i++) {
         const int es = lst.first;
         const uint64_t ew = lst.second + 1 + 9 * i;   // element data words
         const uint64_t ep = ew + 2;                   // element pointers
-        const MshReference &r = refs[i];
-        setText(b, es, ep + 2, r.name);
-        setText(b, es, ep + 3, r.comment);
+        const MshRefView &r = refs[i];
+        setText(b, es, ep + 2, *r.name);
+        setText(b, es, ep + 3, *r.comment);
         b.word(es, ew + 1) = r.length;                // length64
-        if (!r.hashes.empty()) {
-            const uint64_t m = r.hashes.size();
+        if (r.nHashes) {
+            const uint64_t m = r.nHashes;
             if (use64) {
-                auto o = b.alloc(es, ep + 5, m, kList, listUpper(kEight, m));
-                for (uint64_t j = 0; j < m; j++) b.word(o.first, o.second + j) = r.hashes[j];
+                b.alloc(es, ep + 5, m, kList, listUpper(kEight, m), r.hashes);
             } else {
                 auto o = b.alloc(es, ep + 4, (m + 1) / 2, kList, listUpper(kFour, m));
                 uint32_t *p = reinterpret_cast<uint32_t *>(&b.word(o.first, o.second));
                 for (uint64_t j = 0; j < m; j++) p[j] = (uint32_t)r.hashes[j];
             }
-            if (writeCounts && !r.counts.empty()) {
-                const uint64_t c = r.counts.size();
+            if (writeCounts && r.nCounts) {
+                const uint64_t c = r.nCounts;
                 auto o = b.alloc(es, ep + 6, (c + 1) / 2, kList, listUpper(kFour, c));
-                uint32_t *p = reinterpret_cast<uint32_t *>(&b.word(o.first, o.second));
-                for (uint64_t j = 0; j < c; j++) p[j] = r.counts[j];
+                memcpy(&b.word(o.first, o.second), r.counts, c * 4);
                 setBit(b, es, ew, 32, true);
             }
         }
@@ -182,7 +281,34 @@ std::string mshSerialize(const MshHeader &h, const std::vector<MshReference> &re
     setBit(b, rs, rw, 97, h.noncanonical);
     setBit(b, rs, rw, 98, h.preserveCase);
     setText(b, rs, rp + 2, h.alphabet);
+}
+
+std::vector<MshRefView> viewsOf(const std::vector<MshReference> &refs)
+{
+    std::vector<MshRefView> v(refs.size());
+    for (size_t i = 0; i < refs.size(); i++)
+        v[i] = MshRefView{&refs[i].name, &refs[i].comment, refs[i].length, refs[i].hashes.data(),
+                          refs[i].hashes.size(), refs[i].counts.data(), refs[i].counts.size()};
+    return v;
+}
+
+}  // namespace
+
+std::string mshSerialize(const MshHeader &h, const std::vector<MshReference> &refs, bool use64,
+                         bool writeCounts)
+{
+    const std::vector<MshRefView> v = viewsOf(refs);
+    Builder b;
+    build(b, h, v.data(), v.size(), use64, writeCounts);
     return b.serialize();
+}
+
+bool mshWrite(const std::string &path, const MshHeader &h, const MshRefView *refs, uint64_t n,
+              bool use64, bool writeCounts)
+{
+    Builder b;
+    build(b, h, refs, n, use64, writeCounts);
+    return b.write(path);
 }
 
 // ---------------------------------------------------------------------------
@@ -363,9 +489,14 @@ bool mshParse(const std::string &data, MshHeader &h, std::vector<MshReference> *
             const uint64_t take = std::min<uint64_t>(n, maxHashes);
             m.hashes.resize(take);
             const char *base = data.data() + r.addr(s, w);
-            for (uint64_t j = 0; j < take; j++) {
-                if (use64) memcpy(&m.hashes[j], base + 8 * j, 8);
-                else { uint32_t v; memcpy(&v, base + 4 * j, 4); m.hashes[j] = v; }
+            if (use64) {
+                memcpy(m.hashes.data(), base, take * 8);
+            } else {
+                for (uint64_t j = 0; j < take; j++) {
+                    uint32_t v;
+                    memcpy(&v, base + 4 * j, 4);
+                    m.hashes[j] = v;
+                }
             }
         }
         if (listPtr(e, 6, s, w, esz, n)) {

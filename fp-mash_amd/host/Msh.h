@@ -9,6 +9,7 @@
 #pragma once
 
 #include <cstdint>
+#include <cstdio>
 #include <string>
 #include <vector>
 
@@ -38,10 +39,26 @@ struct MshHeader {
     uint64_t referenceCount = 0;
 };
 
+// A reference to serialize without copying its lists (the writer reads them in place).
+struct MshRefView {
+    const std::string *name;
+    const std::string *comment;
+    uint64_t length;
+    const uint64_t *hashes;
+    uint64_t nHashes;
+    const uint32_t *counts;
+    uint64_t nCounts;
+};
+
 // Serialize.  use64 selects hashes64 vs hashes32; counts are written when
 // writeCounts and a reference has counts (Sketch.cpp:584-596).
 std::string mshSerialize(const MshHeader &h, const std::vector<MshReference> &refs, bool use64,
                          bool writeCounts);
+
+// The same bytes written to the file at `path` (hash lists read in place, parallel writes).
+// Returns false if the file cannot be created or written.
+bool mshWrite(const std::string &path, const MshHeader &h, const MshRefView *refs, uint64_t n,
+              bool use64, bool writeCounts);
 
 // Parse a whole file image.  Hash lists are truncated to maxHashes (loadCapnp's
 // truncation to the sketch size, Sketch.cpp:1117-1120, 1135-1138).  use64 picks

@@ -7,33 +7,67 @@
 //    long as the sequence; one more byte is consumed; shorter quality -> -2.
 #include "SeqReader.h"
 
+#include <zlib.h>
+
 #include <cctype>
 #include <cstdio>
+#include <cstring>
 #include <unistd.h>
 
 namespace fpmhost {
 
-SeqReader::SeqReader(const std::string &path)
+bool loadSequenceFile(const std::string &path, std::string &image)
 {
-    fp_ = path == "-" ? gzdopen(dup(fileno(stdin)), "r") : gzopen(path.c_str(), "r");
-    if (fp_) gzbuffer(fp_, 1 << 17);
-}
-
-SeqReader::~SeqReader()
-{
-    if (fp_) gzclose(fp_);
-}
-
-int SeqReader::getc_()
-{
-    if (begin_ >= end_) {
-        if (eof_) return -1;
-        end_ = gzread(fp_, buf_, sizeof(buf_));
-        begin_ = 0;
-        if (end_ < (int)sizeof(buf_)) eof_ = true;
-        if (end_ <= 0) { end_ = 0; return -1; }
+    image.clear();
+    const bool in = path == "-";
+    FILE *f = in ? nullptr : fopen(path.c_str(), "rb");
+    if (!in && !f) return false;
+    unsigned char magic[2] = {0, 0};
+    size_t nm = 0;
+    if (f) {
+        nm = fread(magic, 1, 2, f);
+        if (!(nm == 2 && magic[0] == 0x1f && magic[1] == 0x8b)) {
+            // plain file: one sized read
+            if (fseeko(f, 0, SEEK_END) == 0) {
+                const off_t sz = ftello(f);
+                if (sz > 0 && fseeko(f, 0, SEEK_SET) == 0) {
+                    image.resize((size_t)sz);
+                    image.resize(fread(&image[0], 1, (size_t)sz, f));
+                }
+            }
+            char buf[1 << 16];
+            for (size_t r; (r = fread(buf, 1, sizeof(buf), f)) > 0;) image.append(buf, r);
+            fclose(f);
+            return true;
+        }
+        fclose(f);
     }
-    return buf_[begin_++];
+    // gzip (or stdin, gzip or not): zlib's transparent reader, as the reference's gzread
+    gzFile gz = in ? gzdopen(dup(fileno(stdin)), "r") : gzopen(path.c_str(), "r");
+    if (!gz) return false;
+    gzbuffer(gz, 1 << 18);
+    size_t cap = 1 << 22;
+    image.resize(cap);
+    size_t len = 0;
+    for (;;) {
+        if (len == cap) image.resize(cap *= 2);
+        const int r = gzread(gz, &image[len], (unsigned)std::min<size_t>(cap - len, 1u << 30));
+        if (r < 0) { gzclose(gz); return false; }
+        if (r == 0) break;
+        len += (size_t)r;
+    }
+    gzclose(gz);
+    image.resize(len);
+    return true;
+}
+
+void splitHeader(const char *line, size_t n, std::string &name, std::string &comment)
+{
+    size_t i = 0;
+    while (i < n && !isspace((unsigned char)line[i])) i++;
+    name.assign(line, i);
+    if (i < n && line[i] != '\n') comment.assign(line + i + 1, n - i - 1);
+    else comment.clear();
 }
 
 int SeqReader::read()

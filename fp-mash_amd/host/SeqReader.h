@@ -1,32 +1,37 @@
-// SeqReader.h — FASTA/FASTQ record reader with kseq's rules (kseq.h:170-208),
-// gzip-transparent via zlib (gzopen reads plain files too).  Replaces the
-// KSEQ_INIT(gzFile, gzread) reader of Sketch.cpp:38.
+// SeqReader.h — FASTA/FASTQ input for sketching.
+//
+// loadSequenceFile: the whole (inflated) file image — gzip-transparent like the reference's
+// gzopen / gzread stream (KSEQ_INIT(gzFile, gzread), Sketch.cpp:38); "-" reads stdin.
+// The image normally goes to the device parser (fpm_seq_parse, csrc/seqparse.hip); SeqReader
+// walks an image on the host with kseq's record rules (kseq.h:170-208) for the inputs the
+// device parser hands back (FASTQ quality lines).
 #pragma once
-
-#include <zlib.h>
 
 #include <cstdint>
 #include <string>
 
 namespace fpmhost {
 
+// false if the file cannot be opened or is a corrupt gzip stream
+bool loadSequenceFile(const std::string &path, std::string &image);
+
 class SeqReader {
 public:
-    // path "-" reads stdin
-    explicit SeqReader(const std::string &path);
-    ~SeqReader();
-    bool ok() const { return fp_ != nullptr; }
+    SeqReader(const char *data, size_t n) : p_((const unsigned char *)data), n_(n) {}
     // >= 0: sequence length; -1: end of file; -2: truncated quality (kseq_read)
     int read();
     std::string name, comment, seq;
 
 private:
-    int getc_();
-    gzFile fp_ = nullptr;
-    unsigned char buf_[1 << 16];
-    int begin_ = 0, end_ = 0;
-    bool eof_ = false;
+    int getc_() { return i_ < n_ ? p_[i_++] : -1; }
+    const unsigned char *p_;
+    size_t n_, i_ = 0;
     int last_ = 0;
 };
+
+// kseq's header split of one header line (the bytes after '>' / '@' up to its '\n'): name =
+// up to the first isspace byte; if that byte is not '\n' (here: the line continues) the
+// comment is the rest of the line (kseq.h:179-180).
+void splitHeader(const char *line, size_t n, std::string &name, std::string &comment);
 
 }  // namespace fpmhost

@@ -4,6 +4,7 @@
 #include "Device.h"
 #include "Msh.h"
 #include "SeqReader.h"
+#include "Timing.h"
 
 #include <cmath>
 #include <cstdio>
@@ -11,6 +12,10 @@
 #include <fstream>
 #include <iostream>
 #include <sstream>
+#include <atomic>
+#include <thread>
+#include <algorithm>
+#include <sys/stat.h>
 
 namespace fpmhost {
 
@@ -73,21 +78,50 @@ void Sketch::createIndex() { kmerSpace = pow(parameters.alphabetSize, parameters
 
 static bool readFile(const std::string &path, std::string &out)
 {
-    std::ifstream in(path, std::ios::binary);
-    if (!in) return false;
-    std::ostringstream ss;
-    ss << in.rdbuf();
-    out = ss.str();
+    // one sized read (an ostringstream of rdbuf copied the file twice)
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    out.clear();
+    if (fseeko(f, 0, SEEK_END) == 0) {
+        const off_t n = ftello(f);
+        if (n > 0 && fseeko(f, 0, SEEK_SET) == 0) {
+            out.resize((size_t)n);
+            out.resize(fread(&out[0], 1, (size_t)n, f));
+        }
+    }
+    char buf[1 << 16];   // unsized streams (pipes) or a file that grew
+    for (size_t r; (r = fread(buf, 1, sizeof(buf), f)) > 0;) out.append(buf, r);
+    fclose(f);
     return true;
+}
+
+// The .msh inputs are opened several times (parameters of the first file, the per-file
+// compatibility test, the load: Sketch.cpp:257-336): keep the last image read, keyed by path,
+// size and modification time.
+static const std::string *readMshCached(const std::string &path)
+{
+    static std::string cPath, cData;
+    static struct stat cSt {};
+    struct stat st {};
+    if (stat(path.c_str(), &st) != 0) return nullptr;
+    if (path == cPath && st.st_size == cSt.st_size && st.st_mtim.tv_sec == cSt.st_mtim.tv_sec &&
+        st.st_mtim.tv_nsec == cSt.st_mtim.tv_nsec)
+        return &cData;
+    cPath.clear();
+    if (!readFile(path, cData)) return nullptr;
+    cPath = path;
+    cSt = st;
+    return &cData;
 }
 
 uint64_t Sketch::initParametersFromMsh(const std::string &file)
 {
-    std::string data;
-    if (!readFile(file, data)) {
+    const std::string *img = readMshCached(file);
+    if (!img) {
         std::cerr << "ERROR: could not open \"" << file << "\" for reading." << std::endl;
         exit(1);
     }
+    const std::string &data = *img;
     MshHeader h;
     std::string err;
     if (!mshParse(data, h, nullptr, true, 0, err)) {
@@ -113,8 +147,10 @@ uint64_t Sketch::initParametersFromMsh(const std::string &file)
 // loadCapnp (Sketch.cpp:1059-1219)
 static void loadMsh(const std::string &file, const Parameters &p, std::vector<Reference> &out)
 {
-    std::string data, err;
-    if (!readFile(file, data)) return;
+    std::string err;
+    const std::string *img = readMshCached(file);
+    if (!img) return;
+    const std::string &data = *img;
     MshHeader h;
     std::vector<MshReference> refs;
     if (!mshParse(data, h, &refs, p.use64, p.minHashesPerWindow, err)) {
@@ -134,19 +170,33 @@ static void loadMsh(const std::string &file, const Parameters &p, std::vector<Re
 
 namespace {
 
-// records and groups collected from all sequence files, sketched in one GPU batch
-struct SeqBatch {
-    std::string seq;
-    std::vector<uint64_t> rec_off{0};
-    std::vector<uint32_t> group;
-    uint32_t n_groups = 0;
-    void add(const std::string &s, uint32_t g)
-    {
-        seq += s;
-        rec_off.push_back(seq.size());
-        group.push_back(g);
-    }
+// one input record as the sketch groups see it
+struct SeqRec {
+    std::string name, comment;
+    uint64_t length = 0;
+    uint32_t id = 0;       // record index in the parse (device) or the host batch
 };
+
+// host kseq walk of one image (the fallback for FASTQ quality lines): records appended to
+// `out`, their bytes to `seq` (record r = seq[off[r] .. off[r + 1])).  Returns kseq_read's
+// last status (-1 at a clean end of file, -2 on a truncated quality string).
+int hostRecords(const std::string &image, std::vector<SeqRec> &out, std::string &seq,
+                std::vector<uint64_t> &off)
+{
+    SeqReader rd(image.data(), image.size());
+    int l;
+    while ((l = rd.read()) >= 0) {
+        SeqRec r;
+        r.name = rd.name;
+        r.comment = rd.comment;
+        r.length = (uint64_t)l;
+        r.id = (uint32_t)(off.size() - 1);
+        seq += rd.seq;
+        off.push_back(seq.size());
+        out.push_back(std::move(r));
+    }
+    return l;
+}
 
 }  // namespace
 
@@ -154,10 +204,10 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
                           bool enforceParameters, bool contain)
 {
     parameters = p;
-    // output slots in input order: a slot is either loaded references or a GPU group
-    struct Slot { bool fromGroup; uint32_t group; Reference ref; };
-    std::vector<Slot> slots;
-    SeqBatch batch;
+    // output slots in input order: loaded references, or one sequence file (index into seqFiles)
+    struct Item { bool isSeq; size_t file; std::vector<Reference> refs; };
+    std::vector<Item> items;
+    std::vector<std::string> seqFiles;
 
     for (size_t i = 0; i < files.size(); i++) {
         const std::string &file = files[i];
@@ -210,12 +260,11 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
                           << parameters.minHashesPerWindow << "). Its sketches will be reduced."
                           << std::endl << std::endl;
             }
-            std::vector<Reference> loaded;
-            loadMsh(file, parameters, loaded);
-            for (auto &r : loaded) slots.push_back(Slot{false, 0, std::move(r)});
+            Item it{false, 0, {}};
+            loadMsh(file, parameters, it.refs);
+            items.push_back(std::move(it));
             continue;
         }
-
         if (verbosity > 0)
             std::cerr << (file == "-" ? std::string("Sketching from stdin...")
                                       : "Sketching " + file + "...") << std::endl;
@@ -227,86 +276,202 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
             }
             fclose(f);
         }
-        SeqReader rd(file);
-        if (!rd.ok()) {
-            std::cerr << "ERROR: could not open " << file << std::endl;
-            exit(1);
-        }
-        int l;
-        if (parameters.concatenated) {
-            // sketchFile (Sketch.cpp:1299-1488): one sketch for the whole file
-            Reference ref;
-            const uint32_t g = batch.n_groups++;
-            int count = 0;
-            bool skipped = false;
-            if (file != "-") ref.name = file;
-            while ((l = rd.read()) >= 0) {
-                if (l < parameters.kmerSize) { skipped = true; continue; }
-                if (count == 0) {
-                    if (file == "-") { ref.name = rd.name; ref.comment = rd.comment; }
-                    else ref.comment = rd.name + " " + rd.comment;
-                }
-                count++;
-                ref.length += (uint64_t)l;
-                batch.add(rd.seq, g);
-            }
-            if (count > 1) ref.comment = "[" + std::to_string(count) + " seqs] " + ref.comment + " [...]";
-            if (l != -1) {
-                std::cerr << "\nERROR: reading input files." << std::endl;
-                exit(1);
-            }
-            if (ref.length == 0) {
-                if (skipped)
-                    std::cerr << "\nWARNING: All fasta records in input files were shorter than the "
-                                 "k-mer size (" << parameters.kmerSize << ")." << std::endl;
-                else
-                    std::cerr << "\nERROR: Did not find fasta records in \"input files\"." << std::endl;
-                exit(1);
-            }
-            slots.push_back(Slot{true, g, std::move(ref)});
-        } else {
-            // sketchFileBySequence (Sketch.cpp:478-522): one sketch per record >= k
-            while ((l = rd.read()) >= 0) {
-                if (l < parameters.kmerSize) continue;
-                Reference ref;
-                ref.name = rd.name;
-                ref.comment = rd.comment;
-                ref.length = (uint64_t)l;
-                const uint32_t g = batch.n_groups++;
-                batch.add(rd.seq, g);
-                slots.push_back(Slot{true, g, std::move(ref)});
-            }
-            if (l != -1) {
-                std::cerr << "\nERROR: reading " << file << "." << std::endl;
-                exit(1);
-            }
-        }
+        items.push_back(Item{true, seqFiles.size(), {}});
+        seqFiles.push_back(file);
     }
 
-    if (batch.n_groups) {
-        fpm_sketch_params fp{};
-        fp.kmer_size = (uint32_t)parameters.kmerSize;
-        fp.sketch_size = (uint32_t)parameters.minHashesPerWindow;
-        fp.seed = parameters.seed;
-        fp.use64 = parameters.use64;
-        fp.noncanonical = parameters.noncanonical;
-        fp.preserve_case = parameters.preserveCase;
-        for (int c = 0; c < 256; c++) fp.alphabet[c] = parameters.alphabet[c] ? 1 : 0;
-        const uint64_t s = fp.sketch_size;
-        std::vector<uint64_t> out((size_t)batch.n_groups * s);
-        std::vector<uint32_t> cnt(batch.n_groups);
-        check(fpm_sketch_batch(device(), &fp, batch.seq.data(), batch.rec_off.data(),
-                               (uint32_t)batch.group.size(), batch.group.data(), batch.n_groups,
-                               out.data(), cnt.data()),
-              "sketch");
-        for (auto &sl : slots)
-            if (sl.fromGroup)
-                sl.ref.hashes.assign(out.begin() + (size_t)sl.group * s,
-                                     out.begin() + (size_t)sl.group * s + cnt[sl.group]);
+    if (!seqFiles.empty()) {
+        // file images: gzip streams inflate on their own threads (one stream inflates
+        // serially, several files in parallel)
+        std::vector<std::string> images(seqFiles.size());
+        {
+            std::vector<char> okv(seqFiles.size(), 1);
+            std::atomic<size_t> next{0};
+            auto work = [&]() {
+                for (size_t f; (f = next++) < seqFiles.size();)
+                    okv[f] = loadSequenceFile(seqFiles[f], images[f]) ? 1 : 0;
+            };
+            const size_t nt = std::min<size_t>(seqFiles.size(),
+                                               std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+            std::vector<std::thread> pool;
+            for (size_t t = 1; t < nt; t++) pool.emplace_back(work);
+            work();
+            for (auto &t : pool) t.join();
+            for (size_t f = 0; f < seqFiles.size(); f++)
+                if (!okv[f]) {
+                    std::cerr << "ERROR: could not open " << seqFiles[f] << std::endl;
+                    exit(1);
+                }
+        }
+        phaseMark("read input");
+        fpm_ctx *ctx = device();
+        phaseMark("device context");
+        // records of each file (kseq rules) parsed on the device
+        std::vector<std::vector<SeqRec>> recs(seqFiles.size());
+        fpm_seqtext *parsed = nullptr;
+        uint64_t nRec = 0;
+        int quality = 0;
+        {
+            std::vector<const char *> ptr(seqFiles.size());
+            std::vector<uint64_t> len(seqFiles.size());
+            for (size_t f = 0; f < seqFiles.size(); f++) {
+                ptr[f] = images[f].data();
+                len[f] = images[f].size();
+            }
+            check(fpm_seq_parse(ctx, ptr.data(), len.data(), (uint32_t)seqFiles.size(), &parsed,
+                                &nRec, &quality),
+                  "sequence parse");
+        }
+        phaseMark("device parse (upload + scan + emit)");
+        std::string hostSeq;               // host fallback: the records' bytes
+        std::vector<uint64_t> hostOff{0};
+        if (!quality) {
+            std::vector<uint32_t> seg(nRec);
+            std::vector<uint64_t> ho(nRec), hl(nRec), sl(nRec);
+            check(fpm_seq_records(parsed, seg.data(), ho.data(), hl.data(), sl.data()),
+                  "sequence parse");
+            for (uint64_t r = 0; r < nRec; r++) {
+                const std::string &img = images[seg[r]];
+                // a '>' / '@' as the last byte of a file starts no record (kseq_read returns
+                // -1 when the name read hits the end of the stream)
+                if (ho[r] + 1 >= img.size()) continue;
+                SeqRec x;
+                splitHeader(img.data() + ho[r] + 1, hl[r] - 1, x.name, x.comment);
+                x.length = sl[r];
+                x.id = (uint32_t)r;
+                recs[seg[r]].push_back(std::move(x));
+            }
+        } else {
+            // FASTQ quality lines: kseq's record walk on the host
+            fpm_seq_free(parsed);
+            parsed = nullptr;
+            for (size_t f = 0; f < seqFiles.size(); f++) {
+                if (hostRecords(images[f], recs[f], hostSeq, hostOff) != -1) {
+                    std::cerr << "\nERROR: reading " << (parameters.concatenated ? std::string("input files")
+                                                                                   : seqFiles[f])
+                              << "." << std::endl;
+                    exit(1);
+                }
+            }
+        }
+        phaseMark("record headers");
+
+        // sketch groups: one per file (sketchFile, Sketch.cpp:1299-1488) or one per record
+        // >= k with -i (sketchFileBySequence, :478-522); records < k are skipped (:488-492)
+        const uint64_t nIds = parsed ? nRec : hostOff.size() - 1;
+        std::vector<uint32_t> groupOf(nIds, FPM_NO_GROUP);
+        uint32_t nGroups = 0;
+        std::vector<std::vector<Reference>> fileRefs(seqFiles.size());
+        std::vector<std::vector<uint32_t>> fileGroups(seqFiles.size());
+        for (size_t f = 0; f < seqFiles.size(); f++) {
+            const std::string &file = seqFiles[f];
+            if (parameters.concatenated) {
+                Reference ref;
+                const uint32_t g = nGroups++;
+                int count = 0;
+                bool skipped = false;
+                if (file != "-") ref.name = file;
+                for (const SeqRec &x : recs[f]) {
+                    if (x.length < (uint64_t)parameters.kmerSize) { skipped = true; continue; }
+                    if (count == 0) {
+                        if (file == "-") { ref.name = x.name; ref.comment = x.comment; }
+                        else ref.comment = x.name + " " + x.comment;
+                    }
+                    count++;
+                    ref.length += x.length;
+                    groupOf[x.id] = g;
+                }
+                if (count > 1) ref.comment = "[" + std::to_string(count) + " seqs] " + ref.comment + " [...]";
+                if (ref.length == 0) {
+                    if (skipped)
+                        std::cerr << "\nWARNING: All fasta records in input files were shorter than the "
+                                     "k-mer size (" << parameters.kmerSize << ")." << std::endl;
+                    else
+                        std::cerr << "\nERROR: Did not find fasta records in \"input files\"." << std::endl;
+                    exit(1);
+                }
+                fileRefs[f].push_back(std::move(ref));
+                fileGroups[f].push_back(g);
+            } else {
+                for (SeqRec &x : recs[f]) {
+                    if (x.length < (uint64_t)parameters.kmerSize) continue;
+                    Reference ref;
+                    ref.name = std::move(x.name);
+                    ref.comment = std::move(x.comment);
+                    ref.length = x.length;
+                    const uint32_t g = nGroups++;
+                    groupOf[x.id] = g;
+                    fileRefs[f].push_back(std::move(ref));
+                    fileGroups[f].push_back(g);
+                }
+            }
+        }
+        images.clear();
+        images.shrink_to_fit();
+
+        if (nGroups) {
+            fpm_sketch_params fp{};
+            fp.kmer_size = (uint32_t)parameters.kmerSize;
+            fp.sketch_size = (uint32_t)parameters.minHashesPerWindow;
+            fp.seed = parameters.seed;
+            fp.use64 = parameters.use64;
+            fp.noncanonical = parameters.noncanonical;
+            fp.preserve_case = parameters.preserveCase;
+            for (int c = 0; c < 256; c++) fp.alphabet[c] = parameters.alphabet[c] ? 1 : 0;
+            const uint64_t s = fp.sketch_size;
+            std::vector<uint64_t> out((size_t)nGroups * s);
+            std::vector<uint32_t> cnt(nGroups);
+            fpm_sketch_job *job = nullptr;
+            if (parsed) {
+                check(fpm_sketch_stage_seq(ctx, &fp, parsed, groupOf.data(), nGroups, &job), "sketch");
+            } else {
+                // host-parsed records: only those of a group go to the device
+                std::vector<uint64_t> off{0};
+                std::vector<uint32_t> grp;
+                std::string packed;
+                for (uint64_t r = 0; r < nIds; r++) {
+                    if (groupOf[r] == FPM_NO_GROUP) continue;
+                    packed.append(hostSeq, hostOff[r], hostOff[r + 1] - hostOff[r]);
+                    off.push_back(packed.size());
+                    grp.push_back(groupOf[r]);
+                }
+                check(fpm_sketch_stage(ctx, &fp, packed.data(), off.data(), (uint32_t)grp.size(),
+                                       grp.data(), nGroups, &job),
+                      "sketch");
+            }
+            int rc = fpm_sketch_run(job, nullptr);
+            if (rc == FPM_OK) rc = fpm_sketch_fetch(job, out.data(), cnt.data());
+            fpm_sketch_job_free(job);
+            check(rc, "sketch");
+            phaseMark("device sketch (stage + run + fetch)");
+            // hash lists into the references (threads: the copies are page-fault bound)
+            std::vector<std::pair<size_t, size_t>> all;
+            for (size_t f = 0; f < seqFiles.size(); f++)
+                for (size_t i = 0; i < fileRefs[f].size(); i++) all.push_back({f, i});
+            std::atomic<size_t> nextRef{0};
+            auto copyRefs = [&]() {
+                for (size_t a; (a = nextRef.fetch_add(256)) < all.size();)
+                    for (size_t x = a; x < std::min(all.size(), a + 256); x++) {
+                        const size_t f = all[x].first, i = all[x].second;
+                        const uint32_t g = fileGroups[f][i];
+                        fileRefs[f][i].hashes.assign(out.begin() + (size_t)g * s,
+                                                     out.begin() + (size_t)g * s + cnt[g]);
+                    }
+            };
+            std::vector<std::thread> cp;
+            const size_t ncp = all.size() < 1024 ? 0 : std::min(7u, std::thread::hardware_concurrency());
+            for (size_t t = 0; t < ncp; t++) cp.emplace_back(copyRefs);
+            copyRefs();
+            for (auto &t : cp) t.join();
+        }
+        phaseMark("reference lists");
+        if (parsed) fpm_seq_free(parsed);
+        for (auto &it : items)
+            if (it.isSeq) it.refs = std::move(fileRefs[it.file]);
     }
     references.clear();
-    references.reserve(slots.size());
-    for (auto &sl : slots) references.push_back(std::move(sl.ref));
+    for (auto &it : items)
+        for (auto &r : it.refs) references.push_back(std::move(r));
     createIndex();
     return 0;
 }
@@ -387,22 +552,17 @@ int Sketch::writeToMsh(const std::string &file) const
     h.noncanonical = parameters.noncanonical;
     h.preserveCase = parameters.preserveCase;
     getAlphabetAsString(h.alphabet);
-    std::vector<MshReference> refs(references.size());
+    std::vector<MshRefView> refs(references.size());
     for (size_t i = 0; i < references.size(); i++) {
-        refs[i].name = references[i].name;
-        refs[i].comment = references[i].comment;
-        refs[i].length = references[i].length;
-        refs[i].hashes = references[i].hashes;
-        refs[i].counts = references[i].counts;
+        const Reference &r = references[i];
+        refs[i] = MshRefView{&r.name, &r.comment, r.length, r.hashes.data(), r.hashes.size(),
+                             r.counts.data(), r.counts.size()};
     }
-    const std::string bytes = mshSerialize(h, refs, parameters.use64, parameters.counts);
-    FILE *f = fopen(file.c_str(), "wb");
-    if (!f) {
+    if (!mshWrite(file, h, refs.data(), refs.size(), parameters.use64, parameters.counts)) {
         std::cerr << "ERROR: could not open " << file << " for writing.\n";
         exit(1);
     }
-    fwrite(bytes.data(), 1, bytes.size(), f);
-    fclose(f);
+    phaseMark("msh write");
     return 0;
 }
 

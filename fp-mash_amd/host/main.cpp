@@ -2,14 +2,18 @@
 // verbs.  `fpmash sketch|dist|info|paste|triangle [-fp] ...` is a drop-in for the same
 // `mash` verbs.
 #include "Command.h"
+#include "Timing.h"
 
 int main(int argc, const char **argv)
 {
+    fpmhost::phaseMark("start");
     fpmhost::CommandList commandList("fpmash");
     commandList.addCommand(new fpmhost::CommandSketch());
     commandList.addCommand(new fpmhost::CommandDistance());
     commandList.addCommand(new fpmhost::CommandInfo());
     commandList.addCommand(new fpmhost::CommandPaste());
     commandList.addCommand(new fpmhost::CommandTriangle());
-    return commandList.run(argc, argv);
+    const int rc = commandList.run(argc, argv);
+    fpmhost::phaseMark("command done");
+    return rc;
 }

@@ -2,6 +2,8 @@
 // the writer; prints "same" when the bytes are identical.  CPU only.
 #include "Msh.h"
 
+#include <cstdio>
+#include <unistd.h>
 #include <fstream>
 #include <iostream>
 #include <sstream>
@@ -39,7 +41,22 @@ int main(int argc, char **argv)
         return 0;
     }
     const std::string out = fpmhost::mshSerialize(h, refs, use64, counts);
-    if (argc > 2) std::ofstream(argv[2], std::ios::binary) << out;
-    std::cout << (out == data ? "same" : "differs") << " " << data.size() << " " << out.size() << "\n";
-    return out == data ? 0 : 1;
+    // the file writer (hash lists read in place, parallel pwrite) must give the same bytes
+    std::vector<fpmhost::MshRefView> views;
+    for (auto &r : refs)
+        views.push_back(fpmhost::MshRefView{&r.name, &r.comment, r.length, r.hashes.data(),
+                                            r.hashes.size(), r.counts.data(), r.counts.size()});
+    const std::string path = argc > 2 ? std::string(argv[2]) : "/tmp/msh_roundtrip." + std::to_string(getpid());
+    bool fileSame = fpmhost::mshWrite(path, h, views.data(), views.size(), use64, counts);
+    if (fileSame) {
+        std::ifstream back(path, std::ios::binary);
+        std::stringstream bs;
+        bs << back.rdbuf();
+        fileSame = bs.str() == out;
+    }
+    if (argc <= 2) std::remove(path.c_str());
+    const bool same = out == data && fileSame;
+    std::cout << (same ? "same" : "differs") << " " << data.size() << " " << out.size()
+              << (fileSame ? "" : " (file writer differs)") << "\n";
+    return same ? 0 : 1;
 }

@@ -87,7 +87,8 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 #define FPM_K_PROBE 6
 #define FPM_K_FPTEXT 7
 #define FPM_K_FILL 8
-#define FPM_K_COUNT 9
+#define FPM_K_SEQPARSE 9
+#define FPM_K_COUNT 10
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */
@@ -137,6 +138,30 @@ int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_co
 int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_tiles,
                         uint64_t *n_kmers);
 void fpm_sketch_job_free(fpm_sketch_job *job);
+
+/* ---- FASTA text on the device ------------------------------------------------------
+ * Replaces the main-thread kseq loop that feeds sketching (kseq_read, kseq.h:170-208, in
+ * sketchFileBySequence / sketchFile, Sketch.cpp:478-522, 1299-1488): the n_seg file images
+ * (one per input file, already inflated) go to the device, where records are found (a '>'
+ * or '@' that is the first such byte of its line starts one; the header runs to the next
+ * '\n'; the sequence is every isgraph byte up to the next record) and their sequence bytes
+ * are packed for the sketch kernels without returning to the host.
+ * quality_lines = 1 when a '+' occurs in sequence text (FASTQ: kseq then reads quality
+ * lines, which this parser does not restate): the caller parses such input on the host.
+ * fpm_seq_records: per record, its file, the header's byte offset ('>' / '@') in that file,
+ * the header line's length (to its '\n' or the end of the file) and the sequence length.
+ * fpm_sketch_stage_seq: a sketch job over the parsed records (group_of_rec[r] as in
+ * fpm_sketch_stage, FPM_NO_GROUP = not sketched, e.g. records shorter than k); the job
+ * takes over the packed records (stage once per parse). */
+typedef struct fpm_seqtext fpm_seqtext;
+#define FPM_NO_GROUP 0xFFFFFFFFu
+int fpm_seq_parse(fpm_ctx *ctx, const char *const *seg_text, const uint64_t *seg_len,
+                  uint32_t n_seg, fpm_seqtext **job, uint64_t *n_records, int *quality_lines);
+int fpm_seq_records(fpm_seqtext *job, uint32_t *seg_of_rec, uint64_t *hdr_off, uint64_t *hdr_len,
+                    uint64_t *seq_len);
+int fpm_sketch_stage_seq(fpm_ctx *ctx, const fpm_sketch_params *p, fpm_seqtext *seq,
+                         const uint32_t *group_of_rec, uint32_t n_groups, fpm_sketch_job **job);
+void fpm_seq_free(fpm_seqtext *job);
 
 /* ---- -fp k-finger lines ------------------------------------------------------
  * Replaces the per-line getHashFingerPrint of Sketch::initFromFingerprints

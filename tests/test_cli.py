@@ -353,8 +353,9 @@ def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("block_pairs", [None, "50000"])
-def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs):
+@pytest.mark.parametrize("block_pairs,to_file", [(None, False), ("50000", False), (None, True),
+                                                ("50000", True)])
+def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file):
     """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
     blocks of 50,000 pairs (FPMASH_DIST_BLOCK_PAIRS) written by the formatter threads in
     order: every line equals the oracle's, in the reference's query-major order."""
@@ -366,11 +367,24 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs):
     env = dict(os.environ)
     if block_pairs:
         env["FPMASH_DIST_BLOCK_PAIRS"] = block_pairs
-    p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
-                       capture_output=True, env=env)
+    if to_file:
+        # stdout a regular file: the pieces are pwrite()n at their offsets by the formatter
+        # threads; the file starts with bytes already written (the offsets start after them)
+        with open(tmp_path / "out.tsv", "wb") as f:
+            f.write(b"head\n")
+            f.flush()
+            p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
+                               stdout=f, stderr=subprocess.PIPE, env=env)
+        text = (tmp_path / "out.tsv").read_bytes()
+        assert text.startswith(b"head\n")
+        text = text[5:]
+    else:
+        p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
+                           capture_output=True, env=env)
+        text = p.stdout
     assert p.returncode == 0, p.stderr.decode()
     refs = mshfmt.read_msh(str(tmp_path / "all.msh"))["references"]
     exp = _oracle_dist_lines(oracle, refs, refs, 1000, 21, 4.0 ** 21)
-    got = p.stdout.decode().splitlines()
+    got = text.decode().splitlines()
     assert len(got) == len(exp) == len(refs) ** 2
     assert got == exp
