@@ -590,6 +590,19 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "candidates_all_ranks": cand, "parity": par}
 
 
+def cli_phases(stderr: bytes):
+    """[fpmash] phase: X ms lines (FPMASH_TIMING=1) -> {phase: ms} (repeated phases summed)."""
+    out = {}
+    for line in stderr.decode(errors="replace").splitlines():
+        if line.startswith("[fpmash] ") and line.endswith(" ms") and ": " in line:
+            name, val = line[len("[fpmash] "):-3].rsplit(": ", 1)
+            try:
+                out[name] = out.get(name, 0.0) + float(val)
+            except ValueError:
+                pass
+    return out
+
+
 def cli_leg(args, seqs, cpu=None, check=True):
     """The drop-in CLI end to end (CPU wall / GPU wall of the same command), on
     config C2's batch written as one lyn2vec-style FASTA:
@@ -610,16 +623,17 @@ def cli_leg(args, seqs, cpu=None, check=True):
         fa = os.path.join(tmp, "c2.fa")
         with open(fa, "wb") as f:
             f.write(datagen.fasta_bytes(seqs, ids))
-        env = dict(os.environ)
+        # FPMASH_TIMING=1: the host prints each phase's wall time to stderr (no output change)
+        env = dict(os.environ, FPMASH_TIMING="1")
         t0 = time.perf_counter()
-        subprocess.run([exe, "sketch", "-i", "-k", str(args.k), "-s", str(args.s), "-o", "c2",
-                        "c2.fa"], cwd=tmp, check=True, capture_output=True, env=env)
+        ps = subprocess.run([exe, "sketch", "-i", "-k", str(args.k), "-s", str(args.s), "-o", "c2",
+                             "c2.fa"], cwd=tmp, check=True, capture_output=True, env=env)
         t_sketch = time.perf_counter() - t0
         out_path = os.path.join(tmp, "out.tsv")
         t0 = time.perf_counter()
         with open(out_path, "wb") as f:
-            subprocess.run([exe, "dist", "-p", str(_threads()), "c2.msh", "c2.msh"], cwd=tmp,
-                           check=True, stdout=f, stderr=subprocess.PIPE, env=env)
+            pd = subprocess.run([exe, "dist", "-p", str(_threads()), "c2.msh", "c2.msh"], cwd=tmp,
+                                check=True, stdout=f, stderr=subprocess.PIPE, env=env)
         t_dist = time.perf_counter() - t0
         out_bytes = os.path.getsize(out_path)
         n = len(seqs)
@@ -627,7 +641,8 @@ def cli_leg(args, seqs, cpu=None, check=True):
                "command_dist": "fpmash dist c2.msh c2.msh > out",
                "fasta_bytes": os.path.getsize(fa), "cli_sketch_wall_s": t_sketch,
                "cli_dist_wall_s": t_dist, "dist_lines": n * n, "dist_text_bytes": out_bytes,
-               "dist_lines_per_s": n * n / t_dist, "output_dir": base or tempfile.gettempdir()}
+               "dist_lines_per_s": n * n / t_dist, "output_dir": base or tempfile.gettempdir(),
+               "phases_ms_sketch": cli_phases(ps.stderr), "phases_ms_dist": cli_phases(pd.stderr)}
         if cpu:
             # the CPU port's wall for the same work, from the cpu_baseline leg's rates (its
             # sketch and dist with p-values; text formatting not included)

@@ -77,6 +77,9 @@ struct fpm_ctx {
     // FPM_FILL_SERIAL=1 runs the sparse dist's fill before the candidate compare instead of
     // beside it (measurement only: per-kernel times without the overlap)
     bool fill_serial = false;
+    // FPM_FILL_EARLY=1 (A/B): the fill starts on the side stream with the index build instead
+    // of after the probe
+    bool fill_early = false;
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
     const unsigned long long *last_cand_dev = nullptr;   // the last sparse call's counter
@@ -258,6 +261,7 @@ int fpm_ctx_create(int device, fpm_ctx **out)
     ctx->device = device;
     if (const char *v = getenv("FPM_DENSE_IMG")) ctx->dense_img = atoi(v) != 0;
     if (const char *v = getenv("FPM_FILL_SERIAL")) ctx->fill_serial = atoi(v) != 0;
+    if (const char *v = getenv("FPM_FILL_EARLY")) ctx->fill_early = atoi(v) != 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -522,6 +526,9 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         kp.complement[c] = (c >= 'A' && c <= 'Z') ? (uint8_t)kComplAZ[c - 'A'] : (uint8_t)'N';
     }
     kp.alphabet[0] = 0;   // the separator byte is never a k-mer byte
+    kp.compl_acgt = 1;
+    for (int c = 0; c < 256; c++)
+        if (kp.alphabet[c] && c != 'A' && c != 'C' && c != 'G' && c != 'T') kp.compl_acgt = 0;
 
     // host path: pack records >= k (each followed by 0x00) in group order
     std::vector<uint8_t> packed;
@@ -1345,6 +1352,27 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
     bool fill_pending = false;
+    // the fill of every cell's no-shared-hash values on the side stream (see below)
+    auto launch_fill = [&]() -> int {
+        PairFill fill;
+        fill.dist = fin->dist;
+        fill.pval = fin->pval;
+        fill.pass = fin->pass;
+        fill.max_dist = fin->max_dist;
+        fill.max_pvalue = fin->max_pvalue;
+        HIP_TRY(ensure_aux(ctx));
+        HIP_TRY(hipEventRecord(ctx->ev_in, st));
+        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
+        TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
+        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, Counts{}, fill,
+                                 ctx->aux));
+        tl.done();
+        HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
+        fill_pending = true;
+        return FPM_OK;
+    };
+    if (try_sparse && fin && ctx->fill_early)
+        if (int rc = launch_fill()) return rc;
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
@@ -1495,21 +1523,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             }
             uint32_t *cnum = nullptr, *cden = nullptr;
             if (fin) {
-                PairFill fill;
-                fill.dist = fin->dist;
-                fill.pval = fin->pval;
-                fill.pass = fin->pass;
-                fill.max_dist = fin->max_dist;
-                fill.max_pvalue = fin->max_pvalue;
-                HIP_TRY(ensure_aux(ctx));
-                HIP_TRY(hipEventRecord(ctx->ev_in, st));
-                HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
-                TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-                HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, Counts{},
-                                         fill, ctx->aux));
-                tl.done();
-                HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
-                fill_pending = true;
+                if (!fill_pending)
+                    if (int rc = launch_fill()) return rc;
                 if (rows_merge) {
                     void *cres;
                     HIP_TRY(scratch(ctx, 3, cap * 8, &cres));

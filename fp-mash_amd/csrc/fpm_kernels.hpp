@@ -26,6 +26,7 @@ struct SketchKParams {
     uint32_t use64;
     uint32_t canonical;
     uint32_t preserve_case;
+    uint32_t compl_acgt;    // every alphabet byte is one of A C G T: complement by bit ops
     uint8_t alphabet[256];  // 1 = valid (after uppercasing)
     uint8_t complement[256];
 };

@@ -74,24 +74,62 @@ __device__ void bitonic_sort(uint64_t *keys)
     }
 }
 
+// SWAR helpers on 4 ASCII bytes
+__device__ __forceinline__ uint32_t upper4(uint32_t x)
+{
+    // bytes in 'a'..'z' (0x61..0x7a) lose 0x20 (Sketch.cpp:676-682); per byte: x >= 0x61 and
+    // x <= 0x7a, computed without carries between bytes
+    const uint32_t hi = x & 0x80808080u, lo = x & 0x7f7f7f7fu;
+    const uint32_t ge = (lo + 0x1f1f1f1fu) & ~hi;              // bit 7: lo >= 0x61
+    const uint32_t le = ~(lo + 0x05050505u) & ~hi;             // bit 7: lo <= 0x7a
+    const uint32_t m = (ge & le & 0x80808080u) >> 2;           // 0x20 in the lowercase bytes
+    return x - m;
+}
+
+// complement of A/C/G/T (Sketch.cpp:1223-1250: A<->T, C<->G).  Other bytes never take part in
+// a canonical comparison (their windows are invalid), so their image value is irrelevant.
+__device__ __forceinline__ uint32_t compl4(uint32_t x)
+{
+    // C 0x43 / G 0x47 have bit 1 set: xor 0x04; A 0x41 / T 0x54 clear: xor 0x15
+    const uint32_t b1 = (x >> 1) & 0x01010101u;
+    return x ^ (b1 * 0x04u + (b1 ^ 0x01010101u) * 0x15u);
+}
+
 // K != 0: the k-mer size as a compile-time constant (the window loads, tail masks and
 // Murmur's block / tail branches fold); K = 0 reads p.k.
+//
+// Byte images in LDS (one 16-B global load per 16 bytes, b128 LDS stores):
+//   F[y]     = tile byte y - a0 (uppercased), a0 = byte_off & 15 (F starts on the 16-B
+//              aligned global address below the tile)
+//   R[z]     = reverse complement: tile byte x (x < n) lands at R[rc0 + n - 1 - x], with rc0
+//              chosen so that F's 16-B chunks land on R's 16-B chunks reversed
+//   bad bit y = F[y] is outside the tile or not in the alphabet
+// Thread t hashes the E consecutive windows i = tE .. tE + E - 1: their bytes are one run of
+// F (and of R, backwards), loaded as ~E/4 + 9 dwords once and cut per window by
+// v_alignbyte with compile-time shifts.
 template <int P, int K>
-__global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? 7 : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
 {
-    // byte images padded so that 9-dword window reads past the end stay in bounds
-    constexpr int kImgWords = (P + 32 + 64) / 4;
-    __shared__ uint32_t fwd_img[kImgWords];
-    __shared__ uint32_t rc_img[kImgWords];
-    __shared__ uint32_t badmask[(P + 32 + 64) / 32];
-    __shared__ uint64_t keys[P];
-    __shared__ uint8_t alpha[256];
-    __shared__ uint8_t compl_tab[256];
+    constexpr int E = P / kBlock;                          // windows per thread (P >= 256)
+    constexpr int kRcPad = ((E + 15) / 16) * 16;           // R positions of the last thread's
+                                                           // invalid windows stay >= 0
+    constexpr int kFBytes = ((P + 31 + 15 + 96 + 31) / 32) * 32;   // even number of 16-B chunks
+    constexpr int kRBytes = ((kRcPad + P + 31 + 15 + 96 + 15) / 16) * 16;
+    constexpr int kMaskWords = kFBytes / 32 + 2;
+    // the staging images live inside keys[] (dead before the first key is scattered): 20 KB
+    // of LDS per P = 2048 tile instead of 25.7 KB, 7 tiles per CU instead of 6
+    __shared__ __attribute__((aligned(16))) uint64_t keys[P];
+    static_assert(kFBytes + kRBytes + 4 * kMaskWords + 512 <= 8 * P, "staging fits in keys");
+    uint32_t *const fwd_img = reinterpret_cast<uint32_t *>(keys);
+    uint32_t *const rc_img = fwd_img + kFBytes / 4;
+    uint32_t *const badmask = rc_img + kRBytes / 4;
+    uint8_t *const alpha = reinterpret_cast<uint8_t *>(badmask + kMaskWords);
+    uint8_t *const compl_tab = alpha + 256;
     __shared__ uint32_t scan_tmp[kWaves + 1];
-    __shared__ uint32_t bins[P / 2 + 1];
-    __shared__ uint32_t big_bucket;
+    __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
+    __shared__ uint32_t big_bucket, s_cut;
 
     FPM_PHASE_DECL;
     FPM_PHASE(0);
@@ -99,75 +137,135 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     const uint32_t n = td.n_bytes;
     const uint32_t k = K ? (uint32_t)K : p.k;
     const int tid = threadIdx.x;
+    const uint32_t a0 = (uint32_t)(td.byte_off & 15);
+    const uint8_t *g0 = seq + (td.byte_off - a0);
+    const uint32_t nimg = a0 + n;                          // F bytes holding tile data
+    const uint32_t rc0 = kRcPad + ((16u - (nimg & 15u)) & 15u);
 
     alpha[tid] = p.alphabet[tid];
     compl_tab[tid] = p.complement[tid];
     __syncthreads();
 
-    // ---- stage bytes: uppercase (Sketch.cpp:676-682), validity bitmask, rc image
-    uint8_t *fb = reinterpret_cast<uint8_t *>(fwd_img);
-    uint8_t *rb = reinterpret_cast<uint8_t *>(rc_img);
-    constexpr int kImgBytes = kImgWords * 4;
-    constexpr int kIt = (kImgBytes + kBlock - 1) / kBlock;
-    // every global byte load of the tile issued before the first use (one memory latency
-    // per tile instead of one per pass)
-    uint8_t cb[kIt];
+    // ---- stage the tile: uppercase, validity bits, reverse complement
+    constexpr int kChunks = kFBytes / 16;
+    for (int ch = tid; ch < kChunks; ch += kBlock) {
+        const uint32_t y0 = (uint32_t)ch * 16;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (y0 < nimg) v = *reinterpret_cast<const uint4 *>(g0 + y0);
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint32_t bad = 0;                                  // bit m: F[y0 + m] invalid
 #pragma unroll
-    for (int it = 0; it < kIt; it++) {
-        const int b = tid + it * kBlock;
-        cb[it] = (uint32_t)b < n ? seq[td.byte_off + b] : (uint8_t)0;
-    }
+        for (int q = 0; q < 4; q++) {
+            if (!p.preserve_case) w[q] = upper4(w[q]);
 #pragma unroll
-    for (int it = 0; it < kIt; it++) {
-        const int b = tid + it * kBlock;
-        if (b >= kImgBytes) break;
-        uint8_t c = 0;
-        if ((uint32_t)b < n) {
-            c = cb[it];
-            if (!p.preserve_case && c > 96 && c < 123) c -= 32;
+            for (int b = 0; b < 4; b++) {
+                const uint32_t y = y0 + 4 * q + b;
+                const bool ok = y >= a0 && y < nimg && alpha[(w[q] >> (8 * b)) & 0xffu];
+                bad |= (ok ? 0u : 1u) << (4 * q + b);
+            }
         }
-        fb[b] = c;
-        bool bad = (uint32_t)b >= n || !alpha[c];
-        unsigned long long m = __ballot(bad);
-        if ((tid & 63) == 0 && b / 32 + 1 < (P + 32 + 64) / 32) {
-            badmask[b / 32] = (uint32_t)m;
-            badmask[b / 32 + 1] = (uint32_t)(m >> 32);
+        *reinterpret_cast<uint4 *>(&fwd_img[y0 / 4]) = make_uint4(w[0], w[1], w[2], w[3]);
+        if (p.canonical && y0 < nimg) {
+            // F[y0 .. y0 + 16) = tile bytes x = y0 - a0 + m -> R[rc0 + n - 1 - x], i.e. the 16-B
+            // chunk at zc = rc0 + nimg - 16 - y0 (16-aligned), byte order reversed
+            const uint32_t zc = rc0 + nimg - 16 - y0;
+            uint32_t c[4];
+            if (p.compl_acgt) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) c[q] = compl4(w[q]);
+            } else {
+                // alphabets beyond ACGT: the reference's complement table, byte by byte
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    uint32_t x = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        x |= (uint32_t)compl_tab[(w[q] >> (8 * b)) & 0xffu] << (8 * b);
+                    c[q] = x;
+                }
+            }
+            *reinterpret_cast<uint4 *>(&rc_img[zc / 4]) =
+                make_uint4(__builtin_bswap32(c[3]), __builtin_bswap32(c[2]),
+                           __builtin_bswap32(c[1]), __builtin_bswap32(c[0]));
         }
-        if ((uint32_t)b < n) rb[n - 1 - b] = compl_tab[c];   // reverseComplement Sketch.cpp:1252-1258
-        else rb[b] = 0;
+        // two chunks per badmask word: the odd chunk's bits go to the high half
+        const uint32_t hi = __shfl_down(bad, 1, 64);
+        if ((ch & 1) == 0) badmask[ch / 2] = bad | (hi << 16);
     }
+    if (tid < 2) badmask[kMaskWords - 2 + tid] = 0xffffffffu;
     __syncthreads();
     FPM_PHASE(1);
 
-    // ---- hash every window (one k-mer start per thread per pass)
+    // ---- hash this thread's E consecutive windows
     const uint32_t nk = n >= k ? n - k + 1 : 0;
     const int nw = (k + 3) >> 2;                           // dwords per k-mer
     const uint32_t tail_mask = (k & 3) ? ((1u << (8 * (k & 3))) - 1u) : 0xffffffffu;
     const uint32_t kmask = (k == 32) ? 0xffffffffu : ((1u << k) - 1u);
-    constexpr int E = P / kBlock;                          // keys per thread (P >= 256)
-    uint64_t kr[E];                                        // this thread's keys: i = tid + e*kBlock
+    constexpr int KW = K ? (K + 3) / 4 : 8;                // dwords per window (max)
+    constexpr int W = (E + 3) / 4 + KW + 1;                // dwords covering the E windows
+    uint64_t kr[E];                                        // key of window tE + e
     uint32_t vbits = 0;                                    // bit e: kr[e] is a valid k-mer hash
+    const uint32_t i0 = (uint32_t)tid * E;
 #pragma unroll
-    for (int e = 0; e < E; e++) {
-        const int i = tid + e * kBlock;
-        uint64_t key = ~0ULL;
-        if ((uint32_t)i < nk) {
-            // window [i, i+k) must hold alphabet bytes only (Sketch.cpp:696-713)
-            uint32_t w = i >> 5, sh = i & 31;
-            uint64_t bits = ((uint64_t)badmask[w] | ((uint64_t)badmask[w + 1] << 32)) >> sh;
-            if (((uint32_t)bits & kmask) == 0) {
+    for (int e = 0; e < E; e++) kr[e] = ~0ULL;
+    if (i0 < nk) {
+        // validity of the E windows from one 64-bit read of the bit image
+        const uint32_t yb = a0 + i0;
+        uint32_t okbits = 0;
+        {
+            // bits [yb, yb + 64) of the bit image (E + k - 1 <= 63 of them are used)
+            const uint32_t wq = yb >> 5, sh = yb & 31;
+            uint64_t bits = ((uint64_t)badmask[wq] | ((uint64_t)badmask[wq + 1] << 32)) >> sh;
+            if (sh) bits |= (uint64_t)badmask[wq + 2] << (64 - sh);
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                // window e's k bits start at bit e of `bits` (E + k <= 64 for E <= 32)
+                const bool ok = i0 + e < nk && (((uint32_t)(bits >> e) & kmask) == 0);
+                okbits |= (ok ? 1u : 0u) << e;
+            }
+        }
+        if (okbits) {
+            // forward run: S[m] = the dwords of F from byte yb
+            uint32_t S[W];
+            {
+                const uint32_t q0 = yb >> 2, sh0 = yb & 3;
+                uint32_t D[W + 1];
+#pragma unroll
+                for (int m = 0; m <= W; m++) D[m] = fwd_img[q0 + m];
+#pragma unroll
+                for (int m = 0; m < W; m++) S[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], sh0);
+            }
+            // reverse-complement run: window e's rc bytes start at R[rc0 + n - (i0 + e) - k]
+            // = R[zb + (E - 1 - e)], zb the start for e = E - 1
+            uint32_t SR[W];
+            if (p.canonical) {
+                const uint32_t zb = rc0 + n - i0 - k - (E - 1);
+                const uint32_t qr = zb >> 2, shr = zb & 3;
+                uint32_t D[W + 1];
+#pragma unroll
+                for (int m = 0; m <= W; m++) D[m] = rc_img[qr + m];
+#pragma unroll
+                for (int m = 0; m < W; m++) SR[m] = __builtin_amdgcn_alignbyte(D[m + 1], D[m], shr);
+            }
+#pragma unroll
+            for (int e = 0; e < E; e++) {
+                if (!(okbits >> e & 1)) continue;
                 uint32_t d[8];
 #pragma unroll
                 for (int m = 0; m < 8; m++)
-                    d[m] = (m < nw) ? lds_u32_at(fwd_img, i + 4 * m) : 0u;
+                    d[m] = (m < nw) ? __builtin_amdgcn_alignbyte(S[(e >> 2) + m + 1], S[(e >> 2) + m],
+                                                                 e & 3)
+                                    : 0u;
                 d[nw - 1] &= tail_mask;
                 if (p.canonical) {
                     // canonical = memcmp(fwd, rev) <= 0 ? fwd : rev (Sketch.cpp:719-723)
-                    const uint32_t ro = n - i - k;
+                    const int f = E - 1 - e;   // unrolled: a constant
                     uint32_t r[8];
 #pragma unroll
                     for (int m = 0; m < 8; m++)
-                        r[m] = (m < nw) ? lds_u32_at(rc_img, ro + 4 * m) : 0u;
+                        r[m] = (m < nw) ? __builtin_amdgcn_alignbyte(SR[(f >> 2) + m + 1],
+                                                                     SR[(f >> 2) + m], f & 3)
+                                        : 0u;
                     r[nw - 1] &= tail_mask;
                     int cmp = 0;
 #pragma unroll
@@ -183,12 +281,11 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
                 uint64_t wd[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) wd[j] = (uint64_t)d[2 * j] | ((uint64_t)d[2 * j + 1] << 32);
-                uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
-                key = p.use64 ? h : (h & 0xffffffffULL);   // getHash hash.cpp:30-37
-                vbits |= 1u << e;
+                const uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
+                kr[e] = p.use64 ? h : (h & 0xffffffffULL);   // getHash hash.cpp:30-37
             }
+            vbits = okbits;
         }
-        kr[e] = key;
     }
 
     // ---- long groups: keep only hashes <= the group's bound (the s-th smallest hash of a
@@ -206,13 +303,16 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     // [0, hmax], then insertion sort inside each bucket (~2 keys per bucket).  A bucket
     // holding more than kMaxBucket keys (low-complexity input: many copies of few k-mers)
     // sends the whole tile to the bitonic sort instead.
-    constexpr int NB = P / 2;
+    // ~2 keys per bucket; 4 for the long-record tiles (P >= 4096: C5's chunks keep only the
+    // keys below their group's sampled bound, so their buckets are sparse anyway, and the
+    // smaller table lets 4 tiles share a CU)
+    constexpr int NB = P >= 4096 ? P / 4 : P / 2;
     constexpr int LB = __builtin_ctz(NB);
     constexpr uint32_t kMaxBucket = 32;
     const uint32_t hbits = hmax ? 64 - __clzll(hmax) : 1;
     const uint32_t bshift = hbits > (uint32_t)LB ? hbits - LB : 0;
-    for (int b = tid; b <= NB; b += kBlock) bins[b] = 0;
-    if (tid == 0) big_bucket = 0;
+    for (int b = tid; b < NB; b += kBlock) bins[b] = 0;
+    if (tid == 0) { big_bucket = 0; s_cut = NB; }
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < E; e++)
@@ -231,84 +331,112 @@ __global__ __launch_bounds__(kBlock) void sketch_tiles_kernel(
     }
     uint32_t nvalid;
     uint32_t acc = block_exscan(run, scan_tmp, &nvalid);   // also a barrier over bins[]
+    // the bucket holding sorted position s - 1: every key in a later bucket is larger than
+    // the s smallest keys (duplicates included), so those buckets are left out of the sort
+    // unless duplicates leave fewer than s distinct values below them (then a second pass
+    // places them too)
 #pragma unroll
     for (int u = 0; u < per; u++) {
         const int b = tid * per + u;
-        if (b < NB) { const uint32_t c = bins[b]; bins[b] = acc; acc += c; }
+        if (b < NB) {
+            const uint32_t c = bins[b];
+            bins[b] = acc;
+            if (acc < p.s && acc + c >= p.s) s_cut = (uint32_t)b + 1;
+            acc += c;
+        }
     }
     if (bmax > kMaxBucket) big_bucket = 1;
     __syncthreads();
+    const uint32_t cut = big_bucket ? (uint32_t)NB : s_cut;
+    const uint32_t nkept = cut < (uint32_t)NB ? bins[cut] : nvalid;   // before the scatter
     FPM_PHASE(4);
-    // scatter: afterwards bins[b] = end of bucket b, start = bins[b - 1]; each key keeps
-    // its slot for the in-bucket rank below
-    uint32_t slot[E];
+    uint32_t lo_b = 0, hi_b = cut, nv = nkept;
+    for (int pass = 0; pass < 2; pass++) {
+        // scatter the keys of buckets [lo_b, hi_b): afterwards bins[b] = end of bucket b,
+        // start = bins[b - 1]; each key keeps its slot for the in-bucket rank below
+        uint32_t act = 0;
 #pragma unroll
-    for (int e = 0; e < E; e++)
-        if (vbits >> e & 1) {
-            slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
-            keys[slot[e]] = kr[e];
+        for (int e = 0; e < E; e++) {
+            const uint32_t bk = (uint32_t)(kr[e] >> bshift);
+            act |= ((vbits >> e & 1) && bk >= lo_b && bk < hi_b) ? (1u << e) : 0u;
         }
-    __syncthreads();
-    FPM_PHASE(5);
-    if (!big_bucket) {
-        // in-bucket rank of every key (ties by slot): the bucket's ~2 keys are read with
-        // independent LDS loads, then every key is written to its sorted position (an
-        // insertion sort per bucket was a chain of dependent LDS round trips: 26 % of the
-        // tile's time, tools/micro/sketch_phases.hip)
+        uint32_t slot[E];
 #pragma unroll
         for (int e = 0; e < E; e++)
-            if (vbits >> e & 1) {
-                const uint32_t b = (uint32_t)(kr[e] >> bshift);
-                const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
-                const uint32_t mb = s1 - s0;
-                uint32_t r = 0;
-                // 8 speculative reads cover a bucket of <= 8 keys (Poisson(2) buckets: a
-                // longer one is rare) with one LDS round trip
-#pragma unroll
-                for (uint32_t u = 0; u < 8; u++) {
-                    const uint32_t t = s0 + u;
-                    const uint64_t y = keys[t < (uint32_t)P ? t : (uint32_t)P - 1];
-                    r += (u < mb) & ((y < kr[e]) | ((y == kr[e]) & (t < slot[e])));
-                }
-                for (uint32_t t = s0 + 8; t < s1; t++) {
-                    const uint64_t y = keys[t];
-                    r += (y < kr[e]) | ((y == kr[e]) & (t < slot[e]));
-                }
-                slot[e] = s0 + r;
+            if (act >> e & 1) {
+                slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
+                keys[slot[e]] = kr[e];
             }
         __syncthreads();
+        FPM_PHASE(5);
+        if (!big_bucket) {
+            // in-bucket rank of every key (ties by slot): the bucket's ~2 keys are read with
+            // independent LDS loads, then every key is written to its sorted position (an
+            // insertion sort per bucket was a chain of dependent LDS round trips: 26 % of the
+            // tile's time, tools/micro/sketch_phases.hip)
 #pragma unroll
-        for (int e = 0; e < E; e++)
-            if (vbits >> e & 1) keys[slot[e]] = kr[e];
-        __syncthreads();
-    } else {
-        for (int i = tid; i < P; i += kBlock)
-            if ((uint32_t)i >= nvalid) keys[i] = ~0ULL;
-        __syncthreads();
-        bitonic_sort<P>(keys);
-    }
-    FPM_PHASE(6);
-
-    // ---- first s distinct (ties removed: the heap is a set, MinHashHeap.cpp:74)
-    const int base = tid * E;
-    uint32_t cnt = 0;
+            for (int e = 0; e < E; e++)
+                if (act >> e & 1) {
+                    const uint32_t b = (uint32_t)(kr[e] >> bshift);
+                    const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
+                    const uint32_t mb = s1 - s0;
+                    uint32_t r = 0;
+                    // 8 speculative reads cover a bucket of <= 8 keys (Poisson(2) buckets: a
+                    // longer one is rare) with one LDS round trip
 #pragma unroll
-    for (int e = 0; e < E; e++) {
-        int idx = base + e;
-        if (idx < P && (uint32_t)idx < nvalid && (idx == 0 || keys[idx] != keys[idx - 1])) cnt++;
-    }
-    uint32_t total;
-    uint32_t rank = block_exscan(cnt, scan_tmp, &total);
-    uint64_t *row = out + (uint64_t)td.out_row * p.s;
+                    for (uint32_t u = 0; u < 8; u++) {
+                        const uint32_t t = s0 + u;
+                        const uint64_t y = keys[t < (uint32_t)P ? t : (uint32_t)P - 1];
+                        r += (u < mb) & ((y < kr[e]) | ((y == kr[e]) & (t < slot[e])));
+                    }
+                    for (uint32_t t = s0 + 8; t < s1; t++) {
+                        const uint64_t y = keys[t];
+                        r += (y < kr[e]) | ((y == kr[e]) & (t < slot[e]));
+                    }
+                    slot[e] = s0 + r;
+                }
+            __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; e++) {
-        int idx = base + e;
-        if (idx < P && (uint32_t)idx < nvalid && (idx == 0 || keys[idx] != keys[idx - 1])) {
-            if (rank < p.s) row[rank] = keys[idx];
-            rank++;
+            for (int e = 0; e < E; e++)
+                if (act >> e & 1) keys[slot[e]] = kr[e];
+            __syncthreads();
+        } else {
+            for (int i = tid; i < P; i += kBlock)
+                if ((uint32_t)i >= nvalid) keys[i] = ~0ULL;
+            __syncthreads();
+            bitonic_sort<P>(keys);
         }
+        FPM_PHASE(6);
+
+        // ---- first s distinct of keys[0, nv) (ties removed: the heap is a set,
+        // MinHashHeap.cpp:74)
+        const int base = tid * E;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            int idx = base + e;
+            if (idx < P && (uint32_t)idx < nv && (idx == 0 || keys[idx] != keys[idx - 1])) cnt++;
+        }
+        uint32_t total;
+        uint32_t rank = block_exscan(cnt, scan_tmp, &total);
+        uint64_t *row = out + (uint64_t)td.out_row * p.s;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            int idx = base + e;
+            if (idx < P && (uint32_t)idx < nv && (idx == 0 || keys[idx] != keys[idx - 1])) {
+                if (rank < p.s) row[rank] = keys[idx];
+                rank++;
+            }
+        }
+        // block-uniform: done unless duplicates left fewer than s distinct in the kept buckets
+        if (total >= p.s || hi_b >= (uint32_t)NB) {
+            if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;
+            break;
+        }
+        lo_b = hi_b;
+        hi_b = NB;
+        nv = nvalid;
     }
-    if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;
     FPM_PHASE(7);
     FPM_PHASE_FLUSH;
 }

@@ -26,7 +26,7 @@ int main(int argc, char **argv)
         tiles[r] = TileDesc{(uint64_t)r * (L + 1), (uint32_t)L, (uint32_t)r, 0, 0};
     }
     SketchKParams p{};
-    p.k = k; p.s = s; p.seed = 42; p.use64 = 1; p.canonical = 1; p.preserve_case = 0;
+    p.k = k; p.s = s; p.seed = 42; p.use64 = 1; p.canonical = 1; p.preserve_case = 0; p.compl_acgt = 1;
     for (int c = 0; c < 256; c++) { p.alphabet[c] = 0; p.complement[c] = 'N'; }
     p.alphabet['A'] = p.alphabet['C'] = p.alphabet['G'] = p.alphabet['T'] = 1;
     p.complement['A'] = 'T'; p.complement['T'] = 'A'; p.complement['C'] = 'G'; p.complement['G'] = 'C';
