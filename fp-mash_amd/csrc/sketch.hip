@@ -297,6 +297,29 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
 #pragma unroll
         for (int e = 0; e < E; e++)
             if (kr[e] > hmax) vbits &= ~(1u << e);
+        // the bound keeps a few percent of the keys (C5: ~130 of 4,096): compact them to the
+        // first slots of the threads (key j -> thread j % 256, slot j / 256), so the sort
+        // phases below run one slot instead of E mostly-empty ones (a slot runs for the whole
+        // wave as soon as one lane holds a key)
+        if (E > 1) {
+            uint32_t total;
+            uint32_t at = block_exscan((uint32_t)__popc(vbits), scan_tmp, &total);
+            if (total <= (uint32_t)(kBlock * (E / 2))) {   // block-uniform
+                // keys[] aliases the staging images: every window read is done (the scan's
+                // barriers) before the first write
+#pragma unroll
+                for (int e = 0; e < E; e++)
+                    if (vbits >> e & 1) keys[at++] = kr[e];
+                __syncthreads();
+                vbits = 0;
+#pragma unroll
+                for (int e = 0; e < E; e++) {
+                    const uint32_t j = (uint32_t)tid + (uint32_t)e * kBlock;
+                    if (j < total) { kr[e] = keys[j]; vbits |= 1u << e; }
+                }
+                __syncthreads();
+            }
+        }
     }
 
     // ---- sort: counting sort by the top log2(P/2) bits of the (uniform) hash values in
