@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdlib>
 #include <memory>
 #include <cstdio>
@@ -441,6 +442,24 @@ struct fpm_sketch_job {
     uint64_t *d_thr = nullptr;
     uint32_t sclass_begin[kTileClasses + 1] = {0};
     std::vector<uint32_t> sround_begin;
+    // sampled groups: one-workgroup selection from their bounded tile lists
+    // (group_select_kernel); a pairwise merge plan of the same lists is kept as the fallback
+    // for groups whose keys below the cut do not fit in LDS
+    uint32_t n_sel = 0;
+    SelDesc *d_sel = nullptr;
+    uint32_t *d_sel_rows = nullptr, *d_sel_failed = nullptr, *h_sel_failed = nullptr;
+    MergeDesc *d_fmerge = nullptr;
+    std::vector<uint32_t> fround_begin;
+    std::vector<uint8_t> fround_small;
+    uint32_t n_ssel = 0;                      // sample selections (first n_ssel of d_sel)
+    // fallback merge plans (rows >= n_rows live in d_fb_rows, allocated on first use)
+    std::vector<std::array<uint32_t, 3>> fplan, sfplan;
+    uint32_t n_fb_rows = 0;
+    uint64_t *d_fb_rows = nullptr;
+    uint32_t *d_fb_count = nullptr;
+    MergeDesc *d_sfmerge = nullptr;
+    std::vector<uint32_t> sfround_begin;
+    std::vector<uint8_t> sfround_small;
 };
 
 static void job_release(fpm_sketch_job *j)
@@ -451,6 +470,11 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_merge);
     (void)hipFree(j->d_stiles); (void)hipFree(j->d_smerge); (void)hipFree(j->d_srow);
     (void)hipFree(j->d_thr);
+    (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
+    (void)hipFree(j->d_fmerge);
+    (void)hipFree(j->d_sfmerge);
+    (void)hipFree(j->d_fb_rows); (void)hipFree(j->d_fb_count);
+    if (j->h_sel_failed) (void)hipHostFree(j->h_sel_failed);
 }
 
 extern "C" {
@@ -666,17 +690,56 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             small.push_back(round_max <= merge_small_cap() ? 1 : 0);
         }
     };
-    std::vector<Plan> splan, mplan;
-    std::vector<uint32_t> srb, rb;
-    std::vector<uint8_t> ssmall, msmall;
+    std::vector<Plan> splan, mplan, fplan;
+    std::vector<uint32_t> srb, rb, frb;
+    std::vector<uint8_t> ssmall, msmall, fsmall;
     for (uint32_t g = 0; g < n_groups; g++)
         if (slot_of[g]) srow[slot_of[g] - 1] = slists[g].size() == 1 ? slists[g][0] : 0;
+    // sampled groups select their sketch in one workgroup each (the sample's too); their lists
+    // leave the merge plans for fallback plans (FPM_GROUP_SELECT=0: merges only, A/B)
+    std::vector<SelDesc> sel, ssel;
+    std::vector<uint32_t> sel_rows;
+    static const bool kSelEnv = [] {
+        const char *v = getenv("FPM_GROUP_SELECT");
+        return !v || atoi(v) != 0;
+    }();
+    const bool use_sel = kSelEnv && (uint64_t)s + s / 8 + 64 <= group_select_cap();
+    std::vector<Plan> sfplan;
+    std::vector<uint32_t> sfrb;
+    std::vector<uint8_t> sfsmall;
+    std::vector<std::vector<uint32_t>> sflists(n_groups), flists(n_groups);
+    if (use_sel)
+        for (uint32_t g = 0; g < n_groups; g++) {
+            if (!slot_of[g] || slists[g].size() < 2) continue;
+            const uint32_t r = n_rows++;                    // the sample's sketch row
+            srow[slot_of[g] - 1] = r;
+            ssel.push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)slists[g].size(), r,
+                                   0xFFFFFFFFu});
+            sel_rows.insert(sel_rows.end(), slists[g].begin(), slists[g].end());
+            sflists[g].swap(slists[g]);
+        }
     plan_rounds(slists, [&](uint32_t g) {
         const uint32_t r = n_rows++;
         srow[slot_of[g] - 1] = r;
         return r;
     }, splan, srb, ssmall);
+    if (use_sel)
+        for (uint32_t g = 0; g < n_groups; g++) {
+            if (!slot_of[g] || lists[g].size() < 2) continue;
+            sel.push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)lists[g].size(), g,
+                                  slot_of[g] - 1});
+            sel_rows.insert(sel_rows.end(), lists[g].begin(), lists[g].end());
+            flists[g].swap(lists[g]);
+        }
     plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb, msmall);
+    // the fallback plans' intermediate rows come last: they are allocated only if a selection
+    // fails (a C5 share holds ~1.2 M tile rows of s u64: the fallback rows would double that)
+    const uint32_t n_core = n_rows;
+    if (use_sel) {
+        plan_rounds(sflists, [&](uint32_t g) { return srow[slot_of[g] - 1]; }, sfplan, sfrb,
+                    sfsmall);
+        plan_rounds(flists, [](uint32_t g) { return g; }, fplan, frb, fsmall);
+    }
 
     // tiles ordered by capacity class
     auto order_by_class = [&](const std::vector<TileDesc> &in, std::vector<TileDesc> &out,
@@ -701,7 +764,10 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     job->ctx = ctx;
     job->kp = kp;
     job->n_groups = n_groups;
-    job->n_rows = n_rows;
+    job->n_rows = n_core;
+    job->n_fb_rows = n_rows - n_core;
+    for (auto &pl : fplan) job->fplan.push_back({pl.a, pl.b, pl.c});
+    for (auto &pl : sfplan) job->sfplan.push_back({pl.a, pl.b, pl.c});
     job->seq_bytes = R.host_seq ? packed.size() : R.d_seq_bytes;
     job->n_kmers = n_kmers;
     job->n_tiles = tiles.size();
@@ -712,6 +778,13 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     job->round_small = msmall;
     job->sround_small = ssmall;
     job->n_slots = (uint32_t)srow.size();
+    job->n_ssel = (uint32_t)ssel.size();
+    job->n_sel = (uint32_t)sel.size();
+    job->sfround_begin = sfrb;
+    job->sfround_small = sfsmall;
+    sel.insert(sel.begin(), ssel.begin(), ssel.end());   // d_sel: samples, then groups
+    job->fround_begin = frb;
+    job->fround_small = fsmall;
 
     hipError_t e = hipSuccess;
     auto alloc = [&](void **ptr, size_t bytes) {
@@ -720,16 +793,21 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     if (R.host_seq) alloc((void **)&job->d_seq, packed.size() + 64);
     else { job->d_seq = R.d_seq; R.d_seq = nullptr; }   // the parse's packed records
     alloc((void **)&job->d_tiles, by_class.size() * sizeof(TileDesc));
-    alloc((void **)&job->d_rows, (size_t)n_rows * s * sizeof(uint64_t));
-    alloc((void **)&job->d_count, (size_t)n_rows * sizeof(uint32_t));
+    alloc((void **)&job->d_rows, (size_t)n_core * s * sizeof(uint64_t));
+    alloc((void **)&job->d_count, (size_t)n_core * sizeof(uint32_t));
     // groups without any k-mer keep count 0: zeroed once here (every run rewrites the count
     // of each group that has tiles: the tile kernel or the last merge of its group)
-    if (e == hipSuccess) e = hipMemset(job->d_count, 0, (size_t)n_rows * sizeof(uint32_t));
+    if (e == hipSuccess) e = hipMemset(job->d_count, 0, (size_t)n_core * sizeof(uint32_t));
     alloc((void **)&job->d_merge, mplan.size() * sizeof(MergeDesc));
     alloc((void **)&job->d_stiles, sby_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_smerge, splan.size() * sizeof(MergeDesc));
     alloc((void **)&job->d_srow, srow.size() * sizeof(uint32_t));
     alloc((void **)&job->d_thr, srow.size() * sizeof(uint64_t));
+    alloc((void **)&job->d_sel, sel.size() * sizeof(SelDesc));
+    alloc((void **)&job->d_sel_rows, sel_rows.size() * sizeof(uint32_t));
+    alloc((void **)&job->d_sel_failed, (sel.size() + 2) * sizeof(uint32_t));
+    if (e == hipSuccess && !sel.empty())
+        e = hipHostMalloc((void **)&job->h_sel_failed, 2 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -761,6 +839,11 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         e = hipMemcpy(job->d_smerge, smd.data(), smd.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
     if (e == hipSuccess && !srow.empty())
         e = hipMemcpy(job->d_srow, srow.data(), srow.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !sel.empty())
+        e = hipMemcpy(job->d_sel, sel.data(), sel.size() * sizeof(SelDesc), hipMemcpyHostToDevice);
+    if (e == hipSuccess && !sel_rows.empty())
+        e = hipMemcpy(job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t),
+                      hipMemcpyHostToDevice);
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -768,6 +851,34 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     }
     *job_out = job;
     return FPM_OK;
+}
+
+// the fallback merge plans' descriptors (first failure of a selection): intermediate rows in
+// a buffer of their own
+static int fallback_descs(fpm_sketch_job *job)
+{
+    if (job->d_fmerge || job->d_sfmerge) return FPM_OK;
+    const uint64_t s = job->kp.s;
+    if (job->n_fb_rows) {
+        HIP_TRY(hipMalloc(&job->d_fb_rows, (size_t)job->n_fb_rows * s * sizeof(uint64_t)));
+        HIP_TRY(hipMalloc(&job->d_fb_count, (size_t)job->n_fb_rows * sizeof(uint32_t)));
+    }
+    auto row = [&](uint32_t r) { return r < job->n_rows ? job->d_rows + r * s
+                                                       : job->d_fb_rows + (r - job->n_rows) * s; };
+    auto cnt = [&](uint32_t r) { return r < job->n_rows ? job->d_count + r
+                                                       : job->d_fb_count + (r - job->n_rows); };
+    auto upload = [&](const std::vector<std::array<uint32_t, 3>> &plan, MergeDesc **dst) -> int {
+        std::vector<MergeDesc> md(plan.size());
+        for (size_t i = 0; i < plan.size(); i++)
+            md[i] = MergeDesc{row(plan[i][0]), cnt(plan[i][0]), row(plan[i][1]), cnt(plan[i][1]),
+                              row(plan[i][2]), cnt(plan[i][2])};
+        HIP_TRY(hipMalloc(dst, std::max<size_t>(1, md.size()) * sizeof(MergeDesc)));
+        if (!md.empty())
+            HIP_TRY(hipMemcpy(*dst, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice));
+        return FPM_OK;
+    };
+    if (int rc = upload(job->fplan, &job->d_fmerge)) return rc;
+    return upload(job->sfplan, &job->d_sfmerge);
 }
 
 extern "C" {
@@ -801,14 +912,54 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         }
         return FPM_OK;
     };
+    // failure flags: [0] main selections, [1] sample selections, [2..] per selection
+    uint32_t *fail_main = job->d_sel_failed, *fail_samp = job->d_sel_failed + 1;
+    if (job->n_ssel + job->n_sel)
+        HIP_TRY(hipMemsetAsync(job->d_sel_failed, 0, (job->n_ssel + job->n_sel + 2) * sizeof(uint32_t),
+                               st));
     if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
         if (int rc = tiles_pass(job->d_stiles, job->sclass_begin)) return rc;
+        if (job->n_ssel) {
+            TimedLaunch tl(ctx, FPM_K_MERGE, st);
+            HIP_TRY(launch_group_select(job->d_sel, job->n_ssel, job->d_sel_rows, job->d_rows,
+                                        job->d_count, job->kp.s, job->d_thr, fail_samp, st));
+            tl.done();
+            HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 1, fail_samp, sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, st));
+        }
         if (int rc = merge_pass(job->d_smerge, job->sround_begin, job->sround_small)) return rc;
+        if (job->n_ssel) {
+            HIP_TRY(hipStreamSynchronize(st));
+            if (job->h_sel_failed[1]) {
+                if (int rc = fallback_descs(job)) return rc;
+                if (int rc = merge_pass(job->d_sfmerge, job->sfround_begin, job->sfround_small))
+                    return rc;
+            }
+        }
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
                                         job->kp.s, job->d_thr, st));
     }
     if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
-    return merge_pass(job->d_merge, job->round_begin, job->round_small);
+    if (job->n_sel) {
+        TimedLaunch tl(ctx, FPM_K_MERGE, st);
+        HIP_TRY(launch_group_select(job->d_sel + job->n_ssel, job->n_sel, job->d_sel_rows,
+                                    job->d_rows, job->d_count, job->kp.s, job->d_thr, fail_main,
+                                    st));
+        tl.done();
+        HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, st));
+    }
+    if (int rc = merge_pass(job->d_merge, job->round_begin, job->round_small)) return rc;
+    if (job->n_sel) {
+        // a selection that did not fit (more repeated values below the cut than LDS holds):
+        // the pairwise merges of every sampled group's lists (rare; one host round trip)
+        HIP_TRY(hipStreamSynchronize(st));
+        if (*job->h_sel_failed) {
+            if (int rc = fallback_descs(job)) return rc;
+            return merge_pass(job->d_fmerge, job->fround_begin, job->fround_small);
+        }
+    }
+    return FPM_OK;
 }
 
 int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,

@@ -58,6 +58,15 @@ hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, con
                                    const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                    hipStream_t st);
 uint32_t merge_small_cap();   // list length merge_small_kernel stages in LDS
+// one long group's sketch selected from its bounded tile lists (rows row_ids[row_begin ..
+// row_begin + n_rows)) into out_row; slot: its bound thr[slot] (0xFFFFFFFF: none, the
+// sample pass of long groups)
+struct SelDesc { uint32_t row_begin, n_rows, out_row, slot; };
+uint32_t group_select_cap();   // keys one selection stages in LDS (sketch sizes up to ~0.85 x)
+// *failed |= 1 when a group's keys below the cut do not fit (the caller merges instead)
+hipError_t launch_group_select(const SelDesc *d_desc, uint32_t n, const uint32_t *d_row_ids,
+                               uint64_t *d_rows, uint32_t *d_count, uint32_t s,
+                               const uint64_t *d_thr, uint32_t *d_failed, hipStream_t st);
 // small: the round's lists are estimated short (merge_small_kernel; exact for any length)
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,
                         hipStream_t st);

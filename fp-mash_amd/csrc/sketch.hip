@@ -774,6 +774,192 @@ __global__ __launch_bounds__(kSBlock) void merge_small_kernel(const MergeDesc *_
     }
 }
 
+// ---- one sketch from the bounded tile lists of a long group (C5 genomes), in one workgroup.
+// After the sample bound, a genome's ~1,200 tile lists hold ~16 s keys in all (each list
+// ascending and distinct, lists may share values: repeats across chunks).  Instead of ~11
+// rounds of pairwise merges, the group's workgroup selects directly:
+//   1. a 4096-bucket histogram over [0, bound] of every kept key -> the bucket b1 holding
+//      sorted position T - 1 (T = s plus slack for values repeated across lists)
+//   2. the keys below R = (b1 + 1) buckets (m ~ T of them) are counting-sorted in LDS by a
+//      second 4096-bucket histogram over [0, R), ranked inside their buckets, deduplicated
+//   3. >= s distinct (or every key taken): the first s distinct are the sketch.  Fewer (more
+//      repeats than the slack): T grows by the shortfall and 1-2 run again.
+// A group whose keys below the cut exceed kSelCap fails (flag set); the host then merges
+// that group's lists pairwise instead (fpm_sketch_run).
+constexpr int kSelThreads = 1024;
+constexpr uint32_t kSelCap = 15360;                      // keys staged in LDS (120 KiB)
+constexpr int kSelPer = (kSelCap + kSelThreads - 1) / kSelThreads;   // 15 per thread
+uint32_t group_select_cap() { return kSelCap; }
+
+__device__ __forceinline__ uint32_t bits_of(uint64_t x) { return x ? 64 - __clzll(x) : 0; }
+
+__global__ __launch_bounds__(kSelThreads) void group_select_kernel(
+    const SelDesc *__restrict__ descs, const uint32_t *__restrict__ row_ids,
+    const uint64_t *__restrict__ rows, uint32_t *__restrict__ count, uint32_t s,
+    const uint64_t *__restrict__ thr, uint32_t *__restrict__ failed)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t K[];   // kSelCap keys
+    __shared__ uint32_t h[4096];
+    __shared__ uint32_t wsum[kSelThreads / 64 + 1];
+    __shared__ uint32_t sh_b1;
+    const SelDesc d = descs[blockIdx.x];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    constexpr uint32_t kWaves = kSelThreads / 64;
+    const uint64_t hmax = d.slot == 0xFFFFFFFFu ? ~0ULL : thr[d.slot];   // no bound: a sample
+    const uint32_t sh1 = bits_of(hmax) > 12 ? bits_of(hmax) - 12 : 0;
+    // block sum / exclusive scan of one u32 per thread
+    auto block_scan = [&](uint32_t v, uint32_t &tot) -> uint32_t {
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(x, o, 64);
+            if ((int)lane >= o) x += y;
+        }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = 0, t = 0;
+        for (uint32_t w = 0; w < kWaves; w++) { const uint32_t y = wsum[w]; pre += w < wave ? y : 0u; t += y; }
+        __syncthreads();
+        tot = t;
+        return pre + x - v;
+    };
+    // every kept key of the group with key < lim (lim = 0: all), handed to f(key)
+    auto for_keys = [&](uint64_t lim, auto f) {
+        for (uint32_t ri = wave; ri < d.n_rows; ri += kWaves) {
+            const uint32_t row = row_ids[d.row_begin + ri];
+            const uint32_t c = count[row];
+            const uint64_t *base = rows + (uint64_t)row * s;
+            for (uint32_t i = lane; i < c; i += 64) {
+                const uint64_t key = base[i];
+                if (lim && key >= lim) break;              // lists are ascending
+                f(key);
+            }
+        }
+    };
+    uint32_t T = s + s / 8 + 64;
+    for (;;) {
+        // ---- 1. level-1 histogram over [0, hmax]: the cut R
+        for (uint32_t b = tid; b < 4096; b += kSelThreads) h[b] = 0;
+        __syncthreads();
+        uint32_t mine = 0;
+        for_keys(0, [&](uint64_t key) { atomicAdd(&h[(uint32_t)(key >> sh1)], 1u); mine++; });
+        __syncthreads();
+        uint32_t total;
+        (void)block_scan(mine, total);
+        uint64_t R = 0;                                     // 0: every key
+        uint32_t m = total;
+        if (total > kSelCap || total > T) {
+            // bucket holding position T - 1: thread t scans buckets [4t, 4t + 4)
+            uint32_t c4[4], run = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) { c4[u] = h[tid * 4 + u]; run += c4[u]; }
+            uint32_t tot;
+            uint32_t acc = block_scan(run, tot);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (acc < T && acc + c4[u] >= T) { sh_b1 = tid * 4 + u; }
+                acc += c4[u];
+            }
+            __syncthreads();
+            const uint32_t b1 = sh_b1;
+            // (b1 + 1) << sh1 wraps to 0 only for the last bucket of a full 64-bit range: all keys
+            R = (uint64_t)(b1 + 1) << sh1;
+            // keys below R
+            uint32_t below = 0;
+            for (uint32_t b = tid; b <= b1; b += kSelThreads) below += h[b];
+            uint32_t mb;
+            (void)block_scan(below, mb);
+            m = R ? mb : total;
+        }
+        if (m > kSelCap) {
+            if (tid == 0) atomicOr(failed, 1u);
+            return;
+        }
+        // ---- 2. counting sort of the m keys below R in LDS (4096 buckets over [0, R))
+        const uint32_t sh2 = R ? (bits_of(R - 1) > 12 ? bits_of(R - 1) - 12 : 0) : sh1;
+        __syncthreads();
+        for (uint32_t b = tid; b < 4096; b += kSelThreads) h[b] = 0;
+        __syncthreads();
+        for_keys(R, [&](uint64_t key) { atomicAdd(&h[(uint32_t)(key >> sh2)], 1u); });
+        __syncthreads();
+        {
+            uint32_t c4[4], run = 0;
+#pragma unroll
+            for (int u = 0; u < 4; u++) { c4[u] = h[tid * 4 + u]; run += c4[u]; }
+            uint32_t tot;
+            uint32_t acc = block_scan(run, tot);
+#pragma unroll
+            for (int u = 0; u < 4; u++) { h[tid * 4 + u] = acc; acc += c4[u]; }
+        }
+        __syncthreads();
+        for_keys(R, [&](uint64_t key) { K[atomicAdd(&h[(uint32_t)(key >> sh2)], 1u)] = key; });
+        __syncthreads();
+        // h[b] = end of bucket b; rank inside the bucket (ties by position)
+        uint64_t kk[kSelPer];
+        uint32_t np[kSelPer];
+#pragma unroll
+        for (int u = 0; u < kSelPer; u++) {
+            const uint32_t p = tid + (uint32_t)u * kSelThreads;
+            if (p >= m) continue;
+            const uint64_t key = K[p];
+            const uint32_t b = (uint32_t)(key >> sh2);
+            const uint32_t s0 = b ? h[b - 1] : 0u, s1 = h[b];
+            uint32_t r = 0;
+            for (uint32_t t = s0; t < s1; t++) {
+                const uint64_t y = K[t];
+                r += (y < key) | ((y == key) & (t < p));
+            }
+            kk[u] = key;
+            np[u] = s0 + r;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kSelPer; u++)
+            if (tid + (uint32_t)u * kSelThreads < m) K[np[u]] = kk[u];
+        __syncthreads();
+        // ---- 3. distinct values, the first s of them out
+        uint32_t dc = 0;
+        const uint32_t p0 = tid * kSelPer;
+#pragma unroll
+        for (int u = 0; u < kSelPer; u++) {
+            const uint32_t p = p0 + u;
+            dc += (p < m && (p == 0 || K[p] != K[p - 1])) ? 1u : 0u;
+        }
+        uint32_t dist;
+        uint32_t rank = block_scan(dc, dist);
+        if (dist >= s || R == 0) {
+            uint64_t *out = const_cast<uint64_t *>(rows) + (uint64_t)d.out_row * s;
+#pragma unroll
+            for (int u = 0; u < kSelPer; u++) {
+                const uint32_t p = p0 + u;
+                if (p < m && (p == 0 || K[p] != K[p - 1])) {
+                    if (rank < s) out[rank] = K[p];
+                    rank++;
+                }
+            }
+            if (tid == 0) count[d.out_row] = dist < s ? dist : s;
+            return;
+        }
+        // more repeats than the slack: widen the cut by the shortfall
+        T += 2 * (s - dist) + 64;
+        __syncthreads();
+    }
+}
+
+hipError_t launch_group_select(const SelDesc *d_desc, uint32_t n, const uint32_t *d_row_ids,
+                               uint64_t *d_rows, uint32_t *d_count, uint32_t s,
+                               const uint64_t *d_thr, uint32_t *d_failed, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    const size_t lds = (size_t)kSelCap * 8;
+    hipError_t e = hipFuncSetAttribute((const void *)group_select_kernel,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(group_select_kernel, dim3(n), dim3(kSelThreads), lds, st, d_desc, d_row_ids,
+                       d_rows, d_count, s, d_thr, d_failed);
+    return hipGetLastError();
+}
+
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,
                         hipStream_t st)
 {

@@ -420,18 +420,24 @@ def test_fp_text_parse_matches_oracle(ctx, oracle, use64):
                                  (21, 16385), (21, 50000)])
 def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
     """Groups of >= 32 tiles take the sample pass (every 16th tile sketched first; its s-th
-    smallest hash bounds every tile): the sets still equal the reference heap's."""
+    smallest hash bounds every tile) and, for s <= ~13.5k, the one-workgroup selection from
+    the bounded tile lists (with its merge fallback when the keys below the cut overflow
+    LDS: the repeated unit): the sets still equal the reference heap's."""
     import fpmash
     rng = np.random.default_rng(k * 7 + s)
     unit = rand_seq(rng, 3000)
+    # random 2 kb stretches alternating with one 2 kb unit (80 copies): the unit's values
+    # repeat across the chunks, so the one-workgroup group selection meets duplicates below
+    # its first cut and widens it
+    mosaic = b"".join(rand_seq(rng, 2000) + unit[:2000] for _ in range(80))
     recs = [rand_seq(rng, 300_000),                        # one long record
             unit * 70,                                     # 210 kb of a repeated unit
             rand_seq(rng, 150_000, p_bad=0.001),           # long, with N windows
-            ] + [rand_seq(rng, 60_000) for _ in range(4)]  # a group of 4 x 60 kb records
-    groups = [0, 1, 2, 3, 3, 3, 3]
+            ] + [rand_seq(rng, 60_000) for _ in range(4)] + [mosaic]   # a group of 4 x 60 kb
+    groups = [0, 1, 2, 3, 3, 3, 3, 4]
     P = fpmash.make_params(k=k, s=s)
-    got = ctx.sketch(P, recs, groups=groups, n_groups=4)
-    exp = oracle.sketch_batch(oracle.params(k=k, s=s), recs, groups=groups, n_groups=4)
+    got = ctx.sketch(P, recs, groups=groups, n_groups=5)
+    exp = oracle.sketch_batch(oracle.params(k=k, s=s), recs, groups=groups, n_groups=5)
     check_sketches(got, exp)
 
 
