@@ -70,6 +70,9 @@ def parse():
     ap.add_argument("--no-cli", action="store_true",
                     help="skip the end-to-end CLI leg (fpmash sketch + dist, 1e8 text lines)")
     ap.add_argument("--c5-genomes", type=int, default=1000)
+    ap.add_argument("--no-split", action="store_true",
+                    help="skip the one-genome-over-all-GPUs sketch leg (RCCL min-merge)")
+    ap.add_argument("--split-bases", type=int, default=1_000_000_000)
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
     return ap.parse_args()
@@ -80,7 +83,8 @@ def parse_args_for_test(**kw):
     a = argparse.Namespace(gpus=1, steps=5, warmup=2, n_seqs=10000, seq_len=2000, families=100,
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
-                           no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True)
+                           no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True,
+                           no_split=True, split_bases=1_000_000_000)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -312,11 +316,12 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4, c5=None, cli=None):
+def parity_summary(c2, c3, c4, c5=None, cli=None, split=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
              "c4": c4.get("parity") if c4 else None,
              "c5": c5.get("parity") if c5 else None,
+             "split": split.get("parity") if split else None,
              "cli": cli.get("parity") if cli else None}
     done = [v["ok"] for v in parts.values() if v]
     parts["all_ok"] = all(done) if done else None
@@ -809,10 +814,104 @@ def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21,
     return out
 
 
+_GENOME_BLOCK = 1 << 22
+
+
+def split_genome_range(lo, hi):
+    """Bases [lo, hi) of the split leg's synthetic genome: uniform ACGT generated in 4 Mb
+    blocks from per-block seeds, so any rank builds its own range without the rest."""
+    global _ACGT_LUT
+    if _ACGT_LUT is None:
+        c5_genome(0, 4)                          # builds the byte -> 4 bases table
+    out = []
+    for b in range(lo // _GENOME_BLOCK, (hi + _GENOME_BLOCK - 1) // _GENOME_BLOCK):
+        rng = np.random.default_rng(900_000 + b)
+        r = rng.integers(0, 256, size=_GENOME_BLOCK // 4, dtype=np.uint8)
+        blk = _ACGT_LUT[r].reshape(-1)
+        a, e = max(lo, b * _GENOME_BLOCK) - b * _GENOME_BLOCK, min(hi, (b + 1) * _GENOME_BLOCK) - b * _GENOME_BLOCK
+        out.append(blk[a:e])
+    return np.concatenate(out).tobytes() if out else b""
+
+
+def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, steps=3,
+              warmup=1, parity=True):
+    """One sketch split over the GPUs (north_star: "RCCL ... for the final min-merge where a
+    single sketch exceeds one GPU"): one genome of `length` bases, its k-mer starts sharded
+    into contiguous ranges (fpmash.shard.kmer_shard: k - 1 bases of overlap), each rank
+    sketches its range, and the ranks' bottom-s rows are all-gathered (RCCL over xGMI on an
+    nccl group) and min-merged on the device (fpm_sketch_merge_dev).  Timed step: sketch +
+    gather + merge.  Check (outside the timed steps): the merged sketch equals the sketch of
+    the whole genome in one piece, computed on rank 0 (at N = 1: four parts merged in one
+    process against the whole); the merge itself is pinned to the oracle in
+    tests/test_gpu_parity.py."""
+    from fpmash.shard import kmer_shard, min_merge
+    lo, hi = kmer_shard(length, k, ws, rank)
+    P = fpmash.make_params(k=k, s=s)
+    job = ctx.sketch_job(P, [split_genome_range(lo, hi)], groups=[0], n_groups=1)
+    d_rows, d_cnt, _ng, _stride = job.device_output()
+    st = ctx.stream
+    dev = None
+    if ws > 1 and grp.nccl is not None:
+        import torch
+        dev = torch.device(f"cuda:{local}")
+
+    def step():
+        job.run(st)
+        if ws > 1:
+            return min_merge(ctx, d_rows, d_cnt, s, ws, group=grp.nccl, device=dev)
+        ctx.synchronize()
+        return None
+    for _ in range(warmup):
+        step()
+    ctx.synchronize()
+    grp.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        merged = step()
+    ctx.synchronize()
+    el = grp.max(time.perf_counter() - t0)
+    rows, cnt = job.fetch()
+    job.free()
+    if merged is None:
+        merged = (rows[0, : cnt[0]], int(cnt[0]))
+    out = {"config": f"one {length / 1e9:g} Gb genome, k={k}, s={s}, k-mer starts sharded over "
+                     f"{ws} GPU(s), bottom-s rows all-gathered "
+                     f"({'RCCL' if dev is not None else 'none' if ws == 1 else 'gloo'}) and "
+                     "min-merged on the device",
+           "n_gpus": ws, "bases": length, "steps": steps, "ms_per_step": el / steps * 1e3,
+           "bases_per_s": length / (el / steps), "scaling": "strong"}
+    if parity and rank == 0:
+        t_c = time.perf_counter()
+        whole = ctx.sketch(P, [split_genome_range(0, length)])[0]
+        ok = bool(len(whole) == merged[1] and np.array_equal(whole, merged[0]))
+        res = {"merged_equals_whole": ok}
+        if ws == 1:
+            # four parts merged in this process (the same merge call the ranks make)
+            parts = [split_genome_range(*kmer_shard(length, k, 4, r)) for r in range(4)]
+            sk = ctx.sketch(P, parts)
+            m = np.zeros((4, s), np.uint64)
+            for i, x in enumerate(sk):
+                m[i, : len(x)] = x
+            rows_d = fpmash.DeviceBuffer.from_array(ctx, m)
+            cnt_d = fpmash.DeviceBuffer.from_array(ctx, np.array([len(x) for x in sk], np.uint32))
+            o = fpmash.DeviceBuffer(ctx, s * 8)
+            oc = fpmash.DeviceBuffer(ctx, 4)
+            fpmash._check(fpmash.lib().fpm_sketch_merge_dev(ctx.h, rows_d.ptr, cnt_d.ptr, 4, s,
+                                                            o.ptr, oc.ptr, None))
+            ctx.synchronize()
+            n4 = int(oc.to_array(np.uint32, 1)[0])
+            ok4 = bool(n4 == len(whole) and np.array_equal(o.to_array(np.uint64, s)[:n4], whole))
+            res["four_parts_merged_equal_whole"] = ok4
+            ok = ok and ok4
+        res.update({"ok": ok, "check_s": time.perf_counter() - t_c})
+        out["parity"] = res
+    return out
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
-    grp = Group(ws, local, nccl=not args.no_c4)
+    grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split))
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
     n = len(seqs)
@@ -968,6 +1067,11 @@ def main():
     if not args.no_c5:
         c5 = c5_leg(ctx, grp, ws, rank, n_genomes=args.c5_genomes, parity=not args.no_parity)
 
+    split = None
+    if not args.no_split:
+        split = split_leg(ctx, grp, ws, rank, local, length=args.split_bases,
+                          parity=not args.no_parity)
+
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, seqs)
@@ -1010,12 +1114,13 @@ def main():
             "c3_fp": c3,
             "c4_dist": c4,
             "c5_sketch": c5,
+            "split_sketch": split,
             "cli": cli,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4, c5, cli),
+            "parity": parity_summary(c2par, c3, c4, c5, cli, split),
         }
         print(json.dumps(line))
     job.free()

@@ -70,7 +70,7 @@ struct fpm_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
     // grow-only device scratch, one buffer per named slot (no allocation in steady state)
     struct Slot { void *p = nullptr; size_t bytes = 0; };
-    Slot scratch[16];
+    Slot scratch[20];
     unsigned long long *host_counters = nullptr;   // pinned, for the events read-back
     int dist_mode = FPM_DIST_AUTO;
     // dense walk of u32 lists on 16-bit rank images (FPM_DENSE_IMG=0 turns it off, A/B)
@@ -452,6 +452,7 @@ struct fpm_sketch_job {
     std::vector<uint32_t> fround_begin;
     std::vector<uint8_t> fround_small;
     uint32_t n_ssel = 0;                      // sample selections (first n_ssel of d_sel)
+    std::vector<uint32_t> ssel_begin, sel_begin;   // d_sel offsets of each level
     // fallback merge plans (rows >= n_rows live in d_fb_rows, allocated on first use)
     std::vector<std::array<uint32_t, 3>> fplan, sfplan;
     uint32_t n_fb_rows = 0;
@@ -695,15 +696,59 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     std::vector<uint8_t> ssmall, msmall, fsmall;
     for (uint32_t g = 0; g < n_groups; g++)
         if (slot_of[g]) srow[slot_of[g] - 1] = slists[g].size() == 1 ? slists[g][0] : 0;
-    // sampled groups select their sketch in one workgroup each (the sample's too); their lists
-    // leave the merge plans for fallback plans (FPM_GROUP_SELECT=0: merges only, A/B)
-    std::vector<SelDesc> sel, ssel;
+    // sampled groups select their sketch (and their sample's) with group_select_kernel; their
+    // lists leave the merge plans for fallback plans (FPM_GROUP_SELECT=0: merges only, A/B).
+    // A group with more keys than one workgroup should read (~2^19: a 1 Gb genome's sample
+    // holds 62 M) is split into chunks of rows selected in parallel, then the chunks' sketches
+    // are selected again (a tree of levels, one launch per level).
     std::vector<uint32_t> sel_rows;
+    std::vector<std::vector<SelDesc>> ssel_lv, sel_lv;
     static const bool kSelEnv = [] {
         const char *v = getenv("FPM_GROUP_SELECT");
         return !v || atoi(v) != 0;
     }();
     const bool use_sel = kSelEnv && (uint64_t)s + s / 8 + 64 <= group_select_cap();
+    auto build_sel = [&](const std::vector<uint32_t> &rows0, uint32_t final_row, uint32_t slot,
+                         std::vector<std::vector<SelDesc>> &lv) {
+        constexpr uint64_t kKeysPerWG = 1u << 19;
+        constexpr size_t kRowsPerWG = 4096;
+        std::vector<uint32_t> cur = rows0;
+        for (size_t level = 0;; level++) {
+            if (lv.size() <= level) lv.resize(level + 1);
+            std::vector<std::pair<size_t, size_t>> ch;
+            size_t a = 0;
+            uint64_t acc = 0;
+            for (size_t i = 0; i < cur.size(); i++) {
+                const uint64_t e = est[cur[i]];
+                if (i > a && (acc + e > kKeysPerWG || i - a >= kRowsPerWG)) {
+                    ch.push_back({a, i});
+                    a = i;
+                    acc = 0;
+                }
+                acc += e;
+            }
+            ch.push_back({a, cur.size()});
+            if (ch.size() == 1) {
+                lv[level].push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)cur.size(),
+                                            final_row, slot});
+                sel_rows.insert(sel_rows.end(), cur.begin(), cur.end());
+                return;
+            }
+            std::vector<uint32_t> next;
+            for (auto &c : ch) {
+                const uint32_t r = n_rows++;
+                if (est.size() <= r) est.resize(r + 1, s);
+                uint64_t sum = 0;
+                for (size_t i = c.first; i < c.second; i++) sum += est[cur[i]];
+                est[r] = std::min<uint64_t>(s, sum);
+                lv[level].push_back(SelDesc{(uint32_t)sel_rows.size(),
+                                            (uint32_t)(c.second - c.first), r, slot});
+                sel_rows.insert(sel_rows.end(), cur.begin() + c.first, cur.begin() + c.second);
+                next.push_back(r);
+            }
+            cur.swap(next);
+        }
+    };
     std::vector<Plan> sfplan;
     std::vector<uint32_t> sfrb;
     std::vector<uint8_t> sfsmall;
@@ -713,9 +758,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             if (!slot_of[g] || slists[g].size() < 2) continue;
             const uint32_t r = n_rows++;                    // the sample's sketch row
             srow[slot_of[g] - 1] = r;
-            ssel.push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)slists[g].size(), r,
-                                   0xFFFFFFFFu});
-            sel_rows.insert(sel_rows.end(), slists[g].begin(), slists[g].end());
+            build_sel(slists[g], r, 0xFFFFFFFFu, ssel_lv);
             sflists[g].swap(slists[g]);
         }
     plan_rounds(slists, [&](uint32_t g) {
@@ -726,12 +769,22 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     if (use_sel)
         for (uint32_t g = 0; g < n_groups; g++) {
             if (!slot_of[g] || lists[g].size() < 2) continue;
-            sel.push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)lists[g].size(), g,
-                                  slot_of[g] - 1});
-            sel_rows.insert(sel_rows.end(), lists[g].begin(), lists[g].end());
+            build_sel(lists[g], g, slot_of[g] - 1, sel_lv);
             flists[g].swap(lists[g]);
         }
     plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb, msmall);
+    // d_sel: the sample levels, then the main levels; level boundaries for the launches
+    std::vector<SelDesc> sel;
+    std::vector<uint32_t> ssel_begin{0}, sel_begin;
+    for (auto &l : ssel_lv) {
+        sel.insert(sel.end(), l.begin(), l.end());
+        ssel_begin.push_back((uint32_t)sel.size());
+    }
+    sel_begin.push_back((uint32_t)sel.size());
+    for (auto &l : sel_lv) {
+        sel.insert(sel.end(), l.begin(), l.end());
+        sel_begin.push_back((uint32_t)sel.size());
+    }
     // the fallback plans' intermediate rows come last: they are allocated only if a selection
     // fails (a C5 share holds ~1.2 M tile rows of s u64: the fallback rows would double that)
     const uint32_t n_core = n_rows;
@@ -778,11 +831,12 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     job->round_small = msmall;
     job->sround_small = ssmall;
     job->n_slots = (uint32_t)srow.size();
-    job->n_ssel = (uint32_t)ssel.size();
-    job->n_sel = (uint32_t)sel.size();
+    job->ssel_begin = ssel_begin;
+    job->sel_begin = sel_begin;
+    job->n_ssel = ssel_begin.back();
+    job->n_sel = sel_begin.back() - sel_begin.front();
     job->sfround_begin = sfrb;
     job->sfround_small = sfsmall;
-    sel.insert(sel.begin(), ssel.begin(), ssel.end());   // d_sel: samples, then groups
     job->fround_begin = frb;
     job->fround_small = fsmall;
 
@@ -920,10 +974,13 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
         if (int rc = tiles_pass(job->d_stiles, job->sclass_begin)) return rc;
         if (job->n_ssel) {
-            TimedLaunch tl(ctx, FPM_K_MERGE, st);
-            HIP_TRY(launch_group_select(job->d_sel, job->n_ssel, job->d_sel_rows, job->d_rows,
-                                        job->d_count, job->kp.s, job->d_thr, fail_samp, st));
-            tl.done();
+            for (size_t l = 0; l + 1 < job->ssel_begin.size(); l++) {
+                const uint32_t b = job->ssel_begin[l], n = job->ssel_begin[l + 1] - b;
+                TimedLaunch tl(ctx, FPM_K_MERGE, st);
+                HIP_TRY(launch_group_select(job->d_sel + b, n, job->d_sel_rows, job->d_rows,
+                                            job->d_count, job->kp.s, job->d_thr, fail_samp, st));
+                tl.done();
+            }
             HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 1, fail_samp, sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, st));
         }
@@ -941,11 +998,13 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     }
     if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
     if (job->n_sel) {
-        TimedLaunch tl(ctx, FPM_K_MERGE, st);
-        HIP_TRY(launch_group_select(job->d_sel + job->n_ssel, job->n_sel, job->d_sel_rows,
-                                    job->d_rows, job->d_count, job->kp.s, job->d_thr, fail_main,
-                                    st));
-        tl.done();
+        for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
+            const uint32_t b = job->sel_begin[l], n = job->sel_begin[l + 1] - b;
+            TimedLaunch tl(ctx, FPM_K_MERGE, st);
+            HIP_TRY(launch_group_select(job->d_sel + b, n, job->d_sel_rows, job->d_rows,
+                                        job->d_count, job->kp.s, job->d_thr, fail_main, st));
+            tl.done();
+        }
         HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),
                                hipMemcpyDeviceToHost, st));
     }
@@ -1004,6 +1063,59 @@ void fpm_sketch_job_free(fpm_sketch_job *job)
     if (!job) return;
     job_release(job);
     delete job;
+}
+
+int fpm_sketch_merge_dev(fpm_ctx *ctx, const uint64_t *d_lists, const uint32_t *d_counts,
+                         uint32_t n_lists, uint32_t s, uint64_t *d_out, uint32_t *d_out_count,
+                         void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if ((n_lists && (!d_lists || !d_counts)) || !d_out || !d_out_count || s == 0)
+        return fail(FPM_EINVAL, "sketch_merge_dev: bad argument");
+    hipStream_t st = pick_stream(ctx, stream);
+    if (n_lists == 0) {
+        HIP_TRY(hipMemsetAsync(d_out_count, 0, 4, st));
+        return FPM_OK;
+    }
+    if (n_lists == 1) {
+        HIP_TRY(hipMemcpyAsync(d_out, d_lists, (size_t)s * 8, hipMemcpyDeviceToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_out_count, d_counts, 4, hipMemcpyDeviceToDevice, st));
+        return FPM_OK;
+    }
+    // pairwise rounds (the bottom s of a union = the bottom s of the union of the parts'
+    // bottom s); intermediate lists in scratch rows, the last merge writes d_out
+    void *tmp, *tcnt, *dd;
+    HIP_TRY(scratch(ctx, 16, (size_t)(n_lists - 1) * s * 8, &tmp));
+    HIP_TRY(scratch(ctx, 17, (size_t)(n_lists - 1) * 4, &tcnt));
+    struct L { const uint64_t *p; const uint32_t *c; };
+    std::vector<L> cur(n_lists);
+    for (uint32_t i = 0; i < n_lists; i++) cur[i] = L{d_lists + (uint64_t)i * s, d_counts + i};
+    std::vector<MergeDesc> md;
+    std::vector<uint32_t> rounds{0};
+    uint32_t used = 0;
+    while (cur.size() > 1) {
+        std::vector<L> nxt;
+        for (size_t i = 0; i + 1 < cur.size(); i += 2) {
+            uint64_t *c = cur.size() == 2 ? d_out : (uint64_t *)tmp + (uint64_t)used * s;
+            uint32_t *cc = cur.size() == 2 ? d_out_count : (uint32_t *)tcnt + used;
+            if (cur.size() != 2) used++;
+            md.push_back(MergeDesc{cur[i].p, cur[i].c, cur[i + 1].p, cur[i + 1].c, c, cc});
+            nxt.push_back(L{c, cc});
+        }
+        if (cur.size() % 2) nxt.push_back(cur.back());
+        cur.swap(nxt);
+        rounds.push_back((uint32_t)md.size());
+    }
+    HIP_TRY(scratch(ctx, 18, md.size() * sizeof(MergeDesc), &dd));
+    HIP_TRY(hipStreamSynchronize(st));   // the descriptor buffer may still be read by a prior call
+    HIP_TRY(hipMemcpy(dd, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice));
+    for (size_t r = 0; r + 1 < rounds.size(); r++) {
+        TimedLaunch tl(ctx, FPM_K_MERGE, st);
+        HIP_TRY(launch_merge((const MergeDesc *)dd + rounds[r], rounds[r + 1] - rounds[r], s, false,
+                             st));
+        tl.done();
+    }
+    return FPM_OK;
 }
 
 int fpm_sketch_batch(fpm_ctx *ctx, const fpm_sketch_params *p, const char *seq,

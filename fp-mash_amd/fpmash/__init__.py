@@ -107,6 +107,7 @@ SYMBOLS = [
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),
     ("fpm_refset_free", None, [vp]),
+    ("fpm_sketch_merge_dev", C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp]),
     ("fpm_seq_parse", C.c_int, [vp, C.POINTER(C.c_char_p), u64p, C.c_uint32, C.POINTER(vp),
                                 u64p, C.POINTER(C.c_int)]),
     ("fpm_seq_records", C.c_int, [vp, u32p, u64p, u64p, u64p]),

@@ -139,6 +139,15 @@ int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_ti
                         uint64_t *n_kmers);
 void fpm_sketch_job_free(fpm_sketch_job *job);
 
+/* Bottom-s of the union of n_lists sketches (device rows of stride s, ascending and
+ * distinct, counts[i] entries each) into d_out / d_out_count: the final min-merge when one
+ * sketch is computed in parts (a genome or read set split over GPUs, then all-gathered).
+ * MinHashHeap keeps the s smallest distinct hashes of one stream (MinHashHeap.cpp:68-146);
+ * the s smallest of a union are the s smallest of the union of the parts' s smallest. */
+int fpm_sketch_merge_dev(fpm_ctx *ctx, const uint64_t *d_lists, const uint32_t *d_counts,
+                         uint32_t n_lists, uint32_t s, uint64_t *d_out, uint32_t *d_out_count,
+                         void *stream);
+
 /* ---- FASTA text on the device ------------------------------------------------------
  * Replaces the main-thread kseq loop that feeds sketching (kseq_read, kseq.h:170-208, in
  * sketchFileBySequence / sketchFile, Sketch.cpp:478-522, 1299-1488): the n_seg file images

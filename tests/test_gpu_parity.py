@@ -490,3 +490,35 @@ def test_refset_blocks_match_grid(ctx, oracle, use64, mode):
     assert np.allclose(cat["distance"], di, rtol=1e-12, atol=0)
     assert np.allclose(cat["pvalue"], pv, rtol=1e-12, atol=0)
     assert np.array_equal(cat["pass"], pv <= 0.5)
+
+
+@pytest.mark.parametrize("s", [50, 1000, 10000])
+def test_sketch_merge_dev_matches_whole(ctx, oracle, s):
+    """fpm_sketch_merge_dev (the cross-GPU min-merge): one genome sketched in 1-5 k-mer
+    ranges (fpmash.shard.kmer_shard), the parts' rows merged on the device, equals the
+    oracle's sketch of the whole genome (MinHashHeap semantics), repeats across parts
+    included."""
+    import fpmash
+    from fpmash.shard import kmer_shard
+    rng = np.random.default_rng(s)
+    unit = rand_seq(rng, 5000)
+    genome = rand_seq(rng, 400_000) + unit * 6 + rand_seq(rng, 200_000)
+    exp = oracle.sketch_batch(oracle.params(k=21, s=s), [genome])[0]
+    P = fpmash.make_params(k=21, s=s)
+    for parts in (1, 2, 5):
+        segs = [genome[a:b] for a, b in (kmer_shard(len(genome), 21, parts, r)
+                                         for r in range(parts))]
+        sk = ctx.sketch(P, segs)
+        m = np.zeros((parts, s), np.uint64)
+        for i, x in enumerate(sk):
+            m[i, :len(x)] = x
+        rows = fpmash.DeviceBuffer.from_array(ctx, m)
+        cnts = fpmash.DeviceBuffer.from_array(ctx, np.array([len(x) for x in sk], np.uint32))
+        out = fpmash.DeviceBuffer(ctx, s * 8)
+        oc = fpmash.DeviceBuffer(ctx, 4)
+        fpmash._check(fpmash.lib().fpm_sketch_merge_dev(ctx.h, rows.ptr, cnts.ptr, parts, s,
+                                                        out.ptr, oc.ptr, None))
+        ctx.synchronize()
+        n = int(oc.to_array(np.uint32, 1)[0])
+        assert n == len(exp)
+        assert np.array_equal(out.to_array(np.uint64, s)[:n], exp)

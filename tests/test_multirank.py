@@ -58,3 +58,31 @@ def test_c4_leg_two_ranks_one_gpu():
     for r in res:
         assert r["parity"]["ok"], r
         assert r["parity"]["pairs_sharing"] > 0
+
+
+@pytest.mark.gpu
+def test_split_leg_two_ranks_one_gpu():
+    """bench.split_leg at world size 2 (both ranks on the one visible GPU, bottom-s rows
+    gathered over gloo, merged by fpm_sketch_merge_dev): the merged sketch of the split
+    genome equals the whole genome's sketch."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "_split_gpu_worker.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines()
+           if l.startswith("SPLITRANK ")]
+    assert sorted(r["rank"] for r in res) == [0, 1]
+    r0 = [r for r in res if r["rank"] == 0][0]
+    assert r0["parity"]["ok"] and r0["parity"]["merged_equals_whole"], r0
+
+
+def test_kmer_shard_covers_every_kmer_once():
+    """fpmash.shard.kmer_shard: the ranks' ranges hold every k-mer start exactly once."""
+    from fpmash.shard import kmer_shard
+    for L, k, w in [(100, 21, 1), (100, 21, 3), (1_000_003, 21, 8), (30, 21, 8), (5, 21, 2)]:
+        starts = []
+        for r in range(w):
+            lo, hi = kmer_shard(L, k, w, r)
+            starts += list(range(lo, max(lo, hi - k + 1)))
+        assert starts == list(range(max(0, L - k + 1)))
