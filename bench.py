@@ -182,6 +182,17 @@ def cpu_baseline(args, seqs):
     sketch_rate = passes * n_s * args.seq_len / t_s
     if n_s < n:
         sk = O.sketch_batch(P, seqs, threads=threads)
+    # the reference's own getHash + MinHashHeap (oracle/_ref, compiled from its sources: the
+    # k-mer walk re-driven around them) on the same threads, for a sample of records; its
+    # rate replaces the port's in the step when it is available
+    ref_rate = None
+    t0 = time.perf_counter()
+    n_ref = min(n, max(4 * threads, int(sketch_rate * args.cpu_seconds / 4 / args.seq_len)))
+    rsk = O.ref_sketch_batch(seqs[:n_ref], k=args.k, s=args.s, threads=threads)
+    if rsk is not None:
+        t_r = time.perf_counter() - t0
+        ref_rate = n_ref * args.seq_len / t_r
+        ref_same = all(np.array_equal(a, b) for a, b in zip(rsk, sk[:n_ref]))
     # dist leg: a ref-block x all-queries block of the all-vs-all grid (families included),
     # sized to about cpu_seconds
     lengths = [args.seq_len] * len(sk)
@@ -197,16 +208,28 @@ def cpu_baseline(args, seqs):
                 4.0 ** args.k, threads=threads)
     t_d = time.perf_counter() - t0
     dist_rate = n_r * n_q / t_d
-    step_s = n * args.seq_len / sketch_rate + n * n / dist_rate
+    step_s = n * args.seq_len / (ref_rate or sketch_rate) + n * n / dist_rate
+    extra = {}
+    if ref_rate:
+        extra = {"sketch_kind": "reference: oracle/_ref (hash.cpp, MurmurHash3.cpp, "
+                                "MinHashHeap.cpp, HashSet.cpp ... compiled from the reference's "
+                                "sources) around a restated addMinHashes walk",
+                 "sketch_reference_bases_per_s": ref_rate,
+                 "sketch_reference_records": n_ref,
+                 "sketch_reference_equals_port": bool(ref_same)}
     return {
         "value": n * args.seq_len / step_s,
         "unit": "bases/s",
         "cores": threads,
         "kind": "port",
+        **extra,
         "sample": (f"oracle CPU port on {threads} threads: sketch of {n_s} x {args.seq_len} bp "
                    f"x {passes} pass(es) in {t_s:.1f} s ({sketch_rate / 1e6:.2f} Mbases/s) + dist of a {n_r} x {n_q} "
                    f"pair block in {t_d:.1f} s ({dist_rate / 1e6:.3f} Mpairs/s, with p-values), "
-                   f"extrapolated to {n} seqs + {n * n:.3g} pairs"),
+                   f"extrapolated to {n} seqs + {n * n:.3g} pairs"
+                   + (f"; the step uses the sketch rate of the reference's own getHash + "
+                      f"MinHashHeap (oracle/_ref) on {n_ref} records, {ref_rate / 1e6:.2f} "
+                      "Mbases/s" if ref_rate else "")),
         "sketch_bases_per_s": sketch_rate,
         "dist_pairs_per_s": dist_rate,
         "step_s_extrapolated": step_s,

@@ -255,6 +255,9 @@ constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest
 #ifndef FPM_RANK_EXP
 #define FPM_RANK_EXP 0               // measurement builds: 1 = A loads only, 2 = row setup only
 #endif
+#ifndef FPM_RANK_LAYOUT
+#define FPM_RANK_LAYOUT 0            // 1: lane l ranks A[i0 + l], A[i0 + 64 + l] (A/B)
+#endif
 #ifndef FPM_RANK_LOGB
 #define FPM_RANK_LOGB 12             // log2 buckets for CAP 1024 (CAP 2048: one more)
 #endif
@@ -425,10 +428,20 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
+#if FPM_RANK_LAYOUT == 1
+            // lane l: A[i0 + l] and A[i0 + 64 + l] (8-B loads; consecutive lanes probe
+            // neighbouring B positions: fewer LDS bank conflicts than pairs per lane)
+            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
+            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
+                                                                 0, 0);
+            dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
+            dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
+#else
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(R.rsrc, (t * kChunk + 2 * lane) * 8u,
                                                                  0, 0);
             dst[u].e0 = ((uint64_t)v[1] << 32) | v[0];
             dst[u].e1 = ((uint64_t)v[3] << 32) | v[2];
+#endif
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -459,26 +472,41 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
-            // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
             const int rem = (int)la - (int)i0;
+#if FPM_RANK_LAYOUT == 1
+            // lane l holds i0 + l (e0) and i0 + 64 + l (e1)
+            const int r0 = rem, r1 = rem - 64;               // lanes whose e0 / e1 are valid
+#else
+            // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
             const int r0 = (rem + 1) >> 1, r1 = rem >> 1;   // lanes whose e0 / e1 are valid
+#endif
             const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
             const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
-            const uint32_t below = __builtin_amdgcn_mbcnt_hi(
-                (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u)) +
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(a1 >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
-            const uint32_t k0 = shared_below + below;
+            const uint32_t b0 = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
+            const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
+                (uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
+#if FPM_RANK_LAYOUT == 1
+            const uint32_t k0 = shared_below + b0;
+            const uint32_t k1 = shared_below + (uint32_t)__popcll(a0) + b1;
+            const uint32_t u0 = i0 + lane + j0[g] - k0, u1 = i0 + 64 + lane + j1[g] - k1;
+#else
+            const uint32_t k0 = shared_below + b0 + b1;
             const uint32_t k1 = k0 + (uint32_t)((a0 >> lane) & 1);
             const uint32_t i = i0 + 2 * lane;
             const uint32_t u0 = i + j0[g] - k0, u1 = i + 1 + j1[g] - k1;   // union ranks
+#endif
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
             shared_below += __popcll(a0) + __popcll(a1);
             if (g == kGroup - 1) {
                 const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
+#if FPM_RANK_LAYOUT == 1
+                u_last = (uint32_t)__builtin_amdgcn_readlane((int)(e >= 64 ? u1 : u0), (int)(e & 63));
+#else
                 u_last = (uint32_t)__builtin_amdgcn_readlane((int)((e & 1) ? u1 : u0), (int)(e >> 1));
+#endif
             }
         }
         return u_last;

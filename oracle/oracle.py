@@ -101,6 +101,30 @@ def _p(a, t):
     return a.ctypes.data_as(t)
 
 
+def ref_sketch_batch(seqs, k=21, s=1000, seed=42, threads=1):
+    """-i sketches of `seqs` through the reference's own getHash + MinHashHeap (oracle/_ref,
+    the addMinHashes walk re-driven around them), one record per call on `threads` threads
+    (ctypes releases the GIL).  None when oracle/_ref is not built."""
+    R = ref()
+    if R is None:
+        return None
+    from concurrent.futures import ThreadPoolExecutor
+    alpha = bytearray(256)
+    for c in b"ACGT":
+        alpha[c] = 1
+    alpha = bytes(alpha)
+    use64 = int(4.0 ** k > 2.0 ** 32)
+
+    def one(x):
+        off = np.array([0, len(x)], np.uint64)
+        out = np.zeros(s, np.uint64)
+        n = R.ref_sketch_records(x, _p(off, u64p), 1, k, s, seed, use64, 0, 0, alpha,
+                                 _p(out, u64p), None)
+        return out[:n]
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        return list(ex.map(one, seqs))
+
+
 def params(k=21, s=1000, seed=42, alphabet="ACGT", noncanonical=False, preserve_case=False):
     """Sketch::Parameters as sketchParameterSetup (sketchParameterSetup.cpp:9-126) builds them."""
     P = Params()

@@ -15,7 +15,7 @@ OUT=build/variant_$NAME; mkdir -p "$OUT" lib
 HIPCC=/opt/rocm/bin/hipcc
 HF="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-function -I../include $FLAGS"
 pids=()
-for k in sketch fingerprint dist dist_index; do
+for k in sketch fingerprint dist dist_index seqparse; do
   src="$SRC/$k.hip"
   # KSRC_<name>=path swaps one kernel source (e.g. an older dist.hip beside the current API)
   ov="KSRC_$k"; [ -n "${!ov:-}" ] && src="${!ov}"
