@@ -956,13 +956,25 @@ def main():
     d_len = fpmash.DeviceBuffer.from_array(ctx, lengths)
     st = ctx.stream
 
+    # FPM_BENCH_PREFILL=1: the no-shared-hash cells prefilled beside the sketch kernels
+    # (fpm_dist_prefill_dev); same-box A/B: 1.49-1.50 ms either way (the sketch kernel then
+    # stretches 0.17 -> 0.37 ms), so the one-call form is the default
+    prefill = os.environ.get("FPM_BENCH_PREFILL", "0") != "0"
+
     def step():
+        if prefill:
+            # the grid's no-shared-hash distance / p-value / pass cells need no list: written
+            # on the side stream while the sketches are computed (fpm_dist_prefill_dev)
+            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n, 1.0, 1.0, d_dist.ptr, d_pval.ptr,
+                                                 d_pass.ptr, None))
         job.run(st)
-        # compare + distance + p-value + pass in one call
-        fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
-                                     d_len.ptr, stride, n, 8, args.s, args.k, 4.0 ** args.k,
-                                     1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
-                                     d_pass.ptr, st))
+        # compare + distance + p-value + pass (the candidates and empty pairs rewritten after
+        # the prefill)
+        dist16 = L.fpm_dist_dev16_prefilled if prefill else L.fpm_dist_dev16
+        fpmash._check(dist16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
+                             d_len.ptr, stride, n, 8, args.s, args.k, 4.0 ** args.k,
+                             1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
+                             d_pass.ptr, st))
 
     for _ in range(args.warmup):
         step()

@@ -740,13 +740,15 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
     const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
     for (uint32_t t = blockIdx.x; t < ntask; t += gridDim.x) {
     const uint32_t q = t / nrb, rb = t - q * nrb;
-    const uint32_t lq = qry_len[q];
+    // no lengths (fpm_dist_prefill_dev): every list taken as non-empty (the empty pairs are
+    // fixed up by dist_empty_fixup_kernel once the lengths exist)
+    const uint32_t lq = qry_len ? qry_len[q] : 1u;
     const uint64_t row = (uint64_t)q * n_ref;
     if (VEC) {
         const uint32_t r = rb * kFillCells + threadIdx.x * 4;
         if (r >= n_ref) continue;
         const uint64_t o = row + r;
-        const uint4 rl = *(const uint4 *)(ref_len + r);
+        const uint4 rl = ref_len ? *(const uint4 *)(ref_len + r) : make_uint4(0, 0, 0, 0);
         const uint32_t d[4] = {rl.x + lq, rl.y + lq, rl.z + lq, rl.w + lq};  // <= 2 stride
         uint32_t dn[4], pa = 0;
         double dv[4], pv[4];
@@ -777,7 +779,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         const uint32_t r = rb * kFillCells + u * 256 + threadIdx.x;
         if (r >= n_ref) break;
         const uint64_t o = row + r;
-        const uint32_t d = ref_len[r] + lq;            // both <= stride, no overflow
+        const uint32_t d = (ref_len ? ref_len[r] : 0u) + lq;   // both <= stride, no overflow
         const bool ok = d == 0 || keep1;
         if (numer) {
             numer[o] = 0;
@@ -788,6 +790,35 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         if (fill.pass) fill.pass[o] = ok && pkeep ? 1 : 0;
     }
     }
+}
+
+// After fpm_dist_prefill_dev (every cell written as a pair of non-empty lists sharing no
+// hash): the pairs of two empty lists get distance 0 (numer == denom == 0), p-value 1 and
+// the -d / -v filter at those values.  One thread per query row; only empty rows loop.
+__global__ __launch_bounds__(256) void dist_empty_fixup_kernel(
+    const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
+    uint32_t n_qry, PairFill fill)
+{
+    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= n_qry || qry_len[q] != 0) return;
+    const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
+    const uint64_t row = (uint64_t)q * n_ref;
+    for (uint32_t r = 0; r < n_ref; r++)
+        if (ref_len[r] == 0) {
+            fill.dist[row + r] = 0.0;
+            fill.pval[row + r] = 1.0;
+            if (fill.pass) fill.pass[row + r] = pkeep ? 1 : 0;
+        }
+}
+
+hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
+                                   const uint32_t *d_qry_len, uint32_t n_qry,
+                                   const PairFill &fill, hipStream_t st)
+{
+    if (!n_ref || !n_qry) return hipSuccess;
+    hipLaunchKernelGGL(dist_empty_fixup_kernel, dim3((n_qry + 255) / 256), dim3(256), 0, st,
+                       d_ref_len, n_ref, d_qry_len, n_qry, fill);
+    return hipGetLastError();
 }
 
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
@@ -801,7 +832,7 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
     if (blocks >= (1ULL << 31)) return hipErrorInvalidValue;
     // 16-B stores need 16-B aligned rows of every output (the pass row as 4-B aligned)
     const auto al = [](const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
-    const bool vec = n_ref % 4 == 0 && al(d_ref_len, 16) && al(d_numer, 16) &&
+    const bool vec = n_ref % 4 == 0 && (!d_ref_len || al(d_ref_len, 16)) && al(d_numer, 16) &&
                      al(d_denom, 16) && al(fill.dist, 16) && al(fill.pval, 16) &&
                      al(fill.pass, 4);
     // the full grid: short workgroups hand their slots back to the candidate compare running

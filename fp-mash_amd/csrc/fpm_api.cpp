@@ -89,6 +89,7 @@ struct fpm_ctx {
     // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
+    hipEvent_t ev_prefill = nullptr;       // end of the last fpm_dist_prefill_dev
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
     static constexpr size_t kRingBytes = 8u << 20;
@@ -285,6 +286,7 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
+    if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -1464,6 +1466,9 @@ struct DistFinal {
     double kmer_space, max_dist, max_pvalue;
     double *dist, *pval;
     uint8_t *pass;
+    // the caller ran fpm_dist_prefill_dev on these buffers (ctx->ev_prefill marks its end):
+    // no fill here, the empty pairs are fixed up and every rewrite waits for the prefill
+    bool prefilled = false;
 };
 
 // bucket index geometry for E entries over n_ref rows: ~2.4 entries per bucket (2^nbits >=
@@ -1634,7 +1639,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         fill_pending = true;
         return FPM_OK;
     };
-    if (try_sparse && fin && ctx->fill_early)
+    if (try_sparse && fin && ctx->fill_early && !fin->prefilled)
         if (int rc = launch_fill()) return rc;
     if (try_sparse) {
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
@@ -1785,7 +1790,14 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 tl.done();
             }
             uint32_t *cnum = nullptr, *cden = nullptr;
-            if (fin) {
+            if (fin && fin->prefilled) {
+                if (rows_merge) {
+                    void *cres;
+                    HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
+                    cnum = (uint32_t *)cres;
+                    cden = cnum + cap;
+                }
+            } else if (fin) {
                 if (!fill_pending)
                     if (int rc = launch_fill()) return rc;
                 if (rows_merge) {
@@ -1812,8 +1824,21 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                    st));
                 tl.done();
             }
+            if (fin && fin->prefilled) {
+                // the walk kernel wrote numer / denom only; distance / p-value / pass of the
+                // candidates and the empty pairs overwrite the prefill, so after it
+                PairFill fx;
+                fx.dist = fin->dist;
+                fx.pval = fin->pval;
+                fx.pass = fin->pass;
+                fx.max_dist = fin->max_dist;
+                fx.max_pvalue = fin->max_pvalue;
+                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
+                HIP_TRY(launch_dist_empty_fixup(d_ref_len, n_ref, d_qry_len, n_qry, fx, st));
+            } else if (fin && cnum) {
+                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+            }
             if (fin) {
-                if (cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
                 HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
                                                   cden, cnt, fin->ref_length,
@@ -1875,12 +1900,15 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                          uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
                          double kmer_space, double max_dist, double max_pvalue, Counts cnt,
                          double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream,
-                         const char *who, fpm_refset *rs = nullptr)
+                         const char *who, fpm_refset *rs = nullptr, bool prefilled = false)
 {
     if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
         return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
-    const DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
-                        d_dist, d_pvalue, d_pass};
+    if (prefilled && !ctx->ev_prefill)
+        return fail(FPM_EINVAL, std::string(who) + ": no fpm_dist_prefill_dev on this context");
+    DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
+                  d_dist, d_pvalue, d_pass};
+    fin.prefilled = prefilled;
     bool finalized = false;
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                               qry_stride, n_qry, hash_bytes, sketch_size, cnt, stream, &fin,
@@ -1888,6 +1916,7 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         return rc;
     if (finalized) return FPM_OK;
     hipStream_t st = pick_stream(ctx, stream);
+    if (prefilled) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));   // rewrites every cell
     TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
     HIP_TRY(launch_dist_finalize(cnt, d_ref_length, d_qry_length, n_ref, n_qry, kmer_size,
                                  kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass, st));
@@ -1925,6 +1954,52 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                          d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
                          kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, true},
                          d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev16");
+}
+
+int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double max_dist,
+                         double max_pvalue, double *d_dist, double *d_pvalue, uint8_t *d_pass,
+                         void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!d_dist || !d_pvalue) return fail(FPM_EINVAL, "fpm_dist_prefill_dev: null output");
+    HIP_TRY(ensure_aux(ctx));
+    if (!ctx->ev_prefill) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prefill, hipEventDisableTiming));
+    hipStream_t st = stream ? (hipStream_t)stream : ctx->aux;
+    if (!stream) {
+        // the side stream starts after the work already queued on the context's stream (an
+        // earlier call's rewrites of the same cells)
+        HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_in, 0));
+    }
+    PairFill fill;
+    fill.dist = d_dist;
+    fill.pval = d_pvalue;
+    fill.pass = d_pass;
+    fill.max_dist = max_dist;
+    fill.max_pvalue = max_pvalue;
+    TimedLaunch tl(ctx, FPM_K_FILL, st);
+    HIP_TRY(launch_dist_fill(nullptr, n_ref, nullptr, n_qry, 0, Counts{}, fill, st));
+    tl.done();
+    HIP_TRY(hipEventRecord(ctx->ev_prefill, st));
+    return FPM_OK;
+}
+
+int fpm_dist_dev16_prefilled(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                             const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                             const void *d_qry, const uint32_t *d_qry_len,
+                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
+                             double kmer_space, double max_dist, double max_pvalue,
+                             uint16_t *d_numer, uint16_t *d_denom, double *d_dist,
+                             double *d_pvalue, uint8_t *d_pass, void *stream)
+{
+    if (sketch_size > 65535)
+        return fail(FPM_EINVAL, "fpm_dist_dev16_prefilled: sketch_size must be <= 65535");
+    return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
+                         d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
+                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, true},
+                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev16_prefilled", nullptr,
+                         true);
 }
 
 int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,

@@ -139,6 +139,11 @@ struct PairFill {
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
                             hipStream_t st);
+// (d_ref_len == d_qry_len == nullptr: every list taken as non-empty, fpm_dist_prefill_dev)
+// distance 0 / p-value 1 / pass for the pairs of two empty lists (after such a prefill)
+hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
+                                   const uint32_t *d_qry_len, uint32_t n_qry,
+                                   const PairFill &fill, hipStream_t st);
 // `defaults`: also write (0, min(S, la+lb)) to every numer / denom cell of the row (off
 // when launch_dist_fill already did)
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,

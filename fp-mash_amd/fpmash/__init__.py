@@ -90,6 +90,12 @@ SYMBOLS = [
     ("fpm_dist_dev16", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
                                  C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
                                  C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
+    ("fpm_dist_prefill_dev", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_double, C.c_double, vp,
+                                       vp, vp, vp]),
+    ("fpm_dist_dev16_prefilled", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp,
+                                           C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, C.c_double, C.c_double, C.c_double, vp,
+                                           vp, vp, vp, vp, vp]),
     ("fpm_fp_positional_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p,
                                          C.c_uint64, C.c_uint32, C.c_uint32, C.c_double,
                                          C.c_double, u32p, u32p, f64p, f64p, u8p]),

@@ -244,6 +244,25 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                    uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
                    uint16_t *d_numer, uint16_t *d_denom, double *d_dist, double *d_pvalue,
                    uint8_t *d_pass, void *stream);
+/* The same in two parts, so the output grid's bulk overlaps the sketching of the lists: a
+ * pair of non-empty lists that share no hash has distance 1 and p-value 1 whatever the
+ * lists are (CommandDistance.cpp:404-419, 433-450 at common = 0), so
+ * fpm_dist_prefill_dev writes those values (and the -d / -v pass flag at them) to every
+ * cell of the n_qry x n_ref grid without reading any list (NULL stream: the context's side
+ * stream), and fpm_dist_dev16_prefilled then computes everything else: every cell's counts,
+ * the pairs of two empty lists, and the cells of the pairs that share hashes (those rewrites
+ * wait for the prefill; the rest of the call does not).  Same results as fpm_dist_dev16. */
+int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double max_dist,
+                         double max_pvalue, double *d_dist, double *d_pvalue, uint8_t *d_pass,
+                         void *stream);
+int fpm_dist_dev16_prefilled(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                             const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                             const void *d_qry, const uint32_t *d_qry_len,
+                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
+                             double kmer_space, double max_dist, double max_pvalue,
+                             uint16_t *d_numer, uint16_t *d_denom, double *d_dist,
+                             double *d_pvalue, uint8_t *d_pass, void *stream);
 /* host-buffer convenience: compare + finalize */
 int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
              uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,

@@ -522,3 +522,57 @@ def test_sketch_merge_dev_matches_whole(ctx, oracle, s):
         n = int(oc.to_array(np.uint32, 1)[0])
         assert n == len(exp)
         assert np.array_equal(out.to_array(np.uint64, s)[:n], exp)
+
+
+@pytest.mark.parametrize("self_set", [True, False])
+@pytest.mark.parametrize("maxd,maxp", [(-1.0, -1.0), (1.0, 1.0), (0.5, 1.0), (1.0, 1e-10)])
+def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
+    """fpm_dist_prefill_dev (side stream, no list read) + fpm_dist_dev16_prefilled give the
+    same five outputs as fpm_dist_dev16, empty lists and -d / -v filters included; the
+    counts and p-values also match the oracle."""
+    import fpmash
+    from fpmash import datagen
+    P = fpmash.make_params(k=21, s=500)
+    seqs = datagen.family_dna(8, 12, 1500, sub_rate=(0.0, 0.08), seed=31)
+    seqs += [b"N" * 300, b"", b"ACGT" * 3]          # lists with no k-mer: empty sketches
+    sk = ctx.sketch(P, seqs)
+    qsk = sk if self_set else sk[::-1][:60]
+    w = 500
+    R, rl = fpmash._dense(sk, w, np.uint64)
+    Q, ql = (R, rl) if self_set else fpmash._dense(qsk, w, np.uint64)
+    nr, nq = len(sk), len(qsk)
+    L = fpmash.lib()
+    bufs = []
+
+    def up(a):
+        b = fpmash.DeviceBuffer.from_array(ctx, a)
+        bufs.append(b)
+        return b.ptr
+    dR, drl = up(R), up(rl)
+    dQ, dql = (dR, drl) if self_set else (up(Q), up(ql))
+    lens = np.array([len(x) for x in seqs], np.uint64)
+    qlens = lens if self_set else lens[::-1][:60].copy()
+    dL = up(lens)
+    dqL = dL if self_set else up(qlens)
+    res = []
+    for pre in (False, True):
+        outs = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (2, 2, 8, 8, 1)]
+        bufs.extend(outs)
+        if pre:
+            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr, nq, maxd, maxp, outs[2].ptr,
+                                                 outs[3].ptr, outs[4].ptr, None))
+        f = L.fpm_dist_dev16_prefilled if pre else L.fpm_dist_dev16
+        fpmash._check(f(ctx.h, dR, drl, dL, w, nr, dQ, dql, dqL, w, nq, 8, 500, 21, 4.0 ** 21,
+                        maxd, maxp, *[o.ptr for o in outs], None))
+        ctx.synchronize()
+        res.append([o.to_array(t, nr * nq) for o, t in zip(outs, (np.uint16, np.uint16,
+                                                                   np.float64, np.float64,
+                                                                   np.uint8))])
+    for a, b in zip(res[0], res[1]):
+        assert np.array_equal(a, b)
+    nu, de, di, pv = oracle.dist_grid(sk, list(lens), qsk, list(qlens), 500, 21, 4.0 ** 21)
+    assert np.array_equal(res[1][0], nu) and np.array_equal(res[1][1], de)
+    ok = (res[1][0] > 0)
+    assert np.allclose(res[1][3][ok], pv[ok], rtol=1e-12, atol=0)
+    for b in bufs:
+        b.free()
