@@ -44,7 +44,16 @@ void ensure_exit_handler()
 
 void init_ids()
 {
-    if (const char *dev = getenv("FPMASH_DEVICE")) {
+    if (const char *list = getenv("FPMASH_DEVICE_LIST")) {
+        // explicit ordinals, e.g. "0,0" runs two contexts on one GPU (the tests' stand-in for
+        // a multi-GPU node)
+        for (const char *c = list; *c;) {
+            g_ids.push_back(atoi(c));
+            while (*c && *c != ',') c++;
+            if (*c == ',') c++;
+        }
+        if (g_ids.empty()) g_ids.push_back(0);
+    } else if (const char *dev = getenv("FPMASH_DEVICE")) {
         g_ids.push_back(atoi(dev));
     } else {
         int n = 0;

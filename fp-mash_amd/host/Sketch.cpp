@@ -200,6 +200,178 @@ int hostRecords(const std::string &image, std::vector<SeqRec> &out, std::string 
 
 }  // namespace
 
+// Parse and sketch the sequence files [f0, f1) on one device (the reference's per-file work,
+// Sketch.cpp:249-397 / 478-522 / 1299-1488): fills fileRefs[f] for those files.
+static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
+                        const std::vector<std::string> &seqFiles, std::vector<std::string> &images,
+                        size_t f0, size_t f1, std::vector<std::vector<Reference>> &fileRefs,
+                        bool timing)
+{
+    const size_t nF = f1 - f0;
+    auto mark = [&](const char *what) { if (timing) phaseMark(what); };
+    // records of each file (kseq rules) parsed on the device
+    std::vector<std::vector<SeqRec>> recs(nF);
+    fpm_seqtext *parsed = nullptr;
+    uint64_t nRec = 0;
+    int quality = 0;
+    {
+        std::vector<const char *> ptr(nF);
+        std::vector<uint64_t> len(nF);
+        for (size_t f = 0; f < nF; f++) {
+            ptr[f] = images[f0 + f].data();
+            len[f] = images[f0 + f].size();
+        }
+        check(fpm_seq_parse(ctx, ptr.data(), len.data(), (uint32_t)nF, &parsed,
+                            &nRec, &quality),
+              "sequence parse");
+    }
+    mark("device parse (upload + scan + emit)");
+    std::string hostSeq;               // host fallback: the records' bytes
+    std::vector<uint64_t> hostOff{0};
+    if (!quality) {
+        std::vector<uint32_t> seg(nRec);
+        std::vector<uint64_t> ho(nRec), hl(nRec), sl(nRec);
+        check(fpm_seq_records(parsed, seg.data(), ho.data(), hl.data(), sl.data()),
+              "sequence parse");
+        for (uint64_t r = 0; r < nRec; r++) {
+            const std::string &img = images[f0 + seg[r]];
+            // a '>' / '@' as the last byte of a file starts no record (kseq_read returns
+            // -1 when the name read hits the end of the stream)
+            if (ho[r] + 1 >= img.size()) continue;
+            SeqRec x;
+            splitHeader(img.data() + ho[r] + 1, hl[r] - 1, x.name, x.comment);
+            x.length = sl[r];
+            x.id = (uint32_t)r;
+            recs[seg[r]].push_back(std::move(x));
+        }
+    } else {
+        // FASTQ quality lines: kseq's record walk on the host
+        fpm_seq_free(parsed);
+        parsed = nullptr;
+        for (size_t f = 0; f < nF; f++) {
+            if (hostRecords(images[f0 + f], recs[f], hostSeq, hostOff) != -1) {
+                std::cerr << "\nERROR: reading " << (parameters.concatenated ? std::string("input files")
+                                                                               : seqFiles[f0 + f])
+                          << "." << std::endl;
+                exit(1);
+            }
+        }
+    }
+    mark("record headers");
+
+    // sketch groups: one per file (sketchFile, Sketch.cpp:1299-1488) or one per record
+    // >= k with -i (sketchFileBySequence, :478-522); records < k are skipped (:488-492)
+    const uint64_t nIds = parsed ? nRec : hostOff.size() - 1;
+    std::vector<uint32_t> groupOf(nIds, FPM_NO_GROUP);
+    uint32_t nGroups = 0;
+    std::vector<std::vector<uint32_t>> fileGroups(nF);
+    for (size_t f = 0; f < nF; f++) {
+        const std::string &file = seqFiles[f0 + f];
+        if (parameters.concatenated) {
+            Reference ref;
+            const uint32_t g = nGroups++;
+            int count = 0;
+            bool skipped = false;
+            if (file != "-") ref.name = file;
+            for (const SeqRec &x : recs[f]) {
+                if (x.length < (uint64_t)parameters.kmerSize) { skipped = true; continue; }
+                if (count == 0) {
+                    if (file == "-") { ref.name = x.name; ref.comment = x.comment; }
+                    else ref.comment = x.name + " " + x.comment;
+                }
+                count++;
+                ref.length += x.length;
+                groupOf[x.id] = g;
+            }
+            if (count > 1) ref.comment = "[" + std::to_string(count) + " seqs] " + ref.comment + " [...]";
+            if (ref.length == 0) {
+                if (skipped)
+                    std::cerr << "\nWARNING: All fasta records in input files were shorter than the "
+                                 "k-mer size (" << parameters.kmerSize << ")." << std::endl;
+                else
+                    std::cerr << "\nERROR: Did not find fasta records in \"input files\"." << std::endl;
+                exit(1);
+            }
+            fileRefs[f0 + f].push_back(std::move(ref));
+            fileGroups[f].push_back(g);
+        } else {
+            for (SeqRec &x : recs[f]) {
+                if (x.length < (uint64_t)parameters.kmerSize) continue;
+                Reference ref;
+                ref.name = std::move(x.name);
+                ref.comment = std::move(x.comment);
+                ref.length = x.length;
+                const uint32_t g = nGroups++;
+                groupOf[x.id] = g;
+                fileRefs[f0 + f].push_back(std::move(ref));
+                fileGroups[f].push_back(g);
+            }
+        }
+    }
+    for (size_t f = f0; f < f1; f++) {
+        images[f].clear();
+        images[f].shrink_to_fit();
+    }
+
+    if (nGroups) {
+        fpm_sketch_params fp{};
+        fp.kmer_size = (uint32_t)parameters.kmerSize;
+        fp.sketch_size = (uint32_t)parameters.minHashesPerWindow;
+        fp.seed = parameters.seed;
+        fp.use64 = parameters.use64;
+        fp.noncanonical = parameters.noncanonical;
+        fp.preserve_case = parameters.preserveCase;
+        for (int c = 0; c < 256; c++) fp.alphabet[c] = parameters.alphabet[c] ? 1 : 0;
+        const uint64_t s = fp.sketch_size;
+        std::vector<uint64_t> out((size_t)nGroups * s);
+        std::vector<uint32_t> cnt(nGroups);
+        fpm_sketch_job *job = nullptr;
+        if (parsed) {
+            check(fpm_sketch_stage_seq(ctx, &fp, parsed, groupOf.data(), nGroups, &job), "sketch");
+        } else {
+            // host-parsed records: only those of a group go to the device
+            std::vector<uint64_t> off{0};
+            std::vector<uint32_t> grp;
+            std::string packed;
+            for (uint64_t r = 0; r < nIds; r++) {
+                if (groupOf[r] == FPM_NO_GROUP) continue;
+                packed.append(hostSeq, hostOff[r], hostOff[r + 1] - hostOff[r]);
+                off.push_back(packed.size());
+                grp.push_back(groupOf[r]);
+            }
+            check(fpm_sketch_stage(ctx, &fp, packed.data(), off.data(), (uint32_t)grp.size(),
+                                   grp.data(), nGroups, &job),
+                  "sketch");
+        }
+        int rc = fpm_sketch_run(job, nullptr);
+        if (rc == FPM_OK) rc = fpm_sketch_fetch(job, out.data(), cnt.data());
+        fpm_sketch_job_free(job);
+        check(rc, "sketch");
+        mark("device sketch (stage + run + fetch)");
+        // hash lists into the references (threads: the copies are page-fault bound)
+        std::vector<std::pair<size_t, size_t>> all;
+        for (size_t f = 0; f < nF; f++)
+            for (size_t i = 0; i < fileRefs[f0 + f].size(); i++) all.push_back({f, i});
+        std::atomic<size_t> nextRef{0};
+        auto copyRefs = [&]() {
+            for (size_t a; (a = nextRef.fetch_add(256)) < all.size();)
+                for (size_t x = a; x < std::min(all.size(), a + 256); x++) {
+                    const size_t f = all[x].first, i = all[x].second;
+                    const uint32_t g = fileGroups[f][i];
+                    fileRefs[f0 + f][i].hashes.assign(out.begin() + (size_t)g * s,
+                                                 out.begin() + (size_t)g * s + cnt[g]);
+                }
+        };
+        std::vector<std::thread> cp;
+        const size_t ncp = all.size() < 1024 ? 0 : std::min(7u, std::thread::hardware_concurrency());
+        for (size_t t = 0; t < ncp; t++) cp.emplace_back(copyRefs);
+        copyRefs();
+        for (auto &t : cp) t.join();
+    }
+    mark("reference lists");
+    if (parsed) fpm_seq_free(parsed);
+}
+
 int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameters &p, int verbosity,
                           bool enforceParameters, bool contain)
 {
@@ -304,168 +476,35 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
                 }
         }
         phaseMark("read input");
-        fpm_ctx *ctx = device();
-        phaseMark("device context");
-        // records of each file (kseq rules) parsed on the device
-        std::vector<std::vector<SeqRec>> recs(seqFiles.size());
-        fpm_seqtext *parsed = nullptr;
-        uint64_t nRec = 0;
-        int quality = 0;
-        {
-            std::vector<const char *> ptr(seqFiles.size());
-            std::vector<uint64_t> len(seqFiles.size());
-            for (size_t f = 0; f < seqFiles.size(); f++) {
-                ptr[f] = images[f].data();
-                len[f] = images[f].size();
-            }
-            check(fpm_seq_parse(ctx, ptr.data(), len.data(), (uint32_t)seqFiles.size(), &parsed,
-                                &nRec, &quality),
-                  "sequence parse");
-        }
-        phaseMark("device parse (upload + scan + emit)");
-        std::string hostSeq;               // host fallback: the records' bytes
-        std::vector<uint64_t> hostOff{0};
-        if (!quality) {
-            std::vector<uint32_t> seg(nRec);
-            std::vector<uint64_t> ho(nRec), hl(nRec), sl(nRec);
-            check(fpm_seq_records(parsed, seg.data(), ho.data(), hl.data(), sl.data()),
-                  "sequence parse");
-            for (uint64_t r = 0; r < nRec; r++) {
-                const std::string &img = images[seg[r]];
-                // a '>' / '@' as the last byte of a file starts no record (kseq_read returns
-                // -1 when the name read hits the end of the stream)
-                if (ho[r] + 1 >= img.size()) continue;
-                SeqRec x;
-                splitHeader(img.data() + ho[r] + 1, hl[r] - 1, x.name, x.comment);
-                x.length = sl[r];
-                x.id = (uint32_t)r;
-                recs[seg[r]].push_back(std::move(x));
-            }
-        } else {
-            // FASTQ quality lines: kseq's record walk on the host
-            fpm_seq_free(parsed);
-            parsed = nullptr;
-            for (size_t f = 0; f < seqFiles.size(); f++) {
-                if (hostRecords(images[f], recs[f], hostSeq, hostOff) != -1) {
-                    std::cerr << "\nERROR: reading " << (parameters.concatenated ? std::string("input files")
-                                                                                   : seqFiles[f])
-                              << "." << std::endl;
-                    exit(1);
-                }
-            }
-        }
-        phaseMark("record headers");
-
-        // sketch groups: one per file (sketchFile, Sketch.cpp:1299-1488) or one per record
-        // >= k with -i (sketchFileBySequence, :478-522); records < k are skipped (:488-492)
-        const uint64_t nIds = parsed ? nRec : hostOff.size() - 1;
-        std::vector<uint32_t> groupOf(nIds, FPM_NO_GROUP);
-        uint32_t nGroups = 0;
+        // files over the devices as contiguous ranges balanced by bytes (the reference's -p
+        // threads take files in turn, Sketch.cpp:253); one device: every file on device(0)
         std::vector<std::vector<Reference>> fileRefs(seqFiles.size());
-        std::vector<std::vector<uint32_t>> fileGroups(seqFiles.size());
-        for (size_t f = 0; f < seqFiles.size(); f++) {
-            const std::string &file = seqFiles[f];
-            if (parameters.concatenated) {
-                Reference ref;
-                const uint32_t g = nGroups++;
-                int count = 0;
-                bool skipped = false;
-                if (file != "-") ref.name = file;
-                for (const SeqRec &x : recs[f]) {
-                    if (x.length < (uint64_t)parameters.kmerSize) { skipped = true; continue; }
-                    if (count == 0) {
-                        if (file == "-") { ref.name = x.name; ref.comment = x.comment; }
-                        else ref.comment = x.name + " " + x.comment;
-                    }
-                    count++;
-                    ref.length += x.length;
-                    groupOf[x.id] = g;
-                }
-                if (count > 1) ref.comment = "[" + std::to_string(count) + " seqs] " + ref.comment + " [...]";
-                if (ref.length == 0) {
-                    if (skipped)
-                        std::cerr << "\nWARNING: All fasta records in input files were shorter than the "
-                                     "k-mer size (" << parameters.kmerSize << ")." << std::endl;
-                    else
-                        std::cerr << "\nERROR: Did not find fasta records in \"input files\"." << std::endl;
-                    exit(1);
-                }
-                fileRefs[f].push_back(std::move(ref));
-                fileGroups[f].push_back(g);
-            } else {
-                for (SeqRec &x : recs[f]) {
-                    if (x.length < (uint64_t)parameters.kmerSize) continue;
-                    Reference ref;
-                    ref.name = std::move(x.name);
-                    ref.comment = std::move(x.comment);
-                    ref.length = x.length;
-                    const uint32_t g = nGroups++;
-                    groupOf[x.id] = g;
-                    fileRefs[f].push_back(std::move(ref));
-                    fileGroups[f].push_back(g);
-                }
+        const int nDev = deviceCount();
+        const size_t nParts = std::min<size_t>((size_t)std::max(1, nDev), seqFiles.size());
+        if (nParts <= 1) {
+            fpm_ctx *ctx = device();
+            phaseMark("device context");
+            sketchFiles(ctx, parameters, seqFiles, images, 0, seqFiles.size(), fileRefs, true);
+        } else {
+            uint64_t tot = 0;
+            for (auto &im : images) tot += im.size() + 1;
+            std::vector<size_t> cut{0};
+            uint64_t acc = 0;
+            for (size_t f = 0; f < seqFiles.size(); f++) {
+                acc += images[f].size() + 1;
+                if (cut.size() < nParts && acc * nParts >= tot * cut.size() && f + 1 < seqFiles.size())
+                    cut.push_back(f + 1);
             }
+            cut.push_back(seqFiles.size());
+            std::vector<std::thread> th;
+            for (size_t d = 0; d + 1 < cut.size(); d++)
+                th.emplace_back([&, d] {
+                    sketchFiles(device((int)d), parameters, seqFiles, images, cut[d], cut[d + 1],
+                                fileRefs, false);
+                });
+            for (auto &t : th) t.join();
+            phaseMark("device sketch over all devices");
         }
-        images.clear();
-        images.shrink_to_fit();
-
-        if (nGroups) {
-            fpm_sketch_params fp{};
-            fp.kmer_size = (uint32_t)parameters.kmerSize;
-            fp.sketch_size = (uint32_t)parameters.minHashesPerWindow;
-            fp.seed = parameters.seed;
-            fp.use64 = parameters.use64;
-            fp.noncanonical = parameters.noncanonical;
-            fp.preserve_case = parameters.preserveCase;
-            for (int c = 0; c < 256; c++) fp.alphabet[c] = parameters.alphabet[c] ? 1 : 0;
-            const uint64_t s = fp.sketch_size;
-            std::vector<uint64_t> out((size_t)nGroups * s);
-            std::vector<uint32_t> cnt(nGroups);
-            fpm_sketch_job *job = nullptr;
-            if (parsed) {
-                check(fpm_sketch_stage_seq(ctx, &fp, parsed, groupOf.data(), nGroups, &job), "sketch");
-            } else {
-                // host-parsed records: only those of a group go to the device
-                std::vector<uint64_t> off{0};
-                std::vector<uint32_t> grp;
-                std::string packed;
-                for (uint64_t r = 0; r < nIds; r++) {
-                    if (groupOf[r] == FPM_NO_GROUP) continue;
-                    packed.append(hostSeq, hostOff[r], hostOff[r + 1] - hostOff[r]);
-                    off.push_back(packed.size());
-                    grp.push_back(groupOf[r]);
-                }
-                check(fpm_sketch_stage(ctx, &fp, packed.data(), off.data(), (uint32_t)grp.size(),
-                                       grp.data(), nGroups, &job),
-                      "sketch");
-            }
-            int rc = fpm_sketch_run(job, nullptr);
-            if (rc == FPM_OK) rc = fpm_sketch_fetch(job, out.data(), cnt.data());
-            fpm_sketch_job_free(job);
-            check(rc, "sketch");
-            phaseMark("device sketch (stage + run + fetch)");
-            // hash lists into the references (threads: the copies are page-fault bound)
-            std::vector<std::pair<size_t, size_t>> all;
-            for (size_t f = 0; f < seqFiles.size(); f++)
-                for (size_t i = 0; i < fileRefs[f].size(); i++) all.push_back({f, i});
-            std::atomic<size_t> nextRef{0};
-            auto copyRefs = [&]() {
-                for (size_t a; (a = nextRef.fetch_add(256)) < all.size();)
-                    for (size_t x = a; x < std::min(all.size(), a + 256); x++) {
-                        const size_t f = all[x].first, i = all[x].second;
-                        const uint32_t g = fileGroups[f][i];
-                        fileRefs[f][i].hashes.assign(out.begin() + (size_t)g * s,
-                                                     out.begin() + (size_t)g * s + cnt[g]);
-                    }
-            };
-            std::vector<std::thread> cp;
-            const size_t ncp = all.size() < 1024 ? 0 : std::min(7u, std::thread::hardware_concurrency());
-            for (size_t t = 0; t < ncp; t++) cp.emplace_back(copyRefs);
-            copyRefs();
-            for (auto &t : cp) t.join();
-        }
-        phaseMark("reference lists");
-        if (parsed) fpm_seq_free(parsed);
         for (auto &it : items)
             if (it.isSeq) it.refs = std::move(fileRefs[it.file]);
     }

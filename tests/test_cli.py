@@ -23,8 +23,9 @@ REF_MSH = ["DNA1-sketch.msh", "DNA2-sketch.msh", "DNA3-sketch.msh", "genome1.fna
            "genome2.fna.msh", "genome3.fna.msh", "read1_2.msh", "reads.msh", "test_sequence.msh"]
 
 
-def run(args, cwd=None, check=True):
-    p = subprocess.run([FPMASH] + args, cwd=cwd, capture_output=True)
+def run(args, cwd=None, check=True, env=None):
+    p = subprocess.run([FPMASH] + args, cwd=cwd, capture_output=True,
+                       env=None if env is None else {**os.environ, **env})
     if check and p.returncode != 0:
         raise AssertionError(f"fpmash {args} failed: {p.stderr.decode()}")
     return p
@@ -139,6 +140,40 @@ def test_sketch_individual_matches_oracle(tmp_path, oracle):
         h = r["hashes64"] if r["hashes64"] is not None else np.zeros(0, np.uint64)
         assert np.array_equal(h, e)
     assert not got["concatenated"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("individual", [False, True])
+def test_sketch_files_over_devices(tmp_path, oracle, individual):
+    """Several input files spread over the devices (contiguous ranges balanced by bytes; three
+    contexts on the one GPU stand in for a node): the .msh is byte-identical to the one-device
+    run, and every sketch equals the oracle's."""
+    from fpmash import datagen
+    names, per_file = [], []
+    for f, (n, L) in enumerate([(1, 40000), (7, 900), (3, 5000), (2, 25), (12, 1500)]):
+        seqs = datagen.family_dna(1, n, L, seed=50 + f)[:n]
+        ids = datagen.lyn2vec_ids(len(seqs))
+        (tmp_path / f"f{f}.fa").write_bytes(datagen.fasta_bytes(seqs, ids))
+        names.append(f"f{f}.fa")
+        per_file.append(seqs)
+    flags = ["-i"] if individual else []
+    run(["sketch"] + flags + ["-o", "one"] + names, cwd=tmp_path, env={"FPMASH_DEVICE_LIST": "0"})
+    run(["sketch"] + flags + ["-o", "many"] + names, cwd=tmp_path,
+        env={"FPMASH_DEVICE_LIST": "0,0,0"})
+    one = (tmp_path / "one.msh").read_bytes()
+    assert (tmp_path / "many.msh").read_bytes() == one
+    got = mshfmt.read_msh(one)["references"]
+    if individual:
+        exp = oracle.sketch_batch(oracle.params(), [s for seqs in per_file for s in seqs
+                                                    if len(s) >= 21])
+    else:
+        flat = [s for seqs in per_file for s in seqs]
+        groups = [f for f, seqs in enumerate(per_file) for _ in seqs]
+        exp = oracle.sketch_batch(oracle.params(), flat, groups=groups, n_groups=len(per_file))
+    assert len(got) == len(exp)
+    for r, e in zip(got, exp):
+        h = r["hashes64"] if r["hashes64"] is not None else np.zeros(0, np.uint64)
+        assert np.array_equal(h, e)
 
 
 def c2_fasta(n=10000, seed=1000):
