@@ -463,6 +463,10 @@ struct fpm_sketch_job {
     MergeDesc *d_sfmerge = nullptr;
     std::vector<uint32_t> sfround_begin;
     std::vector<uint8_t> sfround_small;
+    // -M pass (allocated on first use)
+    uint32_t *d_mult = nullptr;
+    unsigned long long *d_first = nullptr;
+    uint64_t *d_ttop = nullptr;
 };
 
 static void job_release(fpm_sketch_job *j)
@@ -477,6 +481,7 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
     (void)hipFree(j->d_fb_rows); (void)hipFree(j->d_fb_count);
+    (void)hipFree(j->d_mult); (void)hipFree(j->d_first); (void)hipFree(j->d_ttop);
     if (j->h_sel_failed) (void)hipHostFree(j->h_sel_failed);
 }
 
@@ -610,6 +615,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         }
     }
     close();
+    for (size_t t = 0; t < tiles.size(); t++) tiles[t].pad = tile_group[t];
 
     // rows: single-tile groups write their final row, others get temp rows
     std::vector<uint32_t> ntile_of(n_groups, 0);
@@ -1047,6 +1053,42 @@ int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_co
     if (out_count && job->n_groups)
         HIP_TRY(hipMemcpy(out_count, job->d_count, (size_t)job->n_groups * sizeof(uint32_t),
                           hipMemcpyDeviceToHost));
+    return FPM_OK;
+}
+
+int fpm_sketch_mult(fpm_sketch_job *job, void *stream, uint32_t *out_mult)
+{
+    if (!job) return fail(FPM_EINVAL, "null job");
+    fpm_ctx *ctx = job->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t st = pick_stream(ctx, stream);
+    const uint64_t s = job->kp.s, ng = job->n_groups;
+    if (!ng) return FPM_OK;
+    if (!job->d_mult) {
+        HIP_TRY(hipMalloc(&job->d_mult, ng * s * sizeof(uint32_t)));
+        HIP_TRY(hipMalloc(&job->d_first, ng * s * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc(&job->d_ttop, ng * sizeof(uint64_t)));
+    }
+    HIP_TRY(hipMemsetAsync(job->d_mult, 0, ng * s * sizeof(uint32_t), st));
+    HIP_TRY(hipMemsetAsync(job->d_first, 0xff, ng * s * sizeof(unsigned long long), st));
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 1)
+            HIP_TRY(launch_mult_ttop(job->d_count, job->n_groups, job->kp.s, job->d_first,
+                                     job->d_ttop, st));
+        for (int c = 0; c < kTileClasses; c++) {
+            const uint32_t b = job->class_begin[c], n = job->class_begin[c + 1] - b;
+            if (!n) continue;
+            TimedLaunch tl(ctx, FPM_K_SKETCH, st);
+            HIP_TRY(launch_sketch_mult(c, pass, job->d_seq, job->d_tiles + b, n, job->kp,
+                                       job->d_rows, job->d_count, job->d_mult, job->d_first,
+                                       job->d_ttop, st));
+            tl.done();
+        }
+    }
+    if (out_mult) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(d2h_staged(ctx, out_mult, job->d_mult, ng * s * sizeof(uint32_t)));
+    }
     return FPM_OK;
 }
 

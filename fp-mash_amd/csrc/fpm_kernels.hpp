@@ -16,7 +16,7 @@ struct TileDesc {
     uint32_t n_bytes;
     uint32_t out_row;   // row of the output (or temp) matrix this tile writes
     uint32_t thr_slot;  // 0: keep every hash; i > 0: keep hashes <= thr[i - 1] (long groups)
-    uint32_t pad;
+    uint32_t pad;       // the tile's group (read by the -M multiplicity pass only)
 };
 
 struct SketchKParams {
@@ -53,6 +53,13 @@ constexpr uint32_t kTileCap[kTileClasses] = {256, 512, 1024, 2048, 4096, 8192};
 hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
                                uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_thr,
                                uint64_t *d_out, uint32_t *d_count, hipStream_t st);
+// -M: pass 0 counts / first positions of the final hashes, pass 1 the final maximum up to T_top
+hipError_t launch_sketch_mult(int cls, int pass, const uint8_t *d_seq, const TileDesc *d_tiles,
+                              uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_rows,
+                              const uint32_t *d_count, uint32_t *d_mult,
+                              unsigned long long *d_first, const uint64_t *d_ttop, hipStream_t st);
+hipError_t launch_mult_ttop(const uint32_t *d_count, uint32_t n_groups, uint32_t s,
+                            const unsigned long long *d_first, uint64_t *d_ttop, hipStream_t st);
 // thr[i] = s-th smallest of sample row srow[i] when it holds s hashes, else no bound
 hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
                                    const uint32_t *d_count, uint32_t s, uint64_t *d_thr,

@@ -95,59 +95,42 @@ __device__ __forceinline__ uint32_t compl4(uint32_t x)
     return x ^ (b1 * 0x04u + (b1 ^ 0x01010101u) * 0x15u);
 }
 
-// K != 0: the k-mer size as a compile-time constant (the window loads, tail masks and
-// Murmur's block / tail branches fold); K = 0 reads p.k.
-//
+// LDS layout of one staged tile (the sketch and the multiplicity kernels)
+template <int P>
+struct TileImg {
+    static constexpr int E = P / kBlock;                   // windows per thread (P >= 256)
+    static constexpr int kRcPad = ((E + 15) / 16) * 16;    // R positions of the last thread's
+                                                           // invalid windows stay >= 0
+    static constexpr int kFBytes = ((P + 31 + 15 + 96 + 31) / 32) * 32;   // even # of 16-B chunks
+    static constexpr int kRBytes = ((kRcPad + P + 31 + 15 + 96 + 15) / 16) * 16;
+    static constexpr int kMaskWords = kFBytes / 32 + 2;
+    static constexpr int kBytes = kFBytes + kRBytes + 4 * kMaskWords + 512;   // + alpha, compl
+};
+
 // Byte images in LDS (one 16-B global load per 16 bytes, b128 LDS stores):
 //   F[y]     = tile byte y - a0 (uppercased), a0 = byte_off & 15 (F starts on the 16-B
 //              aligned global address below the tile)
 //   R[z]     = reverse complement: tile byte x (x < n) lands at R[rc0 + n - 1 - x], with rc0
 //              chosen so that F's 16-B chunks land on R's 16-B chunks reversed
 //   bad bit y = F[y] is outside the tile or not in the alphabet
-// Thread t hashes the E consecutive windows i = tE .. tE + E - 1: their bytes are one run of
-// F (and of R, backwards), loaded as ~E/4 + 9 dwords once and cut per window by
-// v_alignbyte with compile-time shifts.
-template <int P, int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? 7 : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
-    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
-    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+// `img` holds TileImg<P>::kBytes; its alphabet / complement tables (the last 512 bytes) are
+// filled and made visible by the caller.
+template <int P>
+__device__ __forceinline__ void tile_stage(const uint8_t *__restrict__ seq, const TileDesc &td,
+                                           const SketchKParams &p, uint32_t *img, int tid)
 {
-    constexpr int E = P / kBlock;                          // windows per thread (P >= 256)
-    constexpr int kRcPad = ((E + 15) / 16) * 16;           // R positions of the last thread's
-                                                           // invalid windows stay >= 0
-    constexpr int kFBytes = ((P + 31 + 15 + 96 + 31) / 32) * 32;   // even number of 16-B chunks
-    constexpr int kRBytes = ((kRcPad + P + 31 + 15 + 96 + 15) / 16) * 16;
-    constexpr int kMaskWords = kFBytes / 32 + 2;
-    // the staging images live inside keys[] (dead before the first key is scattered): 20 KB
-    // of LDS per P = 2048 tile instead of 25.7 KB, 7 tiles per CU instead of 6
-    __shared__ __attribute__((aligned(16))) uint64_t keys[P];
-    static_assert(kFBytes + kRBytes + 4 * kMaskWords + 512 <= 8 * P, "staging fits in keys");
-    uint32_t *const fwd_img = reinterpret_cast<uint32_t *>(keys);
-    uint32_t *const rc_img = fwd_img + kFBytes / 4;
-    uint32_t *const badmask = rc_img + kRBytes / 4;
-    uint8_t *const alpha = reinterpret_cast<uint8_t *>(badmask + kMaskWords);
-    uint8_t *const compl_tab = alpha + 256;
-    __shared__ uint32_t scan_tmp[kWaves + 1];
-    __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
-    __shared__ uint32_t big_bucket, s_cut;
-
-    FPM_PHASE_DECL;
-    FPM_PHASE(0);
-    const TileDesc td = tiles[blockIdx.x];
+    using I = TileImg<P>;
+    uint32_t *const fwd_img = img;
+    uint32_t *const rc_img = fwd_img + I::kFBytes / 4;
+    uint32_t *const badmask = rc_img + I::kRBytes / 4;
+    const uint8_t *const alpha = reinterpret_cast<const uint8_t *>(badmask + I::kMaskWords);
+    const uint8_t *const compl_tab = alpha + 256;
     const uint32_t n = td.n_bytes;
-    const uint32_t k = K ? (uint32_t)K : p.k;
-    const int tid = threadIdx.x;
     const uint32_t a0 = (uint32_t)(td.byte_off & 15);
     const uint8_t *g0 = seq + (td.byte_off - a0);
     const uint32_t nimg = a0 + n;                          // F bytes holding tile data
-    const uint32_t rc0 = kRcPad + ((16u - (nimg & 15u)) & 15u);
-
-    alpha[tid] = p.alphabet[tid];
-    compl_tab[tid] = p.complement[tid];
-    __syncthreads();
-
-    // ---- stage the tile: uppercase, validity bits, reverse complement
-    constexpr int kChunks = kFBytes / 16;
+    const uint32_t rc0 = I::kRcPad + ((16u - (nimg & 15u)) & 15u);
+    constexpr int kChunks = I::kFBytes / 16;
     for (int ch = tid; ch < kChunks; ch += kBlock) {
         const uint32_t y0 = (uint32_t)ch * 16;
         uint4 v = make_uint4(0, 0, 0, 0);
@@ -192,18 +175,36 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
         const uint32_t hi = __shfl_down(bad, 1, 64);
         if ((ch & 1) == 0) badmask[ch / 2] = bad | (hi << 16);
     }
-    if (tid < 2) badmask[kMaskWords - 2 + tid] = 0xffffffffu;
-    __syncthreads();
-    FPM_PHASE(1);
+    if (tid < 2) badmask[I::kMaskWords - 2 + tid] = 0xffffffffu;
+}
 
-    // ---- hash this thread's E consecutive windows
+// K != 0: the k-mer size as a compile-time constant (the window loads, tail masks and
+// Murmur's block / tail branches fold); K = 0 reads p.k.
+// Thread t hashes the E consecutive windows i = tE .. tE + E - 1 of the staged tile: their
+// bytes are one run of F (and of R, backwards), loaded as ~E/4 + 9 dwords once and cut per
+// window by v_alignbyte with compile-time shifts.  Returns bit e set when kr[e] is the hash
+// of a valid k-mer (kr[e] = ~0 otherwise).
+template <int P, int K>
+__device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKParams &p,
+                                              const uint32_t *img, int tid,
+                                              uint64_t (&kr)[TileImg<P>::E])
+{
+    using I = TileImg<P>;
+    constexpr int E = I::E;
+    const uint32_t *const fwd_img = img;
+    const uint32_t *const rc_img = fwd_img + I::kFBytes / 4;
+    const uint32_t *const badmask = rc_img + I::kRBytes / 4;
+    const uint32_t n = td.n_bytes;
+    const uint32_t k = K ? (uint32_t)K : p.k;
+    const uint32_t a0 = (uint32_t)(td.byte_off & 15);
+    const uint32_t nimg = a0 + n;
+    const uint32_t rc0 = I::kRcPad + ((16u - (nimg & 15u)) & 15u);
     const uint32_t nk = n >= k ? n - k + 1 : 0;
     const int nw = (k + 3) >> 2;                           // dwords per k-mer
     const uint32_t tail_mask = (k & 3) ? ((1u << (8 * (k & 3))) - 1u) : 0xffffffffu;
     const uint32_t kmask = (k == 32) ? 0xffffffffu : ((1u << k) - 1u);
     constexpr int KW = K ? (K + 3) / 4 : 8;                // dwords per window (max)
     constexpr int W = (E + 3) / 4 + KW + 1;                // dwords covering the E windows
-    uint64_t kr[E];                                        // key of window tE + e
     uint32_t vbits = 0;                                    // bit e: kr[e] is a valid k-mer hash
     const uint32_t i0 = (uint32_t)tid * E;
 #pragma unroll
@@ -287,6 +288,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
             vbits = okbits;
         }
     }
+    return vbits;
+}
+
+template <int P, int K>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? 7 : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
+    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+{
+    using I = TileImg<P>;
+    constexpr int E = I::E;
+    // the staging images live inside keys[] (dead before the first key is scattered): 20 KB
+    // of LDS per P = 2048 tile instead of 25.7 KB, 7 tiles per CU instead of 6
+    __shared__ __attribute__((aligned(16))) uint64_t keys[P];
+    static_assert(I::kBytes <= 8 * P, "staging fits in keys");
+    uint32_t *const img = reinterpret_cast<uint32_t *>(keys);
+    uint8_t *const alpha = reinterpret_cast<uint8_t *>(img + (I::kFBytes + I::kRBytes) / 4 +
+                                                       I::kMaskWords);
+    uint8_t *const compl_tab = alpha + 256;
+    __shared__ uint32_t scan_tmp[kWaves + 1];
+    __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
+    __shared__ uint32_t big_bucket, s_cut;
+
+    FPM_PHASE_DECL;
+    FPM_PHASE(0);
+    const TileDesc td = tiles[blockIdx.x];
+    const int tid = threadIdx.x;
+
+    alpha[tid] = p.alphabet[tid];
+    compl_tab[tid] = p.complement[tid];
+    __syncthreads();
+
+    // ---- stage the tile: uppercase, validity bits, reverse complement
+    tile_stage<P>(seq, td, p, img, tid);
+    __syncthreads();
+    FPM_PHASE(1);
+
+    // ---- hash this thread's E consecutive windows
+    uint64_t kr[E];                                        // key of window tE + e
+    uint32_t vbits = tile_hash<P, K>(td, p, img, tid, kr);
 
     // ---- long groups: keep only hashes <= the group's bound (the s-th smallest hash of a
     // sample of the group's tiles, an upper bound of the group's own s-th smallest)
@@ -557,6 +597,129 @@ hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_
     case 5: return launch_p<8192>(d_seq, d_tiles, n_tiles, p, d_thr, d_out, d_count, st);
     default: return hipErrorInvalidValue;
     }
+}
+
+// ---- -M multiplicities: the counts MinHashHeap keeps beside its hashes (MinHashHeap.cpp:68-146,
+// multiplicityMinimum 1; written with -M, Sketch.cpp:584-596).  A hash of the final sketch is
+// never evicted once inserted (an evicted hash has s smaller ones that stay), so its count is
+// every occurrence from its first one on -- except the final maximum M of a full sketch: once
+// the heap holds exactly the final set (position T_top = the last first-occurrence among
+// the final hashes) M is the heap's top and tryInsert rejects it (`hash < top` fails, :73).
+//   pass 0: each window hashing into its group's sketch adds 1 to its count (not M of a full
+//           sketch) and takes the min of its position into first[]
+//   pass 1: windows hashing to M of a full sketch at positions <= T_top add 1 to M's count
+// Position = the window's byte offset in the staged buffer (a group's records are laid out in
+// stream order).  Tiles carry their group in TileDesc::pad.
+__device__ __forceinline__ uint32_t lower_bound_row(const uint64_t *__restrict__ v, uint32_t n,
+                                                    uint64_t x)
+{
+    uint32_t lo = 0;
+    while (n) {
+        const uint32_t h = n >> 1;
+        if (v[lo + h] < x) { lo += h + 1; n -= h + 1; }
+        else n = h;
+    }
+    return lo;
+}
+
+template <int P>
+__global__ __launch_bounds__(kBlock) void sketch_mult_kernel(
+    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
+    const uint64_t *__restrict__ rows, const uint32_t *__restrict__ count, int pass,
+    uint32_t *__restrict__ mult, unsigned long long *__restrict__ first,
+    const uint64_t *__restrict__ ttop)
+{
+    using I = TileImg<P>;
+    constexpr int E = I::E;
+    __shared__ __attribute__((aligned(16))) uint32_t img[I::kBytes / 4];
+    uint8_t *const alpha = reinterpret_cast<uint8_t *>(img + (I::kFBytes + I::kRBytes) / 4 +
+                                                       I::kMaskWords);
+    uint8_t *const compl_tab = alpha + 256;
+    const TileDesc td = tiles[blockIdx.x];
+    const uint32_t g = td.pad;
+    const uint32_t ng = count[g];
+    const bool full = ng >= p.s;
+    // block-uniform exits
+    if (ng == 0) return;
+    if (pass == 1 && (!full || td.byte_off > ttop[g])) return;
+    const int tid = threadIdx.x;
+    alpha[tid] = p.alphabet[tid];
+    compl_tab[tid] = p.complement[tid];
+    __syncthreads();
+    tile_stage<P>(seq, td, p, img, tid);
+    __syncthreads();
+    uint64_t kr[E];
+    const uint32_t vbits = tile_hash<P, 0>(td, p, img, tid, kr);
+    const uint64_t *row = rows + (uint64_t)g * p.s;
+    const uint64_t hmax = row[ng - 1];
+    uint32_t *mrow = mult + (uint64_t)g * p.s;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        if (!(vbits >> e & 1) || kr[e] > hmax) continue;
+        const uint64_t pos = td.byte_off + (uint64_t)tid * E + e;
+        if (pass == 0) {
+            const uint32_t i = lower_bound_row(row, ng, kr[e]);
+            if (row[i] != kr[e]) continue;
+            if (!(full && i == ng - 1)) atomicAdd(&mrow[i], 1u);
+            atomicMin(&first[(uint64_t)g * p.s + i], (unsigned long long)pos);
+        } else if (kr[e] == hmax && pos <= ttop[g]) {
+            atomicAdd(&mrow[ng - 1], 1u);
+        }
+    }
+}
+
+// T_top of each full group: the largest first-occurrence position among its hashes
+__global__ __launch_bounds__(kBlock) void mult_ttop_kernel(const uint32_t *__restrict__ count,
+                                                         uint32_t n_groups, uint32_t s,
+                                                         const unsigned long long *__restrict__ first,
+                                                         uint64_t *__restrict__ ttop)
+{
+    __shared__ unsigned long long red[kWaves];
+    const uint32_t g = blockIdx.x;
+    if (g >= n_groups) return;
+    const uint32_t ng = count[g];
+    unsigned long long m = 0;
+    for (uint32_t i = threadIdx.x; i < ng; i += kBlock) m = max(m, first[(uint64_t)g * s + i]);
+    for (int o = 32; o; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kWaves; w++) m = max(m, red[w]);
+        ttop[g] = m;
+    }
+}
+
+hipError_t launch_sketch_mult(int cls, int pass, const uint8_t *d_seq, const TileDesc *d_tiles,
+                              uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_rows,
+                              const uint32_t *d_count, uint32_t *d_mult,
+                              unsigned long long *d_first, const uint64_t *d_ttop, hipStream_t st)
+{
+    if (n_tiles == 0) return hipSuccess;
+#define FPM_MULT_CASE(c, P)                                                                    \
+    case c:                                                                                    \
+        hipLaunchKernelGGL((sketch_mult_kernel<P>), dim3(n_tiles), dim3(kBlock), 0, st, d_seq,  \
+                           d_tiles, p, d_rows, d_count, pass, d_mult, d_first, d_ttop);         \
+        break;
+    switch (cls) {
+        FPM_MULT_CASE(0, 256)
+        FPM_MULT_CASE(1, 512)
+        FPM_MULT_CASE(2, 1024)
+        FPM_MULT_CASE(3, 2048)
+        FPM_MULT_CASE(4, 4096)
+        FPM_MULT_CASE(5, 8192)
+    default: return hipErrorInvalidValue;
+    }
+#undef FPM_MULT_CASE
+    return hipGetLastError();
+}
+
+hipError_t launch_mult_ttop(const uint32_t *d_count, uint32_t n_groups, uint32_t s,
+                            const unsigned long long *d_first, uint64_t *d_ttop, hipStream_t st)
+{
+    if (n_groups == 0) return hipSuccess;
+    hipLaunchKernelGGL(mult_ttop_kernel, dim3(n_groups), dim3(kBlock), 0, st, d_count, n_groups,
+                       s, d_first, d_ttop);
+    return hipGetLastError();
 }
 
 __global__ void sketch_threshold_kernel(const uint32_t *__restrict__ srow, uint32_t n_slots,

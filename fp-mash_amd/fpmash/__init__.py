@@ -69,6 +69,7 @@ SYMBOLS = [
     ("fpm_sketch_run", C.c_int, [vp, vp]),
     ("fpm_sketch_device_output", C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), u32p, u32p]),
     ("fpm_sketch_fetch", C.c_int, [vp, u64p, u32p]),
+    ("fpm_sketch_mult", C.c_int, [vp, vp, u32p]),
     ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
     ("fpm_sketch_job_free", None, [vp]),
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
@@ -278,6 +279,13 @@ class SketchJob:
         _check(lib().fpm_sketch_fetch(self.h, _p(out, u64p), _p(cnt, u32p)))
         return out[: self.n_groups * s].reshape(self.n_groups, s), cnt[: self.n_groups]
 
+    def mult(self, stream=None):
+        """-M: fpm_sketch_mult -> [n_groups, s] u32 multiplicities (after run())."""
+        s = int(self.params.sketch_size)
+        out = np.zeros(max(self.n_groups, 1) * s, dtype=np.uint32)
+        _check(lib().fpm_sketch_mult(self.h, stream, _p(out, u32p)))
+        return out[: self.n_groups * s].reshape(self.n_groups, s)
+
     def free(self):
         if self.h:
             lib().fpm_sketch_job_free(self.h)
@@ -337,15 +345,20 @@ class Context:
         return {"sparse": sp.value, "events": ev.value, "candidates": ca.value}
 
     # --- sketch -----------------------------------------------------------
-    def sketch(self, params, seqs, groups=None, n_groups=None):
-        """-> list of ascending u64 arrays (one per sketch)."""
+    def sketch(self, params, seqs, groups=None, n_groups=None, counts=False):
+        """-> list of ascending u64 arrays (one per sketch); counts=True (-M): also the list
+        of their u32 multiplicities."""
         job = SketchJob(self, params, seqs, groups, n_groups)
         try:
             job.run()
             rows, cnt = job.fetch()
+            mult = job.mult() if counts else None
         finally:
             job.free()
-        return [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+        hashes = [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+        if counts:
+            return hashes, [mult[i, : cnt[i]].copy() for i in range(len(cnt))]
+        return hashes
 
     def sketch_job(self, params, seqs, groups=None, n_groups=None):
         return SketchJob(self, params, seqs, groups, n_groups)
@@ -372,7 +385,7 @@ class Context:
         return job.value, {"seg": seg[:n], "hdr_off": ho[:n], "hdr_len": hl[:n],
                            "seq_len": sl[:n]}, bool(q.value)
 
-    def sketch_seq(self, params, seq_job, groups, n_groups):
+    def sketch_seq(self, params, seq_job, groups, n_groups, counts=False):
         """fpm_sketch_stage_seq + run + fetch over parsed records (the job takes the packed
         records; free the parse handle with seq_free afterwards)."""
         g = np.ascontiguousarray(groups, dtype=np.uint32)
@@ -386,9 +399,13 @@ class Context:
         try:
             job.run()
             rows, cnt = job.fetch()
+            mult = job.mult() if counts else None
         finally:
             job.free()
-        return [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+        hashes = [rows[i, : cnt[i]].copy() for i in range(len(cnt))]
+        if counts:
+            return hashes, [mult[i, : cnt[i]].copy() for i in range(len(cnt))]
+        return hashes
 
     @staticmethod
     def seq_free(seq_job):

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <iostream>
+#include <map>
 
 namespace fpmhost {
 
@@ -58,9 +59,25 @@ int CommandInfo::run() const
         referenceCount = sketch.getReferenceCount();
     }
     if (counts) {
-        std::cerr << "ERROR: Sketch file does not have hash counts. Re-sketch with -M to use this "
-                     "feature." << std::endl;
-        return 1;
+        // printCounts (CommandInfo.cpp:225-262): per sketch, the histogram of its counts
+        if (sketch.getReferenceCount() == 0) {
+            std::cerr << "ERROR: Sketch file contains no sketches." << std::endl;
+            return 1;
+        }
+        if (!sketch.hasHashCounts()) {
+            std::cerr << "ERROR: Sketch file does not have hash counts. Re-sketch with -M to use "
+                         "this feature." << std::endl;
+            return 1;
+        }
+        std::cout << "#Sketch\tBin\tFrequency" << std::endl;
+        for (uint64_t i = 0; i < sketch.getReferenceCount(); i++) {
+            const Reference &r = sketch.getReference(i);
+            std::map<uint32_t, uint64_t> histogram;
+            for (uint32_t c : r.counts) histogram[c]++;
+            for (auto &e : histogram)
+                std::cout << r.name << '\t' << e.first << '\t' << e.second << std::endl;
+        }
+        return 0;
     }
     std::string alphabet;
     sketch.getAlphabetAsString(alphabet);
@@ -92,6 +109,16 @@ int CommandInfo::run() const
                 std::cout << std::endl;
             }
             std::cout << "      ]" << std::endl;
+            if (r.countsSorted) {
+                // no comma after the hashes list (CommandInfo.cpp:310-325): not valid JSON
+                std::cout << "      \"counts\" :" << std::endl << "      [" << std::endl;
+                for (size_t j = 0; j < r.counts.size(); j++) {
+                    std::cout << "        " << r.counts[j];
+                    if (j + 1 < r.counts.size()) std::cout << ',';
+                    std::cout << std::endl;
+                }
+                std::cout << "      ]" << std::endl;
+            }
             std::cout << (i + 1 < sketch.getReferenceCount() ? "    }," : "    }") << std::endl;
         }
         std::cout << "  ]" << std::endl << "}" << std::endl;

@@ -47,10 +47,6 @@ int CommandSketch::run() const
     const bool fingerprint = options.at("fingerprint").active;
     Parameters parameters;
     parameters.counts = options.at("counts").active;
-    if (parameters.counts) {
-        std::cerr << "ERROR: -M (k-mer multiplicities) is not supported by fpmash." << std::endl;
-        return 1;
-    }
     if (sketchParameterSetup(parameters, *this)) return 1;
     std::vector<std::string> files;
     for (const auto &a : arguments) {

@@ -164,6 +164,7 @@ static void loadMsh(const std::string &file, const Parameters &p, std::vector<Re
         r.length = m.length;
         r.hashes = std::move(m.hashes);
         r.counts = std::move(m.counts);
+        r.countsSorted = m.countsSorted;
         out.push_back(std::move(r));
     }
 }
@@ -345,6 +346,12 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
         }
         int rc = fpm_sketch_run(job, nullptr);
         if (rc == FPM_OK) rc = fpm_sketch_fetch(job, out.data(), cnt.data());
+        // -M: the heap's multiplicities (Sketch.cpp:584-596)
+        std::vector<uint32_t> mult;
+        if (rc == FPM_OK && parameters.counts) {
+            mult.resize((size_t)nGroups * s);
+            rc = fpm_sketch_mult(job, nullptr, mult.data());
+        }
         fpm_sketch_job_free(job);
         check(rc, "sketch");
         mark("device sketch (stage + run + fetch)");
@@ -358,8 +365,13 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
                 for (size_t x = a; x < std::min(all.size(), a + 256); x++) {
                     const size_t f = all[x].first, i = all[x].second;
                     const uint32_t g = fileGroups[f][i];
-                    fileRefs[f0 + f][i].hashes.assign(out.begin() + (size_t)g * s,
-                                                 out.begin() + (size_t)g * s + cnt[g]);
+                    Reference &ref = fileRefs[f0 + f][i];
+                    ref.hashes.assign(out.begin() + (size_t)g * s, out.begin() + (size_t)g * s + cnt[g]);
+                    if (!mult.empty()) {
+                        ref.counts.assign(mult.begin() + (size_t)g * s,
+                                          mult.begin() + (size_t)g * s + cnt[g]);
+                        ref.countsSorted = true;
+                    }
                 }
         };
         std::vector<std::thread> cp;

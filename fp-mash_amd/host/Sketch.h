@@ -40,7 +40,8 @@ struct Reference {
     std::string comment;
     uint64_t length = 0;
     std::vector<uint64_t> hashes;   // hashesSorted (u32 values zero-extended when !use64)
-    std::vector<uint32_t> counts;
+    std::vector<uint32_t> counts;   // -M multiplicities (counts32)
+    bool countsSorted = false;
 };
 
 class Sketch {

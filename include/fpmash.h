@@ -134,6 +134,12 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream);
 int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,
                              uint32_t *n_groups, uint32_t *row_stride);
 int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_count);
+/* -M: the multiplicity of every hash of the final sketches, as MinHashHeap counts them
+ * (MinHashHeap.cpp:68-146 with multiplicityMinimum 1: occurrences from a hash's first one on;
+ * the final maximum of a full sketch stops counting once the heap holds the final set), the
+ * counts32 that sketch -M writes (Sketch.cpp:584-596).  After run() on the same stream;
+ * out_mult: n_groups x sketch_size u32, row g's first out_count[g] entries in hash order. */
+int fpm_sketch_mult(fpm_sketch_job *job, void *stream, uint32_t *out_mult);
 /* bytes the run() kernels read + write by algorithm (for roofline accounting) */
 int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_tiles,
                         uint64_t *n_kmers);

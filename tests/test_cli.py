@@ -69,6 +69,22 @@ def test_info_tabular_and_header():
     assert "Sketches:                      5" in hdr
 
 
+def test_info_counts_histogram_and_dump():
+    """info -c (printCounts, CommandInfo.cpp:225-262) and the counts block of info -d on the
+    reference's counted sketch reads.msh; -c on a sketch without counts fails as the reference's."""
+    h = mshfmt.read_msh(os.path.join(GOLDEN, "reads.msh"))["references"][0]
+    vals, freq = np.unique(h["counts"], return_counts=True)
+    exp = "#Sketch\tBin\tFrequency\n" + "".join(f"reads\t{v}\t{f}\n" for v, f in zip(vals, freq))
+    assert run(["info", "-c", os.path.join(GOLDEN, "reads.msh")]).stdout.decode() == exp
+    d = run(["info", "-d", os.path.join(GOLDEN, "reads.msh")]).stdout.decode()
+    tail = d[d.index('      "counts" :\n'):]
+    body = tail[tail.index("[\n") + 2:tail.index("      ]")]
+    assert [int(x.strip().rstrip(",")) for x in body.splitlines()] == list(h["counts"])
+    assert d.index('      "counts" :') > d.index('      "hashes" :')
+    p = run(["info", "-c", os.path.join(GOLDEN, "DNA1-sketch.msh")], check=False)
+    assert p.returncode == 1 and b"does not have hash counts" in p.stderr
+
+
 def test_cli_fails_loudly_without_device():
     import fpmash
     if fpmash.device_count() > 0:
@@ -174,6 +190,50 @@ def test_sketch_files_over_devices(tmp_path, oracle, individual):
     for r, e in zip(got, exp):
         h = r["hashes64"] if r["hashes64"] is not None else np.zeros(0, np.uint64)
         assert np.array_equal(h, e)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("individual", [False, True])
+def test_sketch_counts_M(tmp_path, oracle, individual):
+    """`sketch -M`: counts32 of every sketch == the oracle heap's multiplicities, and the file
+    is the byte layout of the pinned encoder (mshfmt.write_msh reproduces the counted fixture
+    reads.msh); `info -c` prints their histograms."""
+    from fpmash import datagen
+    rng = np.random.default_rng(5)
+    unit = datagen.family_dna(1, 1, 300, seed=4)[0]
+    per_file = [datagen.family_dna(1, 3, 4000, seed=7) + [unit * 9],
+                [unit * 3 + datagen.family_dna(1, 1, 900, seed=8)[0]],
+                datagen.family_dna(2, 4, 1500, seed=9)]
+    names = []
+    for f, seqs in enumerate(per_file):
+        ids = datagen.lyn2vec_ids(len(seqs), seed=f)
+        (tmp_path / f"m{f}.fa").write_bytes(datagen.fasta_bytes(seqs, ids))
+        names.append(f"m{f}.fa")
+    flags = ["-i"] if individual else []
+    run(["sketch", "-M", "-s", "500"] + flags + ["-o", "m"] + names, cwd=tmp_path)
+    data = (tmp_path / "m.msh").read_bytes()
+    h = mshfmt.read_msh(data)
+    got = h["references"]
+    O = oracle.params(k=21, s=500)
+    if individual:
+        flat = [s for seqs in per_file for s in seqs]
+        eh, ec = oracle.sketch_batch(O, flat, counts=True)
+    else:
+        flat = [s for seqs in per_file for s in seqs]
+        groups = [f for f, seqs in enumerate(per_file) for _ in seqs]
+        eh, ec = oracle.sketch_batch(O, flat, groups=groups, n_groups=len(per_file), counts=True)
+    assert len(got) == len(eh)
+    for r, a, c in zip(got, eh, ec):
+        assert np.array_equal(r["hashes64"], a)
+        assert np.array_equal(r["counts"], c)
+        assert r["countsSorted"]
+    assert any(c.max() > 1 for c in ec)
+    refs = [dict(name=r["name"], comment=r["comment"], length=r["length"], hashes=r["hashes64"],
+                 counts=r["counts"]) for r in got]
+    assert mshfmt.write_msh(h, refs, use64=True, counts=True) == data
+    out = run(["info", "-c", str(tmp_path / "m.msh")]).stdout.decode().splitlines()
+    assert out[0] == "#Sketch\tBin\tFrequency"
+    assert len(out) - 1 == sum(len(np.unique(c)) for c in ec)
 
 
 def c2_fasta(n=10000, seed=1000):
@@ -388,12 +448,15 @@ def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("block_pairs,to_file", [(None, False), ("50000", False), (None, True),
-                                                ("50000", True)])
-def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file):
+@pytest.mark.parametrize("block_pairs,to_file,devices",
+                         [(None, False, None), ("50000", False, None), (None, True, None),
+                          ("50000", True, None), ("50000", False, "0,0"), ("50000", True, "0,0,0")])
+def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file, devices):
     """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
     blocks of 50,000 pairs (FPMASH_DIST_BLOCK_PAIRS) written by the formatter threads in
-    order: every line equals the oracle's, in the reference's query-major order."""
+    order: every line equals the oracle's, in the reference's query-major order.  With
+    FPMASH_DEVICE_LIST the blocks go round the contexts (2-3 on the one GPU standing in for
+    a node's devices)."""
     from fpmash import datagen
     seqs = datagen.family_dna(12, 100, 2000, sub_rate=(0.01, 0.10), seed=23)
     ids = datagen.lyn2vec_ids(len(seqs), seed=23)
@@ -402,6 +465,8 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file)
     env = dict(os.environ)
     if block_pairs:
         env["FPMASH_DIST_BLOCK_PAIRS"] = block_pairs
+    if devices:
+        env["FPMASH_DEVICE_LIST"] = devices
     if to_file:
         # stdout a regular file: the pieces are pwrite()n at their offsets by the formatter
         # threads; the file starts with bytes already written (the offsets start after them)

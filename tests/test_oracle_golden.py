@@ -112,6 +112,23 @@ def test_reads_fixture_sketch(oracle):
         assert e["comment"].startswith(b"[%d seqs] " % len(seqs))
 
 
+def test_reads_counts_fixture(oracle):
+    """reads.msh (`mash sketch -r -I reads reads1.fastq reads2.fastq`, minCov 1): the reference's
+    only counted sketch.  The oracle heap's counts (the -M multiplicities, MinHashHeap.cpp:68-146)
+    over both files' records, streamed alternately (sketchFile's round robin, Sketch.cpp:
+    1411-1419), equal its counts32; so do the counts of the two files streamed one after the
+    other (the counts here do not depend on the order)."""
+    exp = mshfmt.read_msh(os.path.join(GOLDEN, "reads.msh"))["references"][0]
+    a = [r[2] for r in seqio.read_records(os.path.join(GOLDEN, "reads1.fastq.gz"))]
+    b = [r[2] for r in seqio.read_records(os.path.join(GOLDEN, "reads2.fastq.gz"))]
+    P = oracle.params(k=21, s=1000)
+    for recs in ([x for pair in zip(a, b) for x in pair], a + b):
+        h, c = oracle.sketch_batch(P, recs, groups=[0] * len(recs), n_groups=1, counts=True)
+        assert np.array_equal(h[0], exp["hashes64"])
+        assert np.array_equal(c[0], exp["counts"])
+    assert exp["countsSorted"]
+
+
 def test_test_sequence_fixture(oracle):
     exp = mshfmt.read_msh(os.path.join(GOLDEN, "test_sequence.msh"))
     recs = seqio.read_records(os.path.join(GOLDEN, "test_sequence.fasta"))
