@@ -81,6 +81,9 @@ struct fpm_ctx {
     // FPM_FILL_EARLY=1 (A/B): the fill starts on the side stream with the index build instead
     // of after the probe
     bool fill_early = false;
+    bool fill_pre_probe = false;   // FPM_FILL_AT=probe: the side fill starts with the probe
+    int fill_counts = -1;      // the side-stream fill also writes the numer / denom defaults
+                               // (-1: for grids of >= 2^28 pairs; FPM_FILL_COUNTS=0/1 forces)
     int last_sparse = 0;
     uint64_t last_events = 0, last_cand = 0;
     const unsigned long long *last_cand_dev = nullptr;   // the last sparse call's counter
@@ -264,6 +267,8 @@ int fpm_ctx_create(int device, fpm_ctx **out)
     if (const char *v = getenv("FPM_DENSE_IMG")) ctx->dense_img = atoi(v) != 0;
     if (const char *v = getenv("FPM_FILL_SERIAL")) ctx->fill_serial = atoi(v) != 0;
     if (const char *v = getenv("FPM_FILL_EARLY")) ctx->fill_early = atoi(v) != 0;
+    if (const char *v = getenv("FPM_FILL_COUNTS")) ctx->fill_counts = atoi(v) != 0 ? 1 : 0;
+    if (const char *v = getenv("FPM_FILL_AT")) ctx->fill_pre_probe = strcmp(v, "probe") == 0;
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1662,7 +1667,14 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
     bool fill_pending = false;
-    // the fill of every cell's no-shared-hash values on the side stream (see below)
+    // the fill of every cell's no-shared-hash values on the side stream (see below); with
+    // fill_cnt it writes the numer / denom defaults too and the probe writes none: the probe
+    // (event reads, latency-bound, slowed ~3x by any write stream beside it) gets shorter and
+    // the bytes move to the fill beside the rank kernel.
+    // Measured (same box): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 % (the
+    // heavier fill beside the rank kernel costs more than the probe saves), so by grid size.
+    const bool fill_cnt = fin && !fin->prefilled &&
+                          (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0);
     auto launch_fill = [&]() -> int {
         PairFill fill;
         fill.dist = fin->dist;
@@ -1674,8 +1686,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         HIP_TRY(hipEventRecord(ctx->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size, Counts{}, fill,
-                                 ctx->aux));
+        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size,
+                                 fill_cnt ? cnt : Counts{}, fill, ctx->aux));
         tl.done();
         HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
         fill_pending = true;
@@ -1823,11 +1835,13 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // The rank kernel then leaves the grid alone (results per candidate slot), and the
             // candidate finalize, after the fill, scatters them; the literal walk writes cells
             // in place, so it waits for the fill instead.
+            if (fin && !fin->prefilled && ctx->fill_pre_probe && !fill_pending)
+                if (int rc = launch_fill()) return rc;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
-                                          geom, dir, entries, d_ref_len, sketch_size, sym, true,
-                                          self_set, cnt, (uint64_t *)cand, n_cand,
+                                          geom, dir, entries, d_ref_len, sketch_size, sym,
+                                          !fill_cnt, self_set, cnt, (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, p_qry_it, st));
                 tl.done();
             }
