@@ -12,6 +12,8 @@
 #include "fpm_device.hpp"
 #include "fpm_kernels.hpp"
 
+#include <cstdlib>
+
 #include <float.h>
 
 #include <algorithm>
@@ -837,7 +839,11 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
                      al(fill.pass, 4);
     // the full grid: short workgroups hand their slots back to the candidate compare running
     // beside; a capped grid-stride fill (256-4096 workgroups) held them and measured slower
-    const uint32_t grid = (uint32_t)blocks;
+    static const uint64_t kGridCap = [] {
+        const char *v = getenv("FPM_FILL_GRID");   // A/B: cap the grid (grid-stride loop)
+        return v ? strtoull(v, nullptr, 10) : 0ULL;
+    }();
+    const uint32_t grid = (uint32_t)(kGridCap && blocks > kGridCap ? kGridCap : blocks);
 #define FPM_FILL(V, C)                                                                         \
     hipLaunchKernelGGL((dist_fill_kernel<V, C>), dim3(grid), dim3(256), 0, st, d_ref_len, n_ref, \
                        d_qry_len, nrb, (uint32_t)blocks, S, (C *)d_numer, (C *)d_denom, fill)

@@ -91,6 +91,10 @@ struct fpm_ctx {
     // side stream for the sparse dist's fill (a pure write stream that runs beside the
     // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
+    // FPM_FILL_CUS=n (A/B): the side fill on n CUs of its own (CU-masked aux stream) and the
+    // candidate compare on the others (cmp, the complementary mask)
+    hipStream_t cmp = nullptr;
+    hipEvent_t ev_cmp0 = nullptr, ev_cmp1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
     hipEvent_t ev_prefill = nullptr;       // end of the last fpm_dist_prefill_dev
     // pinned staging ring for host -> device copies of pageable caller memory
@@ -178,7 +182,29 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
     if (ctx->aux) return hipSuccess;
     // default priority: a low-priority side stream (or a high-priority main one) measured
     // slower, the fill then trails the candidate compare instead of sharing its CUs
-    hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    static const int kFillCus = [] {
+        const char *v = getenv("FPM_FILL_CUS");
+        return v ? atoi(v) : 0;
+    }();
+    hipError_t e = hipSuccess;
+    int ncu = 0;
+    if (kFillCus > 0) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    if (e == hipSuccess && kFillCus > 0 && kFillCus < ncu) {
+        // the fill's CUs spread evenly over the CU index space (over the XCDs / shader arrays)
+        std::vector<uint32_t> m((ncu + 31) / 32, 0), c((ncu + 31) / 32, 0);
+        for (int i = 0; i < kFillCus; i++) {
+            const int b = (int)((int64_t)i * ncu / kFillCus);
+            m[b / 32] |= 1u << (b % 32);
+        }
+        for (int b = 0; b < ncu; b++)
+            if (!(m[b / 32] >> (b % 32) & 1)) c[b / 32] |= 1u << (b % 32);
+        e = hipExtStreamCreateWithCUMask(&ctx->aux, (uint32_t)m.size(), m.data());
+        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&ctx->cmp, (uint32_t)c.size(), c.data());
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_cmp0, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_cmp1, hipEventDisableTiming);
+    } else if (e == hipSuccess) {
+        e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
+    }
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming);
     return e;
@@ -289,6 +315,9 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->host_counters) (void)hipHostFree(ctx->host_counters);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->cmp) (void)hipStreamDestroy(ctx->cmp);
+    if (ctx->ev_cmp0) (void)hipEventDestroy(ctx->ev_cmp0);
+    if (ctx->ev_cmp1) (void)hipEventDestroy(ctx->ev_cmp1);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
     if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
@@ -1866,19 +1895,30 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             if (fill_pending && (!cnum || ctx->fill_serial))
                 HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             {
-                TimedLaunch tl(ctx, FPM_K_COMPARE, st);
+                // FPM_FILL_CUS: the compare on the CUs the fill does not own
+                const bool on_cmp = ctx->cmp && rows_merge && fill_pending && cnum;
+                hipStream_t cs = on_cmp ? ctx->cmp : st;
+                if (on_cmp) {
+                    HIP_TRY(hipEventRecord(ctx->ev_cmp0, st));
+                    HIP_TRY(hipStreamWaitEvent(cs, ctx->ev_cmp0, 0));
+                }
+                TimedLaunch tl(ctx, FPM_K_COMPARE, cs);
                 if (rows_merge)
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
                                               sketch_size, sym, cnt, cnum, cden,
-                                              st));
+                                              cs));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                                                    qry_stride, hash_bytes, sketch_size, cnt,
                                                    st));
                 tl.done();
+                if (on_cmp) {
+                    HIP_TRY(hipEventRecord(ctx->ev_cmp1, cs));
+                    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_cmp1, 0));
+                }
             }
             if (fin && fin->prefilled) {
                 // the walk kernel wrote numer / denom only; distance / p-value / pass of the
