@@ -182,34 +182,55 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     }
 }
 
-// ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits
-constexpr int kBucketThreads = 512;
+// ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits.
+// A partition of up to `cap` entries (C2: ~9.8k of 1e7 / 1024) is read once into registers
+// (16 per thread), counted, scattered into an LDS copy of its entries and written out
+// coalesced; a larger one (C4: ~49k) reads its slice of tent twice and scatters straight to
+// `entries` (the previous form for every partition: tent read twice and the entries written
+// in scattered 4-B pieces, ~2x the algorithmic bytes).
+constexpr int kBucketThreads = 1024;
+constexpr int kBucketPer = 16;                   // entries per thread in registers
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tent, uint32_t ntiles,
-    const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t *__restrict__ dir,
+    const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t cap, uint32_t *__restrict__ dir,
     uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
 {
-    extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors
+    extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors; then cap entries
     __shared__ uint32_t wsum[kBucketThreads / 64];
     __shared__ unsigned long long wsq[kBucketThreads / 64];
     const uint32_t p = blockIdx.x;
     const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
     const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
     const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
+    uint32_t *const out = sh + nsb;
+    const bool in_lds = s1 - s0 <= cap && cap <= (uint32_t)(kBucketThreads * kBucketPer);
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
-    // 4 independent loads in flight per thread
-    constexpr uint32_t kU = 4;
-    for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
-        uint64_t K[kU];
+    uint64_t K[kBucketPer];
+    if (in_lds) {
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++) {
-            const uint32_t e = e0 + u * kBucketThreads;
+        for (int u = 0; u < kBucketPer; u++) {
+            const uint32_t e = s0 + threadIdx.x + u * kBucketThreads;
             K[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
-        for (uint32_t u = 0; u < kU; u++)
-            if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
+        for (int u = 0; u < kBucketPer; u++)
+            if (s0 + threadIdx.x + u * kBucketThreads < s1)
+                atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
+    } else {
+        // 4 independent loads in flight per thread
+        constexpr uint32_t kU = 4;
+        for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
+            uint64_t Kg[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++) {
+                const uint32_t e = e0 + u * kBucketThreads;
+                Kg[u] = e < s1 ? tent[e] : 0;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kU; u++)
+                if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(Kg[u] >> 32) & sbmask], 1u);
+        }
     }
     __syncthreads();
     // exclusive scan of the nsb counters: per-thread run of `per`, then a block scan
@@ -248,18 +269,30 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         for (int w = 0; w < kBucketThreads / 64; w++) t += wsq[w];
         if (t) atomicAdd(&sqsum[1 + (p & 63)], t);
     }
+    if (in_lds) {
+#pragma unroll
+        for (int u = 0; u < kBucketPer; u++)
+            if (s0 + threadIdx.x + u * kBucketThreads < s1) {
+                const uint32_t pos = atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
+                out[pos] = (uint32_t)K[u];
+            }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < s1 - s0; i += kBucketThreads) entries[s0 + i] = out[i];
+        return;
+    }
+    constexpr uint32_t kU = 4;
     for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
-        uint64_t K[kU];
+        uint64_t Kg[kU];
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++) {
             const uint32_t e = e0 + u * kBucketThreads;
-            K[u] = e < s1 ? tent[e] : 0;
+            Kg[u] = e < s1 ? tent[e] : 0;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
             if (e0 + u * kBucketThreads < s1) {
-                const uint32_t pos = atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
-                entries[s0 + pos] = (uint32_t)K[u];
+                const uint32_t pos = atomicAdd(&sh[(uint32_t)(Kg[u] >> 32) & sbmask], 1u);
+                entries[s0 + pos] = (uint32_t)Kg[u];
             }
     }
 }
@@ -664,9 +697,17 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
                        d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
                        (const uint32_t *)tile_off, g, tent);
+    // LDS copy of a partition's entries when they fit beside the counters (two workgroups per
+    // CU: 80 KiB each at l2 = 12); cap 0 = every partition on the global two-pass path
+    const uint64_t cnt_bytes = (uint64_t)4 << g.l2;
+    const uint32_t cap = cnt_bytes <= 16384 ? (uint32_t)(kBucketThreads * kBucketPer) : 0u;
+    static const hipError_t lds_ok = hipFuncSetAttribute(
+        (const void *)idx_bucket_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        16384 + kBucketThreads * kBucketPer * 4);
+    if (lds_ok != hipSuccess) return lds_ok;
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
-                       (size_t)4 << g.l2, st, (const uint64_t *)tent, ntiles,
-                       (const uint32_t *)tile_off, g, dir, entries, self_events);
+                       (size_t)(cnt_bytes + (uint64_t)cap * 4), st, (const uint64_t *)tent, ntiles,
+                       (const uint32_t *)tile_off, g, cap, dir, entries, self_events);
     if (self_events) hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, self_events);
     return hipGetLastError();
 }
