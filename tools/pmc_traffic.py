@@ -102,7 +102,8 @@ def main():
     os.makedirs(a.work, exist_ok=True)
     # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
     bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline",
-                  "--no-fp-text", "--no-c3", "--no-c4", "--no-c5", "--no-cli", "--no-parity"]
+                  "--no-fp-text", "--no-c3", "--no-c4", "--no-c5", "--no-cli", "--no-split",
+                  "--no-parity"]
     fetch = run_pass("FETCH_SIZE", os.path.join(a.work, "fetch"), bench_args)
     write = run_pass("WRITE_SIZE", os.path.join(a.work, "write"), bench_args)
     # one "launch" of a group that is several kernels (the index build) is one step's worth

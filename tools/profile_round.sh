@@ -19,7 +19,7 @@ timeout -k 10 900 python3 tools/pmc_traffic.py --out $O/pmc_traffic.json \
 cp $O/pmc_traffic.json profiles/$ROUND/pmc_traffic.json && echo "pmc ok"
 rm -rf gpurun_out/pmc_traffic
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o prof --output-format csv \
-  -- python3 bench.py --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-parity \
+  -- python3 bench.py --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-split --no-parity \
   --steps 5 --warmup 2 > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
 cp "$f" $O/kernel_stats_$TAG.csv && echo "stats ok"
