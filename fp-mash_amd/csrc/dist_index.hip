@@ -86,19 +86,45 @@ __device__ __forceinline__ uint32_t row_of(uint32_t e, uint32_t stride, uint64_t
 }
 
 // ---- 0. the largest normalized key among the rows' last entries (the maximum for sorted
-// rows; unsorted rows may hold larger keys, which bucket_of clamps into the last bucket)
-__global__ __launch_bounds__(256) void idx_kmax_kernel(
+// rows; unsorted rows may hold larger keys, which bucket_of clamps into the last bucket).
+// One workgroup: it also zeroes the call's counters first (zero[0 .. nzero), which may hold
+// kmax itself), in place of a separate memset launch.
+constexpr int kKmaxThreads = 1024;
+__global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
-    uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax)
+    uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax,
+    unsigned long long *__restrict__ zero, uint32_t nzero)
 {
+    __shared__ unsigned long long wmax[kKmaxThreads / 64];
+    for (uint32_t i = threadIdx.x; i < nzero; i += kKmaxThreads) zero[i] = 0;
     uint64_t mx = 0;
-    for (uint32_t r = blockIdx.x * 256 + threadIdx.x; r < n_ref; r += gridDim.x * 256) {
-        const uint32_t l = ref_len[r];
-        if (l) mx = max(mx, norm_key(load_key(ref, hash_bytes, (uint64_t)r * stride + l - 1), hash_bytes));
+    // 8 rows per thread per round, their length loads and then their key loads in flight
+    // together (a serial loop paid two dependent L2 round trips per row: 16 us at 10k rows)
+    constexpr int kU = 8;
+    for (uint32_t r0 = threadIdx.x; r0 < n_ref; r0 += kU * kKmaxThreads) {
+        uint32_t l[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t r = r0 + u * kKmaxThreads;
+            l[u] = r < n_ref ? ref_len[r] : 0u;
+        }
+        uint64_t k[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++) {
+            const uint32_t r = r0 + u * kKmaxThreads;
+            k[u] = l[u] ? norm_key(load_key(ref, hash_bytes, (uint64_t)r * stride + l[u] - 1), hash_bytes) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; u++) mx = max(mx, k[u]);
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor((unsigned long long)mx, d, 64));
-    if ((threadIdx.x & 63) == 0 && mx) atomicMax(kmax, (unsigned long long)mx);
+    if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
+    __syncthreads();           // also orders the zeroing before the kmax store
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kKmaxThreads / 64; w++) mx = max(mx, (uint64_t)wmax[w]);
+        *kmax = mx;
+    }
 }
 
 // ---- 1a. level-1 histogram: LDS counters per partition; also flags unsorted /
@@ -663,6 +689,53 @@ hipError_t launch_dedup_rows(const void *in, const uint32_t *in_len, uint64_t in
                : dedup_rows_h<uint32_t>(in, in_len, in_stride, n, S, out, out_len, out_stride, st);
 }
 
+__global__ __launch_bounds__(kPubWords) void publish_kernel(const unsigned long long *__restrict__ src,
+                                                          uint32_t n, unsigned long long *dst,
+                                                          unsigned long long seq)
+{
+    if (threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(dst + kPubWords - 1, seq, __ATOMIC_RELEASE,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned long long *h_dst,
+                          unsigned long long seq, hipStream_t st)
+{
+    if (n >= kPubWords) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(publish_kernel, dim3(1), dim3(kPubWords), 0, st, d_src, n, h_dst, seq);
+    return hipGetLastError();
+}
+
+// scan_sums + scan_add in one launch for up to kScanFoldBlocks blocks: each block sums the
+// block totals before it itself (<= 4096 reads spread over its 256 threads)
+constexpr uint32_t kScanFoldBlocks = 4096;
+__global__ __launch_bounds__(256) void scan_add_fold_kernel(uint32_t *__restrict__ out, uint64_t n,
+                                                           const uint32_t *__restrict__ sums,
+                                                           uint32_t nb, uint32_t *__restrict__ out2,
+                                                           uint32_t *__restrict__ total)
+{
+    __shared__ uint32_t wsum[4];
+    const uint32_t b = blockIdx.x;
+    uint32_t part = 0;
+    for (uint32_t i = threadIdx.x; i < b; i += 256) part += sums[i];
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) part += __shfl_xor(part, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = part;
+    __syncthreads();
+    const uint32_t add = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (total && b == nb - 1 && threadIdx.x == 0) *total = add + sums[b];
+    const uint64_t base = (uint64_t)b * kScanBlock + threadIdx.x * 4;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+        if (base + k < n) {
+            const uint32_t v = out[base + k] + add;
+            out[base + k] = v;
+            if (out2) out2[base + k] = v;
+        }
+}
+
 uint64_t scan_scratch_words(uint64_t n) { return (n + kScanBlock - 1) / kScanBlock + 1; }
 
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
@@ -671,6 +744,11 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
     if (!n) return hipSuccess;
     uint32_t nb = (uint32_t)((n + kScanBlock - 1) / kScanBlock);
     hipLaunchKernelGGL(scan_local_kernel, dim3(nb), dim3(256), 0, st, in, out, n, scratch);
+    if (nb <= kScanFoldBlocks) {
+        hipLaunchKernelGGL(scan_add_fold_kernel, dim3(nb), dim3(256), 0, st, out, n,
+                           (const uint32_t *)scratch, nb, out2, total);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(scan_sums_kernel, dim3(1), dim3(256), 0, st, scratch, nb, total);
     hipLaunchKernelGGL(scan_add_kernel, dim3(nb), dim3(256), 0, st, out, n, scratch, out2);
     return hipGetLastError();
@@ -680,14 +758,13 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
-                            unsigned long long *self_events, hipStream_t st)
+                            unsigned long long *self_events, unsigned long long *zero,
+                            uint32_t nzero, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
-    // *g.kmax zeroed by the caller
-    hipLaunchKernelGGL(idx_kmax_kernel, dim3(std::min<uint32_t>((n_ref + 255) / 256, 256)),
-                       dim3(256), 0, st, d_ref, d_ref_len, stride, n_ref, hash_bytes,
-                       (unsigned long long *)g.kmax);
+    hipLaunchKernelGGL(idx_kmax_kernel, dim3(1), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
+                       stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero);
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
                        d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
                        unsorted, g);

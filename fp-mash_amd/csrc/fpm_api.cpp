@@ -14,6 +14,7 @@
 #include <cstdlib>
 #include <memory>
 #include <cstdio>
+#include <atomic>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -71,7 +72,9 @@ struct fpm_ctx {
     // grow-only device scratch, one buffer per named slot (no allocation in steady state)
     struct Slot { void *p = nullptr; size_t bytes = 0; };
     Slot scratch[20];
-    unsigned long long *host_counters = nullptr;   // pinned, for the events read-back
+    unsigned long long *host_counters = nullptr;   // pinned + mapped, for the events read-back
+    unsigned long long *dev_counters = nullptr;    // its device-side address
+    unsigned long long pub_seq = 0;                // last sequence number published into it
     int dist_mode = FPM_DIST_AUTO;
     // dense walk of u32 lists on 16-bit rank images (FPM_DENSE_IMG=0 turns it off, A/B)
     bool dense_img = true;
@@ -208,6 +211,38 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming);
     return e;
+}
+
+// Device counters -> host (the index build's posting events and sortedness flags, read
+// mid-call to pick the path): publish_kernel copies them into the context's mapped pinned
+// block and then bumps a sequence word, which the host spins on.  A D2H copy + stream sync
+// left the GPU idle ~45 us per call (the sync's wake-up, then the next launch).
+static int read_counters(fpm_ctx *ctx, const unsigned long long *d_src, uint32_t n,
+                         hipStream_t st)
+{
+    if (!ctx->host_counters) {
+        HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, kPubWords * 8,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer((void **)&ctx->dev_counters, ctx->host_counters, 0));
+        memset(ctx->host_counters, 0, kPubWords * 8);
+    }
+    const unsigned long long seq = ++ctx->pub_seq;
+    HIP_TRY(launch_publish(d_src, n, ctx->dev_counters, seq, st));
+    volatile unsigned long long *flag = ctx->host_counters + kPubWords - 1;
+    for (uint64_t spin = 1;; spin++) {
+        if (*flag == seq) break;
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q != hipSuccess && q != hipErrorNotReady) return fail(FPM_EHIP, hipGetErrorString(q));
+            if (q == hipSuccess && *flag != seq) {
+                std::atomic_thread_fence(std::memory_order_seq_cst);
+                if (*flag != seq) return fail(FPM_EHIP, "counter publish did not land");
+            }
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return FPM_OK;
 }
 
 // returns a device buffer of at least `bytes` for scratch slot `id`
@@ -1618,7 +1653,6 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
     if (!rs->sparse_ok) return FPM_OK;
     void *ctr;
     HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
-    if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
     if (!rs->kmax) HIP_TRY(hipMalloc((void **)&rs->kmax, 8));
     uint32_t *unsorted = (uint32_t *)((unsigned long long *)ctr + 66);
     auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom g) -> int {
@@ -1631,20 +1665,17 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
         HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
         HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
         HIP_TRY(slot_buf(rs->slot[5], En * 4, &entries));
-        HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
-        HIP_TRY(hipMemsetAsync(rs->kmax, 0, 8, st));
         TimedLaunch tl(ctx, FPM_K_INDEX, st);
         HIP_TRY(launch_idx_build(rows, len, stride, rs->n_ref, rs->hash_bytes, g,
                                  (uint32_t *)tile_hist, (uint32_t *)tile_off, (uint32_t *)scan_s,
                                  (uint64_t *)tent, (uint32_t *)dir, (uint32_t *)entries,
-                                 unsorted, nullptr, st));
+                                 unsorted, nullptr, (unsigned long long *)ctr, 72, st));
         tl.done();
         return FPM_OK;
     };
     geom.kmax = rs->kmax;
     if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom)) return rc;
-    HIP_TRY(hipMemcpyAsync(ctx->host_counters, ctr, 67 * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
+    if (int rc = read_counters(ctx, (const unsigned long long *)ctr, 67, st)) return rc;
     rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
     rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
     rs->deduped = rs->ref_unsorted && rs->mr <= kDedupMax;
@@ -1729,8 +1760,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const uint64_t NB = 1ULL << geom.nbits;
         void *ctr;
         HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
-        if (!ctx->host_counters) HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, 72 * 8));
-        // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
+            // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
         // [68] the largest indexed key (the bucket scale)
         unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
         uint32_t *unsorted = (uint32_t *)(events + 66);
@@ -1761,8 +1791,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             HIP_TRY(launch_probe_count(p_qry, p_qry_it ? p_qry_it : d_qry_len, p_qry_stride, n_qry,
                                        hash_bytes, geom, dir, events, unsorted, st));
             tl.done();
-            HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
             ev = ctx->host_counters[0];
             const bool q_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
             // deduplicated probe rows are sorted by construction: the query's own order is
@@ -1779,14 +1808,14 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             geom.kmax = events + 68;
             {
                 TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
                 // one set against itself: the query side is the ref side, so its sortedness is
-                // the ref flag and its posting events are sum_b |b|^2 from the bucket pass
+                // the ref flag and its posting events are sum_b |b|^2 from the bucket pass.
+                // The counters are zeroed by the first index kernel.
                 HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
                                          (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                          (uint32_t *)scan_s, (uint64_t *)tent,
                                          (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, st));
+                                         self_set ? events : nullptr, events, 72, st));
                 if (!self_set)
                     HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
                                                (const uint32_t *)dir_, events, unsorted, st));
@@ -1794,8 +1823,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             }
             dir = (const uint32_t *)dir_;
             entries = (const uint32_t *)entries_;
-            HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
             ev = ctx->host_counters[0];
             all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
             // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
@@ -1814,7 +1842,6 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 geom = make_geom(n_ref, (uint64_t)n_ref * mr);
                 geom.kmax = events + 68;
                 TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                HIP_TRY(hipMemsetAsync(ctr, 0, 72 * 8, st));
                 HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, sketch_size,
                                           dref, (uint32_t *)dref_len, mr, st));
                 if (!self_set)
@@ -1824,7 +1851,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                          (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                          (uint32_t *)scan_s, (uint64_t *)tent,
                                          (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, st));
+                                         self_set ? events : nullptr, events, 72, st));
                 p_qry = self_set ? dref : dqry;
                 p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
                 p_qry_stride = self_set ? mr : mq;
@@ -1832,8 +1859,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     HIP_TRY(launch_probe_count(p_qry, p_qry_it, p_qry_stride, n_qry, hash_bytes, geom,
                                                (const uint32_t *)dir_, events, unsorted, st));
                 tl.done();
-                HIP_TRY(hipMemcpyAsync(ctx->host_counters, events, 67 * 8, hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
+                if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
                 ev = ctx->host_counters[0];
             }
         }

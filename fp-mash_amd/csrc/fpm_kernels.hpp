@@ -120,8 +120,14 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
-                            unsigned long long *self_events, hipStream_t st);
+                            unsigned long long *self_events, unsigned long long *zero,
+                            uint32_t nzero, hipStream_t st);   // zero[0..nzero) cleared first
 uint64_t scan_scratch_words(uint64_t n);
+// copy n (<= kPubWords - 1) u64 counters into host-mapped memory, then write `seq` into its
+// last word (system-scope fence between): the host spins on that word
+constexpr uint32_t kPubWords = 128;
+hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned long long *h_dst,
+                          unsigned long long seq, hipStream_t st);
 // each row's first min(len, S, out_stride) entries sorted and deduplicated (dist_index.hip),
 // the index / probe input for unsorted lists; out_stride <= kDedupMax
 constexpr uint32_t kDedupMax = 4096;
