@@ -783,9 +783,11 @@ def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21,
     # kernel times of this rank (HIP events, extra runs outside the timed ones)
     ctx.reset_timing()
     ctx.set_timing(True)
+    ctx.merge_small_spills()                    # reset the counter
     job.run(st)
     ctx.synchronize()
     ctx.set_timing(False)
+    spills = ctx.merge_small_spills()           # small-list merges that overflowed their LDS
     kt = {}
     dev_ms = 0.0
     for kid in (fpmash.K_SKETCH, fpmash.K_MERGE):
@@ -822,7 +824,8 @@ def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21,
                      "alg_bytes": alg,
                      "alg_GBps": alg / (dev_ms * 1e-3) / 1e9 if dev_ms else None,
                      "frac_hbm": alg / (dev_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if dev_ms else None,
-                     "tiles": info["n_tiles"], "kernels": kt},
+                     "tiles": info["n_tiles"], "kernels": kt,
+                     "merge_small_lds_overflows": spills},
            "reassembled_genomes": int(len(rows_all)) if rank == 0 else None}
     if parity and rank == 0:
         from oracle import oracle as O

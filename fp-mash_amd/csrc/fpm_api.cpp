@@ -1098,6 +1098,15 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     return FPM_OK;
 }
 
+int fpm_merge_small_spills(fpm_ctx *ctx, uint64_t *count)
+{
+    if (!count) return fail(FPM_EINVAL, "null argument");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(merge_small_spills(count));
+    return FPM_OK;
+}
+
 int fpm_sketch_device_output(fpm_sketch_job *job, uint64_t **d_hashes, uint32_t **d_count,
                              uint32_t *n_groups, uint32_t *row_stride)
 {

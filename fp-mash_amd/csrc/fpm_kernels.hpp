@@ -75,6 +75,8 @@ hipError_t launch_group_select(const SelDesc *d_desc, uint32_t n, const uint32_t
                                uint64_t *d_rows, uint32_t *d_count, uint32_t s,
                                const uint64_t *d_thr, uint32_t *d_failed, hipStream_t st);
 // small: the round's lists are estimated short (merge_small_kernel; exact for any length)
+// merge_small_kernel launches whose lists overflowed its LDS cap since the last call (reset)
+hipError_t merge_small_spills(uint64_t *count);
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,
                         hipStream_t st);
 

@@ -15,6 +15,9 @@
 namespace fpm {
 
 constexpr int kBlock = 256;
+#ifndef FPM_SK_WPE
+#define FPM_SK_WPE 7       // waves per SIMD asked of the tile kernel for P <= 2048
+#endif
 constexpr int kWaves = kBlock / 64;
 
 // Phase timestamps of the tile kernel for tools/micro/sketch_phases.hip (which defines
@@ -292,7 +295,7 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
 }
 
 template <int P, int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? 7 : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? FPM_SK_WPE : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
 {
@@ -874,6 +877,10 @@ __device__ __forceinline__ uint32_t block_exscan_s(uint32_t v, uint32_t *tmp, ui
     return pre + x - v;
 }
 
+// merges whose lists did not fit kSCap (searched in global memory): the host's length
+// estimate mis-routed them (results are the same, only slower); read by fpm_merge_small_spills
+__device__ unsigned long long g_merge_small_spill;
+
 __global__ __launch_bounds__(kSBlock) void merge_small_kernel(const MergeDesc *__restrict__ descs,
                                                               uint32_t s)
 {
@@ -882,6 +889,7 @@ __global__ __launch_bounds__(kSBlock) void merge_small_kernel(const MergeDesc *_
     const MergeDesc md = descs[blockIdx.x];
     const uint32_t la = *md.alen, lb = md.b ? *md.blen : 0;
     const bool bfit = lb <= kSCap;
+    if (threadIdx.x == 0 && (!bfit || (lb && la > kSCap))) atomicAdd(&g_merge_small_spill, 1ULL);
     if (bfit)
         for (uint32_t j = threadIdx.x; j < lb; j += kSBlock) sl[j] = md.b[j];
     __syncthreads();
@@ -1121,6 +1129,17 @@ hipError_t launch_group_select(const SelDesc *d_desc, uint32_t n, const uint32_t
     hipLaunchKernelGGL(group_select_kernel, dim3(n), dim3(kSelThreads), lds, st, d_desc, d_row_ids,
                        d_rows, d_count, s, d_thr, d_failed);
     return hipGetLastError();
+}
+
+hipError_t merge_small_spills(uint64_t *count)
+{
+    unsigned long long v = 0;
+    hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_merge_small_spill), sizeof(v));
+    if (e != hipSuccess) return e;
+    const unsigned long long z = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_merge_small_spill), &z, sizeof(z));
+    *count = v;
+    return e;
 }
 
 hipError_t launch_merge(const MergeDesc *d_desc, uint32_t n, uint32_t s, bool small,

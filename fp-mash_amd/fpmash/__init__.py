@@ -70,6 +70,7 @@ SYMBOLS = [
     ("fpm_sketch_device_output", C.c_int, [vp, C.POINTER(vp), C.POINTER(vp), u32p, u32p]),
     ("fpm_sketch_fetch", C.c_int, [vp, u64p, u32p]),
     ("fpm_sketch_mult", C.c_int, [vp, vp, u32p]),
+    ("fpm_merge_small_spills", C.c_int, [vp, u64p]),
     ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
     ("fpm_sketch_job_free", None, [vp]),
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
@@ -335,6 +336,12 @@ class Context:
         t, n = C.c_double(), C.c_uint64()
         _check(lib().fpm_ctx_kernel_time(self.h, kernel, C.byref(t), C.byref(n)))
         return t.value, n.value
+
+    def merge_small_spills(self):
+        """fpm_merge_small_spills: small-list merges that overflowed the LDS cap (resets)."""
+        v = np.zeros(1, np.uint64)
+        _check(lib().fpm_merge_small_spills(self.h, _p(v, u64p)))
+        return int(v[0])
 
     def set_dist_mode(self, mode):
         _check(lib().fpm_ctx_set_dist_mode(self.h, mode))

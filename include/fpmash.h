@@ -93,6 +93,9 @@ int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */
 int fpm_ctx_kernel_time(fpm_ctx *ctx, int kernel, double *total_ms, uint64_t *launches);
+/* merges routed to the small-list kernel whose lists overflowed its LDS cap (searched in global
+ * memory instead: same results, slower) since the last call on this device; resets it */
+int fpm_merge_small_spills(fpm_ctx *ctx, uint64_t *count);
 
 /* dist strategy: FPM_DIST_AUTO picks the inverted-index path unless the shared-hash
  * events exceed pairs*S/4; DENSE walks every pair; SPARSE always uses the index.

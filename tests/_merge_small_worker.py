@@ -24,6 +24,7 @@ def main():
     recs = [rand_seq(rng, 300_000), rand_seq(rng, 40_000)] + [rand_seq(rng, 30_000) for _ in range(5)]
     groups = [0, 1, 2, 2, 2, 2, 2]
     with fpmash.Context(0) as ctx:
+        ctx.merge_small_spills()                     # reset the overflow counter
         for k, s in ((21, 1000), (21, 5000), (16, 3000)):
             got = ctx.sketch(fpmash.make_params(k=k, s=s), recs, groups=groups, n_groups=3)
             exp = O.sketch_batch(O.params(k=k, s=s), recs, groups=groups, n_groups=3)
@@ -31,7 +32,12 @@ def main():
                 if not np.array_equal(np.asarray(g), np.asarray(e)):
                     print("mismatch", k, s, len(g), len(e))
                     return 1
-    print("ok")
+        # s = 5000 lists exceed the 2,048-entry cap: the device counter saw them
+        spills = ctx.merge_small_spills()
+        if spills == 0:
+            print("no LDS overflow counted")
+            return 1
+    print("ok", spills)
     return 0
 
 
