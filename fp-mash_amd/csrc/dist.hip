@@ -732,6 +732,9 @@ __global__ __launch_bounds__(256) void dist_finalize_kernel(
 // VEC (n_ref % 4 == 0, so a row starts 4-cell aligned): each lane writes 4 consecutive
 // cells with 16-B stores (1 KiB per wave store; the pass bytes as one dword).
 constexpr uint32_t kFillCells = 1024;
+#ifndef FPM_FILL_NT
+#define FPM_FILL_NT 0     // 1: the fill's stores non-temporal (A/B)
+#endif
 template <bool VEC, typename C>
 __global__ __launch_bounds__(256) void dist_fill_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
@@ -765,6 +768,26 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         // plain stores: non-temporal ones (nt) let the candidate compare beside run 15%
         // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms); 16-B write-through
         // (sc1) buffer stores slowed it 1.9x (0.9 -> 1.67 ms beside the compare)
+#if FPM_FILL_NT
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef double f64x2 __attribute__((ext_vector_type(2)));
+        if (numer) {
+            if constexpr (sizeof(C) == 2) {
+                __builtin_nontemporal_store(u32x2{0u, 0u}, (u32x2 *)(numer + o));
+                __builtin_nontemporal_store(u32x2{dn[0] | (dn[1] << 16), dn[2] | (dn[3] << 16)},
+                                            (u32x2 *)(denom + o));
+            } else {
+                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (u32x4 *)(numer + o));
+                __builtin_nontemporal_store(u32x4{dn[0], dn[1], dn[2], dn[3]}, (u32x4 *)(denom + o));
+            }
+        }
+        __builtin_nontemporal_store(f64x2{dv[0], dv[1]}, (f64x2 *)(fill.dist + o));
+        __builtin_nontemporal_store(f64x2{dv[2], dv[3]}, (f64x2 *)(fill.dist + o + 2));
+        __builtin_nontemporal_store(f64x2{pv[0], pv[1]}, (f64x2 *)(fill.pval + o));
+        __builtin_nontemporal_store(f64x2{pv[2], pv[3]}, (f64x2 *)(fill.pval + o + 2));
+        if (fill.pass) __builtin_nontemporal_store(pa, (uint32_t *)(fill.pass + o));
+#else
         if (numer) {
             store_counts4(numer + o, 0, 0, 0, 0);
             store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
@@ -774,6 +797,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
         *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
         if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+#endif
         continue;
     }
 #pragma unroll
