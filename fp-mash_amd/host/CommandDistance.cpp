@@ -88,6 +88,24 @@ struct Out {
     }
 };
 
+// the same formats into a caller's buffer (the one-append-per-line path): at most
+// kLineNums bytes for the two numbers, two counts and four separators of a line
+constexpr size_t kLineNums = 2 * 32 + 2 * 20 + 4;
+inline char *numTo(char *p, double x)
+{
+    if (x == 1.0) { *p++ = '1'; return p; }
+    if (x == 0.0 && !std::signbit(x)) { *p++ = '0'; return p; }
+    return p + snprintf(p, 32, "%g", x);
+}
+inline char *uTo(char *p, uint64_t x)
+{
+    char t[20];
+    int n = 0;
+    do { t[19 - n++] = (char)('0' + x % 10); x /= 10; } while (x);
+    memcpy(p, t + 20 - n, n);
+    return p + n;
+}
+
 }  // namespace
 
 int CommandDistance::run() const
@@ -266,7 +284,15 @@ int CommandDistance::run() const
               "dist reference set");
     for (auto &t : pinner) t.join();
     phaseMark("rows packed + reference sets on the devices");
+    // reference name (+ ":" comment) of each line, built once
+    std::vector<std::string> refTag(nR);
+    for (uint64_t j = 0; j < nR; j++) {
+        const Reference &rr = sketchRef.getReference(j);
+        refTag[j] = rr.name;
+        if (comment) { refTag[j].push_back(':'); refTag[j] += rr.comment; }
+    }
     auto format = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, std::string &dst) {
+        char line[512];
         Out o;
         o.autoflush = false;
         o.buf.swap(dst);                    // the piece's buffer from earlier blocks (no regrowth)
@@ -287,9 +313,26 @@ int CommandDistance::run() const
                     o.put('\t');
                     if (sl.pa[k]) o.num(sl.di[k]);
                 } else if (sl.pa[k]) {
-                    const Reference &rr = sketchRef.getReference(j);
-                    o.put(rr.name);
-                    if (comment) { o.put(':'); o.put(rr.comment); }
+                    const std::string &tag = refTag[j];
+                    if (tag.size() + qtail.size() + kLineNums <= sizeof(line)) {
+                        // one append per line: the line is assembled in a stack buffer
+                        char *p = line;
+                        memcpy(p, tag.data(), tag.size());
+                        p += tag.size();
+                        memcpy(p, qtail.data(), qtail.size());
+                        p += qtail.size();
+                        p = numTo(p, sl.di[k]);
+                        *p++ = '\t';
+                        p = numTo(p, sl.pv[k]);
+                        *p++ = '\t';
+                        p = uTo(p, sl.nu[k]);
+                        *p++ = '/';
+                        p = uTo(p, sl.de[k]);
+                        *p++ = '\n';
+                        o.buf.append(line, (size_t)(p - line));
+                        continue;
+                    }
+                    o.put(tag);
                     o.put(qtail);
                     o.num(sl.di[k]);
                     o.put('\t');
