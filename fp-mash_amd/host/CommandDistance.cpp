@@ -193,10 +193,16 @@ int CommandDistance::run() const
         if (list) splitFile(arguments[i], queryFiles);
         else queryFiles.push_back(arguments[i]);
     }
-    Sketch sketchQuery;
-    if (fingerprint && tagMSH) sketchQuery.initFromFiles(queryFiles, parameters);
-    else if (fingerprint && tagTXT) sketchQuery.initFromFingerprints(queryFiles, parameters);
-    else sketchQuery.initFromFiles(queryFiles, parameters, 0, true);
+    // `dist X.msh X.msh`: the query set is the reference set (same file, same parameters), so
+    // it is parsed and packed once
+    const bool sameSet = isSketch && !fingerprint && queryFiles.size() == 1 &&
+                         queryFiles[0] == fileReference;
+    Sketch sketchQueryOwn;
+    if (sameSet) {}
+    else if (fingerprint && tagMSH) sketchQueryOwn.initFromFiles(queryFiles, parameters);
+    else if (fingerprint && tagTXT) sketchQueryOwn.initFromFingerprints(queryFiles, parameters);
+    else sketchQueryOwn.initFromFiles(queryFiles, parameters, 0, true);
+    const Sketch &sketchQuery = sameSet ? sketchRef : sketchQueryOwn;
 
     phaseMark("query sketch loaded");
     const uint64_t nR = sketchRef.getReferenceCount(), nQ = sketchQuery.getReferenceCount();
@@ -266,11 +272,14 @@ int CommandDistance::run() const
             check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
             check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
         });
-    std::vector<uint8_t> R, Q;
-    std::vector<uint32_t> rl, ql;
-    std::vector<uint64_t> rL, qL;
+    std::vector<uint8_t> R, Qown;
+    std::vector<uint32_t> rl, qlOwn;
+    std::vector<uint64_t> rL, qLOwn;
     pack(sketchRef, R, rl, rL, width);
-    pack(sketchQuery, Q, ql, qL, width);
+    if (!sameSet) pack(sketchQuery, Qown, qlOwn, qLOwn, width);
+    const std::vector<uint8_t> &Q = sameSet ? R : Qown;
+    const std::vector<uint32_t> &ql = sameSet ? rl : qlOwn;
+    const std::vector<uint64_t> &qL = sameSet ? rL : qLOwn;
 
     // The grid in query blocks (CommandDistance.cpp:224-261 chunks it for the pool): every
     // device holds the reference set with its index built once (fpm_refset_create) and takes
