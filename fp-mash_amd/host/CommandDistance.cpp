@@ -233,9 +233,10 @@ int CommandDistance::run() const
     for (uint64_t i = 0; i < nR; i++) width = std::max<uint64_t>(width, sketchRef.getReference(i).hashes.size());
     for (uint64_t i = 0; i < nQ; i++) width = std::max<uint64_t>(width, sketchQuery.getReference(i).hashes.size());
     const int nDev = nR && nQ ? deviceCount() : 0;
-    // 2 M pairs per block: 58 MB of pinned results per slot (16 M-pair slots made pinning and
-    // unpinning ~1.4 GB cost ~0.6 s of the C2 command)
-    uint64_t blockPairs = 2ULL << 20;
+    // 1 M pairs per block: 29 MB of pinned results per slot (16 M-pair slots made pinning and
+    // unpinning ~1.4 GB cost ~0.6 s of the C2 command; C2 `dist` wall: 4 M 1.27 s, 2 M 1.15 s,
+    // 1 M 1.06-1.09 s, 512 K 1.50 s)
+    uint64_t blockPairs = 1ULL << 20;
     if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
     const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
     const uint64_t nBlocks = nR ? (nQ + block - 1) / block : 0;
