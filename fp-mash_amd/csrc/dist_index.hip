@@ -430,8 +430,9 @@ __global__ __launch_bounds__(256) void probe_count_kernel(
     }
 }
 
-// events[1..64] -> events[0].  (A last-workgroup sum inside the bucket pass instead
-// measured 0.1 ms slower: its done counter is one address taking an atomic per workgroup.)
+// events[1..64] -> events[0] (unused: publish_kernel folds this sum into the read-back).
+// (A last-workgroup sum inside the bucket pass measured 0.1 ms slower: its done counter is
+// one address taking an atomic per workgroup.)
 __global__ void sum64_kernel(unsigned long long *events)
 {
     unsigned long long v = events[1 + threadIdx.x];
@@ -714,7 +715,20 @@ __global__ __launch_bounds__(kPubWords) void publish_kernel(const unsigned long 
                                                           uint32_t n, unsigned long long *dst,
                                                           unsigned long long seq)
 {
-    if (threadIdx.x < n) dst[threadIdx.x] = src[threadIdx.x];
+    // src[0] = the posting events: the sum of the 64 spread partials src[1..64] (the index
+    // build's bucket pass or probe_count_kernel add into those), folded in here
+    unsigned long long ev = (threadIdx.x >= 1 && threadIdx.x <= 64 && n > 64) ? src[threadIdx.x] : 0;
+    for (int d = 32; d > 0; d >>= 1) ev += __shfl_xor(ev, d, 64);
+    __shared__ unsigned long long wsum[kPubWords / 64];
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = ev;
+    __syncthreads();
+    if (threadIdx.x == 0 && n > 64) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < kPubWords / 64; w++) t += wsum[w];
+        dst[0] = t;
+    } else if (threadIdx.x < n) {
+        dst[threadIdx.x] = src[threadIdx.x];
+    }
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(dst + kPubWords - 1, seq, __ATOMIC_RELEASE,
@@ -806,7 +820,6 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)(cnt_bytes + (uint64_t)cap * 4), st, (const uint64_t *)tent, ntiles,
                        (const uint32_t *)tile_off, g, cap, dir, entries, self_events);
-    if (self_events) hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, self_events);
     return hipGetLastError();
 }
 
@@ -818,7 +831,6 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
     if (n) hipLaunchKernelGGL(probe_count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
                               st, d_qry, d_qry_len, stride, n_qry, hash_bytes, g, dir, events,
                               unsorted);
-    hipLaunchKernelGGL(sum64_kernel, dim3(1), dim3(64), 0, st, events);
     return hipGetLastError();
 }
 
