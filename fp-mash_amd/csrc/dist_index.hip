@@ -92,43 +92,56 @@ __device__ __forceinline__ uint32_t row_of(uint32_t e, uint32_t stride, uint64_t
 
 // ---- 0. the largest normalized key among the rows' last entries (the maximum for sorted
 // rows; unsorted rows may hold larger keys, which bucket_of clamps into the last bucket).
-// One workgroup: it also zeroes the call's counters first (zero[0 .. nzero), which may hold
-// kmax itself), in place of a separate memset launch.
-constexpr int kKmaxThreads = 1024;
+// A few workgroups (8 rows per thread in flight); each folds its maximum into acc[0] and the
+// last one to finish (acc[1] counts them) zeroes the call's counters (zero[0 .. nzero), which
+// may hold kmax itself), writes kmax and resets acc for the next call: no memset launch, and
+// not the 14 us of one workgroup walking 10k rows.  acc[0..1] start at zero (scratch()).
+constexpr int kKmaxThreads = 256;
+constexpr int kKmaxU = 8;
 __global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
     uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax,
-    unsigned long long *__restrict__ zero, uint32_t nzero)
+    unsigned long long *__restrict__ zero, uint32_t nzero, unsigned long long *acc)
 {
     __shared__ unsigned long long wmax[kKmaxThreads / 64];
-    for (uint32_t i = threadIdx.x; i < nzero; i += kKmaxThreads) zero[i] = 0;
+    __shared__ uint32_t s_last;
     uint64_t mx = 0;
-    // 8 rows per thread per round, their length loads and then their key loads in flight
-    // together (a serial loop paid two dependent L2 round trips per row: 16 us at 10k rows)
-    constexpr int kU = 8;
-    for (uint32_t r0 = threadIdx.x; r0 < n_ref; r0 += kU * kKmaxThreads) {
-        uint32_t l[kU];
+    const uint32_t step = gridDim.x * kKmaxThreads;
+    for (uint32_t r0 = blockIdx.x * kKmaxThreads + threadIdx.x; r0 < n_ref; r0 += kKmaxU * step) {
+        uint32_t l[kKmaxU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t r = r0 + u * kKmaxThreads;
+        for (int u = 0; u < kKmaxU; u++) {
+            const uint32_t r = r0 + u * step;
             l[u] = r < n_ref ? ref_len[r] : 0u;
         }
-        uint64_t k[kU];
+        uint64_t k[kKmaxU];
 #pragma unroll
-        for (int u = 0; u < kU; u++) {
-            const uint32_t r = r0 + u * kKmaxThreads;
+        for (int u = 0; u < kKmaxU; u++) {
+            const uint32_t r = r0 + u * step;
             k[u] = l[u] ? norm_key(load_key(ref, hash_bytes, (uint64_t)r * stride + l[u] - 1), hash_bytes) : 0;
         }
 #pragma unroll
-        for (int u = 0; u < kU; u++) mx = max(mx, k[u]);
+        for (int u = 0; u < kKmaxU; u++) mx = max(mx, k[u]);
     }
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint64_t)__shfl_xor((unsigned long long)mx, d, 64));
     if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = mx;
-    __syncthreads();           // also orders the zeroing before the kmax store
+    __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kKmaxThreads / 64; w++) mx = max(mx, (uint64_t)wmax[w]);
-        *kmax = mx;
+        atomicMax(&acc[0], (unsigned long long)mx);
+        __threadfence();
+        s_last = atomicAdd(&acc[1], 1ULL) == gridDim.x - 1 ? 1u : 0u;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (uint32_t i = threadIdx.x; i < nzero; i += kKmaxThreads) zero[i] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        *kmax = atomicMax(&acc[0], 0ULL);
+        acc[0] = 0;
+        acc[1] = 0;
     }
 }
 
@@ -794,12 +807,14 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
-                            uint32_t nzero, hipStream_t st)
+                            uint32_t nzero, unsigned long long *acc, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
-    hipLaunchKernelGGL(idx_kmax_kernel, dim3(1), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
-                       stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero);
+    const uint32_t kg = std::max<uint32_t>(1, std::min<uint32_t>(
+        (n_ref + kKmaxThreads * kKmaxU - 1) / (kKmaxThreads * kKmaxU), 64));
+    hipLaunchKernelGGL(idx_kmax_kernel, dim3(kg), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
+                       stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero, acc);
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
                        d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
                        unsorted, g);

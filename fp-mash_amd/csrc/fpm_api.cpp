@@ -245,6 +245,10 @@ static int read_counters(fpm_ctx *ctx, const unsigned long long *d_src, uint32_t
     return FPM_OK;
 }
 
+// the dist counters (scratch slot 7): [0] events, [1..64] per-block partials, [65] candidates,
+// [66] unsorted flag, [68] largest indexed key; [72..73] idx_kmax_kernel's accumulator
+constexpr size_t kCtrWords = 80;
+
 // returns a device buffer of at least `bytes` for scratch slot `id`
 static hipError_t scratch(fpm_ctx *ctx, int id, size_t bytes, void **out)
 {
@@ -257,6 +261,12 @@ static hipError_t scratch(fpm_ctx *ctx, int id, size_t bytes, void **out)
         hipError_t e = hipMalloc(&s.p, b);
         if (e != hipSuccess) return e;
         s.bytes = b;
+        // small buffers (the counters) start zeroed: some words are kept at zero between
+        // calls by the kernels themselves (idx_kmax_kernel's accumulator)
+        if (b <= 4096) {
+            if ((e = hipMemset(s.p, 0, b)) != hipSuccess) return e;
+            if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+        }
     }
     *out = s.p;
     return hipSuccess;
@@ -1661,7 +1671,7 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
     rs->sparse_ok = E > 0 && geom.rbits <= 24 && E < (1ULL << 31);
     if (!rs->sparse_ok) return FPM_OK;
     void *ctr;
-    HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
+    HIP_TRY(scratch(ctx, 7, kCtrWords * 8, &ctr));
     if (!rs->kmax) HIP_TRY(hipMalloc((void **)&rs->kmax, 8));
     uint32_t *unsorted = (uint32_t *)((unsigned long long *)ctr + 66);
     auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom g) -> int {
@@ -1678,7 +1688,7 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
         HIP_TRY(launch_idx_build(rows, len, stride, rs->n_ref, rs->hash_bytes, g,
                                  (uint32_t *)tile_hist, (uint32_t *)tile_off, (uint32_t *)scan_s,
                                  (uint64_t *)tent, (uint32_t *)dir, (uint32_t *)entries,
-                                 unsorted, nullptr, (unsigned long long *)ctr, 72, st));
+                                 unsorted, nullptr, (unsigned long long *)ctr, 72, (unsigned long long *)ctr + 72, st));
         tl.done();
         return FPM_OK;
     };
@@ -1768,7 +1778,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
         void *ctr;
-        HIP_TRY(scratch(ctx, 7, 72 * 8, &ctr));
+        HIP_TRY(scratch(ctx, 7, kCtrWords * 8, &ctr));
             // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
         // [68] the largest indexed key (the bucket scale)
         unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
@@ -1824,7 +1834,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                          (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                          (uint32_t *)scan_s, (uint64_t *)tent,
                                          (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, events, 72, st));
+                                         self_set ? events : nullptr, events, 72, events + 72, st));
                 if (!self_set)
                     HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
                                                (const uint32_t *)dir_, events, unsorted, st));
@@ -1860,7 +1870,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                          (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                          (uint32_t *)scan_s, (uint64_t *)tent,
                                          (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, events, 72, st));
+                                         self_set ? events : nullptr, events, 72, events + 72, st));
                 p_qry = self_set ? dref : dqry;
                 p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
                 p_qry_stride = self_set ? mr : mq;

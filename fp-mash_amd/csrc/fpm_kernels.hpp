@@ -123,7 +123,8 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
-                            uint32_t nzero, hipStream_t st);   // zero[0..nzero) cleared first
+                            uint32_t nzero, unsigned long long *acc, hipStream_t st);
+// zero[0..nzero) is cleared first; acc[0..1]: two words that start at zero and are left at zero
 uint64_t scan_scratch_words(uint64_t n);
 // copy n (<= kPubWords - 1) u64 counters into host-mapped memory, then write `seq` into its
 // last word (system-scope fence between): the host spins on that word
