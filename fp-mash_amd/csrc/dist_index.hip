@@ -194,15 +194,41 @@ __device__ __forceinline__ uint64_t pack_l1(uint64_t K, uint32_t r, const IdxGeo
     return ((uint64_t)sub << 32) | ((uint64_t)key_fp(K, g, mult) << g.rbits) | r;
 }
 
+// The tile's entries are first grouped by partition in LDS (a counting sort on the hist
+// pass's per-tile counts), then written out in slot order: consecutive threads write
+// consecutive tent positions of one partition's run (~16 entries), instead of every lane
+// storing 8 B into a different partition.  Each staged word carries its partition in the top
+// bits (free: the bucket pass reads only the sub-bucket bits and the low u32).
+constexpr uint32_t kPartShift = 54;
+static_assert(kIdxL1 <= 64 - kPartShift, "partition id fits the staged word");
 __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
     uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, uint32_t ntiles,
-    const uint32_t *__restrict__ tile_off, IdxGeom g, uint64_t *__restrict__ tent)
+    const uint32_t *__restrict__ tile_hist, const uint32_t *__restrict__ tile_off, IdxGeom g,
+    uint64_t *__restrict__ tent)
 {
-    __shared__ uint32_t cur[kParts];
+    extern __shared__ __attribute__((aligned(16))) uint64_t stage[];   // kIdxTile words
+    __shared__ uint32_t gbase[kParts], lbase[kParts], lcur[kParts];
+    __shared__ uint32_t wsum[kIdxThreads / 64];
     const uint64_t mult = idx_mult(g);
-    for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads)
-        cur[p] = tile_off[(uint64_t)p * ntiles + blockIdx.x];
+    // per-partition: global base of this tile's run, and its local base (block exscan of the
+    // tile's counts)
+    static_assert(kParts == kIdxThreads, "one partition per thread");
+    {
+        const uint32_t p = threadIdx.x;
+        gbase[p] = tile_off[(uint64_t)p * ntiles + blockIdx.x];
+        const uint32_t c = tile_hist[(uint64_t)p * ntiles + blockIdx.x];
+        const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+        uint32_t x = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) { const uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int w = 0; w < wave; w++) pre += wsum[w];
+        lbase[p] = pre + x - c;
+        lcur[p] = pre + x - c;
+    }
     __syncthreads();
     const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
     for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
@@ -220,9 +246,17 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
 #pragma unroll
         for (int u = 0; u < kIdxU; u++)
             if (v[u]) {
-                const uint32_t pos = atomicAdd(&cur[bucket_of(K[u], g, mult) >> g.l2], 1u);
-                tent[pos] = pack_l1(K[u], rr[u], g, mult);
+                const uint32_t part = bucket_of(K[u], g, mult) >> g.l2;
+                const uint32_t pos = atomicAdd(&lcur[part], 1u);
+                stage[pos] = ((uint64_t)part << kPartShift) | pack_l1(K[u], rr[u], g, mult);
             }
+    }
+    __syncthreads();
+    const uint32_t total = lbase[kParts - 1] + (lcur[kParts - 1] - lbase[kParts - 1]);
+    for (uint32_t i = threadIdx.x; i < total; i += kIdxThreads) {
+        const uint64_t w = stage[i];
+        const uint32_t part = (uint32_t)(w >> kPartShift);
+        tent[gbase[part] + (i - lbase[part])] = w;
     }
 }
 
@@ -821,9 +855,14 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     const uint64_t nh = (uint64_t)kParts * ntiles;
     if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
         return e;
-    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
-                       d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles,
-                       (const uint32_t *)tile_off, g, tent);
+    static const hipError_t stage_ok = hipFuncSetAttribute(
+        (const void *)idx_part_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+        kIdxTile * 8);
+    if (stage_ok != hipSuccess) return stage_ok;
+    hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads),
+                       (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic, n_ref,
+                       hash_bytes, ntiles, (const uint32_t *)tile_hist, (const uint32_t *)tile_off,
+                       g, tent);
     // LDS copy of a partition's entries when they fit beside the counters (two workgroups per
     // CU: 80 KiB each at l2 = 12); cap 0 = every partition on the global two-pass path
     const uint64_t cnt_bytes = (uint64_t)4 << g.l2;
