@@ -52,8 +52,10 @@ METRIC = "bases/s sketched + Mpairs/s dist, k=21 s=1000, 1/2/4/8 MI355X; %HBM ro
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # a C2 step is ~1.4 ms: 20 timed steps after 5 warmup steps cost ~35 ms and steady the
+    # line (5 steps read 2-5 % high: clocks still ramping)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--n-seqs", type=int, default=10000)
     ap.add_argument("--seq-len", type=int, default=2000)
     ap.add_argument("--families", type=int, default=100)
