@@ -249,7 +249,7 @@ def _cpu_model():
     return "unknown"
 
 
-def fp_text_leg(ctx, reps=3):
+def fp_text_leg(ctx, reps=5):
     """C3's -fp input step, reported beside the metric (not part of `value`): parse + hash
     the 1,000,000 CFL k-finger lines `sketch -fp` reads (50 lyn2vec-shaped sequences' CFL
     text, tiled to the line cap: ~30 MB).  Device rate = the parse kernels' HIP-event time;
@@ -257,22 +257,32 @@ def fp_text_leg(ctx, reps=3):
     base = datagen.cfl_text(datagen.random_dna(50, 2000, seed=3), datagen.lyn2vec_ids(50))
     text = base * 10
     lines = text.count(b"\n")
-    ctx.fp_text(text[:100000])                                     # warm
-    ctx.reset_timing()
-    ctx.set_timing(True)
-    t0 = time.perf_counter()
+    for warm in (text[:100000], text):                             # warm (pinned ring too)
+        ctx.fp_text(warm, max_lines=1_000_000)
+    # per call: the HIP-event total of its launches.  The median is reported: an event pair
+    # now and then brackets a host-side stall before the dispatch (one call of 3 read 28 ms
+    # against 0.23 ms for the others, while rocprofv3's kernel trace of the same script gave
+    # 0.24 ms per call; tools/micro/fp_text_time.py)
+    devs, walls = [], []
     for _ in range(reps):
+        ctx.reset_timing()
+        ctx.set_timing(True)
+        t0 = time.perf_counter()
         r = ctx.fp_text(text, max_lines=1_000_000)
-    wall = (time.perf_counter() - t0) / reps
-    ctx.set_timing(False)
-    tot, _cnt = ctx.kernel_time(fpmash.K_FPTEXT)
+        walls.append(time.perf_counter() - t0)
+        ctx.set_timing(False)
+        tot, _cnt = ctx.kernel_time(fpmash.K_FPTEXT)
+        devs.append(tot * 1e-3)
     ctx.reset_timing()
-    dev = tot / reps * 1e-3
+    dev = float(np.median(devs))
+    wall = float(np.median(walls))
     n = len(r["hash"])
     return {"lines": n, "text_bytes": len(text), "device_ms": dev * 1e3,
+            "device_ms_calls": [round(d * 1e3, 4) for d in devs],
             "lines_per_s_device": n / dev, "text_GBps_device": len(text) / dev / 1e9,
             "lines_per_s_wall_pcie": n / wall, "wall_ms": wall * 1e3,
-            "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap)"}
+            "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap); "
+                    f"median of {reps} calls"}
 
 
 def _group_fp_lines(r, text):
