@@ -46,14 +46,35 @@ __device__ __forceinline__ bool fp_is_space(uint8_t c)
     return c == ' ' || (c >= '\t' && c <= '\r');   // isspace in the "C" locale
 }
 
+// newline flags of one 16-B text block (one uint4 load per thread; bytes at or past len are
+// masked: the text buffer has 16 bytes of padding): bit 8 i + 7 of word i set where byte is '\n'
+// (exact zero-byte test of w ^ 0x0A0A0A0A, no carries between bytes)
+__device__ __forceinline__ uint4 nl_flags16(const uint8_t *__restrict__ text, uint64_t b0,
+                                            uint64_t len)
+{
+    const uint4 w = *reinterpret_cast<const uint4 *>(text + b0);
+    uint32_t m[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        const uint32_t x = m[i] ^ 0x0A0A0A0Au;
+        uint32_t f = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;
+        const int64_t valid = (int64_t)len - (int64_t)(b0 + 4 * i);   // bytes of word i in range
+        if (valid < 4) f &= valid <= 0 ? 0u : (1u << (8 * valid)) - 1;
+        m[i] = f;
+    }
+    return make_uint4(m[0], m[1], m[2], m[3]);
+}
+
 __global__ __launch_bounds__(256) void nl_count_kernel(const uint8_t *__restrict__ text,
                                                       uint64_t len, uint32_t *__restrict__ cnt)
 {
     __shared__ uint32_t wsum[4];
     const uint64_t b0 = (uint64_t)blockIdx.x * kTextChunk + threadIdx.x * 16;
     uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) c += (b0 + i < len && text[b0 + i] == '\n');
+    if (b0 < len) {
+        const uint4 f = nl_flags16(text, b0, len);
+        c = __popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w);
+    }
     for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, 64);
     if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
     __syncthreads();
@@ -68,9 +89,9 @@ __global__ __launch_bounds__(256) void nl_scatter_kernel(const uint8_t *__restri
 {
     __shared__ uint32_t wsum[4];
     const uint64_t b0 = (uint64_t)blockIdx.x * kTextChunk + threadIdx.x * 16;
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < 16; i++) c += (b0 + i < len && text[b0 + i] == '\n');
+    uint4 f = make_uint4(0, 0, 0, 0);
+    if (b0 < len) f = nl_flags16(text, b0, len);
+    const uint32_t c = __popc(f.x) + __popc(f.y) + __popc(f.z) + __popc(f.w);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t x = c;
 #pragma unroll
@@ -79,40 +100,74 @@ __global__ __launch_bounds__(256) void nl_scatter_kernel(const uint8_t *__restri
     __syncthreads();
     uint64_t k = blk_off[blockIdx.x] + x - c;
     for (int w = 0; w < wave; w++) k += wsum[w];
-    for (int i = 0; i < 16; i++)
-        if (b0 + i < len && text[b0 + i] == '\n') line_start[++k] = b0 + i + 1;
+    const uint32_t m[4] = {f.x, f.y, f.z, f.w};
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+        for (uint32_t b = m[i]; b; b &= b - 1)
+            line_start[++k] = b0 + 4 * i + (__builtin_ctz(b) >> 3) + 1;
 }
 
-// one lane per line
-__global__ __launch_bounds__(256) void fp_line_kernel(
-    const uint8_t *__restrict__ text, uint64_t len, const uint64_t *__restrict__ line_start,
-    uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
-    uint64_t *__restrict__ id_off, uint32_t *__restrict__ id_len, uint32_t *__restrict__ n_vals,
-    void *__restrict__ hash, uint8_t *__restrict__ new_id)
+// One lane per line, the wave's text span staged in LDS: the 64 lines of a wave (and the line
+// before them, for the new-ID test) are contiguous in the text, so the wave copies that span
+// with 16-B loads and every lane parses its line from LDS, reading each byte once (the
+// former global byte loads ran at 0.3 TB/s).  A span over kFpSpan bytes reads global memory.
+constexpr uint32_t kFpSpan = 4096;
+
+// bytes of a staged span through a one-word cache: the parse walks forward, so 3 of 4 reads
+// come from the register
+struct SpanBytes {
+    const uint32_t *w;
+    uint64_t base;                   // 16-B aligned text position of w[0]
+    uint32_t ci, cw;
+    __device__ __forceinline__ uint8_t operator()(uint64_t q)
+    {
+        const uint32_t o = (uint32_t)(q - base), wi = o >> 2;
+        if (wi != ci) { ci = wi; cw = w[wi]; }
+        return (uint8_t)(cw >> (8 * (o & 3)));
+    }
+};
+
+template <typename Get>
+__device__ __forceinline__ void fp_id_bounds(Get &get, uint64_t b, uint64_t e, uint64_t &ib,
+                                             uint64_t &ie)
 {
-    const uint64_t li = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (li >= n_lines) return;
-    const uint64_t b = line_start[li], e = li < n_nl ? line_start[li + 1] - 1 : len;
     uint64_t p = b;
-    while (p < e && fp_is_space(text[p])) p++;
-    const uint64_t ib = p;
-    while (p < e && !fp_is_space(text[p])) p++;
-    const uint64_t ie = p;
-    // `while (iss >> v)`: optional sign, digits; a non-digit or an overflow ends the line
+    while (p < e && fp_is_space(get(p))) p++;
+    ib = p;
+    while (p < e && !fp_is_space(get(p))) p++;
+    ie = p;
+}
+
+template <typename Get>
+__device__ __forceinline__ void fp_parse_line(Get get, uint64_t li, uint64_t b, uint64_t e,
+                                              uint64_t prev_b, uint32_t seed, uint32_t use64,
+                                              uint64_t *__restrict__ id_off,
+                                              uint32_t *__restrict__ id_len,
+                                              uint32_t *__restrict__ n_vals,
+                                              void *__restrict__ hash,
+                                              uint8_t *__restrict__ new_id)
+{
+    uint64_t ib, ie;
+    fp_id_bounds(get, b, e, ib, ie);
+    uint64_t p = ie;
+    // `while (iss >> v)`: optional sign, digits; a non-digit or an overflow ends the line.
+    // c = the byte at p, 0 past the line end (0 is no space, sign or digit, as a NUL byte)
     uint64_t h1 = seed, h2 = seed, pend = 0, nv = 0;
     if (ie > ib) {
+        uint8_t c = p < e ? get(p) : 0;
         for (;;) {
-            while (p < e && fp_is_space(text[p])) p++;
+            while (fp_is_space(c)) { p++; c = p < e ? get(p) : 0; }
             bool neg = false;
-            if (p < e && (text[p] == '+' || text[p] == '-')) { neg = text[p] == '-'; p++; }
-            if (p >= e || text[p] < '0' || text[p] > '9') break;
+            if (c == '+' || c == '-') { neg = c == '-'; p++; c = p < e ? get(p) : 0; }
+            if (c < '0' || c > '9') break;
             uint64_t v = 0;
             bool ovf = false;
-            while (p < e && text[p] >= '0' && text[p] <= '9') {
-                const uint64_t d = (uint64_t)(text[p] - '0');
+            while (c >= '0' && c <= '9') {
+                const uint64_t d = (uint64_t)(c - '0');
                 if (v > (~0ULL - d) / 10) ovf = true;
                 v = v * 10 + d;
                 p++;
+                c = p < e ? get(p) : 0;
             }
             if (ovf) break;
             if (neg) v = 0 - v;
@@ -135,18 +190,52 @@ __global__ __launch_bounds__(256) void fp_line_kernel(
     // line 0 is compared with the previous file's last ID by the host (2 = unknown)
     uint8_t nid = 2;
     if (li > 0) {
-        uint64_t q = line_start[li - 1];
-        const uint64_t qe = line_start[li] - 1;
-        while (q < qe && fp_is_space(text[q])) q++;
-        const uint64_t pb = q;
-        while (q < qe && !fp_is_space(text[q])) q++;
+        uint64_t pb, pe;
+        Get gp = get;                                        // its own word cache
+        fp_id_bounds(gp, prev_b, b - 1, pb, pe);
         nid = 0;
-        if (q - pb != ie - ib) nid = 1;
+        if (pe - pb != ie - ib) nid = 1;
         else
             for (uint64_t t = 0; t < ie - ib; t++)
-                if (text[pb + t] != text[ib + t]) { nid = 1; break; }
+                if (gp(pb + t) != get(ib + t)) { nid = 1; break; }
     }
     new_id[li] = nid;
+}
+
+__global__ __launch_bounds__(256) void fp_line_kernel(
+    const uint8_t *__restrict__ text, uint64_t len, const uint64_t *__restrict__ line_start,
+    uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
+    uint64_t *__restrict__ id_off, uint32_t *__restrict__ id_len, uint32_t *__restrict__ n_vals,
+    void *__restrict__ hash, uint8_t *__restrict__ new_id)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t span[4][kFpSpan];
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t l0 = (uint64_t)blockIdx.x * 256 + wave * 64;
+    // the wave's span: from the 16-B block holding the previous line's start to the end of
+    // its last line (the text buffer has 16 bytes of padding past len)
+    uint64_t s0 = 0, s1 = 0;
+    if (l0 < n_lines) {
+        s0 = line_start[l0 > 0 ? l0 - 1 : 0] & ~15ULL;
+        const uint64_t ll = min(l0 + 63, n_lines - 1);
+        s1 = ll < n_nl ? line_start[ll + 1] : len;
+    }
+    const bool staged = l0 < n_lines && s1 - s0 <= kFpSpan;
+    if (staged)
+        for (uint64_t off = lane * 16; s0 + off < s1; off += 64 * 16)
+            *reinterpret_cast<uint4 *>(&span[wave][off]) =
+                *reinterpret_cast<const uint4 *>(text + s0 + off);
+    __syncthreads();
+    const uint64_t li = l0 + lane;
+    if (li >= n_lines) return;
+    const uint64_t b = line_start[li], e = li < n_nl ? line_start[li + 1] - 1 : len;
+    const uint64_t prev_b = li > 0 ? line_start[li - 1] : 0;
+    if (staged) {
+        fp_parse_line(SpanBytes{reinterpret_cast<const uint32_t *>(span[wave]), s0, ~0u, 0u}, li,
+                      b, e, prev_b, seed, use64, id_off, id_len, n_vals, hash, new_id);
+    } else {
+        fp_parse_line([&](uint64_t q) { return text[q]; }, li, b, e, prev_b, seed, use64,
+                      id_off, id_len, n_vals, hash, new_id);
+    }
 }
 
 uint32_t text_blocks(uint64_t len) { return (uint32_t)((len + kTextChunk - 1) / kTextChunk); }

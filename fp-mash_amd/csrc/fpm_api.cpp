@@ -13,6 +13,7 @@
 #include <array>
 #include <cstdlib>
 #include <memory>
+#include <mutex>
 #include <cstdio>
 #include <atomic>
 #include <cstring>
@@ -106,7 +107,53 @@ struct fpm_ctx {
     void *ring[kRing] = {};
     hipEvent_t ring_ev[kRing] = {};
     hipStream_t copy = nullptr;
+    // device buffers of released -fp text jobs, reused by the next jobs: a fresh hipMalloc of
+    // tens of MB is cleared by the driver before first use, and a kernel writing it could wait
+    // ~27 ms for that (tools/micro/fp_text_time.py under rocprofv3: fp_line_kernel 0.06 ms,
+    // now and then 27 ms)
+    static constexpr size_t kPoolBytes = size_t(2) << 30;
+    std::vector<std::pair<void *, size_t>> pool;
+    size_t pool_bytes = 0;
+    std::mutex pool_mu;
 };
+
+// smallest pooled buffer of >= bytes (and at most 4x: a 1 GB buffer is not kept busy by a
+// 1 KB request), else a new one
+static hipError_t pool_alloc(fpm_ctx *ctx, void **p, size_t bytes)
+{
+    {
+        std::lock_guard<std::mutex> g(ctx->pool_mu);
+        size_t best = SIZE_MAX, bi = 0;
+        for (size_t i = 0; i < ctx->pool.size(); i++) {
+            const size_t b = ctx->pool[i].second;
+            if (b >= bytes && b <= 4 * bytes + 4096 && b < best) { best = b; bi = i; }
+            if (best == bytes) break;
+        }
+        if (best != SIZE_MAX) {
+            *p = ctx->pool[bi].first;
+            ctx->pool_bytes -= best;
+            ctx->pool[bi] = ctx->pool.back();
+            ctx->pool.pop_back();
+            return hipSuccess;
+        }
+    }
+    return hipMalloc(p, bytes);
+}
+
+// back to the pool (the caller's stream work on it is complete), or freed past kPoolBytes
+static void pool_free(fpm_ctx *ctx, void *p, size_t bytes)
+{
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(ctx->pool_mu);
+        if (ctx->pool_bytes + bytes <= fpm_ctx::kPoolBytes) {
+            ctx->pool.push_back({p, bytes});
+            ctx->pool_bytes += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
 
 static hipError_t ensure_ring(fpm_ctx *ctx)
 {
@@ -371,6 +418,7 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
     }
     if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
+    for (auto &b : ctx->pool) (void)hipFree(b.first);
     delete ctx;
 }
 
@@ -1323,16 +1371,23 @@ struct fpm_fptext {
     uint32_t *d_id_len = nullptr, *d_n_vals = nullptr;
     void *d_hash = nullptr;
     uint8_t *d_new_id = nullptr;
+    std::vector<std::pair<void *, size_t>> bufs;   // every buffer above, with its size
+    template <typename T> hipError_t alloc(T **p, size_t bytes)
+    {
+        void *q = nullptr;
+        const hipError_t e = pool_alloc(ctx, &q, bytes);
+        if (e == hipSuccess) { bufs.push_back({q, bytes}); *p = static_cast<T *>(q); }
+        return e;
+    }
 };
 
 static void fptext_release(fpm_fptext *j)
 {
     if (!j) return;
     (void)hipSetDevice(j->ctx->device);
-    for (void *p : {(void *)j->d_text, (void *)j->d_line_start, (void *)j->d_blk,
-                    (void *)j->d_id_off, (void *)j->d_id_len, (void *)j->d_n_vals, j->d_hash,
-                    (void *)j->d_new_id})
-        if (p) (void)hipFree(p);
+    // the job's kernels ran on the context stream: done before its buffers are handed out again
+    (void)hipStreamSynchronize(j->ctx->stream);
+    for (auto &b : j->bufs) pool_free(j->ctx, b.first, b.second);
 }
 
 extern "C" {
@@ -1351,8 +1406,8 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
     hipStream_t st = ctx->stream;
     const uint32_t nb = text_blocks(text_len);
     const uint64_t scan_w = scan_scratch_words(nb ? nb : 1);
-    HIP_TRY(hipMalloc(&j->d_text, text_len + 16));
-    HIP_TRY(hipMalloc(&j->d_blk, ((size_t)2 * nb + 2 + scan_w) * 4));
+    HIP_TRY(j->alloc(&j->d_text, text_len + 16));
+    HIP_TRY(j->alloc(&j->d_blk, ((size_t)2 * nb + 2 + scan_w) * 4));
     if (text_len) HIP_TRY(h2d_staged(ctx, j->d_text, text, text_len));
     uint32_t *blk_cnt = j->d_blk, *blk_off = j->d_blk + nb, *scan_s = j->d_blk + 2 * nb + 2;
     // newline count first: it sizes the line index
@@ -1368,7 +1423,7 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
         HIP_TRY(hipStreamSynchronize(st));
         n_nl = tot;
     }
-    HIP_TRY(hipMalloc(&j->d_line_start, (n_nl + 1) * 8));
+    HIP_TRY(j->alloc(&j->d_line_start, (n_nl + 1) * 8));
     HIP_TRY(hipMemsetAsync(j->d_line_start, 0, 8, st));
     if (n_nl) {
         TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
@@ -1379,11 +1434,11 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
     const uint64_t nl = std::min(total, max_lines);
     j->n_lines = nl;
     if (nl) {
-        HIP_TRY(hipMalloc(&j->d_id_off, nl * 8));
-        HIP_TRY(hipMalloc(&j->d_id_len, nl * 4));
-        HIP_TRY(hipMalloc(&j->d_n_vals, nl * 4));
-        HIP_TRY(hipMalloc(&j->d_hash, nl * (use64 ? 8 : 4)));
-        HIP_TRY(hipMalloc(&j->d_new_id, nl));
+        HIP_TRY(j->alloc(&j->d_id_off, nl * 8));
+        HIP_TRY(j->alloc(&j->d_id_len, nl * 4));
+        HIP_TRY(j->alloc(&j->d_n_vals, nl * 4));
+        HIP_TRY(j->alloc(&j->d_hash, nl * (use64 ? 8 : 4)));
+        HIP_TRY(j->alloc(&j->d_new_id, nl));
         TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
         HIP_TRY(launch_fp_lines(j->d_text, text_len, j->d_line_start, n_nl, nl, seed, use64,
                                 j->d_id_off, j->d_id_len, j->d_n_vals, j->d_hash, j->d_new_id, st));

@@ -11,7 +11,7 @@ text = datagen.cfl_text(datagen.random_dna(50, 2000, seed=3), datagen.lyn2vec_id
 with fpmash.Context(0) as ctx:
     for warm in (text[:100000], text):
         ctx.fp_text(warm, max_lines=1_000_000)
-    for rep in range(3):
+    for rep in range(int(os.environ.get('REPS', 3))):
         ctx.reset_timing(); ctx.set_timing(True)
         t0 = time.perf_counter()
         r = ctx.fp_text(text, max_lines=1_000_000)
