@@ -4,6 +4,11 @@
 #include "Command.h"
 #include "Timing.h"
 
+#include <cstdio>
+#include <cstdlib>
+#include <iostream>
+#include <unistd.h>
+
 int main(int argc, const char **argv)
 {
     fpmhost::phaseMark("start");
@@ -15,5 +20,16 @@ int main(int argc, const char **argv)
     commandList.addCommand(new fpmhost::CommandTriangle());
     const int rc = commandList.run(argc, argv);
     fpmhost::phaseMark("command done");
+    // Every output is written and the device work is complete (results were fetched): leave
+    // without the HIP runtime's teardown (context, stream and code-object release run from
+    // atexit and the library destructors), which the kernel driver does with the process
+    // anyway.  FPMASH_CLEAN_EXIT=1 keeps the full teardown.
+    const char *clean = getenv("FPMASH_CLEAN_EXIT");
+    if (!(clean && *clean && *clean != '0')) {
+        std::cout.flush();
+        std::cerr.flush();
+        fflush(nullptr);
+        _exit(rc);
+    }
     return rc;
 }

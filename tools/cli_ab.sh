@@ -1,0 +1,12 @@
+set -o pipefail
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "cli" > gpurun_out/t_cli.log 2>&1 || { tail -20 gpurun_out/t_cli.log; exit 1; }
+tail -2 gpurun_out/t_cli.log
+for i in 1 2; do
+for e in 1 0; do
+FPMASH_CLEAN_EXIT=$e timeout -k 10 300 python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-split > gpurun_out/cli_$e$i.json 2>gpurun_out/cli_$e$i.err || { tail -20 gpurun_out/cli_$e$i.err; exit 1; }
+python3 -c "
+import json; d=json.loads(open('gpurun_out/cli_$e$i.json').read().strip().splitlines()[-1]); c=d['cli']
+print('clean_exit=$e', round(c['cli_sketch_wall_s'],3), round(c['cli_dist_wall_s'],3), c['parity']['ok'], {k:round(v,1) for k,v in c['phases_ms_sketch'].items()})"
+done
+done
