@@ -86,6 +86,7 @@ struct fpm_ctx {
     // of after the probe
     bool fill_early = false;
     bool fill_pre_probe = false;   // FPM_FILL_AT=probe: the side fill starts with the probe
+    double fill_split = 0;         // FPM_FILL_SPLIT=f: that fraction of rows beside the probe
     int fill_counts = -1;      // the side-stream fill also writes the numer / denom defaults
                                // (-1: for grids of >= 2^28 pairs; FPM_FILL_COUNTS=0/1 forces)
     int last_sparse = 0;
@@ -387,6 +388,7 @@ int fpm_ctx_create(int device, fpm_ctx **out)
     if (const char *v = getenv("FPM_FILL_EARLY")) ctx->fill_early = atoi(v) != 0;
     if (const char *v = getenv("FPM_FILL_COUNTS")) ctx->fill_counts = atoi(v) != 0 ? 1 : 0;
     if (const char *v = getenv("FPM_FILL_AT")) ctx->fill_pre_probe = strcmp(v, "probe") == 0;
+    if (const char *v = getenv("FPM_FILL_SPLIT")) ctx->fill_split = atof(v);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -1809,24 +1811,37 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     // heavier fill beside the rank kernel costs more than the probe saves), so by grid size.
     const bool fill_cnt = fin && !fin->prefilled &&
                           (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0);
-    auto launch_fill = [&]() -> int {
+    // the side fill of query rows [fill_from, q1): from the current point of `st`
+    uint32_t fill_from = 0;
+    auto launch_fill_rows = [&](uint32_t q1) -> int {
+        const uint32_t q0 = fill_from;
+        const uint64_t off = (uint64_t)q0 * n_ref;
         PairFill fill;
-        fill.dist = fin->dist;
-        fill.pval = fin->pval;
-        fill.pass = fin->pass;
+        fill.dist = fin->dist + off;
+        fill.pval = fin->pval + off;
+        fill.pass = fin->pass + off;
         fill.max_dist = fin->max_dist;
         fill.max_pvalue = fin->max_pvalue;
+        Counts c{};
+        if (fill_cnt) {
+            const uint64_t cb = off * (cnt.c16 ? 2 : 4);
+            c = cnt;
+            c.numer = (char *)cnt.numer + cb;
+            c.denom = (char *)cnt.denom + cb;
+        }
         HIP_TRY(ensure_aux(ctx));
         HIP_TRY(hipEventRecord(ctx->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size,
-                                 fill_cnt ? cnt : Counts{}, fill, ctx->aux));
+        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len + q0, q1 - q0, sketch_size, c, fill,
+                                 ctx->aux));
         tl.done();
         HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
-        fill_pending = true;
+        fill_from = q1;
+        fill_pending = q1 == n_qry;
         return FPM_OK;
     };
+    auto launch_fill = [&]() -> int { return launch_fill_rows(n_qry); };
     if (try_sparse && fin && ctx->fill_early && !fin->prefilled)
         if (int rc = launch_fill()) return rc;
     if (try_sparse) {
@@ -1966,6 +1981,13 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // in place, so it waits for the fill instead.
             if (fin && !fin->prefilled && ctx->fill_pre_probe && !fill_pending)
                 if (int rc = launch_fill()) return rc;
+            // FPM_FILL_SPLIT=f: the first f of the query rows filled beside the probe, the rest
+            // beside the candidate compare (rows in multiples of 8: 16-B aligned row starts)
+            if (fin && !fin->prefilled && ctx->fill_split > 0 && !fill_pending && fill_from == 0) {
+                const uint32_t qs = (uint32_t)(n_qry * ctx->fill_split) & ~7u;
+                if (qs > 0 && qs < n_qry)
+                    if (int rc = launch_fill_rows(qs)) return rc;
+            }
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
@@ -1984,7 +2006,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 }
             } else if (fin) {
                 if (!fill_pending)
-                    if (int rc = launch_fill()) return rc;
+                    if (int rc = launch_fill()) return rc;   // the rows not filled yet
                 if (rows_merge) {
                     void *cres;
                     HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
