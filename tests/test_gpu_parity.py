@@ -391,6 +391,11 @@ def _fp_texts():
         lines.append(idv + sep + sep.join(str(v).encode() for v in vals))
     texts.append(b"\n".join(lines))
     texts.append(D.cfl_text(D.random_dna(30, 300, seed=4), D.lyn2vec_ids(30)))
+    # lines of ~1.5 KB: a wave's 64 lines span more than fp_line_kernel's 4 KB LDS window
+    # (global-memory path), after and between short lines (staged waves)
+    long_lines = [b"L%d " % (i // 3) + b" ".join(str(v).encode() for v in rng.integers(0, 2 ** 40, 120))
+                  for i in range(150)]
+    texts.append(b"\n".join(lines[:200] + long_lines + lines[200:400]) + b"\n")
     return texts
 
 
