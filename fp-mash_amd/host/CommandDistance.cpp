@@ -6,8 +6,10 @@
 #include "Device.h"
 #include "Sketch.h"
 #include "Timing.h"
+#include "HostRows.h"
 
 #include <algorithm>
+#include <memory>
 #include <chrono>
 #include <atomic>
 #include <cmath>
@@ -211,10 +213,13 @@ int CommandDistance::run() const
     const bool use64 = sketchRef.getUse64();
     const uint32_t hb = use64 ? 8 : 4;
     // dense device layout: one row per sketch
-    auto pack = [&](const Sketch &sk, std::vector<uint8_t> &m, std::vector<uint32_t> &len,
-                    std::vector<uint64_t> &L, uint64_t width) {
+    // (zero pages, populated in one call: a value-initialised vector paid a memset and ~20k
+    // page faults on one thread for C2's 80 MB)
+    auto pack = [&](const Sketch &sk, std::unique_ptr<HostRows<uint8_t>> &mp,
+                    std::vector<uint32_t> &len, std::vector<uint64_t> &L, uint64_t width) {
         const uint64_t n = sk.getReferenceCount();
-        m.assign(std::max<uint64_t>(1, n * width) * hb, 0);
+        mp = std::make_unique<HostRows<uint8_t>>(std::max<uint64_t>(1, n * width) * hb);
+        uint8_t *m = mp->data();
         len.resize(n);
         L.resize(n);
         for (uint64_t i = 0; i < n; i++) {
@@ -273,12 +278,12 @@ int CommandDistance::run() const
             check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
             check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
         });
-    std::vector<uint8_t> R, Qown;
+    std::unique_ptr<HostRows<uint8_t>> R, Qown;
     std::vector<uint32_t> rl, qlOwn;
     std::vector<uint64_t> rL, qLOwn;
     pack(sketchRef, R, rl, rL, width);
     if (!sameSet) pack(sketchQuery, Qown, qlOwn, qLOwn, width);
-    const std::vector<uint8_t> &Q = sameSet ? R : Qown;
+    const uint8_t *Q = sameSet ? R->data() : Qown->data();
     const std::vector<uint32_t> &ql = sameSet ? rl : qlOwn;
     const std::vector<uint64_t> &qL = sameSet ? rL : qLOwn;
 
@@ -289,7 +294,7 @@ int CommandDistance::run() const
     // :276-333, consumes the pool's outputs in order).
     std::vector<fpm_refset *> sets(nDev, nullptr);
     for (int d = 0; d < nDev; d++)
-        check(fpm_refset_create(device(d), R.data(), rl.data(), rL.data(), width, (uint32_t)nR,
+        check(fpm_refset_create(device(d), R->data(), rl.data(), rL.data(), width, (uint32_t)nR,
                                 hb, (uint32_t)sketchSize, &sets[d]),
               "dist reference set");
     for (auto &t : pinner) t.join();
@@ -387,7 +392,7 @@ int CommandDistance::run() const
                     cv.wait(lk, [&] { return written + nSlots > b; });
                 }
                 const uint64_t q0 = b * block, nq = std::min(block, nQ - q0);
-                check(fpm_refset_dist(sets[d], Q.data() + q0 * width * hb, ql.data() + q0,
+                check(fpm_refset_dist(sets[d], Q + q0 * width * hb, ql.data() + q0,
                                       qL.data() + q0, width, (uint32_t)nq, (uint32_t)sketchSize,
                                       (uint32_t)sketchRef.getKmerSize(), sketchRef.getKmerSpace(),
                                       distanceMax, pValueMax, sl.nu, sl.de, sl.di, sl.pv, sl.pa),

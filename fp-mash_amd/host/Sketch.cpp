@@ -5,6 +5,7 @@
 #include "Msh.h"
 #include "SeqReader.h"
 #include "Timing.h"
+#include "HostRows.h"
 
 #include <cmath>
 #include <cstdio>
@@ -15,7 +16,6 @@
 #include <atomic>
 #include <thread>
 #include <algorithm>
-#include <sys/mman.h>
 #include <sys/stat.h>
 
 namespace fpmhost {
@@ -201,30 +201,6 @@ int hostRecords(const std::string &image, std::vector<SeqRec> &out, std::string 
 }
 
 }  // namespace
-
-// Host array for the device's sketch rows (80 MB at C2): anonymous pages (zero, no memset),
-// huge pages where the kernel allows them, populated up front in one call instead of ~20k
-// first-touch page faults inside the fetch copy (a value-initialised std::vector paid both).
-template <typename T>
-struct HostRows {
-    T *p = nullptr;
-    size_t bytes = 0;
-    explicit HostRows(size_t n) : bytes(std::max<size_t>(n * sizeof(T), 1))
-    {
-        void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-        if (q == MAP_FAILED) throw std::bad_alloc();
-        (void)madvise(q, bytes, MADV_HUGEPAGE);
-#ifdef MADV_POPULATE_WRITE
-        (void)madvise(q, bytes, MADV_POPULATE_WRITE);   // best effort (Linux >= 5.14)
-#endif
-        p = static_cast<T *>(q);
-    }
-    ~HostRows() { munmap(p, bytes); }
-    HostRows(const HostRows &) = delete;
-    HostRows &operator=(const HostRows &) = delete;
-    T *data() { return p; }
-    T *begin() { return p; }
-};
 
 // Parse and sketch the sequence files [f0, f1) on one device (the reference's per-file work,
 // Sketch.cpp:249-397 / 478-522 / 1299-1488): fills fileRefs[f] for those files.
