@@ -259,10 +259,10 @@ def fp_text_leg(ctx, reps=5):
     lines = text.count(b"\n")
     for warm in (text[:100000], text):                             # warm (pinned ring too)
         ctx.fp_text(warm, max_lines=1_000_000)
-    # per call: the HIP-event total of its launches.  The median is reported: an event pair
-    # now and then brackets a host-side stall before the dispatch (one call of 3 read 28 ms
-    # against 0.23 ms for the others, while rocprofv3's kernel trace of the same script gave
-    # 0.24 ms per call; tools/micro/fp_text_time.py)
+    # per call: the HIP-event total of its launches.  The median is reported: one call in a
+    # process (the 4th, every run) has its fp_line launch take 21-29 ms in rocprofv3's trace
+    # too, pooled or fresh buffers alike, against ~0.12 ms for every other call
+    # (tools/micro/fp_text_time.py, profiles/r02/fp_text_time.log); the list is in the line
     devs, walls = [], []
     for _ in range(reps):
         ctx.reset_timing()
