@@ -497,89 +497,136 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
            steps=3, warmup=1, parity=True):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
     the ranks (strong scaling).  A timed step is the whole job on every rank:
-      1. sketch its contiguous shard of families (each family generated from its own seed,
+      1. sketch its contiguous block of families (each family generated from its own seed,
          so the data does not depend on the GPU count);
-      2. all-gather the sketch rows, counts and lengths (RCCL over xGMI, the "nccl" backend,
+      2. all-gather the sketch rows and counts (RCCL over xGMI, the "nccl" backend,
          N x s x 8 B = 400 MB at n = 50k) -- the job's only exchange: the reference set fits
          every GPU's HBM many times over, so no min-merge / ring rotation is needed;
-      3. dist of its query rows against all n references: shared-hash counts, distance,
-         FP64 p-value, pass flags, left in HBM (the index over the references is built
-         inside the step).
-    With one rank there is no gather and the queries are the references (the library's
-    symmetric self path)."""
-    from fpmash.shard import all_gather_rows, shard_range
+      3. its share of the n x n grid (fpmash.shard.pair_block_jobs): every unordered pair of
+         blocks is compared on one rank and written twice (the grid and its transpose:
+         sorted sketches give symmetric results), so each rank indexes only its own block
+         (plus, for even N, one more block), compares ~n^2 / 2N pairs and writes ~n^2 / N
+         cells: shared-hash counts, distance, FP64 p-value, pass flags, left in HBM (the
+         indexes are rebuilt inside the step).
+    With one rank there is no gather and the whole grid is the library's symmetric self
+    path (fpm_dist_dev16 with the queries = the references)."""
+    import ctypes as C
+    from fpmash.shard import all_gather_rows, pair_block_jobs, shard_range
     fams = n // members
     n = fams * members
-    f_lo, f_hi = shard_range(fams, ws, rank)
-    lo, hi = f_lo * members, f_hi * members
+    bounds = [tuple(x * members for x in shard_range(fams, ws, r)) for r in range(ws)]
+    lo, hi = bounds[rank]
     n_loc = hi - lo
     seqs = []
-    for f in range(f_lo, f_hi):
+    for f in range(lo // members, hi // members):
         seqs += datagen.family_dna(1, members, seq_len, sub_rate=(0.01, 0.10), seed=4000 + f)
     P = fpmash.make_params(k=k, s=s)
     job = ctx.sketch_job(P, seqs)
     d_rows, d_cnt, _ng, stride = job.device_output()
     L = fpmash.lib()
     st = ctx.stream
-    outs = [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]
     g = {}
+    jobs = pair_block_jobs(bounds, rank)
     if ws > 1:
         import torch
         # RCCL gathers device tensors over xGMI; without an nccl group (the 2-rank GPU test
-        # on one card) the same rows go through gloo on host tensors and back to the device
+        # on one card) the same rows go through gloo on host tensors and back to the device.
+        # The gathered rows land in persistent buffers (the refsets borrow pointers into them)
         on_dev = grp.nccl is not None
         dev = torch.device(f"cuda:{local}") if on_dev else torch.device("cpu")
         loc_rows = torch.empty((n_loc, stride), dtype=torch.int64, device=dev)
         loc_cnt = torch.empty((n_loc, 1), dtype=torch.int32, device=dev)
         loc_len = torch.full((n_loc, 1), seq_len, dtype=torch.int64, device=dev)
-        g["len"] = all_gather_rows(loc_len, n, ws, group=grp.nccl)
-        if not on_dev:
+        g["rows"] = torch.empty((n, stride), dtype=torch.int64, device=dev)
+        g["cnt"] = torch.empty((n, 1), dtype=torch.int32, device=dev)
+        g["len"] = all_gather_rows(loc_len, n, ws, group=grp.nccl, bounds=bounds)
+        if on_dev:
+            torch.cuda.synchronize(dev)
+            R, C_, Ln = g["rows"].data_ptr(), g["cnt"].data_ptr(), g["len"].data_ptr()
+        else:
             g["d_rows"] = fpmash.DeviceBuffer(ctx, n * stride * 8)
             g["d_cnt"] = fpmash.DeviceBuffer(ctx, n * 4)
             g["d_len"] = fpmash.DeviceBuffer.from_array(ctx, g["len"].numpy())
+            R, C_, Ln = g["d_rows"].ptr, g["d_cnt"].ptr, g["d_len"].ptr
+        outs = []
+        for j in jobs:
+            (rl, rh), (ql, qh) = j["ref"], j["qry"]
+            cells = (rh - rl) * (qh - ql)
+            o = {"p": [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]}
+            if j["kind"] == "mirror":
+                o["m"] = [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]
+            outs.append(o)
     else:
         d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, seq_len, np.uint64))
+        outs = [{"p": [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]}]
+    refsets = {}
     phase = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
+
+    def gather():
+        if on_dev:
+            fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
+            fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
+        else:
+            fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
+            fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
+        ctx.synchronize()
+        all_gather_rows(loc_rows, n, ws, group=grp.nccl, bounds=bounds, out=g["rows"])
+        all_gather_rows(loc_cnt, n, ws, group=grp.nccl, bounds=bounds, out=g["cnt"])
+        if on_dev:
+            torch.cuda.synchronize(dev)
+        else:
+            fpmash._check(L.fpm_memcpy_h2d(ctx.h, R, g["rows"].data_ptr(), n * stride * 8))
+            fpmash._check(L.fpm_memcpy_h2d(ctx.h, C_, g["cnt"].data_ptr(), n * 4))
+
+    def dist_share():
+        for rs in refsets.values():
+            fpmash._check(L.fpm_refset_reindex(rs, st))
+        for j, o in zip(jobs, outs):
+            (rl, rh), (ql, qh) = j["ref"], j["qry"]
+            rs = refsets[(rl, rh)]
+            q = (R + ql * stride * 8, C_ + ql * 4, Ln + ql * 8, stride, qh - ql)
+            if j["kind"] == "self":
+                fpmash._check(L.fpm_refset_dist_dev(rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
+                                                    *[b.ptr for b in o["p"]], st))
+            else:
+                fpmash._check(L.fpm_refset_dist_mirror_dev(
+                    rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0, *[b.ptr for b in o["p"]],
+                    *[b.ptr for b in o["m"]], st))
 
     def run(timed):
         t0 = time.perf_counter()
         job.run(st)
         if timed:
             ctx.synchronize()
+        t1 = time.perf_counter()
         if ws > 1:
-            if on_dev:
-                fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_rows.data_ptr(), d_rows,
-                                               n_loc * stride * 8))
-                fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
-            else:
-                fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_rows.data_ptr(), d_rows,
-                                               n_loc * stride * 8))
-                fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
-            ctx.synchronize()
-            t1 = time.perf_counter()
-            g["rows"] = all_gather_rows(loc_rows, n, ws, group=grp.nccl)
-            g["cnt"] = all_gather_rows(loc_cnt, n, ws, group=grp.nccl)
-            if on_dev:
-                torch.cuda.synchronize(dev)
-                R, C_, Ln = g["rows"].data_ptr(), g["cnt"].data_ptr(), g["len"].data_ptr()
-            else:
-                fpmash._check(L.fpm_memcpy_h2d(ctx.h, g["d_rows"].ptr, g["rows"].data_ptr(),
-                                               n * stride * 8))
-                fpmash._check(L.fpm_memcpy_h2d(ctx.h, g["d_cnt"].ptr, g["cnt"].data_ptr(), n * 4))
-                R, C_, Ln = g["d_rows"].ptr, g["d_cnt"].ptr, g["d_len"].ptr
-        else:
-            t1 = time.perf_counter()
-            R, C_, Ln = d_rows, d_cnt, d_len.ptr
+            gather()
         t2 = time.perf_counter()
-        fpmash._check(L.fpm_dist_dev16(ctx.h, R, C_, Ln, stride, n, R + lo * stride * 8,
-                                     C_ + lo * 4, Ln + lo * 8, stride, n_loc, 8, s, k, 4.0 ** k,
-                                     1.0, 1.0, *[o.ptr for o in outs], st))
+        if ws > 1:
+            dist_share()
+        else:
+            fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                         d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
+                                         1.0, 1.0, *[b.ptr for b in outs[0]["p"]], st))
         if timed:
             ctx.synchronize()
             t3 = time.perf_counter()
             phase["sketch"] += t1 - t0
             phase["gather"] += t2 - t1
             phase["dist"] += t3 - t2
+    if ws > 1:
+        # the indexes live as long as the leg (rebuilt in every step by fpm_refset_reindex)
+        job.run(st)
+        ctx.synchronize()
+        gather()
+        for j in jobs:
+            rl, rh = j["ref"]
+            if (rl, rh) not in refsets:
+                h = C.c_void_p()
+                fpmash._check(L.fpm_refset_create_dev(ctx.h, R + rl * stride * 8, C_ + rl * 4,
+                                                      Ln + rl * 8, stride, rh - rl, 8, s,
+                                                      C.byref(h)))
+                refsets[(rl, rh)] = h
     for _ in range(warmup):
         run(False)
     ctx.synchronize()
@@ -596,7 +643,8 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     run(True)                                   # one more step, phase-timed (not in el)
     par = None
     if parity and (rank == 0 or parity == "all"):
-        # the CPU leg's checker: 50 of this rank's query rows x all n references
+        # the CPU leg's checker: sampled rows of each of this rank's grids (and their
+        # transposes) x all their references
         from oracle import oracle as O
         t_c = time.perf_counter()
         if ws > 1:
@@ -605,27 +653,47 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         else:
             rows_h, cnt_h = job.fetch()
         refs = [rows_h[i, :cnt_h[i]] for i in range(n)]
-        lens = [seq_len] * n
-        q = sample_rows(n_loc, 50, salt=4)
-        gr = O.dist_grid(refs, lens, [refs[lo + int(x)] for x in q], [seq_len] * len(q), s, k,
-                         4.0 ** k, threads=_threads())
-        par = check_grid_rows(outs, n, q, gr)
-        par["check_s"] = time.perf_counter() - t_c
-    for b in outs:
-        b.free()
+        grids = []
+        for j, o in zip(jobs, outs):
+            (rl, rh), (ql, qh) = j["ref"], j["qry"]
+            grids.append((o["p"], (rl, rh), (ql, qh)))
+            if j["kind"] == "mirror":
+                grids.append((o["m"], (ql, qh), (rl, rh)))
+        per = max(4, 50 // len(grids))
+        res = []
+        for gi, (bufs, (rl, rh), (ql, qh)) in enumerate(grids):
+            q = sample_rows(qh - ql, per, salt=4 + gi)
+            gr = O.dist_grid(refs[rl:rh], [seq_len] * (rh - rl), [refs[ql + int(x)] for x in q],
+                             [seq_len] * len(q), s, k, 4.0 ** k, threads=_threads())
+            res.append(check_grid_rows(bufs, rh - rl, q, gr))
+        par = {"grids": len(grids), "rows": int(sum(r_["rows"] for r_ in res)),
+               "pairs": int(sum(r_["pairs"] for r_ in res)),
+               "pairs_sharing": int(sum(r_["pairs_sharing"] for r_ in res)),
+               "ok": all(r_["ok"] for r_ in res), "check_s": time.perf_counter() - t_c}
+    for rs in refsets.values():
+        L.fpm_refset_free(rs)
+    for o in outs:
+        for bl in o.values():
+            for b in bl:
+                b.free()
     if ws == 1:
         d_len.free()
     for key in ("d_rows", "d_cnt", "d_len"):
         if key in g:
             g[key].free()
     job.free()
+    cells = sum((j["ref"][1] - j["ref"][0]) * (j["qry"][1] - j["qry"][0]) *
+                (2 if j["kind"] == "mirror" else 1) for j in jobs)
     return {"config": f"C4: all-vs-all dist of {n} family-structured {seq_len} bp sketches "
-                      f"(k={k}, s={s}); a step = sketch own shard + all-gather of the sketch "
-                      f"rows (RCCL) + dist of own query rows vs all, {ws} GPU(s)",
+                      f"(k={k}, s={s}); a step = sketch own block + all-gather of the sketch "
+                      f"rows (RCCL) + this rank's block pairs (each unordered pair compared once, "
+                      f"grid + transpose written), {ws} GPU(s)",
             "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
             "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
+            "jobs_rank0": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
+                           for j in jobs], "cells_rank0": cells,
             "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
             "candidates_all_ranks": cand, "parity": par}
 
@@ -842,12 +910,15 @@ def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21,
     if parity and rank == 0:
         from oracle import oracle as O
         t_c = time.perf_counter()
-        idx = sorted({0, n_genomes - 1})
+        # parity="all" (the multi-rank GPU test): every genome, so the reassembled file order
+        # is checked across the shard boundaries too
+        idx = list(range(n_genomes)) if parity == "all" else sorted({0, n_genomes - 1})
         exp = O.sketch_batch(O.params(k=k, s=s), [c5_genome(g, length) for g in idx],
-                             threads=2)
+                             threads=max(2, min(len(idx), _threads())))
         ok = [bool(int(cnt_all[g]) == len(e) and np.array_equal(rows_all[g, :len(e)], e))
               for g, e in zip(idx, exp)]
         out["parity"] = {"genomes_checked": idx, "sketch_exact": ok, "ok": all(ok),
+                         "shards": balanced_file_shards(lengths, ws),
                          "check_s": time.perf_counter() - t_c}
     return out
 

@@ -918,7 +918,8 @@ __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
     C *__restrict__ numer, C *__restrict__ denom,
     const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
     uint32_t n_ref, uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
-    double *__restrict__ dist, double *__restrict__ pval, uint8_t *__restrict__ pass)
+    double *__restrict__ dist, double *__restrict__ pval, uint8_t *__restrict__ pass,
+    MirrorOut mir)
 {
     const uint64_t n = *n_cand;
     for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
@@ -946,6 +947,13 @@ __global__ __launch_bounds__(256) void dist_cand_finalize_kernel(
             finalize_cell(o2, nm, dn, ref_length[q], qry_length[r], kmer_size, kmer_space,
                           max_dist, max_pvalue, dist, pval, pass);
         }
+        if (mir.dist) {        // transposed grid: ref r as the query, query q as the ref
+            const uint64_t o2 = (uint64_t)r * mir.n_qry + q;
+            ((C *)mir.cnt.numer)[o2] = (C)nm;
+            ((C *)mir.cnt.denom)[o2] = (C)dn;
+            finalize_cell(o2, nm, dn, qry_length[q], ref_length[r], kmer_size, kmer_space,
+                          max_dist, max_pvalue, mir.dist, mir.pval, mir.pass);
+        }
     }
 }
 
@@ -956,15 +964,17 @@ hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long
                                      const uint64_t *d_qry_length, uint32_t n_ref,
                                      uint32_t kmer_size, double kmer_space, double max_dist,
                                      double max_pvalue, double *d_dist, double *d_pvalue,
-                                     uint8_t *d_pass, hipStream_t st)
+                                     uint8_t *d_pass, const MirrorOut &mir, hipStream_t st)
 {
     if (!cap) return hipSuccess;
+    if (mir.dist && (!mir.cnt.numer || !mir.cnt.denom || mir.cnt.c16 != cnt.c16 || !d_cnum))
+        return hipErrorInvalidValue;
     const uint64_t blocks = std::min<uint64_t>((cap + 255) / 256, 4096);
 #define FPM_CFIN(C)                                                                          \
     hipLaunchKernelGGL(dist_cand_finalize_kernel<C>, dim3((uint32_t)blocks), dim3(256), 0, st,  \
                        d_cand, d_n_cand, (uint32_t)sym, d_cnum, d_cden, (C *)cnt.numer,        \
                        (C *)cnt.denom, d_ref_length, d_qry_length, n_ref, kmer_size,           \
-                       kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass)
+                       kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass, mir)
     if (cnt.c16) FPM_CFIN(uint16_t);
     else FPM_CFIN(uint32_t);
 #undef FPM_CFIN

@@ -27,6 +27,7 @@
 #include "fpm_kernels.hpp"
 
 #include <algorithm>
+#include <atomic>
 
 namespace fpm {
 
@@ -836,6 +837,22 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
     return hipGetLastError();
 }
 
+// The dynamic-LDS limit of a kernel is a per-device attribute: set it once per (kernel slot,
+// device ordinal) on the device current for the launch (contexts on several GPUs in one
+// process each get their own).
+static hipError_t dyn_lds_attr(int slot, const void *fn, int bytes)
+{
+    constexpr int kMaxDev = 64;
+    static std::atomic<int> done[2][kMaxDev];
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    if (dev < 0 || dev >= kMaxDev) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (done[slot][dev].load(std::memory_order_acquire)) return hipSuccess;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    if (e == hipSuccess) done[slot][dev].store(1, std::memory_order_release);
+    return e;
+}
+
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
@@ -855,10 +872,8 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     const uint64_t nh = (uint64_t)kParts * ntiles;
     if (hipError_t e = launch_exscan(tile_hist, tile_off, nullptr, nh, scan_s, tile_off + nh, st))
         return e;
-    static const hipError_t stage_ok = hipFuncSetAttribute(
-        (const void *)idx_part_scatter_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-        kIdxTile * 8);
-    if (stage_ok != hipSuccess) return stage_ok;
+    if (hipError_t e = dyn_lds_attr(0, (const void *)idx_part_scatter_kernel, kIdxTile * 8))
+        return e;
     hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads),
                        (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic, n_ref,
                        hash_bytes, ntiles, (const uint32_t *)tile_hist, (const uint32_t *)tile_off,
@@ -867,10 +882,9 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     // CU: 80 KiB each at l2 = 12); cap 0 = every partition on the global two-pass path
     const uint64_t cnt_bytes = (uint64_t)4 << g.l2;
     const uint32_t cap = cnt_bytes <= 16384 ? (uint32_t)(kBucketThreads * kBucketPer) : 0u;
-    static const hipError_t lds_ok = hipFuncSetAttribute(
-        (const void *)idx_bucket_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-        16384 + kBucketThreads * kBucketPer * 4);
-    if (lds_ok != hipSuccess) return lds_ok;
+    if (hipError_t e = dyn_lds_attr(1, (const void *)idx_bucket_kernel,
+                                    16384 + kBucketThreads * kBucketPer * 4))
+        return e;
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
                        (size_t)(cnt_bytes + (uint64_t)cap * 4), st, (const uint64_t *)tent, ntiles,
                        (const uint32_t *)tile_off, g, cap, dir, entries, self_events);

@@ -1656,6 +1656,12 @@ struct DistFinal {
     // the caller ran fpm_dist_prefill_dev on these buffers (ctx->ev_prefill marks its end):
     // no fill here, the empty pairs are fixed up and every rewrite waits for the prefill
     bool prefilled = false;
+    // the transposed grid too (fpm_refset_dist_mirror_dev): filled beside the primary grid and
+    // its candidate cells scattered by the candidate finalize; compare_impl sets *mirrored
+    // when it wrote it (the sorted sparse path), else dist_dev_impl computes it by a second,
+    // swapped call
+    MirrorOut mir{};
+    bool *mirrored = nullptr;
 };
 
 // bucket index geometry for E entries over n_ref rows: ~2.4 entries per bucket (2^nbits >=
@@ -1809,8 +1815,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     // the bytes move to the fill beside the rank kernel.
     // Measured (same box): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 % (the
     // heavier fill beside the rank kernel costs more than the probe saves), so by grid size.
+    const bool want_mir = fin && fin->mir.dist && !self_set;
     const bool fill_cnt = fin && !fin->prefilled &&
-                          (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0);
+                          (want_mir ||
+                           (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
     // the side fill of query rows [fill_from, q1): from the current point of `st`
     uint32_t fill_from = 0;
     auto launch_fill_rows = [&](uint32_t q1) -> int {
@@ -1835,6 +1843,15 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
         HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len + q0, q1 - q0, sketch_size, c, fill,
                                  ctx->aux));
+        if (want_mir && q1 == n_qry) {
+            // the transposed grid: the ref rows as queries against the query rows
+            PairFill mf = fill;
+            mf.dist = fin->mir.dist;
+            mf.pval = fin->mir.pval;
+            mf.pass = fin->mir.pass;
+            HIP_TRY(launch_dist_fill(d_qry_len, n_qry, d_ref_len, n_ref, sketch_size, fin->mir.cnt,
+                                     mf, ctx->aux));
+        }
         tl.done();
         HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
         fill_from = q1;
@@ -1973,6 +1990,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
             const bool sym = rows_merge && self_set;
+            // a transposed grid is written from the rank kernel's candidate results (sorted
+            // distinct lists: symmetric); its fill needs the whole-grid form (no split)
             // with `fin`: every cell's no-shared-hash values, written on the side stream
             // beside the candidate compare (it needs only the list lengths; beside the
             // index build or the probe it slowed both, they move as many bytes as it does).
@@ -1983,7 +2002,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 if (int rc = launch_fill()) return rc;
             // FPM_FILL_SPLIT=f: the first f of the query rows filled beside the probe, the rest
             // beside the candidate compare (rows in multiples of 8: 16-B aligned row starts)
-            if (fin && !fin->prefilled && ctx->fill_split > 0 && !fill_pending && fill_from == 0) {
+            if (fin && !fin->prefilled && ctx->fill_split > 0 && !fill_pending && fill_from == 0 &&
+                !want_mir) {
                 const uint32_t qs = (uint32_t)(n_qry * ctx->fill_split) & ~7u;
                 if (qs > 0 && qs < n_qry)
                     if (int rc = launch_fill_rows(qs)) return rc;
@@ -2058,13 +2078,19 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             }
             if (fin) {
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
+                MirrorOut mir{};
+                if (want_mir && cnum && fill_pending) {
+                    mir = fin->mir;
+                    mir.n_qry = n_qry;
+                }
                 HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
                                                   cden, cnt, fin->ref_length,
                                                   fin->qry_length,
                                                   n_ref, fin->kmer_size, fin->kmer_space,
                                                   fin->max_dist, fin->max_pvalue, fin->dist,
-                                                  fin->pval, fin->pass, st));
+                                                  fin->pval, fin->pass, mir, st));
                 tl.done();
+                if (mir.dist && fin->mirrored) *fin->mirrored = true;
                 *finalized = true;
             }
             ctx->last_sparse = rows_merge ? 2 : 1;
@@ -2118,7 +2144,8 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                          uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
                          double kmer_space, double max_dist, double max_pvalue, Counts cnt,
                          double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream,
-                         const char *who, fpm_refset *rs = nullptr, bool prefilled = false)
+                         const char *who, fpm_refset *rs = nullptr, bool prefilled = false,
+                         const MirrorOut *mirror = nullptr)
 {
     if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
         return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
@@ -2127,19 +2154,32 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
                   d_dist, d_pvalue, d_pass};
     fin.prefilled = prefilled;
-    bool finalized = false;
+    bool finalized = false, mirrored = false;
+    if (mirror) {
+        fin.mir = *mirror;
+        fin.mirrored = &mirrored;
+    }
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                               qry_stride, n_qry, hash_bytes, sketch_size, cnt, stream, &fin,
                               &finalized, rs))
         return rc;
-    if (finalized) return FPM_OK;
+    // the transposed grid, when the compare could not scatter it (dense path, unsorted lists:
+    // their literal walk is not symmetric): the swapped call, ref and query sets exchanged
+    auto mirror_swapped = [&]() -> int {
+        if (!mirror || mirrored) return FPM_OK;
+        return dist_dev_impl(ctx, d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, d_ref,
+                             d_ref_len, d_ref_length, ref_stride, n_ref, hash_bytes, sketch_size,
+                             kmer_size, kmer_space, max_dist, max_pvalue, mirror->cnt,
+                             mirror->dist, mirror->pval, mirror->pass, stream, who);
+    };
+    if (finalized) return mirror_swapped();
     hipStream_t st = pick_stream(ctx, stream);
     if (prefilled) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));   // rewrites every cell
     TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
     HIP_TRY(launch_dist_finalize(cnt, d_ref_length, d_qry_length, n_ref, n_qry, kmer_size,
                                  kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass, st));
     tl.done();
-    return FPM_OK;
+    return mirror_swapped();
 }
 
 extern "C" {
@@ -2406,6 +2446,45 @@ int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry
                          sketch_size, kmer_size, kmer_space, max_dist, max_pvalue,
                          Counts{d_numer, d_denom, count_bytes == 2}, d_dist, d_pvalue, d_pass,
                          stream, "fpm_refset_dist_dev", rs);
+}
+
+int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                               const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                               uint32_t sketch_size, uint32_t count_bytes, uint32_t kmer_size,
+                               double kmer_space, double max_dist, double max_pvalue,
+                               void *d_numer, void *d_denom, double *d_dist, double *d_pvalue,
+                               uint8_t *d_pass, void *m_numer, void *m_denom, double *m_dist,
+                               double *m_pvalue, uint8_t *m_pass, void *stream)
+{
+    if (!rs) return fail(FPM_EINVAL, "refset_dist_mirror: null set");
+    if (sketch_size != rs->sketch_size)
+        return fail(FPM_EINVAL, "refset_dist_mirror: sketch_size differs from the set's");
+    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
+    if (count_bytes == 2 && sketch_size > 65535)
+        return fail(FPM_EINVAL, "refset_dist_mirror: u16 counts need sketch_size <= 65535");
+    if (!m_numer || !m_denom || !m_dist || !m_pvalue)
+        return fail(FPM_EINVAL, "refset_dist_mirror: mirror numer / denom / distance / p-value required");
+    if (d_qry == rs->ref)
+        return fail(FPM_EINVAL, "refset_dist_mirror: the query rows are the reference rows "
+                                "(use fpm_refset_dist_dev: that grid is its own transpose)");
+    MirrorOut mir;
+    mir.cnt = Counts{m_numer, m_denom, count_bytes == 2};
+    mir.dist = m_dist;
+    mir.pval = m_pvalue;
+    mir.pass = m_pass;
+    mir.n_qry = n_qry;
+    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
+                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
+                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue,
+                         Counts{d_numer, d_denom, count_bytes == 2}, d_dist, d_pvalue, d_pass,
+                         stream, "fpm_refset_dist_mirror_dev", rs, false, &mir);
+}
+
+int fpm_refset_reindex(fpm_refset *rs, void *stream)
+{
+    if (!rs) return fail(FPM_EINVAL, "refset_reindex: null set");
+    if (int rc = set_device(rs->ctx)) return rc;
+    return refset_build_index(rs, pick_stream(rs->ctx, stream));
 }
 
 int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,

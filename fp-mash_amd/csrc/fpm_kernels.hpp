@@ -215,8 +215,18 @@ hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
                                   uint32_t *d_numer, uint32_t *d_denom, double *d_dist,
                                   double *d_pvalue, uint8_t *d_pass, hipStream_t st);
 
+// The transposed grid of a rectangular compare (fpm_refset_dist_mirror_dev): cell (r, q) at
+// r * n_qry + q holds the pair "query r of the ref set against ref q of the query set".  For
+// sorted distinct lists (numer, denom) is symmetric, and so are distance and p-value.
+struct MirrorOut {
+    Counts cnt;
+    double *dist = nullptr, *pval = nullptr;
+    uint8_t *pass = nullptr;
+    uint32_t n_qry = 0;
+};
 // distance / p-value / pass of the candidate cells only (after the candidate compare), and
-// of each mirror cell (r, q) when `sym`; the other cells hold the probe's PairFill values
+// of each mirror cell (r, q) when `sym`, or of its cell in the transposed grid `mir` (when
+// mir.dist is set); the other cells hold the probe's PairFill values
 hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                      uint64_t cap, bool sym, const uint32_t *d_cnum,
                                      const uint32_t *d_cden, Counts cnt,
@@ -224,7 +234,7 @@ hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long
                                      const uint64_t *d_qry_length, uint32_t n_ref,
                                      uint32_t kmer_size, double kmer_space, double max_dist,
                                      double max_pvalue, double *d_dist, double *d_pvalue,
-                                     uint8_t *d_pass, hipStream_t st);
+                                     uint8_t *d_pass, const MirrorOut &mir, hipStream_t st);
 hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
                                 double kmer_space, double max_dist, double max_pvalue,

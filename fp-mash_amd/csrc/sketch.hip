@@ -58,6 +58,68 @@ __device__ __forceinline__ uint32_t block_exscan(uint32_t v, uint32_t *tmp, uint
     return ex;
 }
 
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// The first s distinct values of the ascending keys[0, nv) to row[0, s): slot i = e * 256 + tid
+// (round e, lane-consecutive), kept iff it starts a run of equal keys; its rank = the kept
+// count of the (round, wave) pairs before it + its lane prefix in the wave's ballot.  Stores
+// of consecutive lanes land at consecutive ranks.  `wcnt` holds E * 4 + 1 dwords of LDS;
+// *total = the distinct count (all of keys[0, nv), not capped at s).
+template <int P>
+__device__ __forceinline__ void write_distinct(const uint64_t *keys, uint32_t nv, uint64_t *row,
+                                               uint32_t s, uint32_t *wcnt, uint32_t *total, int tid)
+{
+    constexpr int E = P / kBlock;
+    constexpr int NW = E * kWaves;
+    constexpr int PL = (NW + 63) / 64;                     // pairs per lane of the scan
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * kBlock + tid);
+        const bool f = i < nv && (i == 0 || keys[i] != keys[i - 1]);
+        const uint64_t m = __ballot(f);
+        if (lane == 0) wcnt[e * kWaves + wave] = (uint32_t)__popcll(m);
+    }
+    __syncthreads();
+    if (tid < 64) {
+        uint32_t v[PL], sum = 0;
+#pragma unroll
+        for (int q = 0; q < PL; q++) {
+            const int i = tid * PL + q;
+            v[q] = i < NW ? wcnt[i] : 0u;
+            sum += v[q];
+        }
+        uint32_t x = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        uint32_t ex = x - sum;
+#pragma unroll
+        for (int q = 0; q < PL; q++) {
+            const int i = tid * PL + q;
+            if (i < NW) wcnt[i] = ex;
+            ex += v[q];
+        }
+        if (tid == 63) wcnt[NW] = x;
+    }
+    __syncthreads();
+    *total = wcnt[NW];
+#pragma unroll
+    for (int e = 0; e < E; e++) {
+        const uint32_t i = (uint32_t)(e * kBlock + tid);
+        const uint64_t key = i < nv ? keys[i] : 0ULL;
+        const bool f = i < nv && (i == 0 || key != keys[i - 1]);
+        const uint64_t m = __ballot(f);
+        const uint32_t rank = wcnt[e * kWaves + wave] + lane_prefix(m);
+        if (f && rank < s) row[rank] = key;
+    }
+}
+
 // Bitonic sort of P keys in LDS, ascending (fallback for tiles with crowded buckets).
 template <int P>
 __device__ void bitonic_sort(uint64_t *keys)
@@ -310,6 +372,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
                                                        I::kMaskWords);
     uint8_t *const compl_tab = alpha + 256;
     __shared__ uint32_t scan_tmp[kWaves + 1];
+    __shared__ uint32_t wcnt[E * kWaves + 1];
     __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
     __shared__ uint32_t big_bucket, s_cut;
 
@@ -418,19 +481,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
     FPM_PHASE(4);
     uint32_t lo_b = 0, hi_b = cut, nv = nkept;
     for (int pass = 0; pass < 2; pass++) {
+        // an opaque copy of the shift per pass: otherwise the compiler hoists every key's
+        // bucket addresses (2 x E VGPRs) out of this loop and spills (72-VGPR budget at P = 2048)
+        uint32_t bsh = bshift;
+        asm volatile("" : "+v"(bsh));
         // scatter the keys of buckets [lo_b, hi_b): afterwards bins[b] = end of bucket b,
         // start = bins[b - 1]; each key keeps its slot for the in-bucket rank below
         uint32_t act = 0;
 #pragma unroll
         for (int e = 0; e < E; e++) {
-            const uint32_t bk = (uint32_t)(kr[e] >> bshift);
+            const uint32_t bk = (uint32_t)(kr[e] >> bsh);
             act |= ((vbits >> e & 1) && bk >= lo_b && bk < hi_b) ? (1u << e) : 0u;
         }
         uint32_t slot[E];
 #pragma unroll
         for (int e = 0; e < E; e++)
             if (act >> e & 1) {
-                slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
+                slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bsh)], 1u);
                 keys[slot[e]] = kr[e];
             }
         __syncthreads();
@@ -443,7 +510,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
 #pragma unroll
             for (int e = 0; e < E; e++)
                 if (act >> e & 1) {
-                    const uint32_t b = (uint32_t)(kr[e] >> bshift);
+                    const uint32_t b = (uint32_t)(kr[e] >> bsh);
                     const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
                     const uint32_t mb = s1 - s0;
                     uint32_t r = 0;
@@ -475,25 +542,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
         FPM_PHASE(6);
 
         // ---- first s distinct of keys[0, nv) (ties removed: the heap is a set,
-        // MinHashHeap.cpp:74)
-        const int base = tid * E;
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            int idx = base + e;
-            if (idx < P && (uint32_t)idx < nv && (idx == 0 || keys[idx] != keys[idx - 1])) cnt++;
-        }
+        // MinHashHeap.cpp:74).  Lane-consecutive slots (slot e * 256 + tid), so the row is
+        // written by consecutive lanes at consecutive ranks (coalesced); a slot's rank is
+        // the distinct count of the (round, wave) pairs before it + its lane prefix.
         uint32_t total;
-        uint32_t rank = block_exscan(cnt, scan_tmp, &total);
-        uint64_t *row = out + (uint64_t)td.out_row * p.s;
-#pragma unroll
-        for (int e = 0; e < E; e++) {
-            int idx = base + e;
-            if (idx < P && (uint32_t)idx < nv && (idx == 0 || keys[idx] != keys[idx - 1])) {
-                if (rank < p.s) row[rank] = keys[idx];
-                rank++;
-            }
-        }
+        write_distinct<P>(keys, nv, out + (uint64_t)td.out_row * p.s, p.s, wcnt, &total, tid);
         // block-uniform: done unless duplicates left fewer than s distinct in the kept buckets
         if (total >= p.s || hi_b >= (uint32_t)NB) {
             if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;

@@ -111,6 +111,11 @@ SYMBOLS = [
     ("fpm_refset_dist_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32,
                                       C.c_uint32, C.c_uint32, C.c_double, C.c_double, C.c_double,
                                       vp, vp, vp, vp, vp, vp]),
+    ("fpm_refset_dist_mirror_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32,
+                                             C.c_uint32, C.c_uint32, C.c_double, C.c_double,
+                                             C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                             vp]),
+    ("fpm_refset_reindex", C.c_int, [vp, vp]),
     ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),

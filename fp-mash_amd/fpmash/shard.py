@@ -14,22 +14,81 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
-def all_gather_rows(local, n_total: int, world: int, group=None):
+def all_gather_rows(local, n_total: int, world: int, group=None, bounds=None, out=None):
     """Concatenate every rank's `local` rows (a [n_local, w] tensor, any dtype) in rank
-    order.  Shards may differ by one row: each is padded to the largest before the
-    collective and the padding is dropped afterwards."""
+    order.  Shards may differ in size (`bounds`: each rank's [lo, hi), default
+    shard_range): each is padded to the largest before the collective and the padding is
+    dropped afterwards.  `out`: a preallocated [n_total, w] tensor to write into (its storage
+    stays put across calls, so device pointers into it stay valid)."""
     import torch
     import torch.distributed as dist
 
-    m = max(hi - lo for lo, hi in (shard_range(n_total, world, r) for r in range(world)))
+    if bounds is None:
+        bounds = [shard_range(n_total, world, r) for r in range(world)]
+    m = max(hi - lo for lo, hi in bounds)
     shape = (m,) + tuple(local.shape[1:])
     buf = torch.zeros(shape, dtype=local.dtype, device=local.device)
     buf[: local.shape[0]] = local
     parts = [torch.empty_like(buf) for _ in range(world)]
     dist.all_gather(parts, buf, group=group)
-    out = [parts[r][: hi - lo] for r, (lo, hi) in
-           enumerate(shard_range(n_total, world, r) for r in range(world))]
-    return torch.cat(out, dim=0)
+    pieces = [parts[r][: hi - lo] for r, (lo, hi) in enumerate(bounds)]
+    if out is None:
+        return torch.cat(pieces, dim=0)
+    torch.cat(pieces, dim=0, out=out)
+    return out
+
+
+def pair_block_jobs(bounds, rank: int):
+    """The all-vs-all dist of one set split into contiguous row blocks (`bounds`: block b =
+    rows [lo, hi), block b owned by rank b), dealt so that every UNORDERED pair of rows is
+    compared on exactly one rank and every ordered cell (query q, ref r) of the n x n grid is
+    written on exactly one rank.  The results of sorted distinct sketches are symmetric
+    (compareSketches, CommandDistance.cpp:365-430, is a merge of two sets), so a pair of
+    blocks is compared once and written twice (fpm_refset_dist_mirror_dev), and a block
+    against itself takes the library's symmetric self path.  Rank i indexes its own block
+    and compares, as queries against it:
+      * its own block ("self": one grid, the symmetric path);
+      * the rows of the (ws - 1) // 2 blocks after it (cyclic), and for even ws the first
+        half of block i + ws/2 when i < ws/2 ("mirror": grid qry x ref + its transpose);
+      * for even ws and i >= ws/2: the second half of its own block against block i - ws/2
+        (a second index), the other half of the pair {i - ws/2, i}.
+    Each rank then compares ~n^2 / (2 ws) pairs and writes ~n^2 / ws cells.  Returns a list of
+    {"kind": "self" | "mirror", "ref": (lo, hi), "qry": (lo, hi)}; contiguous query blocks are
+    merged into one job (a cyclic wrap splits them)."""
+    ws = len(bounds)
+    lo, hi = bounds[rank]
+    jobs = [{"kind": "self", "ref": (lo, hi), "qry": (lo, hi)}]
+    if ws == 1:
+        return [j for j in jobs if hi > lo]
+    h = ws // 2
+    segs = []
+    for d in range(1, (ws - 1) // 2 + 1):
+        segs.append(list(bounds[(rank + d) % ws]))
+    if ws % 2 == 0 and rank < h:
+        blo, bhi = bounds[rank + h]
+        segs.append([blo, blo + (bhi - blo) // 2])
+    merged = []
+    for a, b in segs:
+        if merged and merged[-1][1] == a:
+            merged[-1][1] = b
+        else:
+            merged.append([a, b])
+    for a, b in merged:
+        jobs.append({"kind": "mirror", "ref": (lo, hi), "qry": (a, b)})
+    if ws % 2 == 0 and rank >= h:
+        jobs.append({"kind": "mirror", "ref": tuple(bounds[rank - h]),
+                     "qry": (lo + (hi - lo) // 2, hi)})
+    return [j for j in jobs if j["ref"][1] > j["ref"][0] and j["qry"][1] > j["qry"][0]]
+
+
+def job_cells(job):
+    """The ordered cells (query row, ref row) a pair_block_jobs job writes: the grid rows x
+    columns, and for a mirror job its transpose too."""
+    (rl, rh), (ql, qh) = job["ref"], job["qry"]
+    cells = [(q, r) for q in range(ql, qh) for r in range(rl, rh)]
+    if job["kind"] == "mirror":
+        cells += [(r, q) for q in range(ql, qh) for r in range(rl, rh)]
+    return cells
 
 
 def kmer_shard(length: int, k: int, world: int, rank: int) -> tuple[int, int]:
@@ -57,6 +116,9 @@ def min_merge(ctx, d_row: int, d_count: int, s: int, world: int, group=None, dev
     dev = device if device is not None else torch.device("cpu")
     row = torch.zeros((1, s + 1), dtype=torch.int64, device=dev)   # hashes, then the count
     if device is not None:
+        # the zero fill ran on torch's stream; ctx's stream is non-blocking and unordered
+        # with it, so the fill must finish before the copies below land in `row`
+        torch.cuda.synchronize(dev)
         fpmash._check(L.fpm_memcpy_d2d(ctx.h, row.data_ptr(), d_row, s * 8))
         fpmash._check(L.fpm_memcpy_d2d(ctx.h, row.data_ptr() + s * 8, d_count, 4))
         ctx.synchronize()

@@ -486,7 +486,7 @@ int CommandDistance::run() const
     if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
     if (writeFailed) {
         std::cerr << "ERROR: writing the distance output failed." << std::endl;
-        exit(1);
+        fatalExit();
     }
     if (timingOn())
         fprintf(stderr, "[fpmash] writer: waited %.1f ms for blocks, wrote for %.1f ms\n", waitMs,

@@ -2,7 +2,10 @@
 
 #include <cstdlib>
 #include <iostream>
+#include <memory>
 #include <mutex>
+#include <unistd.h>
+#include <cstdio>
 #include <thread>
 #include <vector>
 
@@ -11,6 +14,7 @@ namespace fpmhost {
 namespace {
 std::vector<fpm_ctx *> g_ctx;
 std::vector<int> g_ids;
+std::unique_ptr<std::once_flag[]> g_ctx_once;   // one context creation per device slot
 std::once_flag g_once;
 std::mutex g_mu;
 std::thread g_warm;
@@ -63,15 +67,29 @@ void init_ids()
         if (g_ids.empty()) g_ids.push_back(0);   // fpm_ctx_create reports the missing device
     }
     g_ctx.assign(g_ids.size(), nullptr);
+    g_ctx_once.reset(new std::once_flag[g_ids.size()]);
     ensure_exit_handler();
 }
 }  // namespace
+
+// Errors end the process the reference's way (message, status 1), from whichever thread
+// meets them: GPU, pinner and formatter threads may still be running, so the process leaves
+// with _exit after flushing, without the atexit teardown that would destroy the contexts
+// those threads are using.
+void fatalExit()
+{
+    std::cout.flush();
+    std::cerr.flush();
+    fflush(stdout);
+    fflush(stderr);
+    _exit(1);
+}
 
 void check(int rc, const char *what)
 {
     if (rc != FPM_OK) {
         std::cerr << "ERROR: " << what << ": " << fpm_last_error() << std::endl;
-        exit(1);
+        fatalExit();
     }
 }
 
@@ -87,15 +105,16 @@ void warmDevices()
     ensure_exit_handler();
     std::lock_guard<std::mutex> lk(g_mu);
     if (g_warm.joinable()) return;
-    // HIP runtime start-up (device enumeration + context streams: ~0.1-0.25 s) runs beside
-    // the caller's input reading; a context that fails to come up is reported by the first
-    // device() call on the main thread
+    // HIP runtime start-up (device enumeration + the first context's streams: ~0.1-0.25 s)
+    // runs beside the caller's input reading.  Only the first device is warmed: the others
+    // are created on first use (device(i)), once the command knows how many parts it spreads,
+    // so a single-file sketch on an 8-GPU node does not bring up 8 contexts.  A context that
+    // fails to come up is reported by the first device() call.
     g_warm = std::thread([] {
         std::call_once(g_once, init_ids);
-        for (size_t i = 0; i < g_ids.size(); i++) {
-            std::lock_guard<std::mutex> lk2(g_mu);
-            if (!g_ctx[i] && fpm_ctx_create(g_ids[i], &g_ctx[i]) != FPM_OK) g_ctx[i] = nullptr;
-        }
+        std::call_once(g_ctx_once[0], [] {
+            if (fpm_ctx_create(g_ids[0], &g_ctx[0]) != FPM_OK) g_ctx[0] = nullptr;
+        });
     });
 }
 
@@ -103,8 +122,15 @@ fpm_ctx *device(int i)
 {
     std::call_once(g_warm_join, join_warm);
     std::call_once(g_once, init_ids);
-    std::lock_guard<std::mutex> lk(g_mu);
-    if (!g_ctx[i]) check(fpm_ctx_create(g_ids[i], &g_ctx[i]), "MI355X device");
+    // per-device creation (device threads bring their contexts up in parallel); a failed
+    // warm-up of device 0 is retried here and reported
+    std::call_once(g_ctx_once[i], [i] {
+        if (fpm_ctx_create(g_ids[i], &g_ctx[i]) != FPM_OK) g_ctx[i] = nullptr;
+    });
+    if (!g_ctx[i]) {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_ctx[i]) check(fpm_ctx_create(g_ids[i], &g_ctx[i]), "MI355X device");
+    }
     return g_ctx[i];
 }
 

@@ -17,5 +17,8 @@ int deviceCount();
 void warmDevices();
 fpm_ctx *device(int i = 0);
 void check(int rc, const char *what);
+// exit status 1 after flushing stdout / stderr, without the atexit context teardown (safe from
+// any thread: other threads may still be using the contexts)
+[[noreturn]] void fatalExit();
 
 }  // namespace fpmhost

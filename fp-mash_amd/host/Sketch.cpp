@@ -37,7 +37,7 @@ void splitFile(const std::string &file, std::vector<std::string> &lines)
     std::ifstream in(file);
     if (in.fail()) {
         std::cerr << "ERROR: Could not open " << file << ".\n";
-        exit(1);
+        fatalExit();
     }
     std::string line;
     while (std::getline(in, line))
@@ -98,11 +98,21 @@ static bool readFile(const std::string &path, std::string &out)
 
 // The .msh inputs are opened several times (parameters of the first file, the per-file
 // compatibility test, the load: Sketch.cpp:257-336): keep the last image read, keyed by path,
-// size and modification time.
+// size and modification time, until its load (loadMsh) has parsed it.  Main thread only (no
+// locking): every caller is on the command's main thread.
+static std::string g_mshPath, g_mshData;
+static struct stat g_mshSt {};
+
+static void releaseMshCache()
+{
+    g_mshPath.clear();
+    std::string().swap(g_mshData);
+}
+
 static const std::string *readMshCached(const std::string &path)
 {
-    static std::string cPath, cData;
-    static struct stat cSt {};
+    std::string &cPath = g_mshPath, &cData = g_mshData;
+    struct stat &cSt = g_mshSt;
     struct stat st {};
     if (stat(path.c_str(), &st) != 0) return nullptr;
     if (path == cPath && st.st_size == cSt.st_size && st.st_mtim.tv_sec == cSt.st_mtim.tv_sec &&
@@ -120,14 +130,14 @@ uint64_t Sketch::initParametersFromMsh(const std::string &file)
     const std::string *img = readMshCached(file);
     if (!img) {
         std::cerr << "ERROR: could not open \"" << file << "\" for reading." << std::endl;
-        exit(1);
+        fatalExit();
     }
     const std::string &data = *img;
     MshHeader h;
     std::string err;
     if (!mshParse(data, h, nullptr, true, 0, err)) {
         std::cerr << "ERROR: " << file << ": " << err << std::endl;
-        exit(1);
+        fatalExit();
     }
     parameters.kmerSize = (int)h.kmerSize;
     parameters.error = h.error;
@@ -156,7 +166,7 @@ static void loadMsh(const std::string &file, const Parameters &p, std::vector<Re
     std::vector<MshReference> refs;
     if (!mshParse(data, h, &refs, p.use64, p.minHashesPerWindow, err)) {
         std::cerr << "ERROR: " << file << ": " << err << std::endl;
-        exit(1);
+        fatalExit();
     }
     for (auto &m : refs) {
         Reference r;
@@ -168,6 +178,7 @@ static void loadMsh(const std::string &file, const Parameters &p, std::vector<Re
         r.countsSorted = m.countsSorted;
         out.push_back(std::move(r));
     }
+    releaseMshCache();   // parsed: the image is not needed past its load
 }
 
 namespace {
@@ -255,7 +266,7 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
                 std::cerr << "\nERROR: reading " << (parameters.concatenated ? std::string("input files")
                                                                                : seqFiles[f0 + f])
                           << "." << std::endl;
-                exit(1);
+                fatalExit();
             }
         }
     }
@@ -292,7 +303,7 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
                                  "k-mer size (" << parameters.kmerSize << ")." << std::endl;
                 else
                     std::cerr << "\nERROR: Did not find fasta records in \"input files\"." << std::endl;
-                exit(1);
+                fatalExit();
             }
             fileRefs[f0 + f].push_back(std::move(ref));
             fileGroups[f].push_back(g);
@@ -457,7 +468,7 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
             FILE *f = fopen(file.c_str(), "r");
             if (!f) {
                 std::cerr << "ERROR: could not open " << file << " for reading." << std::endl;
-                exit(1);
+                fatalExit();
             }
             fclose(f);
         }
@@ -485,7 +496,7 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
             for (size_t f = 0; f < seqFiles.size(); f++)
                 if (!okv[f]) {
                     std::cerr << "ERROR: could not open " << seqFiles[f] << std::endl;
-                    exit(1);
+                    fatalExit();
                 }
         }
         phaseMark("read input");
@@ -540,7 +551,7 @@ void Sketch::initFromFingerprints(const std::vector<std::string> &files, const P
         if (!readFile(file, text)) {
             std::cerr << "ERROR: Could not open fingerprint file " << file << " for reading."
                       << std::endl;
-            exit(1);
+            fatalExit();
         }
         // parse + hash on the device (getline / `iss >> id` / `while (iss >> v)` /
         // getHashFingerPrint per line, Sketch.cpp:82-101, 131), at most the lines left
@@ -580,7 +591,7 @@ void Sketch::initFromFingerprints(const std::vector<std::string> &files, const P
                 // the reference dereferences a null Reference here (Sketch.cpp:131-134)
                 std::cerr << "ERROR: fingerprint line " << i + 1 << " of " << file
                           << " continues ID \"" << lastID << "\" from a previous file." << std::endl;
-                exit(1);
+                fatalExit();
             }
             cur->hashes.push_back(parameters.use64 ? h64[i] : (uint64_t)h32[i]);
             cur->length += nv;
@@ -612,7 +623,7 @@ int Sketch::writeToMsh(const std::string &file) const
     }
     if (!mshWrite(file, h, refs.data(), refs.size(), parameters.use64, parameters.counts)) {
         std::cerr << "ERROR: could not open " << file << " for writing.\n";
-        exit(1);
+        fatalExit();
     }
     phaseMark("msh write");
     return 0;

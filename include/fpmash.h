@@ -304,6 +304,25 @@ int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry
                         double kmer_space, double max_dist, double max_pvalue, void *d_numer,
                         void *d_denom, double *d_dist, double *d_pvalue, uint8_t *d_pass,
                         void *stream);
+/* The same compare, plus its transposed grid: m_* cell (r, q) at r * n_qry + q holds what
+ * fpm_refset_dist_dev would give for query r of the reference set against reference q of the
+ * query rows (the pair seen from the other side, CommandDistance.cpp:224-261 with the two
+ * sketches exchanged).  For the sorted distinct lists of the k-mer path the candidate
+ * results are scattered to both grids (compareSketches' counts are symmetric there, and so
+ * are distance and p-value); otherwise (unsorted -fp lists, dense path) the transposed grid
+ * is computed by the swapped call.  Multi-GPU all-vs-all dist deals unordered block pairs
+ * to the ranks with this call (fpmash/shard.py: pair_block_jobs).  The query rows must not
+ * be the set's own rows (that grid is its own transpose: fpm_refset_dist_dev). */
+int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                               const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                               uint32_t sketch_size, uint32_t count_bytes, uint32_t kmer_size,
+                               double kmer_space, double max_dist, double max_pvalue,
+                               void *d_numer, void *d_denom, double *d_dist, double *d_pvalue,
+                               uint8_t *d_pass, void *m_numer, void *m_denom, double *m_dist,
+                               double *m_pvalue, uint8_t *m_pass, void *stream);
+/* Rebuild the set's bucket index from its (device, borrowed) rows in place, e.g. after the
+ * rows were rewritten by a new sketch run; no reallocation when the geometry is unchanged. */
+int fpm_refset_reindex(fpm_refset *rs, void *stream);
 int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
                     const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
                     uint32_t sketch_size, uint32_t kmer_size, double kmer_space, double max_dist,

@@ -1,8 +1,9 @@
-"""Worker for test_multirank.test_c4_leg_two_ranks_one_gpu (-m gpu): bench.c4_leg, the C4
-job (sketch own shard -> all-gather of the sketch rows -> dist of own query rows vs all),
-on two ranks that share the one visible GPU through libfpmash, with the rows gathered over
-gloo.  Every rank checks 50 of its query rows against the oracle; rank 0 also checks the
-gathered reference set against a single-process sketch of all sequences."""
+"""Worker for test_multirank.test_c4_leg_ranks_one_gpu (-m gpu): bench.c4_leg, the C4 job
+(sketch own block -> all-gather of the sketch rows -> this rank's block pairs of the all-vs-all
+grid, fpmash.shard.pair_block_jobs: own block on the symmetric self path, the other block
+pairs as a grid + its transpose through fpm_refset_dist_mirror_dev), on WORLD_SIZE ranks that
+share the one visible GPU through libfpmash, with the rows gathered over gloo.  Every rank
+checks sampled rows of each of its grids and transposes against the oracle."""
 import json
 import os
 import sys
@@ -21,8 +22,9 @@ def main():
     ctx = fpmash.Context(0)
     r = bench.c4_leg(ctx, grp, ws, rank, 0, n=3000, members=100, s=1000, k=21, steps=1,
                      warmup=1, parity="all")
-    out = {"rank": rank, "parity": r["parity"], "pairs": r["pairs"],
-           "candidates_all_ranks": r["candidates_all_ranks"], "path": r["path_rank0"]}
+    out = {"rank": rank, "parity": r["parity"], "pairs": r["pairs"], "jobs": r["jobs_rank0"],
+           "cells": r["cells_rank0"], "candidates_all_ranks": r["candidates_all_ranks"],
+           "path": r["path_rank0"]}
     print("C4RANK " + json.dumps(out), flush=True)
     grp.barrier()
     ctx.close()

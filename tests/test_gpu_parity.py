@@ -581,3 +581,80 @@ def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
     assert np.allclose(res[1][3][ok], pv[ok], rtol=1e-12, atol=0)
     for b in bufs:
         b.free()
+
+
+@pytest.mark.parametrize("mode", ["sorted", "fp", "dense"])
+def test_refset_mirror_matches_oracle(ctx, oracle, mode):
+    """fpm_refset_dist_mirror_dev (the block pairs of the sharded C4 all-vs-all): the grid
+    (queries x refs) and its transpose (refs as queries x the query rows as refs) both equal
+    the oracle's grids of the two orientations; sorted u64 sketches take the sparse path that
+    scatters the candidate results to both grids, unsorted -fp u32 lists (not symmetric under
+    the literal walk) and a forced dense walk compute the transpose by the swapped call.
+    Empty lists and the -d / -v filters included."""
+    import ctypes as C
+    import fpmash
+    from fpmash import datagen
+    rng = np.random.default_rng(23)
+    if mode == "fp":
+        lists = [rng.integers(0, 40, size=int(rng.integers(1, 300))).astype(np.uint32)
+                 for _ in range(70)]
+        S, k, space, use64 = 200, 1, 10.0, False
+    else:
+        seqs = datagen.family_dna(7, 10, 1500, sub_rate=(0.0, 0.1), seed=29)
+        lists = oracle.sketch_batch(oracle.params(k=21, s=300), seqs)
+        lists[5] = lists[5][:0]                        # an empty sketch on each side
+        lists[50] = lists[50][:0]
+        S, k, space, use64 = 300, 21, 4.0 ** 21, True
+    lengths = [int(len(x)) * 7 + 1000 for x in lists]
+    refs, qrys = lists[:33], lists[33:]                 # disjoint row sets (two blocks)
+    rl, ql = lengths[:33], lengths[33:]
+    w = max(len(x) for x in lists)
+    dt = np.uint64 if use64 else np.uint32
+    R, rlen = fpmash._dense(refs, w, dt)
+    Q, qlen = fpmash._dense(qrys, w, dt)
+    L = fpmash.lib()
+    keep = []
+
+    def up(a):
+        b = fpmash.DeviceBuffer.from_array(ctx, np.ascontiguousarray(a))
+        keep.append(b)
+        return b.ptr
+    dR, drl, dRL = up(R), up(rlen), up(np.array(rl, np.uint64))
+    dQ, dql, dQL = up(Q), up(qlen), up(np.array(ql, np.uint64))
+    nr, nq = len(refs), len(qrys)
+    prim = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (4, 4, 8, 8, 1)]
+    mirr = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (4, 4, 8, 8, 1)]
+    keep += prim + mirr
+    # the grids are small (AUTO would walk them densely): force the index path for the
+    # sorted and -fp cases
+    ctx.set_dist_mode(1 if mode == "dense" else 2)
+    h = C.c_void_p()
+    try:
+        fpmash._check(L.fpm_refset_create_dev(ctx.h, dR, drl, dRL, w, nr, 8 if use64 else 4, S,
+                                              C.byref(h)))
+        for rep in range(2):                            # a second call after a reindex
+            if rep:
+                fpmash._check(L.fpm_refset_reindex(h, None))
+            fpmash._check(L.fpm_refset_dist_mirror_dev(h, dQ, dql, dQL, w, nq, S, 4, k, space,
+                                                       0.9, 0.5, *[b.ptr for b in prim],
+                                                       *[b.ptr for b in mirr], None))
+            ctx.synchronize()
+            types = (np.uint32, np.uint32, np.float64, np.float64, np.uint8)
+            got_p = [b.to_array(t, nr * nq) for b, t in zip(prim, types)]
+            got_m = [b.to_array(t, nr * nq) for b, t in zip(mirr, types)]
+            for got, (a, al, b, bl) in ((got_p, (refs, rl, qrys, ql)),
+                                        (got_m, (qrys, ql, refs, rl))):
+                nu, de, di, pv = oracle.dist_grid(a, al, b, bl, S, k, space, use64=use64)
+                assert np.array_equal(got[0], nu) and np.array_equal(got[1], de)
+                assert np.allclose(got[2], di, rtol=1e-12, atol=0)
+                ok = (di <= 0.9)
+                assert np.allclose(got[3][ok], pv[ok], rtol=1e-12, atol=0)
+                assert np.array_equal(got[4].astype(bool), ok & (pv <= 0.5))
+        if mode == "sorted":
+            assert ctx.last_dist_stats()["sparse"] == 2
+    finally:
+        if h:
+            L.fpm_refset_free(h)
+        ctx.set_dist_mode(0)
+        for b in keep:
+            b.free()

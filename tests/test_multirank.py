@@ -45,19 +45,54 @@ def test_shard_gather_two_ranks():
 
 
 @pytest.mark.gpu
-def test_c4_leg_two_ranks_one_gpu():
-    """bench.c4_leg at world size 2 through libfpmash (both ranks on the one visible GPU,
-    rows gathered over gloo): each rank's dist rows of the sharded job match the oracle."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+@pytest.mark.parametrize("ws", [2, 3])
+def test_c4_leg_ranks_one_gpu(ws):
+    """bench.c4_leg at world size 2 and 3 through libfpmash (all ranks on the one visible GPU,
+    rows gathered over gloo): every rank's grids and transposes (block pairs, including the
+    half-block split of even world sizes) match the oracle, and the ranks' cells add up to the
+    whole n x n grid."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ws}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "_c4_gpu_worker.py")]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines() if l.startswith("C4RANK ")]
-    assert sorted(r["rank"] for r in res) == [0, 1]
+    assert sorted(r["rank"] for r in res) == list(range(ws))
+    assert sum(r["cells"] for r in res) == res[0]["pairs"]
     for r in res:
         assert r["parity"]["ok"], r
         assert r["parity"]["pairs_sharing"] > 0
+        assert any(j["kind"] == "mirror" for j in r["jobs"])
+
+
+@pytest.mark.gpu
+def test_c5_leg_two_ranks_one_gpu():
+    """bench.c5_leg at world size 2 (both ranks on the one visible GPU, sketch rows gathered
+    over gloo): uneven file shards (7 genomes over 2 ranks), and every genome of the ordered
+    reassembly on rank 0 equals the oracle's sketch of that file (Sketch.cpp:346-356)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "_c5_gpu_worker.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines()
+           if l.startswith("C5RANK ")]
+    assert sorted(r["rank"] for r in res) == [0, 1]
+    assert sorted(r["genomes_local"] for r in res) == [3, 4]
+    r0 = [r for r in res if r["rank"] == 0][0]
+    assert r0["reassembled"] == 7
+    assert r0["parity"]["genomes_checked"] == list(range(7))
+    assert r0["parity"]["ok"] and all(r0["parity"]["sketch_exact"]), r0
+
+
+def test_balanced_file_shards_cover_in_order():
+    """bench.balanced_file_shards: contiguous, in file order, every file exactly once."""
+    import bench
+    for lengths, ws in [([5] * 7, 2), ([1, 100, 1, 1, 1], 2), ([3] * 1000, 8), ([1, 2], 4)]:
+        sh = bench.balanced_file_shards(lengths, ws)
+        assert len(sh) == ws and sh[0][0] == 0 and sh[-1][1] == len(lengths)
+        assert all(a[1] == b[0] for a, b in zip(sh, sh[1:]))
+        assert all(lo <= hi for lo, hi in sh)
 
 
 @pytest.mark.gpu
@@ -86,3 +121,52 @@ def test_kmer_shard_covers_every_kmer_once():
             lo, hi = kmer_shard(L, k, w, r)
             starts += list(range(lo, max(lo, hi - k + 1)))
         assert starts == list(range(max(0, L - k + 1)))
+
+
+@pytest.mark.parametrize("ws", [1, 2, 3, 4, 5, 6, 7, 8])
+def test_pair_block_jobs_cover_every_cell_once(ws):
+    """fpmash.shard.pair_block_jobs (the sharded C4 all-vs-all): over all ranks, every ordered
+    cell (q, r) of the n x n grid is written exactly once, each unordered pair is compared on
+    one rank only, and the ranks' compared pairs are balanced."""
+    from fpmash.shard import job_cells, pair_block_jobs, shard_range
+    import random
+    rng = random.Random(ws)
+    for n in (ws, 3 * ws + 1, 40):
+        if n < ws:
+            continue
+        # uneven blocks (contiguous family shards), as bench.c4_leg makes them
+        fams = max(ws, n // 3)
+        fb = [shard_range(fams, ws, r) for r in range(ws)]
+        cuts = sorted(rng.sample(range(1, n), fams - 1)) if fams > 1 else []
+        edges = [0] + cuts + [n]
+        bounds = [(edges[a], edges[b]) for a, b in fb]
+        seen = {}
+        work = []
+        for r in range(ws):
+            w = 0
+            for j in pair_block_jobs(bounds, r):
+                for c in job_cells(j):
+                    seen[c] = seen.get(c, 0) + 1
+                (rl, rh), (ql, qh) = j["ref"], j["qry"]
+                w += (rh - rl) * (qh - ql) / (2 if j["kind"] == "self" else 1)
+            work.append(w)
+        assert len(seen) == n * n and set(seen.values()) == {1}, (ws, n)
+        assert abs(sum(work) - n * n / 2) <= n, (work, n)
+
+
+def test_pair_block_jobs_balanced_at_c4_shape():
+    """At C4's 500 families x 100 members the per-rank compared pairs stay within 5 % of
+    n^2 / (2 ws) at ws = 2, 4, 8 (the cells written within 5 % of n^2 / ws)."""
+    from fpmash.shard import pair_block_jobs, shard_range
+    n, members = 50_000, 100
+    for ws in (2, 4, 8):
+        bounds = [tuple(x * members for x in shard_range(n // members, ws, r)) for r in range(ws)]
+        for r in range(ws):
+            w = cells = 0
+            for j in pair_block_jobs(bounds, r):
+                (rl, rh), (ql, qh) = j["ref"], j["qry"]
+                a = (rh - rl) * (qh - ql)
+                w += a / 2 if j["kind"] == "self" else a
+                cells += a if j["kind"] == "self" else 2 * a
+            assert abs(w / (n * n / (2 * ws)) - 1) < 0.05, (ws, r, w)
+            assert abs(cells / (n * n / ws) - 1) < 0.05, (ws, r, cells)
