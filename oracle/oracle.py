@@ -66,6 +66,10 @@ def lib():
         L.orc_binomial_q.argtypes = [C.c_uint64, C.c_double, C.c_uint64]
         L.orc_positional.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_int,
                                      u64p, u64p, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.orc_write_dist_text.restype = C.c_int
+        L.orc_write_dist_text.argtypes = [C.c_char_p, C.c_char_p, u64p, C.c_uint32, u32p,
+                                          C.c_uint32, u32p, u32p, f64p, f64p, C.c_void_p,
+                                          C.c_int]
         L.orc_dist_grid.restype = C.c_int
         L.orc_dist_grid.argtypes = [C.c_void_p, u32p, u64p, C.c_uint64, C.c_uint32,
                                     C.c_void_p, u32p, u64p, C.c_uint64, C.c_uint32,
@@ -93,6 +97,15 @@ def ref():
         R.ref_sketch_records.argtypes = [C.c_char_p, u64p, C.c_uint, C.c_int, C.c_ulonglong,
                                          C.c_uint, C.c_int, C.c_int, C.c_int, C.c_char_p,
                                          u64p, u32p]
+        R.ref_sketch_batch_mt.restype = None
+        R.ref_sketch_batch_mt.argtypes = [C.c_char_p, u64p, C.c_uint, C.c_int, C.c_ulonglong,
+                                          C.c_uint, C.c_int, C.c_int, C.c_int, C.c_char_p,
+                                          C.c_int, u64p, u64p]
+        R.ref_kseq_records.restype = C.c_void_p
+        R.ref_kseq_records.argtypes = [C.c_char_p, u64p, C.POINTER(C.c_int), u64p]
+        R.ref_kseq_scan.restype = C.c_int
+        R.ref_kseq_scan.argtypes = [C.c_char_p, u64p, u64p]
+        R.ref_free.argtypes = [C.c_void_p]
         _REF = R
     return _REF
 
@@ -103,26 +116,62 @@ def _p(a, t):
 
 def ref_sketch_batch(seqs, k=21, s=1000, seed=42, threads=1):
     """-i sketches of `seqs` through the reference's own getHash + MinHashHeap (oracle/_ref,
-    the addMinHashes walk re-driven around them), one record per call on `threads` threads
-    (ctypes releases the GIL).  None when oracle/_ref is not built."""
+    the addMinHashes walk re-driven around them), one heap per record, records taken in turn
+    by `threads` C++ threads (ref_sketch_batch_mt: one call for the whole batch, no Python
+    dispatch per record).  None when oracle/_ref is not built."""
     R = ref()
     if R is None:
         return None
-    from concurrent.futures import ThreadPoolExecutor
     alpha = bytearray(256)
     for c in b"ACGT":
         alpha[c] = 1
     alpha = bytes(alpha)
     use64 = int(4.0 ** k > 2.0 ** 32)
+    buf, off = pack_records(seqs)
+    out = np.zeros((len(seqs), s), np.uint64)
+    cnt = np.zeros(len(seqs), np.uint64)
+    R.ref_sketch_batch_mt(buf, _p(off, u64p), len(seqs), k, s, seed, use64, 0, 0, alpha,
+                          max(1, threads), _p(out, u64p), _p(cnt, u64p))
+    return [out[i, :int(cnt[i])] for i in range(len(seqs))]
 
-    def one(x):
-        off = np.array([0, len(x)], np.uint64)
-        out = np.zeros(s, np.uint64)
-        n = R.ref_sketch_records(x, _p(off, u64p), 1, k, s, seed, use64, 0, 0, alpha,
-                                 _p(out, u64p), None)
-        return out[:n]
-    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
-        return list(ex.map(one, seqs))
+
+def ref_kseq_records(path):
+    """The reference's kseq.h reader (oracle/_ref: kseq_read over gzopen, as
+    Sketch.cpp:478-522 reads a file): ([(name, comment, seq, qual) bytes], last kseq_read
+    return: -1 clean end, -2 truncated quality).  None when oracle/_ref is not built."""
+    R = ref()
+    if R is None:
+        return None
+    n, st, nb = C.c_uint64(), C.c_int(), C.c_uint64()
+    p = R.ref_kseq_records(os.fsencode(path), C.byref(n), C.byref(st), C.byref(nb))
+    if not p:
+        raise OSError(f"kseq: cannot open {path}")
+    try:
+        raw = C.string_at(p, nb.value)
+    finally:
+        R.ref_free(p)
+    recs, at = [], 0
+    for _ in range(n.value):
+        f = []
+        for _ in range(4):
+            ln = int.from_bytes(raw[at:at + 8], "little")
+            f.append(raw[at + 8:at + 8 + ln])
+            at += 8 + ln
+        recs.append(tuple(f))
+    return recs, st.value
+
+
+def ref_kseq_scan(path):
+    """kseq_read + the per-record sequence copy over a file (the reference's input step):
+    (records, bases), or None when oracle/_ref is not built."""
+    R = ref()
+    if R is None:
+        return None
+    n, b = C.c_uint64(), C.c_uint64()
+    rc = R.ref_kseq_scan(os.fsencode(path), C.byref(n), C.byref(b))
+    if rc == -3:
+        raise OSError(f"kseq: cannot open {path}")
+    return n.value, b.value
 
 
 def params(k=21, s=1000, seed=42, alphabet="ACGT", noncanonical=False, preserve_case=False):
@@ -281,3 +330,24 @@ def dist_grid(ref_lists, ref_lengths, qry_lists, qry_lengths, sketch_size, k, km
                              _p(pv, f64p) if with_pvalue else None, threads)
     assert rc == 0
     return nu[:n], de[:n], di[:n], (pv[:n] if with_pvalue else None)
+
+
+def write_dist_text(path, names, qry_rows, numer, denom, dist, pval, passed=None,
+                    flush_each=True):
+    """The reference's dist text step (writeOutput, CommandDistance.cpp:276-333: ostream
+    formatting, `endl` per line) for the grid block of query rows `qry_rows` x all refs
+    (numer ... [len(qry_rows) * len(names)], query-major) into `path`."""
+    off = np.zeros(len(names) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in names])
+    q = np.ascontiguousarray(qry_rows, np.uint32)
+    nu = np.ascontiguousarray(numer, np.uint32)
+    de = np.ascontiguousarray(denom, np.uint32)
+    di = np.ascontiguousarray(dist, np.float64)
+    pv = np.ascontiguousarray(pval, np.float64)
+    pa = None if passed is None else np.ascontiguousarray(passed, np.uint8)
+    rc = lib().orc_write_dist_text(os.fsencode(path), b"".join(names), _p(off, u64p), len(names),
+                                   _p(q, u32p), len(q), _p(nu, u32p), _p(de, u32p), _p(di, f64p),
+                                   _p(pv, f64p), None if pa is None else pa.ctypes.data,
+                                   int(flush_each))
+    if rc:
+        raise OSError(f"write_dist_text: {rc}")

@@ -13,8 +13,17 @@
 #include "hash.h"
 #include "MinHashHeap.h"
 
+#include <zlib.h>
+#include <atomic>
+#include <cstdlib>
 #include <cstring>
+#include <string>
+#include <thread>
 #include <vector>
+
+// the reference's own FASTA/FASTQ reader (header-only kseq.h, instantiated as Sketch.cpp:38 does)
+#include "kseq.h"
+KSEQ_INIT(gzFile, gzread)
 
 extern "C" {
 
@@ -108,5 +117,92 @@ unsigned long long ref_sketch_records(const char *seq, const unsigned long long 
     }
     return (unsigned long long)list.size();
 }
+
+// -i sketches of n_rec records (one heap each) on `threads` std::threads taking records in
+// turn (the reference's -p pool hands records to workers one at a time): the reference-heap
+// CPU rate without a per-record ctypes hop.  Record r's list lands in out_hashes[r * s ...],
+// its size in out_n[r].
+void ref_sketch_batch_mt(const char *seq, const unsigned long long *rec_off, unsigned n_rec,
+                         int k, unsigned long long s, unsigned seed, int use64, int noncanonical,
+                         int preserve_case, const unsigned char *alphabet, int threads,
+                         unsigned long long *out_hashes, unsigned long long *out_n)
+{
+    std::atomic<unsigned> next(0);
+    auto work = [&]() {
+        for (unsigned r; (r = next.fetch_add(1)) < n_rec;)
+            out_n[r] = ref_sketch_records(seq, rec_off + r, 1, k, s, seed, use64, noncanonical,
+                                          preserve_case, alphabet, out_hashes + (size_t)r * s,
+                                          nullptr);
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < threads; t++) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+}
+
+// kseq_read over a (optionally gzip'd) file, as sketchFileBySequence (Sketch.cpp:478-522)
+// reads it: every record's name, comment, sequence and quality strings.  Serialised into one
+// malloc'd buffer (free with ref_free): per record u64 lengths then bytes of name, comment,
+// seq, qual.  *status = kseq_read's last return (-1: clean end, -2: truncated quality), *n =
+// records.  Returns null when the file cannot be opened.
+unsigned char *ref_kseq_records(const char *path, unsigned long long *n, int *status,
+                                unsigned long long *bytes)
+{
+    gzFile fp = gzopen(path, "r");
+    if (!fp) return nullptr;
+    kseq_t *seq = kseq_init(fp);
+    std::string out;
+    unsigned long long cnt = 0;
+    int l;
+    auto put = [&](const kstring_t &x) {
+        unsigned long long len = x.l;
+        out.append((const char *)&len, 8);
+        if (len) out.append(x.s, len);
+    };
+    while ((l = kseq_read(seq)) >= 0) {
+        put(seq->name);
+        put(seq->comment);
+        put(seq->seq);
+        put(seq->qual);
+        cnt++;
+    }
+    kseq_destroy(seq);
+    gzclose(fp);
+    unsigned char *buf = (unsigned char *)malloc(out.size() ? out.size() : 1);
+    memcpy(buf, out.data(), out.size());
+    *n = cnt;
+    *status = l;
+    *bytes = out.size();
+    return buf;
+}
+
+// kseq_read + the per-record sequence copy (Sketch.cpp:502-506) of a file, counting records
+// and bases: the reference's input step alone, for the CPU baseline's CLI leg.
+static void sink_fn(const char *, size_t) {}
+static void (*volatile g_sink)(const char *, size_t) = sink_fn;   // keeps the copy observable
+
+int ref_kseq_scan(const char *path, unsigned long long *n_rec, unsigned long long *n_bases)
+{
+    gzFile fp = gzopen(path, "r");
+    if (!fp) return -3;
+    kseq_t *seq = kseq_init(fp);
+    unsigned long long c = 0, b = 0;
+    int l;
+    while ((l = kseq_read(seq)) >= 0) {
+        char *copy = new char[l ? l : 1];
+        memcpy(copy, seq->seq.s, l);
+        g_sink(copy, (size_t)l);
+        b += (unsigned long long)l;
+        delete[] copy;
+        c++;
+    }
+    kseq_destroy(seq);
+    gzclose(fp);
+    *n_rec = c;
+    *n_bases = b;
+    return l;
+}
+
+void ref_free(void *p) { free(p); }
 
 }  // extern "C"
