@@ -1503,6 +1503,106 @@ static void seqtext_release(fpm_seqtext *j)
 
 extern "C" {
 
+}  // extern "C"
+
+// The FASTQ path of fpm_seq_parse (seqparse.hip: 4-line records verified against kseq_read):
+// newline index, lines per file, record table + packed bases.  *ok = false when a record does
+// not read the 4-line way (nothing of the job changed then).
+namespace {
+// device scratch freed on every return path
+struct TmpBufs {
+    std::vector<void *> p;
+    ~TmpBufs() { for (void *x : p) (void)hipFree(x); }
+    template <typename T> hipError_t get(T **out, size_t bytes)
+    {
+        void *q = nullptr;
+        const hipError_t e = hipMalloc(&q, bytes ? bytes : 16);
+        if (e == hipSuccess) { p.push_back(q); *out = static_cast<T *>(q); }
+        return e;
+    }
+};
+}  // namespace
+
+static int fastq_parse(fpm_ctx *ctx, fpm_seqtext *j, uint64_t text_bytes, hipStream_t st, bool *ok)
+{
+    *ok = false;
+    const uint32_t n_seg = (uint32_t)j->seg_off.size();
+    TmpBufs tmp;
+    const uint32_t nb = text_blocks(text_bytes);
+    const uint64_t scan_w = scan_scratch_words(nb ? nb : 1);
+    uint32_t *blk;
+    HIP_TRY(tmp.get(&blk, ((size_t)2 * nb + 2 + scan_w) * 4));
+    uint32_t *blk_cnt = blk, *blk_off = blk + nb, *scan_s = blk + 2 * nb + 2;
+    TimedLaunch tl(ctx, FPM_K_SEQPARSE, st);
+    HIP_TRY(launch_fp_nl_count(j->d_text, text_bytes, blk_cnt, blk_off, scan_s, st));
+    uint32_t n_nl = 0;
+    HIP_TRY(hipMemcpyAsync(&n_nl, blk_off + nb, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    uint64_t *line_start, *d_seg, *file_lines;
+    HIP_TRY(tmp.get(&line_start, ((size_t)n_nl + 1) * 8));
+    HIP_TRY(hipMemsetAsync(line_start, 0, 8, st));
+    HIP_TRY(launch_fp_nl_scatter(j->d_text, text_bytes, blk_off, line_start, st));
+    std::vector<uint64_t> seg(2 * (size_t)n_seg), fl(2 * (size_t)n_seg);
+    for (uint32_t f = 0; f < n_seg; f++) {
+        seg[2 * f] = j->seg_off[f];
+        seg[2 * f + 1] = j->seg_len[f];
+    }
+    HIP_TRY(tmp.get(&d_seg, seg.size() * 8));
+    HIP_TRY(tmp.get(&file_lines, seg.size() * 8));
+    if (n_seg) HIP_TRY(hipMemcpyAsync(d_seg, seg.data(), seg.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_fq_files(line_start, (uint64_t)n_nl + 1, d_seg, n_seg, file_lines, st));
+    if (n_seg) HIP_TRY(hipMemcpyAsync(fl.data(), file_lines, fl.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint64_t> base(n_seg ? n_seg : 1, 0);
+    uint64_t n_rec = 0;
+    for (uint32_t f = 0; f < n_seg; f++) {
+        base[f] = n_rec;
+        n_rec += fl[2 * f + 1] / 4;
+    }
+    uint64_t *d_base, *d_rec, *d_scan, *d_total;
+    uint32_t *d_fail;
+    HIP_TRY(tmp.get(&d_base, base.size() * 8));
+    HIP_TRY(hipMalloc((void **)&d_rec, (size_t)(n_rec ? n_rec : 1) * 5 * 8));
+    tmp.p.push_back(d_rec);
+    HIP_TRY(tmp.get(&d_scan, ((n_rec + 1023) / 1024 + 1) * 8));
+    HIP_TRY(tmp.get(&d_total, 16));
+    HIP_TRY(tmp.get(&d_fail, 4));
+    HIP_TRY(hipMemcpyAsync(d_base, base.data(), base.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(d_fail, 0, 4, st));
+    HIP_TRY(hipMemsetAsync(d_total, 0, 16, st));
+    HIP_TRY(launch_fq_records(j->d_text, line_start, d_seg, file_lines, d_base, n_seg, n_rec, d_rec,
+                              d_scan, d_total, d_fail, nullptr, st));
+    uint64_t total = 0;
+    uint32_t failed = 0;
+    HIP_TRY(hipMemcpyAsync(&total, d_total, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(&failed, d_fail, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (failed) {
+        tl.done();
+        return FPM_OK;
+    }
+    uint8_t *d_out;
+    HIP_TRY(hipMalloc((void **)&d_out, total + n_rec + 64));
+    if (hipError_t e = launch_fq_emit(j->d_text, n_rec, d_rec, d_out, st)) {
+        (void)hipFree(d_out);
+        return fail(FPM_EHIP, std::string("fastq emit: ") + hipGetErrorString(e));
+    }
+    tl.done();
+    if (hipError_t e = hipStreamSynchronize(st)) {
+        (void)hipFree(d_out);
+        return fail(FPM_EHIP, std::string("fastq emit: ") + hipGetErrorString(e));
+    }
+    tmp.p.erase(std::find(tmp.p.begin(), tmp.p.end(), (void *)d_rec));   // the job keeps it
+    j->d_rec = d_rec;
+    j->d_out = d_out;
+    j->n_rec = n_rec;
+    j->total_kept = total;
+    *ok = true;
+    return FPM_OK;
+}
+
+extern "C" {
+
 int fpm_seq_parse(fpm_ctx *ctx, const char *const *seg_text, const uint64_t *seg_len,
                   uint32_t n_seg, fpm_seqtext **job, uint64_t *n_records, int *quality_lines)
 {
@@ -1527,7 +1627,8 @@ int fpm_seq_parse(fpm_ctx *ctx, const char *const *seg_text, const uint64_t *seg
     if (n_chunks64 > 0xFFFFFFFFull) return fail(FPM_EINVAL, "seq_parse: input too large");
     const uint32_t n_chunks = (uint32_t)n_chunks64;
     hipStream_t st = ctx->stream;
-    HIP_TRY(hipMalloc(&j->d_text, text_bytes ? text_bytes : 16));
+    // 64 bytes of slack: the FASTQ emit reads whole 64-byte windows past a sequence line
+    HIP_TRY(hipMalloc(&j->d_text, text_bytes + 64));
     HIP_TRY(hipMalloc(&j->d_reset, n_chunks ? n_chunks : 1));
     HIP_TRY(hipMalloc(&j->d_xf, (size_t)(n_chunks ? n_chunks : 1) * seq_xf_bytes()));
     HIP_TRY(hipMalloc(&j->d_cin, (size_t)(n_chunks ? n_chunks : 1) * seq_cin_bytes()));
@@ -1547,6 +1648,20 @@ int fpm_seq_parse(fpm_ctx *ctx, const char *const *seg_text, const uint64_t *seg
         tl.done();
         HIP_TRY(hipMemcpyAsync(tot, j->d_totals, sizeof(tot), hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (tot[2]) {
+        // a '+' in sequence text: FASTQ.  The 4-line layout is parsed on the device and every
+        // record verified against kseq_read's quality rules; a file that does not read that way
+        // leaves *quality_lines set and the caller walks the files on the host
+        bool parsed = false;
+        if (int rc = fastq_parse(ctx, j.get(), text_bytes, st, &parsed)) return rc;
+        if (parsed) {
+            for (void **p : {(void **)&j->d_text, (void **)&j->d_xf, (void **)&j->d_cin})
+                if (*p) { (void)hipFree(*p); *p = nullptr; }
+            *n_records = j->n_rec;
+            *job = j.release();
+            return FPM_OK;
+        }
     }
     j->n_rec = tot[0];
     j->total_kept = tot[1];

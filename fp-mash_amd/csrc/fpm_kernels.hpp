@@ -207,6 +207,20 @@ hipError_t launch_seq_emit(const uint8_t *d_text, uint32_t n_chunks, const void 
                            uint64_t *d_hdr_end, uint64_t *d_kept_at, uint64_t *d_seq_off,
                            uint64_t *d_seq_len, uint8_t *d_out, hipStream_t st);
 
+// FASTQ, 4-line records verified against kseq_read's quality rules (seqparse.hip).
+// d_seg = (offset, length) per file in the text; d_file_lines = (first line, lines) per file
+hipError_t launch_fq_files(const uint64_t *d_line_start, uint64_t n_starts, const uint64_t *d_seg,
+                           uint32_t n_seg, uint64_t *d_file_lines, hipStream_t st);
+// record table in d_rec (hdr_pos | hdr_end | kept_at | seq_off | seq_len), *d_fail != 0 when a
+// record does not read the 4-line way; d_scan holds (n_rec + 1023) / 1024 u64, *d_total = bases
+hipError_t launch_fq_records(const uint8_t *d_text, const uint64_t *d_line_start,
+                             const uint64_t *d_seg, const uint64_t *d_file_lines,
+                             const uint64_t *d_rec_base, uint32_t n_seg, uint64_t n_rec,
+                             uint64_t *d_rec, uint64_t *d_scan, uint64_t *d_total, uint32_t *d_fail,
+                             uint8_t *d_out, hipStream_t st);
+hipError_t launch_fq_emit(const uint8_t *d_text, uint64_t n_rec, uint64_t *d_rec, uint8_t *d_out,
+                          hipStream_t st);
+
 // triangle -fp positional compare (dist.hip)
 hipError_t launch_positional_grid(const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,

@@ -4,7 +4,8 @@
 //    comment is the rest of the line (a '\r' of a CRLF file stays in it);
 //  * sequence = isgraph bytes until the next '>', '+' or '@' (or EOF);
 //  * FASTQ: skip the '+' line, then read quality bytes (33..127) until it is as
-//    long as the sequence; one more byte is consumed; shorter quality -> -2.
+//    long as the sequence; one more byte is consumed; shorter quality -> -2;
+//  * a 0xff byte reads as end of file in those loops (ks_getc of a signed char buffer).
 #include "SeqReader.h"
 
 #include <zlib.h>
@@ -81,20 +82,18 @@ int SeqReader::read()
     name.clear();
     comment.clear();
     seq.clear();
-    // name: up to isspace (ks_getuntil KS_SEP_SPACE)
-    bool any = false;
-    while ((c = getc_()) != -1 && !isspace(c)) { name.push_back((char)c); any = true; }
-    if (c == -1 && !any) return -1;
+    // name: up to isspace (ks_getuntil KS_SEP_SPACE: -1 only when the stream is at its end)
+    if (i_ >= n_) return -1;
+    while ((c = raw_()) != -1 && !isspace(c)) name.push_back((char)c);
     if (c != '\n' && c != -1) {
-        while ((c = getc_()) != -1 && c != '\n') comment.push_back((char)c);
+        while ((c = raw_()) != -1 && c != '\n') comment.push_back((char)c);
     }
     while ((c = getc_()) != -1 && c != '>' && c != '+' && c != '@')
         if (isgraph(c)) seq.push_back((char)c);
+    // at a -1 (end of file, or a 0xff byte) last_char keeps this record's marker: the next
+    // read takes the bytes after it as a header, as kseq_read does
     if (c == '>' || c == '@') last_ = c;
-    if (c != '+') {
-        if (c == -1) last_ = 0;
-        return (int)seq.size();
-    }
+    if (c != '+') return (int)seq.size();
     while ((c = getc_()) != -1 && c != '\n') {}
     if (c == -1) return -2;
     size_t q = 0;

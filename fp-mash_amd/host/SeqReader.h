@@ -23,7 +23,16 @@ public:
     std::string name, comment, seq;
 
 private:
-    int getc_() { return i_ < n_ ? p_[i_++] : -1; }
+    // ks_getc: (int) of a `char` buffer byte, so 0xff reads as -1 (end of file) on x86; it is
+    // consumed and the stream goes on (kseq.h:66-76)
+    int getc_()
+    {
+        if (i_ >= n_) return -1;
+        const int c = p_[i_++];
+        return c == 0xff ? -1 : c;
+    }
+    // ks_getuntil's direct buffer scan (name / comment): every byte is data
+    int raw_() { return i_ < n_ ? p_[i_++] : -1; }
     const unsigned char *p_;
     size_t n_, i_ = 0;
     int last_ = 0;

@@ -140,6 +140,20 @@ void ref_sketch_batch_mt(const char *seq, const unsigned long long *rec_off, uns
     for (auto &t : pool) t.join();
 }
 
+// kseq_read writes seq.s[seq.l] = 0 after the sequence loop (kseq.h:194) into a buffer it only
+// allocates once a base is stored: a stream whose FIRST record has no sequence byte (">x" at
+// EOF, ">x\n>y...") dereferences a null pointer there and the reference crashes.  The driver
+// pre-sizes the buffers, so such a record reads as an empty sequence -- the definition the
+// device parser and tests/seqio.py use.
+static kseq_t *presized(kseq_t *seq)
+{
+    seq->seq.m = 256;
+    seq->seq.s = (char *)malloc(seq->seq.m);
+    seq->qual.m = 256;
+    seq->qual.s = (char *)malloc(seq->qual.m);
+    return seq;
+}
+
 // kseq_read over a (optionally gzip'd) file, as sketchFileBySequence (Sketch.cpp:478-522)
 // reads it: every record's name, comment, sequence and quality strings.  Serialised into one
 // malloc'd buffer (free with ref_free): per record u64 lengths then bytes of name, comment,
@@ -150,7 +164,7 @@ unsigned char *ref_kseq_records(const char *path, unsigned long long *n, int *st
 {
     gzFile fp = gzopen(path, "r");
     if (!fp) return nullptr;
-    kseq_t *seq = kseq_init(fp);
+    kseq_t *seq = presized(kseq_init(fp));
     std::string out;
     unsigned long long cnt = 0;
     int l;
@@ -185,7 +199,7 @@ int ref_kseq_scan(const char *path, unsigned long long *n_rec, unsigned long lon
 {
     gzFile fp = gzopen(path, "r");
     if (!fp) return -3;
-    kseq_t *seq = kseq_init(fp);
+    kseq_t *seq = presized(kseq_init(fp));
     unsigned long long c = 0, b = 0;
     int l;
     while ((l = kseq_read(seq)) >= 0) {

@@ -1,13 +1,37 @@
-"""GPU parity of the device FASTA parser (csrc/seqparse.hip, fpm_seq_parse) against the
-kseq record rules (kseq.h:170-208) restated in tests/seqio.py, and of sketches of the
-parsed records against the oracle.  Records, names, comments and sequence lengths must be
-identical; sketches bit-exact."""
+"""GPU parity of the device FASTA / FASTQ parser (csrc/seqparse.hip, fpm_seq_parse) against
+the reference's kseq.h compiled into oracle/_ref (kseq_read over the file, as
+Sketch.cpp:478-522 reads it; tests/seqio.py, the Python restatement pinned to it, where
+oracle/_ref is absent), and of sketches of the parsed records against the oracle.  Records,
+names, comments and sequence lengths must be identical; sketches bit-exact."""
+import gzip
+import os
+import tempfile
+
 import numpy as np
 import pytest
 
 import seqio
+from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
+
+
+def kseq_records(data):
+    """[(name, comment, seq)] of kseq_read over `data`: the compiled kseq.h when built, else
+    seqio; None where kseq_read returns -2 (truncated quality)."""
+    from oracle import oracle as O
+    if O.ref() is None:
+        try:
+            return seqio.parse(data)
+        except ValueError:
+            return None
+    with tempfile.NamedTemporaryFile(suffix=".fq", delete=False) as f:
+        f.write(data)
+    try:
+        recs, st = O.ref_kseq_records(f.name)
+    finally:
+        os.unlink(f.name)
+    return None if st == -2 else [(n, c, s) for n, c, s, _q in recs]
 
 
 def device_records(ctx, files):
@@ -35,7 +59,7 @@ def device_records(ctx, files):
 
 
 def expected(files):
-    return [[(n, c, len(s)) for n, c, s in seqio.parse(f)] for f in files]
+    return [[(n, c, len(s)) for n, c, s in kseq_records(f)] for f in files]
 
 
 def fasta(rng, n_rec, lo, hi, width=70, crlf=False, lower=0.0):
@@ -144,4 +168,81 @@ def test_seq_parse_sketch_matches_oracle(ctx, oracle, per_record):
     exp = oracle.sketch_batch(O, flat, groups=grp, n_groups=len(want_groups))
     assert len(got) == len(exp)
     for a, b in zip(got, exp):
+        assert np.array_equal(a, b)
+
+
+def fastq(rng, n_rec, lo, hi, crlf=False, at_rate=0.0):
+    out = bytearray()
+    nl = b"\r\n" if crlf else b"\n"
+    for i in range(n_rec):
+        L = int(rng.integers(lo, hi + 1))
+        seq = np.frombuffer(b"ACGTN", np.uint8)[rng.integers(0, 5, L)].tobytes()
+        q = rng.integers(35, 74, L).astype(np.uint8)
+        if at_rate:
+            q[rng.random(L) < at_rate] = ord("@")      # Q31 in Phred+33: '@' in quality lines
+        out += b"@r%d/1 len=%d" % (i, L) + nl + seq + nl + b"+" + nl + q.tobytes() + nl
+    return bytes(out)
+
+
+FASTQ_OK = [
+    b"@r1 x\nACGT\n+\nIIII\n@r2\nGGGG\n+r2\nII@I\n",
+    b"@r1\r\nACGT\r\n+\r\nIIII\r\n@r2\r\nGG\r\n+\r\nII\r\n",
+    b"@e\n\n+\n\n@f\nA\n+\nI",
+    b"@r1\nAC GT\n+\nI I I I\n",
+    b"@h\xff1 c\nACGT\n+\nIIII\n\n\n",
+]
+FASTQ_HOST = [
+    b"@r1\nAC\nGT\n+\nII\nII\n@r2\nA\n+\nI\n",        # multi-line: host walk
+    b"@r1\nACGT\n+\nIIII@x\n>y\nAC\n",                    # quality longer than the bases
+    b"@r1\nAC\xffGT\n+\nIIII\n",                          # 0xff in the sequence line
+    b"junk\n@r1\nACGT\n+\nIIII\n",                         # bytes before the first header
+]
+
+
+@pytest.mark.parametrize("i", range(len(FASTQ_OK)))
+def test_fastq_device_parse(ctx, i):
+    """4-line FASTQ (CRLF, '@' in quality, empty records, spaces, 0xff in a header) parsed on
+    the device == kseq_read's records; no host walk needed."""
+    files = [FASTQ_OK[i]]
+    got, quality, job = device_records(ctx, files)
+    ctx.seq_free(job)
+    assert not quality
+    assert got == expected(files)
+
+
+@pytest.mark.parametrize("i", range(len(FASTQ_HOST)))
+def test_fastq_not_four_line_goes_to_host(ctx, i):
+    """FASTQ that kseq_read does not read the 4-line way is handed back to the host walk."""
+    _got, quality, job = device_records(ctx, [FASTQ_HOST[i]])
+    ctx.seq_free(job)
+    assert quality
+
+
+def test_fastq_fixtures_and_random_device_parse(ctx, oracle):
+    """reads1/2.fastq.gz (the fork's fixtures, inflated) and random FASTQ with '@'-rich quality
+    and CRLF, several files in one parse: records == kseq_read's, and the -i sketches of the
+    device-packed records == the oracle's."""
+    import fpmash
+    rng = np.random.default_rng(9)
+    files = [gzip.open(os.path.join(GOLDEN, "reads1.fastq.gz")).read(),
+             fastq(rng, 500, 0, 400, at_rate=0.2),
+             gzip.open(os.path.join(GOLDEN, "reads2.fastq.gz")).read(),
+             fastq(rng, 50, 2000, 9000, crlf=True)]
+    got, quality, job = device_records(ctx, files)
+    try:
+        assert not quality
+        exp = [kseq_records(f) for f in files]
+        assert got == [[(n, c, len(s)) for n, c, s in e] for e in exp]
+        flat = [s for e in exp for _n, _c, s in e]
+        groups = np.array([i if len(s) >= 21 else fpmash.NO_GROUP for i, s in enumerate(flat)],
+                          np.uint32)
+        keep = [s for s in flat if len(s) >= 21]
+        g = np.cumsum(groups != fpmash.NO_GROUP) - 1
+        groups = np.where(groups == fpmash.NO_GROUP, groups, g).astype(np.uint32)
+        sk = ctx.sketch_seq(fpmash.make_params(k=21, s=1000), job, groups, len(keep))
+    finally:
+        ctx.seq_free(job)
+    want = oracle.sketch_batch(oracle.params(k=21, s=1000), keep)
+    assert len(sk) == len(want)
+    for a, b in zip(sk, want):
         assert np.array_equal(a, b)

@@ -2,7 +2,7 @@ set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r03b
-timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -x -q -k "mirror or refset" --timeout 120 --timeout-method thread > gpurun_out/r03b/pytest.log 2>&1 || { tail -30 gpurun_out/r03b/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_seqparse.py tests/test_cli.py -q -k "mirror or refset or seq_parse or fastq" --timeout 120 --timeout-method thread > gpurun_out/r03b/pytest.log 2>&1 || { tail -30 gpurun_out/r03b/pytest.log; exit 1; }
 tail -2 gpurun_out/r03b/pytest.log
 timeout -k 10 120 python tools/micro/fp_stall.py > gpurun_out/r03b/fp_stall.log 2>&1 || { tail -20 gpurun_out/r03b/fp_stall.log; exit 1; }
 cat gpurun_out/r03b/fp_stall.log
