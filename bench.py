@@ -46,6 +46,40 @@ def _latest_pmc():
 
 
 PMC_TRAFFIC = _latest_pmc()
+
+
+def leg_counters(leg):
+    """A side leg's per-kernel counters (tools/pmc_traffic.py --leg, the newest
+    profiles/rNN/pmc_<leg>.json, measured on the GPU box): average launch time, HBM traffic
+    rate against the 8 TB/s peak, VALU-issue fraction, wave-state split, L2 hit rate and LDS
+    bank-conflict cycles, and the bound those numbers point to (the leg's bound claims are
+    read from here, not asserted).  None when no profile exists."""
+    import glob
+    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{leg}.json")))
+    if not found:
+        return None
+    d = json.load(open(found[-1]))
+    ks = {}
+    for k, v in d.get("kernels", {}).items():
+        if not v.get("avg_ns"):
+            continue
+        hbm = (v.get("traffic_GBps") or 0.0) / HBM_PEAK_GBS
+        valu = v.get("valu_issue_frac") or 0.0
+        ws_ = v.get("wave_state_frac") or {}
+        if max(hbm, valu) >= 0.5:
+            bound = "hbm" if hbm >= valu else "valu-issue"
+        else:
+            bound = "latency (waves waiting %.0f %%, issue-stalled %.0f %%)" % (
+                100 * ws_.get("waiting", 0.0), 100 * ws_.get("issue_stall", 0.0))
+        ks[k] = {"avg_ms": v["avg_ns"] * 1e-6, "calls": v.get("calls"),
+                 "traffic_bytes": v.get("traffic_bytes"), "frac_hbm": hbm,
+                 "valu_issue_frac": valu, "wave_state_frac": ws_,
+                 "l2_hit_frac": (v.get("l2") or {}).get("hit_frac"),
+                 "lds_bank_conflict_cycles": (v.get("l2") or {}).get("lds_bank_conflict_cycles"),
+                 "bound_by_counters": bound}
+    return {"source": os.path.relpath(found[-1], ROOT), "command": d.get("command"),
+            "kernels": dict(sorted(ks.items(), key=lambda kv: -kv[1]["avg_ms"] *
+                                   (kv[1]["calls"] or 1)))}
 METRIC = "bases/s sketched + Mpairs/s dist, k=21 s=1000, 1/2/4/8 MI355X; %HBM roofline"
 
 
@@ -1228,6 +1262,10 @@ def main():
     if not args.no_split:
         split = split_leg(ctx, grp, ws, rank, local, length=args.split_bases,
                           parity=not args.no_parity)
+
+    for leg, r_ in (("c3", c3), ("c4", c4), ("c5", c5)):
+        if r_ is not None:
+            r_["counters"] = leg_counters(leg)
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

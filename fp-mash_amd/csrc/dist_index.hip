@@ -102,7 +102,8 @@ constexpr int kKmaxU = 8;
 __global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
     uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax,
-    unsigned long long *__restrict__ zero, uint32_t nzero, unsigned long long *acc)
+    unsigned long long *__restrict__ zero, uint32_t nzero, unsigned long long *acc,
+    uint32_t *__restrict__ zero32, uint32_t nzero32)
 {
     __shared__ unsigned long long wmax[kKmaxThreads / 64];
     __shared__ uint32_t s_last;
@@ -138,6 +139,7 @@ __global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     if (!s_last) return;
     __threadfence();
     for (uint32_t i = threadIdx.x; i < nzero; i += kKmaxThreads) zero[i] = 0;
+    for (uint32_t i = threadIdx.x; i < nzero32; i += kKmaxThreads) zero32[i] = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         *kmax = atomicMax(&acc[0], 0ULL);
@@ -261,6 +263,102 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
     }
 }
 
+// ---- 1b'. one-pass level 1 (g.cap != 0): the tile counts its partitions itself (LDS
+// histogram), takes its run of each partition by one global atomic on part_fill[p] (tiles of
+// a partition land in completion order: the level-2 pass sorts inside the partition anyway),
+// and writes the runs into the partition's slot [p * cap, (p + 1) * cap) of tent.  Hash keys
+// are uniform, so cap = mean + 6 sigma + 64 holds every partition; a run past it sets
+// *overflow (the caller rebuilds with the exact two-pass form).  No histogram pass over the
+// keys and no scan launches.  Also flags unsorted rows (as idx_part_hist_kernel does).
+__global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
+    const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint32_t stride,
+    uint64_t magic, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
+    uint32_t *__restrict__ part_fill, uint64_t *__restrict__ tent, uint32_t *__restrict__ unsorted,
+    uint32_t *__restrict__ overflow)
+{
+    extern __shared__ __attribute__((aligned(16))) uint64_t stage[];   // kIdxTile words
+    __shared__ uint32_t gbase[kParts], lbase[kParts], lcur[kParts];
+    __shared__ uint32_t wsum[kIdxThreads / 64];
+    static_assert(kParts == kIdxThreads, "one partition per thread");
+    const uint64_t mult = idx_mult(g);
+    lcur[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
+    bool uns = false;
+    // pass 1: the tile's partition counts (and the sortedness flags)
+    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+        uint64_t key[kIdxU];
+        bool v[kIdxU], nx[kIdxU];
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
+            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+            const uint32_t la = e < n ? ref_len[min(r, n_ref - 1)] : 0;
+            v[u] = e < n && i < la;
+            nx[u] = v[u] && i + 1 < la;
+            key[u] = v[u] ? load_key(ref, hash_bytes, e) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            uint64_t nk = __shfl_down((unsigned long long)key[u], 1, 64);
+            if (lane == 63 && nx[u])
+                nk = load_key(ref, hash_bytes, (uint64_t)e0 + c0 + u * kIdxThreads + threadIdx.x + 1);
+            uns |= nx[u] && !(key[u] < nk);
+            if (v[u]) atomicAdd(&lcur[bucket_of(norm_key(key[u], hash_bytes), g, mult) >> g.l2], 1u);
+        }
+    }
+    if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
+    __syncthreads();
+    {
+        // this tile's run of partition p: local base (block exscan), global base (one atomic)
+        const uint32_t p = threadIdx.x, c = lcur[p];
+        const int wave = threadIdx.x >> 6;
+        uint32_t x = c;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) { const uint32_t y = __shfl_up(x, d, 64); if ((int)lane >= d) x += y; }
+        if (lane == 63) wsum[wave] = x;
+        __syncthreads();
+        uint32_t pre = 0;
+        for (int w = 0; w < wave; w++) pre += wsum[w];
+        lbase[p] = pre + x - c;
+        lcur[p] = pre + x - c;
+        gbase[p] = c ? atomicAdd(&part_fill[p], c) : 0u;
+    }
+    __syncthreads();
+    // pass 2: the keys again (L2-resident), grouped by partition in LDS
+    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+        uint64_t K[kIdxU];
+        uint32_t rr[kIdxU];
+        bool v[kIdxU];
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++) {
+            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
+            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+            v[u] = e < n && i < ref_len[min(r, n_ref - 1)];
+            rr[u] = r;
+            K[u] = v[u] ? norm_key(load_key(ref, hash_bytes, e), hash_bytes) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < kIdxU; u++)
+            if (v[u]) {
+                const uint32_t part = bucket_of(K[u], g, mult) >> g.l2;
+                const uint32_t pos = atomicAdd(&lcur[part], 1u);
+                stage[pos] = ((uint64_t)part << kPartShift) | pack_l1(K[u], rr[u], g, mult);
+            }
+    }
+    __syncthreads();
+    const uint32_t total = lcur[kParts - 1];
+    bool over = false;
+    for (uint32_t i = threadIdx.x; i < total; i += kIdxThreads) {
+        const uint64_t w = stage[i];
+        const uint32_t part = (uint32_t)(w >> kPartShift);
+        const uint32_t at = gbase[part] + (i - lbase[part]);    // within the partition's slot
+        if (at < g.cap) tent[(uint64_t)part * g.cap + at] = w;
+        else over = true;
+    }
+    if (__any(over) && lane == 0) atomicOr(overflow, 1u);
+}
+
 // ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits.
 // A partition of up to `cap` entries (C2: ~9.8k of 1e7 / 1024) is read once into registers
 // (16 per thread), counted, scattered into an LDS copy of its entries and written out
@@ -268,18 +366,43 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
 // `entries` (the previous form for every partition: tent read twice and the entries written
 // in scattered 4-B pieces, ~2x the algorithmic bytes).
 constexpr int kBucketThreads = 1024;
+static_assert(kBucketThreads == (int)kParts, "one-pass build: one partition fill per thread");
 constexpr int kBucketPer = 16;                   // entries per thread in registers
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
-    const uint64_t *__restrict__ tent, uint32_t ntiles,
+    const uint64_t *__restrict__ tent_all, uint32_t ntiles,
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t cap, uint32_t *__restrict__ dir,
-    uint32_t *__restrict__ entries, unsigned long long *__restrict__ sqsum)
+    uint32_t *__restrict__ entries_all, unsigned long long *__restrict__ sqsum,
+    const uint32_t *__restrict__ part_fill)
 {
     extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors; then cap entries
     __shared__ uint32_t wsum[kBucketThreads / 64];
     __shared__ unsigned long long wsq[kBucketThreads / 64];
     const uint32_t p = blockIdx.x;
-    const uint32_t s0 = tile_off[(uint64_t)p * ntiles];
-    const uint32_t s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
+    // this partition's entries are tent[s0, s1) and go to entries[s0, s1) (exact build), or
+    // (one-pass build) tent[p * g.cap, + fill) going to entries from the sum of the fills of
+    // the partitions before it (one fill per thread, block-reduced)
+    uint32_t s0, s1;
+    const uint64_t *tent = tent_all;
+    uint32_t *entries = entries_all;
+    if (part_fill) {
+        const uint32_t f = min(part_fill[threadIdx.x], g.cap);
+        uint32_t below = threadIdx.x < p ? f : 0u;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) below += __shfl_xor(below, d, 64);
+        if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = below;
+        __syncthreads();
+        uint32_t o = 0;
+        for (int w = 0; w < kBucketThreads / 64; w++) o += wsum[w];
+        __syncthreads();
+        const uint32_t mine = min(part_fill[p], g.cap);
+        // the buffers are addressed from s0 on: shift them so tent[s0] is the slot's first
+        tent = tent_all + (uint64_t)p * g.cap - o;
+        s0 = o;
+        s1 = o + mine;
+    } else {
+        s0 = tile_off[(uint64_t)p * ntiles];
+        s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
+    }
     const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
     uint32_t *const out = sh + nsb;
     const bool in_lds = s1 - s0 <= cap && cap <= (uint32_t)(kBucketThreads * kBucketPer);
@@ -843,7 +966,7 @@ hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint
 static hipError_t dyn_lds_attr(int slot, const void *fn, int bytes)
 {
     constexpr int kMaxDev = 64;
-    static std::atomic<int> done[2][kMaxDev];
+    static std::atomic<int> done[3][kMaxDev];
     int dev = 0;
     if (hipError_t e = hipGetDevice(&dev)) return e;
     if (dev < 0 || dev >= kMaxDev) return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
@@ -853,19 +976,44 @@ static hipError_t dyn_lds_attr(int slot, const void *fn, int bytes)
     return e;
 }
 
+uint64_t idx_tent_words(const IdxGeom &g, uint64_t E)
+{
+    return g.cap ? (uint64_t)kParts * g.cap : E;
+}
+
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
-                            uint32_t nzero, unsigned long long *acc, hipStream_t st)
+                            uint32_t nzero, unsigned long long *acc, uint32_t *part_fill,
+                            uint32_t *overflow, hipStream_t st)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
     const uint32_t kg = std::max<uint32_t>(1, std::min<uint32_t>(
         (n_ref + kKmaxThreads * kKmaxU - 1) / (kKmaxThreads * kKmaxU), 64));
+    const bool one_pass = g.cap != 0 && part_fill && overflow;
     hipLaunchKernelGGL(idx_kmax_kernel, dim3(kg), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
-                       stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero, acc);
+                       stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero, acc,
+                       one_pass ? part_fill : nullptr, one_pass ? kParts : 0u);
+    const uint64_t cnt_bytes0 = (uint64_t)4 << g.l2;
+    const uint32_t lds_cap = cnt_bytes0 <= 16384 ? (uint32_t)(kBucketThreads * kBucketPer) : 0u;
+    if (hipError_t e = dyn_lds_attr(1, (const void *)idx_bucket_kernel,
+                                    16384 + kBucketThreads * kBucketPer * 4))
+        return e;
+    if (one_pass) {
+        if (hipError_t e = dyn_lds_attr(2, (const void *)idx_part_scatter1_kernel, kIdxTile * 8))
+            return e;
+        hipLaunchKernelGGL(idx_part_scatter1_kernel, dim3(ntiles), dim3(kIdxThreads),
+                           (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic,
+                           n_ref, hash_bytes, g, part_fill, tent, unsorted, overflow);
+        hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
+                           (size_t)(cnt_bytes0 + (uint64_t)lds_cap * 4), st, (const uint64_t *)tent,
+                           ntiles, (const uint32_t *)nullptr, g, lds_cap, dir, entries, self_events,
+                           (const uint32_t *)part_fill);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
                        d_ref_len, (uint32_t)stride, magic, n_ref, hash_bytes, ntiles, tile_hist,
                        unsorted, g);
@@ -880,14 +1028,10 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                        g, tent);
     // LDS copy of a partition's entries when they fit beside the counters (two workgroups per
     // CU: 80 KiB each at l2 = 12); cap 0 = every partition on the global two-pass path
-    const uint64_t cnt_bytes = (uint64_t)4 << g.l2;
-    const uint32_t cap = cnt_bytes <= 16384 ? (uint32_t)(kBucketThreads * kBucketPer) : 0u;
-    if (hipError_t e = dyn_lds_attr(1, (const void *)idx_bucket_kernel,
-                                    16384 + kBucketThreads * kBucketPer * 4))
-        return e;
     hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
-                       (size_t)(cnt_bytes + (uint64_t)cap * 4), st, (const uint64_t *)tent, ntiles,
-                       (const uint32_t *)tile_off, g, cap, dir, entries, self_events);
+                       (size_t)(cnt_bytes0 + (uint64_t)lds_cap * 4), st, (const uint64_t *)tent,
+                       ntiles, (const uint32_t *)tile_off, g, lds_cap, dir, entries, self_events,
+                       (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 

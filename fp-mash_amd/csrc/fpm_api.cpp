@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <array>
 #include <cstdlib>
 #include <memory>
@@ -1784,6 +1785,12 @@ struct DistFinal {
 // >= 8 bits).  4K level-2 counters (16 KiB of LDS) and a 16 MB directory at the bench's
 // E = 1e7.  Same-box A/B: E/2 buckets cost 0.04 ms more in the bucket pass than the extra
 // probe events saved; E/8 a wash.
+// FPM_IDX_ONEPASS=0: always the exact two-pass index build (A/B)
+static const bool g_idx_one_pass = [] {
+    const char *v = getenv("FPM_IDX_ONEPASS");
+    return !(v && v[0] == '0');
+}();
+
 static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
 {
     IdxGeom geom{};
@@ -1795,7 +1802,51 @@ static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
     geom.rbits = rbits;
     geom.fbits = 32 - rbits;
     geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
+    // one-pass level 1: each partition's slot holds mean + 6 sigma + 64 entries (hash keys
+    // are uniform over the indexed range; skewed keys overflow and take the exact build)
+    const double mean = (double)E / (double)(1u << kIdxL1);
+    geom.cap = g_idx_one_pass ? (uint32_t)(((uint64_t)(mean + 6.0 * std::sqrt(mean)) + 64 + 63) & ~63ull)
+                              : 0u;
     return geom;
+}
+
+// One index build (launch_idx_build) and the read-back of its counters (events, sortedness,
+// the one-pass overflow flag at word 67), after `then` (work queued behind the build, e.g.
+// the query side's probe count).  The one-pass build first; if a level-1 partition overflowed
+// its slot, the exact two-pass build (g.cap = 0) replaces it.
+template <typename Then>
+static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint64_t stride,
+                       uint32_t n_ref, uint32_t hash_bytes, IdxGeom &g, uint32_t *dir,
+                       uint32_t *entries, unsigned long long *ctr, bool self_events,
+                       hipStream_t st, Then then)
+{
+    for (;;) {
+        const uint64_t E = (uint64_t)n_ref * stride;
+        const uint64_t nh = (uint64_t)(1u << kIdxL1) * g.ntiles;
+        void *tile_hist, *tile_off, *tent, *scan_s, *part_fill;
+        HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
+        HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
+        HIP_TRY(scratch(ctx, 2, idx_tent_words(g, E) * 8, &tent));
+        HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
+        HIP_TRY(scratch(ctx, 16, (size_t)(1u << kIdxL1) * 4, &part_fill));
+        uint32_t *unsorted = (uint32_t *)(ctr + 66), *overflow = (uint32_t *)(ctr + 67);
+        {
+            TimedLaunch tl(ctx, FPM_K_INDEX, st);
+            HIP_TRY(launch_idx_build(rows, len, stride, n_ref, hash_bytes, g,
+                                     (uint32_t *)tile_hist, (uint32_t *)tile_off,
+                                     (uint32_t *)scan_s, (uint64_t *)tent, dir, entries, unsorted,
+                                     self_events ? ctr : nullptr, ctr, 72, ctr + 72,
+                                     (uint32_t *)part_fill, overflow, st));
+            if (int rc = then()) return rc;
+            tl.done();
+        }
+        if (int rc = read_counters(ctx, ctr, 68, st)) return rc;
+        if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
+            g.cap = 0;
+            continue;
+        }
+        return FPM_OK;
+    }
 }
 
 // A reference set resident on the device with its bucket index built once (fpm_refset_*):
@@ -1851,28 +1902,17 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
     void *ctr;
     HIP_TRY(scratch(ctx, 7, kCtrWords * 8, &ctr));
     if (!rs->kmax) HIP_TRY(hipMalloc((void **)&rs->kmax, 8));
-    uint32_t *unsorted = (uint32_t *)((unsigned long long *)ctr + 66);
-    auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom g) -> int {
-        const uint64_t nh = (uint64_t)(1u << kIdxL1) * g.ntiles;
+    auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom &g) -> int {
         const uint64_t En = (uint64_t)rs->n_ref * stride;
-        void *tile_hist, *tile_off, *tent, *dir, *entries, *scan_s;
-        HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
-        HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
-        HIP_TRY(scratch(ctx, 2, En * 8, &tent));
-        HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
+        void *dir, *entries;
         HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
         HIP_TRY(slot_buf(rs->slot[5], En * 4, &entries));
-        TimedLaunch tl(ctx, FPM_K_INDEX, st);
-        HIP_TRY(launch_idx_build(rows, len, stride, rs->n_ref, rs->hash_bytes, g,
-                                 (uint32_t *)tile_hist, (uint32_t *)tile_off, (uint32_t *)scan_s,
-                                 (uint64_t *)tent, (uint32_t *)dir, (uint32_t *)entries,
-                                 unsorted, nullptr, (unsigned long long *)ctr, 72, (unsigned long long *)ctr + 72, st));
-        tl.done();
-        return FPM_OK;
+        return build_index(ctx, rows, len, stride, rs->n_ref, rs->hash_bytes, g, (uint32_t *)dir,
+                           (uint32_t *)entries, (unsigned long long *)ctr, false, st,
+                           [] { return FPM_OK; });
     };
     geom.kmax = rs->kmax;
     if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom)) return rc;
-    if (int rc = read_counters(ctx, (const unsigned long long *)ctr, 67, st)) return rc;
     rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
     rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
     rs->deduped = rs->ref_unsorted && rs->mr <= kDedupMax;
@@ -1977,11 +2017,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (try_sparse && fin && ctx->fill_early && !fin->prefilled)
         if (int rc = launch_fill()) return rc;
     if (try_sparse) {
-        const uint64_t nh = (uint64_t)(1u << kIdxL1) * geom.ntiles;
         const uint64_t NB = 1ULL << geom.nbits;
         void *ctr;
         HIP_TRY(scratch(ctx, 7, kCtrWords * 8, &ctr));
-            // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
+        // ctr: [0] events, [1..64] per-block partial events, [65] candidates, [66] unsorted flag,
+        // [67] the one-pass index build's overflow flag,
         // [68] the largest indexed key (the bucket scale)
         unsigned long long *events = (unsigned long long *)ctr, *n_cand = events + 65;
         uint32_t *unsorted = (uint32_t *)(events + 66);
@@ -2019,32 +2059,26 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // what the walk needs, so test the originals when the index is deduplicated
             all_sorted = !rs->ref_unsorted && (rs->deduped ? false : !q_unsorted);
         } else {
-            void *tile_hist, *tile_off, *tent, *dir_, *entries_, *scan_s;
-            HIP_TRY(scratch(ctx, 0, nh * 4, &tile_hist));
-            HIP_TRY(scratch(ctx, 1, (nh + 1) * 4, &tile_off));
-            HIP_TRY(scratch(ctx, 2, E * 8, &tent));
+            void *dir_, *entries_;
             HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir_));
             HIP_TRY(scratch(ctx, 5, E * 4, &entries_));
-            HIP_TRY(scratch(ctx, 6, scan_scratch_words(nh) * 4, &scan_s));
             geom.kmax = events + 68;
-            {
-                TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                // one set against itself: the query side is the ref side, so its sortedness is
-                // the ref flag and its posting events are sum_b |b|^2 from the bucket pass.
-                // The counters are zeroed by the first index kernel.
-                HIP_TRY(launch_idx_build(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
-                                         (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                         (uint32_t *)scan_s, (uint64_t *)tent,
-                                         (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, events, 72, events + 72, st));
-                if (!self_set)
-                    HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes, geom,
-                                               (const uint32_t *)dir_, events, unsorted, st));
-                tl.done();
-            }
+            // one set against itself: the query side is the ref side, so its sortedness is
+            // the ref flag and its posting events are sum_b |b|^2 from the bucket pass.
+            // The counters are zeroed by the first index kernel.
+            if (int rc = build_index(ctx, d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
+                                     (uint32_t *)dir_, (uint32_t *)entries_, events, self_set, st,
+                                     [&]() -> int {
+                                         if (!self_set)
+                                             HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride,
+                                                                        n_qry, hash_bytes, geom,
+                                                                        (const uint32_t *)dir_,
+                                                                        events, unsorted, st));
+                                         return FPM_OK;
+                                     }))
+                return rc;
             dir = (const uint32_t *)dir_;
             entries = (const uint32_t *)entries_;
-            if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
             ev = ctx->host_counters[0];
             all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
             // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
@@ -2062,25 +2096,29 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 }
                 geom = make_geom(n_ref, (uint64_t)n_ref * mr);
                 geom.kmax = events + 68;
-                TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, sketch_size,
-                                          dref, (uint32_t *)dref_len, mr, st));
-                if (!self_set)
-                    HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                              sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
-                HIP_TRY(launch_idx_build(dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes, geom,
-                                         (uint32_t *)tile_hist, (uint32_t *)tile_off,
-                                         (uint32_t *)scan_s, (uint64_t *)tent,
-                                         (uint32_t *)dir_, (uint32_t *)entries_, unsorted,
-                                         self_set ? events : nullptr, events, 72, events + 72, st));
+                {
+                    TimedLaunch tl(ctx, FPM_K_INDEX, st);
+                    HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
+                                              sketch_size, dref, (uint32_t *)dref_len, mr, st));
+                    if (!self_set)
+                        HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                                  sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
+                    tl.done();
+                }
                 p_qry = self_set ? dref : dqry;
                 p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
                 p_qry_stride = self_set ? mr : mq;
-                if (!self_set)
-                    HIP_TRY(launch_probe_count(p_qry, p_qry_it, p_qry_stride, n_qry, hash_bytes, geom,
-                                               (const uint32_t *)dir_, events, unsorted, st));
-                tl.done();
-                if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
+                if (int rc = build_index(ctx, dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes,
+                                         geom, (uint32_t *)dir_, (uint32_t *)entries_, events,
+                                         self_set, st, [&]() -> int {
+                                             if (!self_set)
+                                                 HIP_TRY(launch_probe_count(
+                                                     p_qry, p_qry_it, p_qry_stride, n_qry,
+                                                     hash_bytes, geom, (const uint32_t *)dir_,
+                                                     events, unsorted, st));
+                                             return FPM_OK;
+                                         }))
+                    return rc;
                 ev = ctx->host_counters[0];
             }
         }

@@ -117,14 +117,24 @@ struct IdxGeom {
     // device pointer: the largest indexed key (idx_kmax_kernel), from which every kernel
     // derives the bucket scale (bucket_of / key_fp in dist_index.hip)
     const unsigned long long *kmax;
+    // level-1 partition capacity of the one-pass scatter (tent holds kParts x cap entries,
+    // each tile appends to its partitions by one atomic per partition); 0 = the exact
+    // two-pass build (histogram + scan, tent holds E entries)
+    uint32_t cap;
 };
+// entries of the level-1 staging buffer `tent` the build needs
+uint64_t idx_tent_words(const IdxGeom &g, uint64_t E);
 hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64_t stride,
                             uint32_t n_ref, uint32_t hash_bytes, IdxGeom g, uint32_t *tile_hist,
                             uint32_t *tile_off, uint32_t *scan_s, uint64_t *tent,
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
-                            uint32_t nzero, unsigned long long *acc, hipStream_t st);
-// zero[0..nzero) is cleared first; acc[0..1]: two words that start at zero and are left at zero
+                            uint32_t nzero, unsigned long long *acc, uint32_t *part_fill,
+                            uint32_t *overflow, hipStream_t st);
+// zero[0..nzero) is cleared first; acc[0..1]: two words that start at zero and are left at zero.
+// One-pass build (g.cap != 0): part_fill holds 2^kIdxL1 u32 (cleared by the build), *overflow
+// (inside zero[]) is set when a partition exceeded cap: the index is then unusable and the
+// caller rebuilds with g.cap = 0
 uint64_t scan_scratch_words(uint64_t n);
 // copy n (<= kPubWords - 1) u64 counters into host-mapped memory, then write `seq` into its
 // last word (system-scope fence between): the host spins on that word

@@ -19,7 +19,7 @@ print('$s', 'c4', round(d['c4_dist']['ms_per_step'],3), d['c4_dist']['phase_ms_r
       continue
     fi
     env "${envs[@]}" timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline \
-      --no-c3 --no-c4 --no-c5 --no-cli --no-fp-text --no-parity > gpurun_out/env_$tag$i.json 2>&1 || exit 1
+      --no-c3 --no-c4 --no-c5 --no-cli --no-fp-text --no-split --no-parity > gpurun_out/env_$tag$i.json 2>&1 || exit 1
     python3 -c "
 import json; d=json.loads(open('gpurun_out/env_$tag$i.json').read().strip().splitlines()[-1])
 print('$s', round(d['ms_per_step'],4), {k[:12]:round(v['avg_ms'],3) for k,v in d['kernels'].items()})"

@@ -32,7 +32,10 @@ with fpmash.Context(0) as ctx:
         if fetch:
             a = arrays or [np.zeros(n, t) for t in (np.uint64, np.uint32, np.uint32, np.uint32,
                                                     np.uint8)]
-            fpmash._check(L.fpm_fp_text_fetch(job, *[x.ctypes.data for x in a]))
+            P = fpmash._p
+            fpmash._check(L.fpm_fp_text_fetch(job, P(a[0], fpmash.u64p), P(a[1], fpmash.u32p),
+                                              P(a[2], fpmash.u32p), a[3].ctypes.data,
+                                              P(a[4], fpmash.u8p)))
         L.fpm_fp_text_free(job)
         return n
 

@@ -51,11 +51,22 @@ def group_of(name: str):
     return None
 
 
+def kernel_key(name: str) -> str:
+    """A kernel's short name: 'void fpm::rank_rows_kernel<1024, unsigned short>(...)' ->
+    'rank_rows_kernel<1024, unsigned short>'."""
+    n = name.split("(")[0].strip()
+    for pre in ("void ", "fpm::"):
+        n = n.replace(pre, "")
+    return n
+
+
+GROUP_BY = {"fn": group_of}
+
+
 def run_pass(counter, outdir: str, bench_args: list[str]) -> dict:
     counters = [counter] if isinstance(counter, str) else list(counter)
     cmd = ["rocprofv3", "--pmc"] + counters + ["-d", outdir, "-o", "pmc", "--output-format",
-                                               "csv", "--", sys.executable,
-                                               os.path.join(ROOT, "bench.py")] + bench_args
+                                               "csv", "--", sys.executable] + bench_args
     env = dict(os.environ, TMPDIR="/tmp")
     with open(os.path.join(outdir + ".log"), "w") as log:
         subprocess.run(cmd, check=True, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
@@ -68,7 +79,7 @@ def run_pass(counter, outdir: str, bench_args: list[str]) -> dict:
     for row in csv.DictReader(open(files[0])):
         if row["Counter_Name"] not in per_disp:
             continue
-        g = group_of(row["Kernel_Name"])
+        g = GROUP_BY["fn"](row["Kernel_Name"])
         if g is None:
             continue
         per_disp[row["Counter_Name"]][(g, row["Dispatch_Id"])] += float(row["Counter_Value"])
@@ -92,18 +103,52 @@ def per_launch(per_disp: dict, launches: dict) -> dict:
     return {g: tot[g] * 1024.0 / launches[g] for g in tot if launches.get(g)}
 
 
+def kernel_times(outdir: str, bench_args: list[str]) -> dict:
+    """Average duration (ns) and calls per kernel key from a --kernel-trace --stats pass."""
+    cmd = ["rocprofv3", "--kernel-trace", "--stats", "-d", outdir, "-o", "kt", "--output-format",
+           "csv", "--", sys.executable] + bench_args
+    env = dict(os.environ, TMPDIR="/tmp")
+    with open(os.path.join(outdir + ".log"), "w") as log:
+        subprocess.run(cmd, check=True, cwd=ROOT, env=env, stdout=log, stderr=subprocess.STDOUT,
+                       timeout=600)
+    files = glob.glob(os.path.join(outdir, "**", "*kernel_trace.csv"), recursive=True)
+    if not files:
+        raise SystemExit(f"no kernel trace under {outdir}")
+    tot = collections.defaultdict(float)
+    calls = collections.defaultdict(int)
+    for row in csv.DictReader(open(files[0])):
+        k = GROUP_BY["fn"](row["Kernel_Name"])
+        if k is None:
+            continue
+        tot[k] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+        calls[k] += 1
+    return {k: {"avg_ns": tot[k] / calls[k], "calls": calls[k]} for k in tot}
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r02", "pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"))
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--leg", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: the bench step, kernels grouped as bench.py reports them; "
+                         "c3 / c4 / c5: tools/leg_run.py --leg, per kernel, with durations")
     a = ap.parse_args()
+    a.work = a.work + ("" if a.leg == "c2" else "_" + a.leg)
     os.makedirs(a.work, exist_ok=True)
-    # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
-    bench_args = ["--steps", str(a.steps), "--warmup", str(a.warmup), "--no-cpu-baseline",
-                  "--no-fp-text", "--no-c3", "--no-c4", "--no-c5", "--no-cli", "--no-split",
-                  "--no-parity"]
+    if a.leg == "c2":
+        # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
+        bench_args = [os.path.join(ROOT, "bench.py"), "--steps", str(a.steps), "--warmup",
+                      str(a.warmup), "--no-cpu-baseline", "--no-fp-text", "--no-c3", "--no-c4",
+                      "--no-c5", "--no-cli", "--no-split", "--no-parity"]
+    else:
+        bench_args = [os.path.join(ROOT, "tools", "leg_run.py"), "--leg", a.leg]
+        if a.leg == "c5":
+            # 250 of the 1,000 genomes (per-launch counters of 2.5x fewer tiles; each of the
+            # five passes regenerates the genomes on the host)
+            bench_args += ["--c5-genomes", "250"]
+        GROUP_BY["fn"] = kernel_key
     fetch = run_pass("FETCH_SIZE", os.path.join(a.work, "fetch"), bench_args)
     write = run_pass("WRITE_SIZE", os.path.join(a.work, "write"), bench_args)
     # one "launch" of a group that is several kernels (the index build) is one step's worth
@@ -136,13 +181,31 @@ def main():
                         "hit_frac": hit / (hit + miss) if hit + miss else None,
                         "lds_bank_conflict_cycles":
                             l2k.get("SQ_LDS_BANK_CONFLICT", {}).get(g, 0.0) / 1024.0}
+    if a.leg != "c2":
+        kt = kernel_times(os.path.join(a.work, "kt"), bench_args)
+        for k, v in res.items():
+            t = kt.get(k)
+            if not t:
+                continue
+            v["avg_ns"] = t["avg_ns"]
+            v["calls"] = t["calls"]
+            secs = t["avg_ns"] * 1e-9
+            v["traffic_GBps"] = v["traffic_bytes"] / secs / 1e9 if secs else None
+            # wave64 VALU instructions per launch / (launch time x 1024 SIMDs x 2.4 GHz / 2)
+            v["valu_issue_frac"] = (v["sq"].get("insts_valu", 0.0) / (secs * 1024 * 2.4e9 / 2)
+                                    if secs else None)
     out = {
+        "leg": a.leg,
+        "command": " ".join(["python3"] + [os.path.relpath(x, ROOT) if x.startswith(ROOT) else x
+                                           for x in bench_args]),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
-                  f"bench.py --steps {a.steps} --warmup {a.warmup}; bytes per launch = "
+                  f"the command above; bytes per launch = "
                   "2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE, KiB x 1024; includes "
                   "Infinity-Cache traffic. A third pass: SQ instruction counts and the "
                   "wave-state split (active / issue-stall / waiting) per launch; a fourth: "
-                  "L2 (TCC) hit / miss requests and LDS bank-conflict cycles",
+                  "L2 (TCC) hit / miss requests and LDS bank-conflict cycles; side legs add a "
+                  "--kernel-trace --stats pass for each kernel's average launch time, the "
+                  "achieved traffic rate and the VALU-issue fraction",
         "kernels": res,
     }
     os.makedirs(os.path.dirname(a.out), exist_ok=True)

@@ -2,7 +2,7 @@ set -o pipefail
 cd /root/repo
 export TMPDIR=/tmp
 mkdir -p gpurun_out/r03b
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_seqparse.py tests/test_cli.py -q -k "mirror or refset or seq_parse or fastq" --timeout 120 --timeout-method thread > gpurun_out/r03b/pytest.log 2>&1 || { tail -30 gpurun_out/r03b/pytest.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests/ -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/r03b/pytest.log 2>&1 || { tail -30 gpurun_out/r03b/pytest.log; exit 1; }
 tail -2 gpurun_out/r03b/pytest.log
 timeout -k 10 120 python tools/micro/fp_stall.py > gpurun_out/r03b/fp_stall.log 2>&1 || { tail -20 gpurun_out/r03b/fp_stall.log; exit 1; }
 cat gpurun_out/r03b/fp_stall.log
@@ -13,3 +13,7 @@ for ws in 2 4 8; do
 done
 timeout -k 10 240 python tools/c4_rank_share.py --ws 8 --rank 7 > gpurun_out/r03b/c4_share_ws8_r7.json 2> gpurun_out/r03b/c4_share_ws8_r7.err || { tail -20 gpurun_out/r03b/c4_share_ws8_r7.err; exit 1; }
 cut -c1-900 gpurun_out/r03b/c4_share_ws8_r7.json
+timeout -k 10 400 bash tools/env_ab.sh FPM_IDX_ONEPASS=0 > gpurun_out/r03b/env_ab_c2.txt 2>&1 || { tail -20 gpurun_out/r03b/env_ab_c2.txt; exit 1; }
+cat gpurun_out/r03b/env_ab_c2.txt
+AB_LEG=c4 timeout -k 10 600 bash tools/env_ab.sh FPM_IDX_ONEPASS=0 > gpurun_out/r03b/env_ab_c4.txt 2>&1 || { tail -20 gpurun_out/r03b/env_ab_c4.txt; exit 1; }
+cat gpurun_out/r03b/env_ab_c4.txt
