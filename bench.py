@@ -1304,7 +1304,8 @@ def main():
                      "device_ms_per_step": di_ms,
                      "pairs_with_shared_hashes_frac_sample": float((numer_sample > 0).mean()),
                      "path": fpmash.DIST_PATHS[int(dstats["sparse"])],
-                     "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"]},
+                     "posting_events": dstats["events"], "candidate_pairs": dstats["candidates"],
+                     "index_one_pass_rebuilds": ctx.index_rebuilds()},
             "fp_text": fp_leg,
             "c3_fp": c3,
             "c4_dist": c4,

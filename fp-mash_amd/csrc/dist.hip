@@ -260,6 +260,9 @@ constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest
 #ifndef FPM_RANK_LAYOUT
 #define FPM_RANK_LAYOUT 0            // 1: lane l ranks A[i0 + l], A[i0 + 64 + l] (A/B)
 #endif
+#ifndef FPM_RANK_KEQ
+#define FPM_RANK_KEQ 0               // 1: the 64-bit confirm read only on an equal 32-bit key (A/B)
+#endif
 #ifndef FPM_RANK_LOGB
 #define FPM_RANK_LOGB 12             // log2 buckets for CAP 1024 (CAP 2048: one more)
 #endif
@@ -289,11 +292,35 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     if constexpr (NP > 0) {
         const uint32_t ka = (uint32_t)(a >> kshift);
         uint32_t p = lo;
+#if FPM_RANK_KEQ
+        // the 64-bit confirm read only where a's key is one of B's (the keys are distinct and
+        // order B: a key below ka is a value below a, a key above it a value above; only an
+        // equal key leaves a's order and equality to the full values)
+        bool keq = false;
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const uint32_t k = K32[lo + q];
+            p += k < ka ? 1u : 0u;
+            keq |= k == ka;
+        }
+        keq = keq && !over;
+        j = p;
+        bool eq = false;
+        if (__builtin_amdgcn_ballot_w64(keq)) {
+            if (keq) {
+                const uint64_t v = Bs[p];
+                j = p + (v < a ? 1u : 0u);
+                eq = v == a;
+            }
+        }
+        return __builtin_amdgcn_ballot_w64(eq);
+#else
 #pragma unroll
         for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
         const uint64_t v = Bs[p];
         j = p + (v < a ? 1u : 0u);
         return __builtin_amdgcn_ballot_w64(v == a) & ~__builtin_amdgcn_ballot_w64(over);
+#endif
     } else {
         uint32_t jj = lo;
         uint64_t eqm = 0;

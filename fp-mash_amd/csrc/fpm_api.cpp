@@ -114,6 +114,7 @@ struct fpm_ctx {
     // ~27 ms for that (tools/micro/fp_text_time.py under rocprofv3: fp_line_kernel 0.06 ms,
     // now and then 27 ms)
     static constexpr size_t kPoolBytes = size_t(2) << 30;
+    uint64_t idx_rebuilds = 0;             // one-pass index builds that overflowed a slot
     std::vector<std::pair<void *, size_t>> pool;
     size_t pool_bytes = 0;
     std::mutex pool_mu;
@@ -501,6 +502,13 @@ int fpm_ctx_last_dist_stats(fpm_ctx *ctx, int *sparse, uint64_t *events, uint64_
         ctx->last_cand = v;
     }
     if (candidates) *candidates = ctx->last_cand;
+    return FPM_OK;
+}
+
+int fpm_ctx_index_rebuilds(fpm_ctx *ctx, uint64_t *count)
+{
+    if (!ctx || !count) return fail(FPM_EINVAL, "null argument");
+    *count = ctx->idx_rebuilds;
     return FPM_OK;
 }
 
@@ -1802,11 +1810,15 @@ static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
     geom.rbits = rbits;
     geom.fbits = 32 - rbits;
     geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
-    // one-pass level 1: each partition's slot holds mean + 6 sigma + 64 entries (hash keys
-    // are uniform over the indexed range; skewed keys overflow and take the exact build)
+    // one-pass level 1: each partition's slot holds 1.5 x the mean + 6 sigma + 64 entries.
+    // Bottom-s sketch values are uniform below each row's own maximum, and the rows' maxima
+    // differ, so the density over the indexed range [0, kmax] tapers towards kmax and the low
+    // partitions run ~10 % above the mean (C2: a 6-sigma slot overflowed on every build);
+    // skewed keys (repeated -fp values) overflow and take the exact build
     const double mean = (double)E / (double)(1u << kIdxL1);
-    geom.cap = g_idx_one_pass ? (uint32_t)(((uint64_t)(mean + 6.0 * std::sqrt(mean)) + 64 + 63) & ~63ull)
-                              : 0u;
+    geom.cap = g_idx_one_pass
+                   ? (uint32_t)(((uint64_t)(1.5 * mean + 6.0 * std::sqrt(mean)) + 64 + 63) & ~63ull)
+                   : 0u;
     return geom;
 }
 
@@ -1843,6 +1855,7 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
         if (int rc = read_counters(ctx, ctr, 68, st)) return rc;
         if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
             g.cap = 0;
+            ctx->idx_rebuilds++;
             continue;
         }
         return FPM_OK;

@@ -116,6 +116,7 @@ SYMBOLS = [
                                              C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                              vp]),
     ("fpm_refset_reindex", C.c_int, [vp, vp]),
+    ("fpm_ctx_index_rebuilds", C.c_int, [vp, u64p]),
     ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),
@@ -350,6 +351,12 @@ class Context:
 
     def set_dist_mode(self, mode):
         _check(lib().fpm_ctx_set_dist_mode(self.h, mode))
+
+    def index_rebuilds(self):
+        """one-pass index builds redone by the exact build (a level-1 slot overflowed)"""
+        v = C.c_uint64()
+        _check(lib().fpm_ctx_index_rebuilds(self.h, C.byref(v)))
+        return v.value
 
     def last_dist_stats(self):
         sp, ev, ca = C.c_int(), C.c_uint64(), C.c_uint64()

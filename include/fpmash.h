@@ -89,6 +89,9 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 #define FPM_K_FILL 8
 #define FPM_K_SEQPARSE 9
 #define FPM_K_COUNT 10
+/* one-pass bucket-index builds (dist_index.hip) that overflowed a level-1 slot and were
+ * redone by the exact two-pass build, since the context was created */
+int fpm_ctx_index_rebuilds(fpm_ctx *ctx, uint64_t *count);
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */

@@ -658,3 +658,64 @@ def test_refset_mirror_matches_oracle(ctx, oracle, mode):
         ctx.set_dist_mode(0)
         for b in keep:
             b.free()
+
+
+def test_index_one_pass_holds_sketch_partitions(ctx, oracle):
+    """The one-pass index build (level-1 slots of 1.5 x mean + 6 sigma) takes bottom-s sketch
+    rows without a rebuild (their values taper towards the largest indexed key), and the
+    sparse dist over it equals the oracle on sampled rows."""
+    import fpmash
+    from fpmash import datagen
+    seqs = datagen.family_dna(40, 50, 2000, sub_rate=(0.01, 0.1), seed=41)
+    sk = ctx.sketch(fpmash.make_params(k=21, s=1000), seqs)
+    before = ctx.index_rebuilds()
+    lengths = [len(x) for x in seqs]
+    rows = list(range(0, len(sk), 97))
+    ctx.set_dist_mode(2)
+    try:
+        d = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths)
+    finally:
+        ctx.set_dist_mode(0)
+    assert ctx.index_rebuilds() == before
+    nu, de, di, pv = oracle.dist_grid(sk, lengths, [sk[r] for r in rows], [lengths[r] for r in rows],
+                                      1000, 21, 4.0 ** 21)
+    n = len(sk)
+    got_nu = np.concatenate([d["numer"][r * n:(r + 1) * n] for r in rows])
+    got_de = np.concatenate([d["denom"][r * n:(r + 1) * n] for r in rows])
+    assert np.array_equal(got_nu, nu) and np.array_equal(got_de, de)
+
+
+def test_index_exact_build_forced():
+    """FPM_IDX_ONEPASS=0 (read at library load: a child process) forces the exact two-pass
+    index build; the sorted and the -fp dist grids still equal the oracle."""
+    import subprocess
+    import sys
+    code = r"""
+import os, sys
+sys.path[:0] = [%r, %r]
+import numpy as np
+import fpmash
+from fpmash import datagen
+from oracle import oracle as O
+with fpmash.Context(0) as ctx:
+    ctx.set_dist_mode(2)
+    seqs = datagen.family_dna(6, 10, 1500, sub_rate=(0.0, 0.1), seed=7)
+    sk = O.sketch_batch(O.params(k=21, s=300), seqs)
+    L = [len(x) for x in seqs]
+    d = ctx.dist(sk, sk, 300, ref_lengths=L, qry_lengths=L)
+    nu, de, _, _ = O.dist_grid(sk, L, sk, L, 300, 21, 4.0 ** 21)
+    assert np.array_equal(d["numer"], nu) and np.array_equal(d["denom"], de)
+    rng = np.random.default_rng(3)
+    fl = [rng.integers(0, 40, size=int(rng.integers(1, 300))).astype(np.uint32) for _ in range(50)]
+    FL = [len(x) * 7 for x in fl]
+    d = ctx.dist(fl, fl, 200, use64=False, k=1, kmer_space=10.0, ref_lengths=FL, qry_lengths=FL)
+    nu, de, _, _ = O.dist_grid(fl, FL, fl, FL, 200, 1, 10.0, use64=False)
+    assert np.array_equal(d["numer"], nu) and np.array_equal(d["denom"], de)
+    assert ctx.index_rebuilds() == 0
+print("exact-ok")
+""" % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+       os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fp-mash_amd"))
+    env = dict(os.environ, FPM_IDX_ONEPASS="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0 and "exact-ok" in r.stdout, r.stdout + r.stderr

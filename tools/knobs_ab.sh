@@ -10,7 +10,7 @@ for i in 1 2; do
   for n in "$@"; do
     L=$PWD/fp-mash_amd/lib/libfpmash_$n.so; [ "$n" = base ] && L=$PWD/fp-mash_amd/lib/libfpmash.so
     FPMASH_LIB=$L timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline \
-      --no-c3 --no-c4 --no-c5 --no-cli --no-fp-text --no-parity > gpurun_out/kn_$n$i.json 2>&1 || exit 1
+      --no-c3 --no-c4 --no-c5 --no-cli --no-fp-text --no-split --no-parity > gpurun_out/kn_$n$i.json 2>&1 || exit 1
     python3 -c "
 import json; d=json.loads(open('gpurun_out/kn_$n$i.json').read().strip().splitlines()[-1])
 print('$n', round(d['ms_per_step'],4), {k[:12]:round(v['avg_ms'],3) for k,v in d['kernels'].items()})"

@@ -17,3 +17,7 @@ timeout -k 10 400 bash tools/env_ab.sh FPM_IDX_ONEPASS=0 > gpurun_out/r03b/env_a
 cat gpurun_out/r03b/env_ab_c2.txt
 AB_LEG=c4 timeout -k 10 600 bash tools/env_ab.sh FPM_IDX_ONEPASS=0 > gpurun_out/r03b/env_ab_c4.txt 2>&1 || { tail -20 gpurun_out/r03b/env_ab_c4.txt; exit 1; }
 cat gpurun_out/r03b/env_ab_c4.txt
+FPMASH_LIB=$PWD/fp-mash_amd/lib/libfpmash_keq.so timeout -k 10 200 python -u -m pytest tests/test_gpu_parity.py -q -k "dist or refset" --timeout 120 --timeout-method thread > gpurun_out/r03b/pytest_keq.log 2>&1 || { tail -30 gpurun_out/r03b/pytest_keq.log; exit 1; }
+tail -1 gpurun_out/r03b/pytest_keq.log
+timeout -k 10 500 bash tools/knobs_ab.sh base keq lay1 keqlay1 > gpurun_out/r03b/knobs_rank.txt 2>&1 || { tail -20 gpurun_out/r03b/knobs_rank.txt; exit 1; }
+cat gpurun_out/r03b/knobs_rank.txt
