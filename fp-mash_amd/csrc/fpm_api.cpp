@@ -230,6 +230,45 @@ static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
     return hipSuccess;
 }
 
+// Caller memory that is not page-locked goes through the context's pinned ring (d2h_staged)
+// and is never handed to hipMemcpy directly: the runtime locks a large pageable buffer for the
+// DMA (a userptr mapping), and when the caller later frees it (numpy / malloc give such
+// buffers back with munmap) the kernel driver evicts and restores the process's GPU queues,
+// which stalled whatever ran on the GPU for ~20-30 ms (tools/micro/fp_clock.hip: a ticker
+// wave on its own stream saw a 26 ms gap next to the -fp text fetch into freshly malloc'd
+// arrays).  FPM_PAGEABLE_DIRECT=1 restores the direct copies (A/B).
+static const bool g_pageable_direct = [] {
+    const char *v = getenv("FPM_PAGEABLE_DIRECT");
+    return v && v[0] == '1';
+}();
+
+static bool host_pinned(const void *p)
+{
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// device -> caller host memory, synchronous; the caller has ordered `src`'s producers
+static hipError_t copy_out(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!bytes) return hipSuccess;
+    if (g_pageable_direct || bytes < (64u << 10) || host_pinned(dst))
+        return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    return d2h_staged(ctx, dst, src, bytes);
+}
+
+// caller host memory -> device, synchronous
+static hipError_t copy_in(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!bytes) return hipSuccess;
+    if (g_pageable_direct || host_pinned(src)) return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    return h2d_staged(ctx, dst, src, bytes);
+}
+
 static hipError_t ensure_aux(fpm_ctx *ctx)
 {
     if (ctx->aux) return hipSuccess;
@@ -463,7 +502,7 @@ int fpm_memcpy_d2h(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (int rc = set_device(ctx)) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (bytes) HIP_TRY(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    HIP_TRY(copy_out(ctx, dst, src, bytes));
     return FPM_OK;
 }
 
@@ -1028,22 +1067,19 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     const std::vector<MergeDesc> md = descs(mplan), smd = descs(splan);
     if (!packed.empty()) e = h2d_staged(ctx, job->d_seq, packed.data(), packed.size());
     if (e == hipSuccess && !by_class.empty())
-        e = hipMemcpy(job->d_tiles, by_class.data(), by_class.size() * sizeof(TileDesc),
-                      hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_tiles, by_class.data(), by_class.size() * sizeof(TileDesc));
     if (e == hipSuccess && !md.empty())
-        e = hipMemcpy(job->d_merge, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_merge, md.data(), md.size() * sizeof(MergeDesc));
     if (e == hipSuccess && !sby_class.empty())
-        e = hipMemcpy(job->d_stiles, sby_class.data(), sby_class.size() * sizeof(TileDesc),
-                      hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_stiles, sby_class.data(), sby_class.size() * sizeof(TileDesc));
     if (e == hipSuccess && !smd.empty())
-        e = hipMemcpy(job->d_smerge, smd.data(), smd.size() * sizeof(MergeDesc), hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_smerge, smd.data(), smd.size() * sizeof(MergeDesc));
     if (e == hipSuccess && !srow.empty())
-        e = hipMemcpy(job->d_srow, srow.data(), srow.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_srow, srow.data(), srow.size() * sizeof(uint32_t));
     if (e == hipSuccess && !sel.empty())
-        e = hipMemcpy(job->d_sel, sel.data(), sel.size() * sizeof(SelDesc), hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_sel, sel.data(), sel.size() * sizeof(SelDesc));
     if (e == hipSuccess && !sel_rows.empty())
-        e = hipMemcpy(job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t),
-                      hipMemcpyHostToDevice);
+        e = copy_in(ctx, job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t));
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -1074,7 +1110,7 @@ static int fallback_descs(fpm_sketch_job *job)
                               row(plan[i][2]), cnt(plan[i][2])};
         HIP_TRY(hipMalloc(dst, std::max<size_t>(1, md.size()) * sizeof(MergeDesc)));
         if (!md.empty())
-            HIP_TRY(hipMemcpy(*dst, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice));
+            HIP_TRY(copy_in(job->ctx, *dst, md.data(), md.size() * sizeof(MergeDesc)));
         return FPM_OK;
     };
     if (int rc = upload(job->fplan, &job->d_fmerge)) return rc;
@@ -1198,8 +1234,7 @@ int fpm_sketch_fetch(fpm_sketch_job *job, uint64_t *out_hashes, uint32_t *out_co
         HIP_TRY(d2h_staged(ctx, out_hashes, job->d_rows,
                            (size_t)job->n_groups * job->kp.s * sizeof(uint64_t)));
     if (out_count && job->n_groups)
-        HIP_TRY(hipMemcpy(out_count, job->d_count, (size_t)job->n_groups * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost));
+        HIP_TRY(copy_out(ctx, out_count, job->d_count, (size_t)job->n_groups * sizeof(uint32_t)));
     return FPM_OK;
 }
 
@@ -1299,7 +1334,7 @@ int fpm_sketch_merge_dev(fpm_ctx *ctx, const uint64_t *d_lists, const uint32_t *
     }
     HIP_TRY(scratch(ctx, 18, md.size() * sizeof(MergeDesc), &dd));
     HIP_TRY(hipStreamSynchronize(st));   // the descriptor buffer may still be read by a prior call
-    HIP_TRY(hipMemcpy(dd, md.data(), md.size() * sizeof(MergeDesc), hipMemcpyHostToDevice));
+    HIP_TRY(copy_in(ctx, dd, md.data(), md.size() * sizeof(MergeDesc)));
     for (size_t r = 0; r + 1 < rounds.size(); r++) {
         TimedLaunch tl(ctx, FPM_K_MERGE, st);
         HIP_TRY(launch_merge((const MergeDesc *)dd + rounds[r], rounds[r + 1] - rounds[r], s, false,
@@ -1351,14 +1386,14 @@ int fpm_fp_hash_lines(fpm_ctx *ctx, const uint64_t *vals, const uint64_t *line_o
     hipError_t e = hipMalloc((void **)&dv, (nv ? nv : 1) * 8);
     if (e == hipSuccess) e = hipMalloc((void **)&doff, (n_lines + 1) * 8);
     if (e == hipSuccess) e = hipMalloc(&dout, ob);
-    if (e == hipSuccess && nv) e = hipMemcpy(dv, vals, nv * 8, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = hipMemcpy(doff, line_off, (n_lines + 1) * 8, hipMemcpyHostToDevice);
+    if (e == hipSuccess && nv) e = copy_in(ctx, dv, vals, nv * 8);
+    if (e == hipSuccess) e = copy_in(ctx, doff, line_off, (n_lines + 1) * 8);
     int rc = FPM_OK;
     if (e != hipSuccess) rc = fail(FPM_EHIP, std::string("fp staging: ") + hipGetErrorString(e));
     if (!rc) rc = fpm_fp_hash_lines_dev(ctx, dv, doff, n_lines, seed, use64, dout, nullptr);
     if (!rc) {
         e = hipStreamSynchronize(ctx->stream);
-        if (e == hipSuccess) e = hipMemcpy(out, dout, ob, hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = copy_out(ctx, out, dout, ob);
         if (e != hipSuccess) rc = fail(FPM_EHIP, std::string("fp fetch: ") + hipGetErrorString(e));
     }
     (void)hipFree(dv); (void)hipFree(doff); (void)hipFree(dout);
@@ -1467,15 +1502,15 @@ int fpm_fp_text_fetch(fpm_fptext *j, uint64_t *id_off, uint32_t *id_len, uint32_
     if (int rc = set_device(j->ctx)) return rc;
     hipStream_t st = j->ctx->stream;
     const uint64_t n = j->n_lines;
-    if (n) {
-        if (id_off) HIP_TRY(hipMemcpyAsync(id_off, j->d_id_off, n * 8, hipMemcpyDeviceToHost, st));
-        if (id_len) HIP_TRY(hipMemcpyAsync(id_len, j->d_id_len, n * 4, hipMemcpyDeviceToHost, st));
-        if (n_vals) HIP_TRY(hipMemcpyAsync(n_vals, j->d_n_vals, n * 4, hipMemcpyDeviceToHost, st));
-        if (hash)
-            HIP_TRY(hipMemcpyAsync(hash, j->d_hash, n * (j->use64 ? 8 : 4), hipMemcpyDeviceToHost, st));
-        if (new_id) HIP_TRY(hipMemcpyAsync(new_id, j->d_new_id, n, hipMemcpyDeviceToHost, st));
-    }
     HIP_TRY(hipStreamSynchronize(st));
+    if (n) {
+        fpm_ctx *ctx = j->ctx;
+        if (id_off) HIP_TRY(copy_out(ctx, id_off, j->d_id_off, n * 8));
+        if (id_len) HIP_TRY(copy_out(ctx, id_len, j->d_id_len, n * 4));
+        if (n_vals) HIP_TRY(copy_out(ctx, n_vals, j->d_n_vals, n * 4));
+        if (hash) HIP_TRY(copy_out(ctx, hash, j->d_hash, n * (j->use64 ? 8 : 4)));
+        if (new_id) HIP_TRY(copy_out(ctx, new_id, j->d_new_id, n));
+    }
     return FPM_OK;
 }
 
@@ -2467,7 +2502,7 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
     auto up = [&](DevBuf &b, const void *h, size_t bytes) {
         if (e != hipSuccess) return;
         e = hipMalloc(&b.p, bytes ? bytes : 16);
-        if (e == hipSuccess && h && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess && h && bytes) e = copy_in(ctx, b.p, h, bytes);
     };
     // one set against itself (dist X.msh X.msh): upload once; the grid call then sees
     // identical device inputs and may use the pair symmetry
@@ -2501,11 +2536,11 @@ int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint6
                                         (uint32_t *)nu.p, (uint32_t *)de.p, nullptr);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(ctx->stream));
-    if (out_numer) HIP_TRY(hipMemcpy(out_numer, nu.p, np * 4, hipMemcpyDeviceToHost));
-    if (out_denom) HIP_TRY(hipMemcpy(out_denom, de.p, np * 4, hipMemcpyDeviceToHost));
-    if (out_dist) HIP_TRY(hipMemcpy(out_dist, di.p, np * 8, hipMemcpyDeviceToHost));
-    if (out_pvalue) HIP_TRY(hipMemcpy(out_pvalue, pv.p, np * 8, hipMemcpyDeviceToHost));
-    if (out_pass) HIP_TRY(hipMemcpy(out_pass, pa.p, np, hipMemcpyDeviceToHost));
+    if (out_numer) HIP_TRY(copy_out(ctx, out_numer, nu.p, np * 4));
+    if (out_denom) HIP_TRY(copy_out(ctx, out_denom, de.p, np * 4));
+    if (out_dist) HIP_TRY(copy_out(ctx, out_dist, di.p, np * 8));
+    if (out_pvalue) HIP_TRY(copy_out(ctx, out_pvalue, pv.p, np * 8));
+    if (out_pass) HIP_TRY(copy_out(ctx, out_pass, pa.p, np));
     return FPM_OK;
 }
 
@@ -2572,15 +2607,11 @@ int fpm_refset_create(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
     HIP_TRY(hipMalloc(&rs->own[0], mb));
     HIP_TRY(hipMalloc(&rs->own[1], std::max<size_t>(16, (size_t)n_ref * 4)));
     HIP_TRY(hipMalloc(&rs->own[2], std::max<size_t>(16, (size_t)n_ref * 8)));
-    hipStream_t st = ctx->stream;
     if ((size_t)n_ref * ref_stride)
-        HIP_TRY(hipMemcpyAsync(rs->own[0], ref, (size_t)n_ref * ref_stride * hash_bytes,
-                               hipMemcpyHostToDevice, st));
+        HIP_TRY(copy_in(ctx, rs->own[0], ref, (size_t)n_ref * ref_stride * hash_bytes));
     if (n_ref) {
-        HIP_TRY(hipMemcpyAsync(rs->own[1], ref_len, (size_t)n_ref * 4, hipMemcpyHostToDevice, st));
-        if (ref_length)
-            HIP_TRY(hipMemcpyAsync(rs->own[2], ref_length, (size_t)n_ref * 8, hipMemcpyHostToDevice,
-                                   st));
+        HIP_TRY(copy_in(ctx, rs->own[1], ref_len, (size_t)n_ref * 4));
+        if (ref_length) HIP_TRY(copy_in(ctx, rs->own[2], ref_length, (size_t)n_ref * 8));
     }
     rs->ref = rs->own[0];
     rs->ref_len = (const uint32_t *)rs->own[1];
@@ -2675,11 +2706,11 @@ int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
     HIP_TRY(slot_buf(rs->qslot[5], np * 8, &di));
     HIP_TRY(slot_buf(rs->qslot[6], np * 8, &pv));
     HIP_TRY(slot_buf(rs->qslot[7], np, &pa));
-    HIP_TRY(hipMemcpyAsync(q, qry, (size_t)n_qry * qry_stride * rs->hash_bytes,
-                           hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(ql, qry_len, (size_t)n_qry * 4, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));            // the query slots are free to overwrite
+    HIP_TRY(copy_in(ctx, q, qry, (size_t)n_qry * qry_stride * rs->hash_bytes));
+    HIP_TRY(copy_in(ctx, ql, qry_len, (size_t)n_qry * 4));
     if (qry_length)
-        HIP_TRY(hipMemcpyAsync(qL, qry_length, (size_t)n_qry * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(copy_in(ctx, qL, qry_length, (size_t)n_qry * 8));
     else
         HIP_TRY(hipMemsetAsync(qL, 0, (size_t)n_qry * 8, st));
     if (int rc = fpm_refset_dist_dev(rs, q, (const uint32_t *)ql, (const uint64_t *)qL, qry_stride,
@@ -2687,13 +2718,14 @@ int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
                                      max_pvalue, nu, de, (double *)di, (double *)pv,
                                      (uint8_t *)pa, st))
         return rc;
-    // results: caller memory (pinned from fpm_host_alloc copies at full PCIe rate)
-    if (out_numer) HIP_TRY(hipMemcpyAsync(out_numer, nu, np * 4, hipMemcpyDeviceToHost, st));
-    if (out_denom) HIP_TRY(hipMemcpyAsync(out_denom, de, np * 4, hipMemcpyDeviceToHost, st));
-    if (out_dist) HIP_TRY(hipMemcpyAsync(out_dist, di, np * 8, hipMemcpyDeviceToHost, st));
-    if (out_pvalue) HIP_TRY(hipMemcpyAsync(out_pvalue, pv, np * 8, hipMemcpyDeviceToHost, st));
-    if (out_pass) HIP_TRY(hipMemcpyAsync(out_pass, pa, np, hipMemcpyDeviceToHost, st));
+    // results: caller memory (pinned from fpm_host_alloc copies at full PCIe rate, pageable
+    // memory through the context's pinned ring)
     HIP_TRY(hipStreamSynchronize(st));
+    if (out_numer) HIP_TRY(copy_out(ctx, out_numer, nu, np * 4));
+    if (out_denom) HIP_TRY(copy_out(ctx, out_denom, de, np * 4));
+    if (out_dist) HIP_TRY(copy_out(ctx, out_dist, di, np * 8));
+    if (out_pvalue) HIP_TRY(copy_out(ctx, out_pvalue, pv, np * 8));
+    if (out_pass) HIP_TRY(copy_out(ctx, out_pass, pa, np));
     return FPM_OK;
 }
 
@@ -2728,7 +2760,7 @@ int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_le
     auto up = [&](DevBuf &b, const void *h, size_t bytes) {
         if (e != hipSuccess) return;
         e = hipMalloc(&b.p, bytes ? bytes : 16);
-        if (e == hipSuccess && h && bytes) e = hipMemcpy(b.p, h, bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess && h && bytes) e = copy_in(ctx, b.p, h, bytes);
     };
     up(r, ref, (size_t)n_ref * ref_stride * hash_bytes);
     up(rl, ref_len, (size_t)n_ref * 4);
@@ -2746,11 +2778,11 @@ int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_le
                                    max_pvalue, (uint32_t *)nu.p, (uint32_t *)de.p, (double *)di.p,
                                    (double *)pv.p, (uint8_t *)pa.p, st));
     HIP_TRY(hipStreamSynchronize(st));
-    if (out_numer) HIP_TRY(hipMemcpy(out_numer, nu.p, np * 4, hipMemcpyDeviceToHost));
-    if (out_denom) HIP_TRY(hipMemcpy(out_denom, de.p, np * 4, hipMemcpyDeviceToHost));
-    if (out_dist) HIP_TRY(hipMemcpy(out_dist, di.p, np * 8, hipMemcpyDeviceToHost));
-    if (out_pvalue) HIP_TRY(hipMemcpy(out_pvalue, pv.p, np * 8, hipMemcpyDeviceToHost));
-    if (out_pass) HIP_TRY(hipMemcpy(out_pass, pa.p, np, hipMemcpyDeviceToHost));
+    if (out_numer) HIP_TRY(copy_out(ctx, out_numer, nu.p, np * 4));
+    if (out_denom) HIP_TRY(copy_out(ctx, out_denom, de.p, np * 4));
+    if (out_dist) HIP_TRY(copy_out(ctx, out_dist, di.p, np * 8));
+    if (out_pvalue) HIP_TRY(copy_out(ctx, out_pvalue, pv.p, np * 8));
+    if (out_pass) HIP_TRY(copy_out(ctx, out_pass, pa.p, np));
     return FPM_OK;
 }
 

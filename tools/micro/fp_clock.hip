@@ -8,6 +8,7 @@
 //   hipcc --offload-arch=gfx950 -O2 -I../../include fp_clock.hip -L../../fp-mash_amd/lib \
 //         -lfpmash -Wl,-rpath,'$ORIGIN/../../fp-mash_amd/lib' -o fp_clock
 #include <hip/hip_runtime.h>
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -80,6 +81,7 @@ int main()
     }
     fpm_ctx_synchronize(ctx);
     const auto h0 = std::chrono::steady_clock::now();
+    double worst_call = 0;
     hipLaunchKernelGGL(ticker, dim3(1), dim3(64), 0, ts, d_log, d_n, cap, 60000000ull);   // 0.6 s
     for (int c = 0; c < 40; c++) {
         fpm_ctx_reset_timing(ctx);
@@ -101,6 +103,7 @@ int main()
         const auto b = std::chrono::steady_clock::now();
         double ms; uint64_t l;
         fpm_ctx_kernel_time(ctx, FPM_K_FPTEXT, &ms, &l);
+        worst_call = std::max(worst_call, ms);
         printf("call %2d: host %.3f..%.3f ms, kernels %.3f ms\n", c,
                std::chrono::duration<double, std::milli>(a - h0).count(),
                std::chrono::duration<double, std::milli>(b - h0).count(), ms);
@@ -110,6 +113,11 @@ int main()
     hipMemcpy(&n_log, d_n, 4, hipMemcpyDeviceToHost);
     std::vector<Sample> lg(n_log);
     hipMemcpy(lg.data(), d_log, n_log * sizeof(Sample), hipMemcpyDeviceToHost);
+    double worst_gap = 0;
+    for (unsigned i = 1; i < n_log; i++)
+        worst_gap = std::max(worst_gap, (double)(lg[i].rt - lg[i - 1].rt) / 100.0);
+    printf("SUMMARY worst kernel-time call %.3f ms, worst ticker gap %.1f us, pageable_direct=%s\n",
+           worst_call, worst_gap, getenv("FPM_PAGEABLE_DIRECT") ? getenv("FPM_PAGEABLE_DIRECT") : "0");
     printf("ticker: %u samples (gaps > 20 us and one per ms)\n", n_log);
     for (unsigned i = 1; i < n_log; i++) {
         const double drt = (double)(lg[i].rt - lg[i - 1].rt) / 100.0;        // us
