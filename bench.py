@@ -293,10 +293,11 @@ def fp_text_leg(ctx, reps=5):
     lines = text.count(b"\n")
     for warm in (text[:100000], text):                             # warm (pinned ring too)
         ctx.fp_text(warm, max_lines=1_000_000)
-    # per call: the HIP-event total of its launches.  The median is reported: one call in a
-    # process (the 4th, every run) has its fp_line launch take 21-29 ms in rocprofv3's trace
-    # too, pooled or fresh buffers alike, against ~0.12 ms for every other call
-    # (tools/micro/fp_text_time.py, profiles/r02/fp_text_time.log); the list is in the line
+    # per call: the HIP-event total of its launches; the mean over the calls is reported, with
+    # the list.  (Round 2 saw one call in five take 21-34 ms: the runtime page-locked the
+    # pageable result arrays for the fetch, and releasing them made the driver evict and restore
+    # the process's GPU queues -- a GPU-wide 12-30 ms stall, tools/micro/fp_clock.hip,
+    # profiles/r03/fp_stall/.  Caller memory now goes through the context's pinned ring.)
     devs, walls = [], []
     for _ in range(reps):
         ctx.reset_timing()
@@ -308,15 +309,16 @@ def fp_text_leg(ctx, reps=5):
         tot, _cnt = ctx.kernel_time(fpmash.K_FPTEXT)
         devs.append(tot * 1e-3)
     ctx.reset_timing()
-    dev = float(np.median(devs))
-    wall = float(np.median(walls))
+    dev = float(np.mean(devs))
+    wall = float(np.mean(walls))
     n = len(r["hash"])
     return {"lines": n, "text_bytes": len(text), "device_ms": dev * 1e3,
             "device_ms_calls": [round(d * 1e3, 4) for d in devs],
+            "device_ms_max": max(devs) * 1e3,
             "lines_per_s_device": n / dev, "text_GBps_device": len(text) / dev / 1e9,
             "lines_per_s_wall_pcie": n / wall, "wall_ms": wall * 1e3,
             "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap); "
-                    f"median of {reps} calls"}
+                    f"mean of {reps} calls"}
 
 
 def _group_fp_lines(r, text):
