@@ -47,7 +47,13 @@ const char kComplAZ[26] = {'T', 'V', 'G', 'H', 'N', 'N', 'C', 'D', 'N', 'N', 'M'
 // Tile sizing: small records are packed up to kPackKmers k-mer starts per tile,
 // long records are cut into kChunkKmers-start chunks (k-1 bytes of halo).
 constexpr uint32_t kPackKmers = 2048;
-constexpr uint32_t kChunkKmers = 4096;
+// FPM_CHUNK_KMERS=2048 cuts long records into 2048-start chunks (the P = 2048 tile kernel:
+// 7 waves per SIMD against 4 for P = 4096) -- an A/B switch for the C5 shape
+static const uint32_t kChunkKmers = [] {
+    const char *v = getenv("FPM_CHUNK_KMERS");
+    const uint32_t c = v ? (uint32_t)atoi(v) : 4096u;
+    return (c == 1024 || c == 2048 || c == 4096 || c == 8192) ? c : 4096u;
+}();
 
 int tile_class(uint32_t nstarts)
 {

@@ -2,7 +2,8 @@
 # tools/env_ab.sh "VAR=VAL[,VAR=VAL]" ... — same-box A/B of runtime switches (FPM_FILL_EARLY,
 # FPM_DENSE_IMG, ...) on the C2 step: each setting ("base" = none) runs twice, alternating,
 # 20 timed steps each; one line per run: setting, ms/step, per-kernel averages.
-# AB_LEG=c4: the C4 leg instead (50k-sketch all-vs-all, 3 timed steps), its ms/step.
+# AB_LEG=c4: the C4 leg instead (50k-sketch all-vs-all, 3 timed steps), its ms/step;
+# AB_LEG=c5: the C5 leg (tools/leg_run.py --leg c5: 1,000 x 5 Mb, one timed step).
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
@@ -10,6 +11,13 @@ for i in 1 2; do
   for s in base "$@"; do
     envs=(); [ "$s" != base ] && IFS=',' read -ra envs <<< "$s"
     tag=$(echo "$s" | tr -c 'A-Za-z0-9' '_')
+    if [ "${AB_LEG:-c2}" = c5 ]; then
+      env "${envs[@]}" timeout -k 10 300 python tools/leg_run.py --leg c5 > gpurun_out/env_$tag$i.json 2>&1 || exit 1
+      python3 -c "
+import json; d=json.loads(open('gpurun_out/env_$tag$i.json').read().strip().splitlines()[-1])
+print('$s', 'c5', round(d['ms_per_step'],3), {k: round(v['ms'],3) for k, v in d['rank0']['kernels'].items()})"
+      continue
+    fi
     if [ "${AB_LEG:-c2}" = c4 ]; then
       env "${envs[@]}" timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
         --no-c3 --no-c5 --no-cli --no-fp-text --no-split --no-parity > gpurun_out/env_$tag$i.json 2>&1 || exit 1

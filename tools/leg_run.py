@@ -27,7 +27,7 @@ def main():
         elif a.leg == "c4":
             r = bench.c4_leg(ctx, grp, 1, 0, 0, steps=2, warmup=1, parity=False)
         else:
-            r = bench.c5_leg(ctx, grp, 1, 0, n_genomes=a.c5_genomes, steps=1, warmup=1,
+            r = bench.c5_leg(ctx, grp, 1, 0, n_genomes=a.c5_genomes, steps=3, warmup=1,
                              parity=False)
     print(json.dumps(r, default=str))
 
