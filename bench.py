@@ -734,12 +734,15 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "candidates_all_ranks": cand, "parity": par}
 
 
-def cli_phases(stderr: bytes):
-    """[fpmash] phase: X ms lines (FPMASH_TIMING=1) -> {phase: ms} (repeated phases summed)."""
+def cli_phases(stderr: bytes, prefix="[fpmash] "):
+    """[fpmash] phase: X ms lines (FPMASH_TIMING=1) -> {phase: ms} (repeated phases summed).
+    prefix "[fpmash-warm] ": the device warm-up thread's own steps (runtime start, context,
+    staging ring), which run beside the main thread's input read; the main thread's wait for
+    them is its "device context" phase."""
     out = {}
     for line in stderr.decode(errors="replace").splitlines():
-        if line.startswith("[fpmash] ") and line.endswith(" ms") and ": " in line:
-            name, val = line[len("[fpmash] "):-3].rsplit(": ", 1)
+        if line.startswith(prefix) and line.endswith(" ms") and ": " in line:
+            name, val = line[len(prefix):-3].rsplit(": ", 1)
             try:
                 out[name] = out.get(name, 0.0) + float(val)
             except ValueError:
@@ -786,7 +789,8 @@ def cli_leg(args, seqs, cpu=None, check=True):
                "fasta_bytes": os.path.getsize(fa), "cli_sketch_wall_s": t_sketch,
                "cli_dist_wall_s": t_dist, "dist_lines": n * n, "dist_text_bytes": out_bytes,
                "dist_lines_per_s": n * n / t_dist, "output_dir": base or tempfile.gettempdir(),
-               "phases_ms_sketch": cli_phases(ps.stderr), "phases_ms_dist": cli_phases(pd.stderr)}
+               "phases_ms_sketch": cli_phases(ps.stderr), "phases_ms_dist": cli_phases(pd.stderr),
+               "warm_thread_ms_sketch": cli_phases(ps.stderr, "[fpmash-warm] ")}
         ph_s, ph_d = res["phases_ms_sketch"], res["phases_ms_dist"]
         if cpu:
             # the same command on the CPU (CPU wall / GPU wall of the same work):

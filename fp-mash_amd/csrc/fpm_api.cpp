@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <cstdio>
 #include <atomic>
 #include <cstring>
@@ -114,7 +115,6 @@ struct fpm_ctx {
     static constexpr size_t kRingBytes = 8u << 20;
     void *ring[kRing] = {};
     hipEvent_t ring_ev[kRing] = {};
-    hipStream_t copy = nullptr;
     // device buffers of released -fp text jobs, reused by the next jobs: a fresh hipMalloc of
     // tens of MB is cleared by the driver before first use, and a kernel writing it could wait
     // ~27 ms for that (tools/micro/fp_text_time.py under rocprofv3: fp_line_kernel 0.06 ms,
@@ -164,15 +164,35 @@ static void pool_free(fpm_ctx *ctx, void *p, size_t bytes)
     (void)hipFree(p);
 }
 
+// Synchronous copies and memsets run on the context stream, after the work queued there, and
+// never on the null stream: the null stream's first use in a process creates one more
+// hardware queue (~9 ms in the CLI's trace), and a separate copy stream cost another ~8 ms of
+// start-up for no overlap the synchronous copies could use.
 static hipError_t ensure_ring(fpm_ctx *ctx)
 {
     hipError_t e = hipSuccess;
-    if (ctx->copy) return e;
+    if (ctx->ring_ev[fpm_ctx::kRing - 1]) return e;
     for (int i = 0; e == hipSuccess && i < fpm_ctx::kRing; i++) {
-        e = hipHostMalloc(&ctx->ring[i], fpm_ctx::kRingBytes, hipHostMallocDefault);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ring_ev[i], hipEventDisableTiming);
+        if (!ctx->ring[i]) e = hipHostMalloc(&ctx->ring[i], fpm_ctx::kRingBytes, hipHostMallocDefault);
+        if (e == hipSuccess && !ctx->ring_ev[i])
+            e = hipEventCreateWithFlags(&ctx->ring_ev[i], hipEventDisableTiming);
     }
-    if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->copy, hipStreamNonBlocking);
+    return e;
+}
+
+// synchronous copy on the context stream (ordered after the work queued there)
+static hipError_t copy_sync(fpm_ctx *ctx, void *dst, const void *src, size_t bytes,
+                            hipMemcpyKind kind)
+{
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    return e;
+}
+
+static hipError_t memset_sync(fpm_ctx *ctx, void *dst, int v, size_t bytes)
+{
+    hipError_t e = hipMemsetAsync(dst, v, bytes, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     return e;
 }
 
@@ -183,7 +203,7 @@ static hipError_t ensure_ring(fpm_ctx *ctx)
 static hipError_t h2d_staged(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!bytes) return hipSuccess;
-    if (bytes < (1u << 20)) return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    if (bytes < (1u << 20)) return copy_sync(ctx, dst, src, bytes, hipMemcpyHostToDevice);
     hipError_t e = ensure_ring(ctx);
     if (e != hipSuccess) return e;
     const char *s = static_cast<const char *>(src);
@@ -194,13 +214,13 @@ static hipError_t h2d_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
         const size_t n = std::min(fpm_ctx::kRingBytes, bytes - off);
         if (used[slot] && (e = hipEventSynchronize(ctx->ring_ev[slot])) != hipSuccess) return e;
         memcpy(ctx->ring[slot], s + off, n);
-        if ((e = hipMemcpyAsync(d + off, ctx->ring[slot], n, hipMemcpyHostToDevice, ctx->copy)) !=
+        if ((e = hipMemcpyAsync(d + off, ctx->ring[slot], n, hipMemcpyHostToDevice, ctx->stream)) !=
             hipSuccess)
             return e;
-        if ((e = hipEventRecord(ctx->ring_ev[slot], ctx->copy)) != hipSuccess) return e;
+        if ((e = hipEventRecord(ctx->ring_ev[slot], ctx->stream)) != hipSuccess) return e;
         used[slot] = true;
     }
-    return hipStreamSynchronize(ctx->copy);
+    return hipStreamSynchronize(ctx->stream);
 }
 
 static hipError_t ensure_ring(fpm_ctx *ctx);
@@ -210,7 +230,7 @@ static hipError_t ensure_ring(fpm_ctx *ctx);
 static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!bytes) return hipSuccess;
-    if (bytes < (64u << 10)) return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+    if (bytes < (64u << 10)) return copy_sync(ctx, dst, src, bytes, hipMemcpyDeviceToHost);
     hipError_t e = ensure_ring(ctx);
     if (e != hipSuccess) return e;
     const char *s = static_cast<const char *>(src);
@@ -220,8 +240,8 @@ static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
     auto issue = [&](size_t i) -> hipError_t {
         const int slot = (int)(i % fpm_ctx::kRing);
         const size_t off = i * R, n = std::min(R, bytes - off);
-        hipError_t x = hipMemcpyAsync(ctx->ring[slot], s + off, n, hipMemcpyDeviceToHost, ctx->copy);
-        if (x == hipSuccess) x = hipEventRecord(ctx->ring_ev[slot], ctx->copy);
+        hipError_t x = hipMemcpyAsync(ctx->ring[slot], s + off, n, hipMemcpyDeviceToHost, ctx->stream);
+        if (x == hipSuccess) x = hipEventRecord(ctx->ring_ev[slot], ctx->stream);
         return x;
     };
     for (size_t i = 0; i < std::min<size_t>(n_pieces, fpm_ctx::kRing); i++)
@@ -263,7 +283,7 @@ static hipError_t copy_out(fpm_ctx *ctx, void *dst, const void *src, size_t byte
 {
     if (!bytes) return hipSuccess;
     if (g_pageable_direct || bytes < (64u << 10) || host_pinned(dst))
-        return hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost);
+        return copy_sync(ctx, dst, src, bytes, hipMemcpyDeviceToHost);
     return d2h_staged(ctx, dst, src, bytes);
 }
 
@@ -271,7 +291,7 @@ static hipError_t copy_out(fpm_ctx *ctx, void *dst, const void *src, size_t byte
 static hipError_t copy_in(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!bytes) return hipSuccess;
-    if (g_pageable_direct || host_pinned(src)) return hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice);
+    if (g_pageable_direct || host_pinned(src)) return copy_sync(ctx, dst, src, bytes, hipMemcpyHostToDevice);
     return h2d_staged(ctx, dst, src, bytes);
 }
 
@@ -359,8 +379,7 @@ static hipError_t scratch(fpm_ctx *ctx, int id, size_t bytes, void **out)
         // small buffers (the counters) start zeroed: some words are kept at zero between
         // calls by the kernels themselves (idx_kmax_kernel's accumulator)
         if (b <= 4096) {
-            if ((e = hipMemset(s.p, 0, b)) != hipSuccess) return e;
-            if ((e = hipDeviceSynchronize()) != hipSuccess) return e;
+            if ((e = memset_sync(ctx, s.p, 0, b)) != hipSuccess) return e;
         }
     }
     *out = s.p;
@@ -466,9 +485,26 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
     }
-    if (ctx->copy) (void)hipStreamDestroy(ctx->copy);
     for (auto &b : ctx->pool) (void)hipFree(b.first);
     delete ctx;
+}
+
+int fpm_ctx_warm(fpm_ctx *ctx)
+{
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(ensure_ring(ctx));
+    // one 1 MB copy each way between the ring and the device: the first DMA of a process
+    // sets up its copy path (~8-11 ms inside the first staged upload in the CLI's trace)
+    constexpr size_t kWarm = 1u << 20;
+    void *d = nullptr;
+    HIP_TRY(hipMalloc(&d, kWarm));
+    hipError_t e = hipMemcpyAsync(d, ctx->ring[0], kWarm, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(ctx->ring[1], d, kWarm, hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    const hipError_t f = hipFree(d);
+    HIP_TRY(e);
+    HIP_TRY(f);
+    return FPM_OK;
 }
 
 void *fpm_ctx_stream(fpm_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
@@ -1042,7 +1078,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     alloc((void **)&job->d_count, (size_t)n_core * sizeof(uint32_t));
     // groups without any k-mer keep count 0: zeroed once here (every run rewrites the count
     // of each group that has tiles: the tile kernel or the last merge of its group)
-    if (e == hipSuccess) e = hipMemset(job->d_count, 0, (size_t)n_core * sizeof(uint32_t));
+    if (e == hipSuccess) e = memset_sync(ctx, job->d_count, 0, (size_t)n_core * sizeof(uint32_t));
     alloc((void **)&job->d_merge, mplan.size() * sizeof(MergeDesc));
     alloc((void **)&job->d_stiles, sby_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_smerge, splan.size() * sizeof(MergeDesc));
@@ -1922,6 +1958,7 @@ struct fpm_refset {
     bool ref_unsorted = false;    // some reference row is unsorted / carries duplicates
     bool deduped = false;         // the index holds launch_dedup_rows copies (slots 10, 11)
     uint64_t mr = 0;              // their row stride
+    uint64_t self_events = 0;     // sum_b |b|^2: the posting events of the set against itself
     // per-query-block host buffers (fpm_refset_dist): pinned staging + device copies
     void *h_stage = nullptr;
     size_t h_stage_bytes = 0;
@@ -1961,13 +1998,16 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
         void *dir, *entries;
         HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
         HIP_TRY(slot_buf(rs->slot[5], En * 4, &entries));
+        // the bucket pass also sums the self events (a query block that is the set itself
+        // then needs no probe count)
         return build_index(ctx, rows, len, stride, rs->n_ref, rs->hash_bytes, g, (uint32_t *)dir,
-                           (uint32_t *)entries, (unsigned long long *)ctr, false, st,
+                           (uint32_t *)entries, (unsigned long long *)ctr, true, st,
                            [] { return FPM_OK; });
     };
     geom.kmax = rs->kmax;
     if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom)) return rc;
     rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
+    rs->self_events = ctx->host_counters[0];
     rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
     rs->deduped = rs->ref_unsorted && rs->mr <= kDedupMax;
     if (rs->deduped) {
@@ -2085,7 +2125,16 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const uint32_t *dir = nullptr, *entries = nullptr;
         uint64_t ev = 0;
         bool all_sorted = true;
-        if (rs) {
+        if (rs && self_set && !rs->deduped) {
+            // the resident set against itself: its posting events and sortedness are the
+            // index build's (sum_b |b|^2, the reference flag), no probe count
+            geom = rs->geom;
+            dir = (const uint32_t *)rs->slot[4].p;
+            entries = (const uint32_t *)rs->slot[5].p;
+            ev = rs->self_events;
+            all_sorted = !rs->ref_unsorted;
+            HIP_TRY(hipMemsetAsync(ctr, 0, 67 * 8, st));   // the candidate counter among them
+        } else if (rs) {
             // resident index: count this block's posting events (and its sortedness)
             geom = rs->geom;
             dir = (const uint32_t *)rs->slot[4].p;

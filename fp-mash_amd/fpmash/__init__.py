@@ -51,6 +51,7 @@ SYMBOLS = [
     ("fpm_ctx_destroy", None, [vp]),
     ("fpm_ctx_stream", vp, [vp]),
     ("fpm_ctx_synchronize", C.c_int, [vp]),
+    ("fpm_ctx_warm", C.c_int, [vp]),
     ("fpm_malloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
     ("fpm_free", C.c_int, [vp, vp]),
     ("fpm_memcpy_h2d", C.c_int, [vp, vp, vp, C.c_size_t]),

@@ -1,5 +1,7 @@
 #include "Device.h"
+#include "Timing.h"
 
+#include <chrono>
 #include <cstdlib>
 #include <iostream>
 #include <memory>
@@ -20,9 +22,20 @@ std::mutex g_mu;
 std::thread g_warm;
 std::once_flag g_warm_join;
 
+double g_warm_ms[3] = {-1, -1, -1};
+
+// FPMASH_TIMING=1: the warm-up thread's own steps, on lines of their own ("[fpmash-warm]":
+// not main-thread phases; the main thread's wait for them is its "device context" phase)
 void join_warm()
 {
-    if (g_warm.joinable()) g_warm.join();
+    if (!g_warm.joinable()) return;
+    g_warm.join();
+    if (timingOn() && g_warm_ms[0] >= 0)
+        fprintf(stderr,
+                "[fpmash-warm] runtime start + device enumeration: %.3f ms\n"
+                "[fpmash-warm] context (stream): %.3f ms\n"
+                "[fpmash-warm] staging ring + first copy: %.3f ms\n",
+                g_warm_ms[0], g_warm_ms[1], g_warm_ms[2]);
 }
 
 void release()
@@ -111,10 +124,24 @@ void warmDevices()
     // so a single-file sketch on an 8-GPU node does not bring up 8 contexts.  A context that
     // fails to come up is reported by the first device() call.
     g_warm = std::thread([] {
+        using clk = std::chrono::steady_clock;
+        const auto t0 = clk::now();
         std::call_once(g_once, init_ids);
+        const auto t1 = clk::now();
         std::call_once(g_ctx_once[0], [] {
             if (fpm_ctx_create(g_ids[0], &g_ctx[0]) != FPM_OK) g_ctx[0] = nullptr;
         });
+        const auto t2 = clk::now();
+        // the staging ring and the first DMA, before the first upload needs them
+        static const bool noWarm = getenv("FPM_NO_WARM") != nullptr;   // A/B
+        if (g_ctx[0] && !noWarm) (void)fpm_ctx_warm(g_ctx[0]);
+        const auto t3 = clk::now();
+        auto ms = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        g_warm_ms[0] = ms(t0, t1);
+        g_warm_ms[1] = ms(t1, t2);
+        g_warm_ms[2] = ms(t2, t3);
     });
 }
 

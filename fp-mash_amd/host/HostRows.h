@@ -16,15 +16,20 @@ template <typename T>
 struct HostRows {
     T *p = nullptr;
     size_t bytes = 0;
-    explicit HostRows(size_t n) : bytes(std::max<size_t>(n * sizeof(T), 1))
+    // populate = false: the caller runs populate() later (e.g. on a thread beside device work)
+    explicit HostRows(size_t n, bool populateNow = true) : bytes(std::max<size_t>(n * sizeof(T), 1))
     {
         void *q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
         if (q == MAP_FAILED) throw std::bad_alloc();
         (void)madvise(q, bytes, MADV_HUGEPAGE);
-#ifdef MADV_POPULATE_WRITE
-        (void)madvise(q, bytes, MADV_POPULATE_WRITE);   // best effort (Linux >= 5.14)
-#endif
         p = static_cast<T *>(q);
+        if (populateNow) populate();
+    }
+    void populate()
+    {
+#ifdef MADV_POPULATE_WRITE
+        (void)madvise(p, bytes, MADV_POPULATE_WRITE);   // best effort (Linux >= 5.14)
+#endif
     }
     ~HostRows() { munmap(p, bytes); }
     HostRows(const HostRows &) = delete;

@@ -13,10 +13,12 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <unistd.h>
 
 namespace fpmhost {
@@ -109,9 +111,13 @@ public:
         return out;
     }
 
-    // the same bytes as serialize() into a file: sized first, then written by up to 8
-    // threads with pwrite over disjoint byte ranges (80 MB of a C2 .msh: page allocation of
-    // the output file dominated a single-threaded write)
+    // the same bytes as serialize() into a file.  Large messages: space reserved with
+    // fallocate, the file mapped, and the blocks copied in by up to 16 threads over disjoint
+    // byte ranges (page faults of a shared mapping run in parallel; pwrite calls on one file
+    // serialise on its inode lock: 80 MB of a C2 .msh took ~40 ms that way on /dev/shm).
+    // Small messages, file systems without fallocate, and FPMASH_MSH_WRITE=pwrite (A/B) take
+    // the pwrite path; a failed reservation never leaves a mapping that could fault past the
+    // end of the device.
     bool write(const std::string &path) const
     {
         const std::vector<uint32_t> table = segmentTable();
@@ -119,32 +125,70 @@ public:
         std::vector<uint64_t> at(B.size() + 1, 0);
         for (size_t i = 0; i < B.size(); i++) at[i + 1] = at[i] + B[i].second;
         const uint64_t total = at.back();
-        const int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0666);
+        const int fd = open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0666);
         if (fd < 0) return false;
-        bool ok = ftruncate(fd, (off_t)total) == 0;
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        const unsigned nt = total < (8u << 20) ? 1u : std::min(8u, hw);
-        std::atomic<bool> good{ok};
-        auto part = [&](unsigned t) {
-            const uint64_t a = total * t / nt, e = total * (t + 1) / nt;
+        const unsigned nt = total < (8u << 20) ? 1u : std::min(16u, hw);
+        static const bool usePwrite = [] {
+            const char *v = getenv("FPMASH_MSH_WRITE");
+            return v && strcmp(v, "pwrite") == 0;
+        }();
+        // blocks overlapping [a, e): fn(block index, first byte, end byte)
+        auto forRange = [&](uint64_t a, uint64_t e, auto fn) {
             size_t i = std::upper_bound(at.begin(), at.end(), a) - at.begin() - 1;
             for (uint64_t pos = a; pos < e && i < B.size(); i++) {
                 const uint64_t b0 = std::max(pos, at[i]), b1 = std::min(e, at[i + 1]);
-                for (uint64_t q = b0; q < b1;) {
-                    const ssize_t w = pwrite(fd, B[i].first + (q - at[i]), (size_t)(b1 - q), (off_t)q);
-                    if (w <= 0) { good = false; return; }
-                    q += (uint64_t)w;
-                }
+                if (b1 > b0 && !fn(i, b0, b1)) return false;
                 pos = b1;
             }
+            return true;
         };
-        if (ok) {
+        auto parallel = [&](auto part) {
+            std::atomic<bool> good{true};
             std::vector<std::thread> th;
-            for (unsigned t = 1; t < nt; t++) th.emplace_back(part, t);
-            part(0);
+            for (unsigned t = 1; t < nt; t++)
+                th.emplace_back([&, t] { if (!part(t)) good = false; });
+            if (!part(0)) good = false;
             for (auto &x : th) x.join();
+            return good.load();
+        };
+        bool ok = false, done = false;
+        if (nt > 1 && !usePwrite && fallocate(fd, 0, 0, (off_t)total) == 0) {
+            void *m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            if (m != MAP_FAILED) {
+                char *dst = static_cast<char *>(m);
+                ok = parallel([&](unsigned t) {
+                    // 2 MB-aligned ranges: no page is faulted in by two threads
+                    const uint64_t a = (total * t / nt) & ~((uint64_t(2) << 20) - 1);
+                    const uint64_t e = t + 1 == nt ? total : (total * (t + 1) / nt) & ~((uint64_t(2) << 20) - 1);
+#ifdef MADV_POPULATE_WRITE
+                    // the range's pages allocated in one call (not one fault per 4 KB page)
+                    if (e > a) (void)madvise(dst + a, (size_t)(e - a), MADV_POPULATE_WRITE);
+#endif
+                    return forRange(a, e, [&](size_t i, uint64_t b0, uint64_t b1) {
+                        memcpy(dst + b0, B[i].first + (b0 - at[i]), (size_t)(b1 - b0));
+                        return true;
+                    });
+                });
+                if (munmap(m, total) != 0) ok = false;
+                done = true;
+            }
         }
-        ok = good.load();
+        if (!done) {
+            ok = ftruncate(fd, (off_t)total) == 0 &&
+                 parallel([&](unsigned t) {
+                     return forRange(total * t / nt, total * (t + 1) / nt,
+                                     [&](size_t i, uint64_t b0, uint64_t b1) {
+                         for (uint64_t q = b0; q < b1;) {
+                             const ssize_t w = pwrite(fd, B[i].first + (q - at[i]),
+                                                      (size_t)(b1 - q), (off_t)q);
+                             if (w <= 0) return false;
+                             q += (uint64_t)w;
+                         }
+                         return true;
+                     });
+                 });
+        }
         if (close(fd) != 0) ok = false;
         return ok;
     }

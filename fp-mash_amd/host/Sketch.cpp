@@ -14,6 +14,8 @@
 #include <iostream>
 #include <sstream>
 #include <atomic>
+#include <memory>
+#include <mutex>
 #include <thread>
 #include <algorithm>
 #include <sys/stat.h>
@@ -215,10 +217,13 @@ int hostRecords(const std::string &image, std::vector<SeqRec> &out, std::string 
 
 // Parse and sketch the sequence files [f0, f1) on one device (the reference's per-file work,
 // Sketch.cpp:249-397 / 478-522 / 1299-1488): fills fileRefs[f] for those files.
+// With `stores`, the references point into the fetched host arrays (Reference::hashView),
+// which are appended to *stores (under *storeMu) to keep them alive.
 static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
                         const std::vector<std::string> &seqFiles, std::vector<std::string> &images,
                         size_t f0, size_t f1, std::vector<std::vector<Reference>> &fileRefs,
-                        bool timing)
+                        bool timing, std::vector<std::shared_ptr<void>> *stores = nullptr,
+                        std::mutex *storeMu = nullptr)
 {
     const size_t nF = f1 - f0;
     auto mark = [&](const char *what) { if (timing) phaseMark(what); };
@@ -336,7 +341,11 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
         fp.preserve_case = parameters.preserveCase;
         for (int c = 0; c < 256; c++) fp.alphabet[c] = parameters.alphabet[c] ? 1 : 0;
         const uint64_t s = fp.sketch_size;
-        HostRows<uint64_t> out((size_t)nGroups * s);
+        // the output rows' pages (80 MB for C2: ~4 ms of page allocation and zeroing) are
+        // populated on a thread beside the staging and the sketch kernels
+        auto outp = std::make_shared<HostRows<uint64_t>>((size_t)nGroups * s, false);
+        HostRows<uint64_t> &out = *outp;
+        std::thread populate([&out] { out.populate(); });
         std::vector<uint32_t> cnt(nGroups);
         fpm_sketch_job *job = nullptr;
         if (parsed) {
@@ -357,9 +366,11 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
                   "sketch");
         }
         int rc = fpm_sketch_run(job, nullptr);
+        populate.join();
         if (rc == FPM_OK) rc = fpm_sketch_fetch(job, out.data(), cnt.data());
         // -M: the heap's multiplicities (Sketch.cpp:584-596)
-        std::vector<uint32_t> mult;
+        auto multp = std::make_shared<std::vector<uint32_t>>();
+        std::vector<uint32_t> &mult = *multp;
         if (rc == FPM_OK && parameters.counts) {
             mult.resize((size_t)nGroups * s);
             rc = fpm_sketch_mult(job, nullptr, mult.data());
@@ -367,6 +378,26 @@ static void sketchFiles(fpm_ctx *ctx, const Parameters &parameters,
         fpm_sketch_job_free(job);
         check(rc, "sketch");
         mark("device sketch (stage + run + fetch)");
+        if (stores) {
+            // views into the fetched arrays (kept alive by the Sketch)
+            for (size_t f = 0; f < nF; f++)
+                for (size_t i = 0; i < fileRefs[f0 + f].size(); i++) {
+                    const uint32_t g = fileGroups[f][i];
+                    Reference &ref = fileRefs[f0 + f][i];
+                    ref.hashView = out.data() + (size_t)g * s;
+                    ref.viewCount = cnt[g];
+                    if (!mult.empty()) {
+                        ref.countView = mult.data() + (size_t)g * s;
+                        ref.countsSorted = true;
+                    }
+                }
+            std::lock_guard<std::mutex> lk(*storeMu);
+            stores->push_back(outp);
+            if (!mult.empty()) stores->push_back(multp);
+            mark("reference lists");
+            if (parsed) fpm_seq_free(parsed);
+            return;
+        }
         // hash lists into the references (threads: the copies are page-fault bound)
         std::vector<std::pair<size_t, size_t>> all;
         for (size_t f = 0; f < nF; f++)
@@ -503,12 +534,14 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
         // files over the devices as contiguous ranges balanced by bytes (the reference's -p
         // threads take files in turn, Sketch.cpp:253); one device: every file on device(0)
         std::vector<std::vector<Reference>> fileRefs(seqFiles.size());
+        std::mutex storeMu;
         const int nDev = deviceCount();
         const size_t nParts = std::min<size_t>((size_t)std::max(1, nDev), seqFiles.size());
         if (nParts <= 1) {
             fpm_ctx *ctx = device();
             phaseMark("device context");
-            sketchFiles(ctx, parameters, seqFiles, images, 0, seqFiles.size(), fileRefs, true);
+            sketchFiles(ctx, parameters, seqFiles, images, 0, seqFiles.size(), fileRefs, true,
+                        rowViews ? &rowStores : nullptr, &storeMu);
         } else {
             uint64_t tot = 0;
             for (auto &im : images) tot += im.size() + 1;
@@ -524,7 +557,7 @@ int Sketch::initFromFiles(const std::vector<std::string> &files, const Parameter
             for (size_t d = 0; d + 1 < cut.size(); d++)
                 th.emplace_back([&, d] {
                     sketchFiles(device((int)d), parameters, seqFiles, images, cut[d], cut[d + 1],
-                                fileRefs, false);
+                                fileRefs, false, rowViews ? &rowStores : nullptr, &storeMu);
                 });
             for (auto &t : th) t.join();
             phaseMark("device sketch over all devices");
@@ -618,8 +651,8 @@ int Sketch::writeToMsh(const std::string &file) const
     std::vector<MshRefView> refs(references.size());
     for (size_t i = 0; i < references.size(); i++) {
         const Reference &r = references[i];
-        refs[i] = MshRefView{&r.name, &r.comment, r.length, r.hashes.data(), r.hashes.size(),
-                             r.counts.data(), r.counts.size()};
+        refs[i] = MshRefView{&r.name, &r.comment, r.length, r.hashData(), r.hashCount(),
+                             r.countData(), r.countCount()};
     }
     if (!mshWrite(file, h, refs.data(), refs.size(), parameters.use64, parameters.counts)) {
         std::cerr << "ERROR: could not open " << file << " for writing.\n";

@@ -6,6 +6,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -42,6 +43,15 @@ struct Reference {
     std::vector<uint64_t> hashes;   // hashesSorted (u32 values zero-extended when !use64)
     std::vector<uint32_t> counts;   // -M multiplicities (counts32)
     bool countsSorted = false;
+    // rows fetched from the device and read in place (Sketch::keepDeviceRows): the sketch
+    // command writes them into the .msh without first copying 8 B per hash into `hashes`
+    const uint64_t *hashView = nullptr;
+    const uint32_t *countView = nullptr;
+    uint32_t viewCount = 0;
+    size_t hashCount() const { return hashView ? viewCount : hashes.size(); }
+    const uint64_t *hashData() const { return hashView ? hashView : hashes.data(); }
+    size_t countCount() const { return countView ? viewCount : counts.size(); }
+    const uint32_t *countData() const { return countView ? countView : counts.data(); }
 };
 
 class Sketch {
@@ -73,7 +83,10 @@ public:
     uint64_t getReferenceCount() const { return references.size(); }
     double getRandomKmerChance(uint64_t i) const;
     int getMinKmerSize(uint64_t i) const;
-    bool hasHashCounts() const { return !references.empty() && !references[0].counts.empty(); }
+    bool hasHashCounts() const { return !references.empty() && references[0].countCount() != 0; }
+    // sequence inputs keep their sketch rows in the fetched host arrays (Reference::hashView)
+    // instead of per-reference vectors: for a caller that only writes the .msh
+    void keepDeviceRows() { rowViews = true; }
     void setReferenceName(int i, const std::string &n) { references[i].name = n; }
     void setReferenceComment(int i, const std::string &c) { references[i].comment = c; }
 
@@ -83,6 +96,8 @@ public:
 
 private:
     void createIndex();
+    bool rowViews = false;
+    std::vector<std::shared_ptr<void>> rowStores;   // the host arrays the views point into
 };
 
 void setAlphabetFromString(Parameters &p, const char *characters);

@@ -64,6 +64,10 @@ int fpm_ctx_create(int device, fpm_ctx **out);
 void fpm_ctx_destroy(fpm_ctx *ctx);
 void *fpm_ctx_stream(fpm_ctx *ctx);          /* the context's hipStream_t */
 int fpm_ctx_synchronize(fpm_ctx *ctx);
+/* first-use costs of a process up front: the pinned staging ring and one small DMA each way
+ * (~15-25 ms in a fresh process, paid by the first staged upload otherwise).  Optional; for a caller that can run it beside other start-up work (the CLI's
+ * device warm-up thread). */
+int fpm_ctx_warm(fpm_ctx *ctx);
 
 /* device memory helpers (for bindings that own no allocator) */
 int fpm_malloc(fpm_ctx *ctx, void **dptr, size_t bytes);
