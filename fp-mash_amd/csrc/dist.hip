@@ -345,6 +345,10 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? FPM_RANK_LOGB : FPM_RANK_LOGB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
+    // fixed-size LDS arrays: their compile-time offsets fold into the ds_read instructions.
+    // (Sizing them by the launch instead — 20.3 KB at s = 1000, 8 workgroups per CU — put a
+    // runtime base add on every probe read: the kernel ran 0.645 -> 0.70 ms beside the fill
+    // at 6, 7 or 8 workgroups per CU alike, same-box A/B r03o.)
     __shared__ uint64_t Bs[CAP + kRankProbeMax];
     __shared__ uint32_t K32[CAP + kRankProbeMax];      // 32-bit keys of B (rank_chunk)
     __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
@@ -699,10 +703,56 @@ __device__ double beta_cf(double a, double b, double x, double epsabs)
     return cf;
 }
 
+// Regularized incomplete gamma for the asymptotic branches below (shape < 10: the series
+// under a + 1, Legendre's continued fraction above), as the oracle restates
+// gsl_sf_gamma_inc_P / _Q there (only union sizes above 1e5 reach it; inlined: an out-of-line
+// call gave the finalize kernels a 16 B/lane stack frame, i.e. scratch)
+__device__ double lngamma_pos(double x)
+{
+    return lngammastar(x) + (x - 0.5) * log(x) - x + 0.91893853320467274178;
+}
+
+__device__ __forceinline__ double gamma_inc_PQ(double a, double x, bool upper)
+{
+    if (x <= 0.0) return upper ? 1.0 : 0.0;
+    if (x < a + 1.0) {
+        double sum = 1.0, term = 1.0;
+        for (int n = 1; n < 100000; n++) {
+            term *= x / (a + n);
+            sum += term;
+            if (term < sum * DBL_EPSILON) break;
+        }
+        const double P = exp(a * log(x) - x - lngamma_pos(a + 1.0)) * sum;
+        return upper ? 1.0 - P : P;
+    }
+    const double tiny = 1e-300;
+    double b = x + 1.0 - a, c = 1.0 / tiny, d = 1.0 / b, h = d;
+    for (int i = 1; i < 100000; i++) {
+        const double an = -(double)i * ((double)i - a);
+        b += 2.0;
+        d = an * d + b;
+        if (fabs(d) < tiny) d = tiny;
+        c = b + an / c;
+        if (fabs(c) < tiny) c = tiny;
+        d = 1.0 / d;
+        const double del = d * c;
+        h *= del;
+        if (fabs(del - 1.0) < DBL_EPSILON) break;
+    }
+    const double Q = exp(a * log(x) - x - lngamma_pos(a)) * h;
+    return upper ? Q : 1.0 - Q;
+}
+
+// gsl_cdf_beta_P = beta_inc_AXPY(1, 0, ...): the asymptotic regimes of A&S 26.5.17 (union
+// sizes above 1e5), then the general continued fraction
 __device__ double beta_P(double x, double a, double b)
 {
     if (x == 0.0) return 0.0;
     if (x == 1.0) return 1.0;
+    if (a > 1e5 && b < 10 && x > a / (a + b))
+        return gamma_inc_PQ(b, -(a + (b - 1.0) / 2.0) * log(x), true);
+    if (b > 1e5 && a < 10 && x < b / (a + b))
+        return gamma_inc_PQ(a, -(b + (a - 1.0) / 2.0) * log1p(-x), false);
     double pre = exp(-lnbeta(a, b) + a * log(x) + b * log1p(-x));
     if (x < (a + 1.0) / (a + b + 2.0)) return pre * beta_cf(a, b, x, 0.0) / a;
     double epsabs = DBL_EPSILON / fabs(pre / b);

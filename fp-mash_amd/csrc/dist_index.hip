@@ -616,8 +616,17 @@ __global__ void sum64_kernel(unsigned long long *events)
 // a wave scan flattens the 64 buckets into one event range, and the lanes then read
 // consecutive entries of that range (coalesced).  The owner hash of each event comes from
 // a per-wave byte map filled by the lanes for 1024-event windows (one LDS read per event).
+// 8 waves per SIMD (FPM_PROBE_WPE=0 drops the attribute, A/B): the kernel waits on its
+// event loads most of the time, and at 105 SGPRs the compiler's own allocation left 7
+#ifndef FPM_PROBE_WPE
+#define FPM_PROBE_WPE 8
+#endif
 template <typename C>
-__global__ __launch_bounds__(256) void probe_rows_kernel(
+__global__ __launch_bounds__(256)
+#if FPM_PROBE_WPE
+__attribute__((amdgpu_waves_per_eu(FPM_PROBE_WPE)))
+#endif
+void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,

@@ -114,7 +114,52 @@ def pvalue_table():
     return rows
 
 
+def pvalue_asymp_table():
+    """GSL's asymptotic regimes of gsl_cdf_beta_P (cdf/beta_inc.c, A&S 26.5.17), reached by
+    pValue only when the union size n passed as its sketch size exceeds 1e5 (a = x,
+    b = n - x + 1; the regime tests are made in double arithmetic, as GSL makes them):
+      b > 1e5, a < 10, r < b/(a+b):  P(a, -N log1p(-r)),  N = b + (a-1)/2
+      a > 1e5, b < 10, r > a/(a+b):  Q(b, -N log r),      N = a + (b-1)/2
+    and the general regime (the incomplete beta) for the neighbours that miss them.  "q" is
+    the branch's formula at 50 digits (what the restatement must reproduce), "exact" the
+    regularized incomplete beta itself (how far GSL's approximation sits from it)."""
+    import mpmath as mp
+    mp.mp.dps = 50
+    rows = []
+
+    def row(x, n, r):
+        a, b = float(x), float(n - x + 1)
+        A, B = mp.mpf(x), mp.mpf(n - x + 1)
+        ex = mp.betainc(A, B, 0, r, regularized=True)
+        if b > 1e5 and a < 10 and r < b / (a + b):
+            branch = "small_a"
+            q = mp.gammainc(A, 0, -(B + (A - 1) / 2) * mp.log1p(-mp.mpf(r)), regularized=True)
+        elif a > 1e5 and b < 10 and r > a / (a + b):
+            branch = "large_a"
+            q = mp.gammainc(B, -(A + (B - 1) / 2) * mp.log(mp.mpf(r)), mp.inf, regularized=True)
+        else:
+            branch, q = "general", ex
+        rows.append({"x": x, "n": n, "r": r, "branch": branch, "q": mp.nstr(q, 30),
+                     "exact": mp.nstr(ex, 30)})
+
+    for n in (100001, 100009, 150000, 400000, 1000000, 4000000):
+        for x in range(1, 11):
+            for r in (1e-12, 3.7e-10, 2.2e-6, 1e-5, 1e-4):
+                row(x, n, r)
+    for n in (100001, 200000, 1000000):
+        for j in range(0, 10):
+            for r in (1.0 - 1e-7, 1.0 - 1e-6, 1.0 - 2e-6):
+                row(n - j, n, r)
+    return rows
+
+
 def main():
+    if "--pvalue-asymp" in sys.argv:
+        rows = pvalue_asymp_table()
+        with open(os.path.join(HERE, "pvalue_asymp.json"), "w") as f:
+            json.dump(rows, f, indent=0)
+        print({"pvalue_asymp": len(rows)})
+        return
     gold = {
         "murmur": murmur_kats(),
         "fp": fp_kats(),

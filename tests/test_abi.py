@@ -43,14 +43,18 @@ def test_no_device_fails_loudly():
 def test_library_is_gfx950_code_object():
     import subprocess
     import fpmash
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading",
-                          fpmash.LIB_PATH], capture_output=True, text=True, cwd="/tmp")
+    import shutil
+    import tempfile
+    # --offloading extracts the code objects next to its input: run it on a copy in a
+    # scratch directory (not beside the in-tree library, which travels to the GPU box)
+    with tempfile.TemporaryDirectory() as d:
+        lib = os.path.join(d, "libfpmash.so")
+        shutil.copy(fpmash.LIB_PATH, lib)
+        out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib],
+                             capture_output=True, text=True, cwd=d)
     if out.returncode != 0:
         pytest.skip("llvm-objdump unavailable")
     assert "gfx950" in out.stdout + out.stderr
-    for f in os.listdir("/tmp"):
-        if f.startswith("libfpmash.so.") and ("gfx" in f or "host" in f):
-            os.unlink(os.path.join("/tmp", f))
 
 
 def test_params_match_oracle(oracle):

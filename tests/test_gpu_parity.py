@@ -719,3 +719,42 @@ print("exact-ok")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                        timeout=110)
     assert r.returncode == 0 and "exact-ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_pvalue_asymptotic_branches_on_device(ctx, oracle):
+    """Union sizes above 1e5 (pValue's sketch-size argument is the denominator): the device
+    finalize takes GSL's asymptotic regimes of the incomplete beta like the oracle (pinned to
+    mpmath by test_pvalue_asymptotic_branches_vs_mpmath), u32 counts through
+    fpm_dist_finalize_dev, every cell rtol 1e-12."""
+    import ctypes as C
+    import fpmash
+    L = fpmash.lib()
+    rng = np.random.default_rng(11)
+    cells = []
+    for n in (100001, 100005, 250000, 1000000, 4000000):
+        for x in range(0, 12):                  # small a (and its general neighbours)
+            cells.append((x, n))
+        for j in range(0, 12):                  # large a, small b
+            cells.append((n - j, n))
+    n_qry = len(cells)
+    ref_len = np.array([5e3, 3e5, 5e6, 4.6e9, 1.2e11], dtype=np.uint64)
+    qry_len = rng.choice(ref_len, size=n_qry).astype(np.uint64)
+    n_ref = len(ref_len)
+    numer = np.zeros((n_qry, n_ref), np.uint32)
+    denom = np.zeros((n_qry, n_ref), np.uint32)
+    for q, (x, n) in enumerate(cells):
+        numer[q, :] = x
+        denom[q, :] = n
+    for k, space in ((21, 4.0 ** 21), (3, 4.0 ** 3), (9, 4.0 ** 9)):
+        bufs = [fpmash.DeviceBuffer.from_array(ctx, a) for a in (numer, denom, ref_len, qry_len)]
+        outs = [fpmash.DeviceBuffer(ctx, n_qry * n_ref * b) for b in (8, 8, 1)]
+        fpmash._check(L.fpm_dist_finalize_dev(ctx.h, *[b.ptr for b in bufs], n_ref, n_qry, k,
+                                              space, 1.0, 1.0, *[o.ptr for o in outs], None))
+        ctx.synchronize()
+        pv = outs[1].to_array(np.float64, n_qry * n_ref).reshape(n_qry, n_ref)
+        exp = np.array([[oracle.pvalue(int(numer[q, r]), int(ref_len[r]), int(qry_len[q]), space,
+                                       int(denom[q, r])) for r in range(n_ref)]
+                        for q in range(n_qry)])
+        np.testing.assert_allclose(pv, exp, rtol=RTOL, atol=0)
+        for b in bufs + outs:
+            b.free()

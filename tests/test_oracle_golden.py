@@ -59,6 +59,24 @@ def test_pvalue_vs_mpmath(oracle):
         assert got == pytest.approx(q, rel=1e-12, abs=0), row
 
 
+def test_pvalue_asymptotic_branches_vs_mpmath(oracle):
+    """gsl_cdf_beta_P's asymptotic regimes (A&S 26.5.17: a or b > 1e5, union sizes above 1e5)
+    and their general-regime neighbours, against 50-digit evaluations of the same formulas
+    (tests/golden/pvalue_asymp.json, made by make_golden.py --pvalue-asymp).  GSL's
+    approximation itself sits up to ~3e-9 from the exact incomplete beta there; the
+    restatement reproduces the approximation."""
+    import json
+    rows = json.load(open(os.path.join(GOLDEN, "pvalue_asymp.json")))
+    assert {r["branch"] for r in rows} == {"small_a", "large_a", "general"}
+    for row in rows:
+        q = float(row["q"])
+        got = oracle.binomial_q(row["x"] - 1, row["r"], row["n"])
+        if q < 1e-300:
+            assert got < 1e-290
+            continue
+        assert got == pytest.approx(q, rel=1e-12, abs=0), row
+
+
 def _fp_expected(name):
     return mshfmt.read_msh(os.path.join(GOLDEN, name))
 
