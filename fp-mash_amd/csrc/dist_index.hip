@@ -572,23 +572,44 @@ __global__ __launch_bounds__(256) void scan_add_kernel(uint32_t *__restrict__ ou
 // matching entries, and the work the row probe does).  Also flags unsorted /
 // duplicate-carrying query rows.  One atomic per workgroup into one of 64 spread
 // counters (a single counter serialises).
+// kPC consecutive hashes per thread, their key loads and then their directory reads issued
+// together (one hash per thread waited out three dependent global loads in a row)
+constexpr uint32_t kPC = 4;
 __global__ __launch_bounds__(256) void probe_count_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t hash_bytes, IdxGeom g, const uint32_t *__restrict__ dir,
     unsigned long long *__restrict__ events, uint32_t *__restrict__ unsorted)
 {
     __shared__ unsigned long long wsum[4];
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = (uint64_t)n_qry * stride;
+    const uint64_t e0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kPC;
     uint64_t ev = 0;
     uint32_t uns = 0;
-    if (e < (uint64_t)n_qry * stride) {
-        const uint32_t q = (uint32_t)(e / stride), j = (uint32_t)(e % stride);
-        const uint32_t lq = qry_len[q];
-        if (j < lq) {
-            const uint64_t key = load_key(qry, hash_bytes, e);
-            const uint64_t b = bucket_of(norm_key(key, hash_bytes), g, idx_mult(g));
-            ev = dir[b + 1] - dir[b];
-            if (j + 1 < lq && !(key < load_key(qry, hash_bytes, e + 1))) uns = 1;
+    if (e0 < n) {
+        uint32_t q = (uint32_t)(e0 / stride), j = (uint32_t)(e0 - (uint64_t)q * stride);
+        uint64_t key[kPC + 1];
+        uint32_t jj[kPC], lq[kPC];
+        bool ok[kPC + 1];
+#pragma unroll
+        for (uint32_t u = 0; u <= kPC; u++) {
+            const uint32_t l = q < n_qry ? qry_len[q] : 0u;
+            ok[u] = j < l;
+            key[u] = ok[u] ? load_key(qry, hash_bytes, (uint64_t)q * stride + j) : 0;
+            if (u < kPC) { jj[u] = j; lq[u] = l; }
+            if (++j == stride) { j = 0; q++; }
+        }
+        uint32_t d0[kPC], d1[kPC];
+#pragma unroll
+        for (uint32_t u = 0; u < kPC; u++) {
+            const uint64_t b = bucket_of(norm_key(key[u], hash_bytes), g, idx_mult(g));
+            d0[u] = ok[u] ? dir[b] : 0u;
+            d1[u] = ok[u] ? dir[b + 1] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kPC; u++) {
+            ev += d1[u] - d0[u];
+            // the next value of the same row (jj + 1 < lq: not past the row's list)
+            if (ok[u] && jj[u] + 1 < lq[u] && !(key[u] < key[u + 1])) uns = 1;
         }
     }
     for (int d = 32; d > 0; d >>= 1) ev += __shfl_down(ev, d, 64);
@@ -634,7 +655,8 @@ void probe_rows_kernel(
     uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, C *__restrict__ numer,
     C *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg,
-    const uint32_t *__restrict__ qry_it_len)
+    const uint32_t *__restrict__ qry_it_len, uint32_t *__restrict__ q_unsorted,
+    unsigned long long *__restrict__ events)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
@@ -669,12 +691,21 @@ void probe_rows_kernel(
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
     // loaded together (their global loads overlap) before the batches are expanded
     constexpr int kB = 4;
+    uint64_t ev_w = 0;      // this wave's posting events (with `events`)
+    uint32_t uns = 0;       // an out-of-order or repeated value in the row (with `q_unsorted`)
     for (uint32_t jb = wave * 64; jb < lit; jb += 256 * kB) {
         uint32_t st_b[kB], cnt_b[kB], tgt_b[kB];
 #pragma unroll
         for (int bi = 0; bi < kB; bi++) {
             const uint32_t j = jb + 256 * bi + lane;
-            const uint64_t K = j < lit ? norm_key(load_key(qry, hash_bytes, rowoff + j), hash_bytes) : 0;
+            const uint64_t raw = j < lit ? load_key(qry, hash_bytes, rowoff + j) : 0;
+            if (q_unsorted) {
+                // the next value of the row: the next lane's, or a load for the last lane
+                uint64_t nx = __shfl_down(raw, 1, 64);
+                if (lane == 63 && j + 1 < lit) nx = load_key(qry, hash_bytes, rowoff + j + 1);
+                if (j + 1 < lit && !(raw < nx)) uns = 1;
+            }
+            const uint64_t K = j < lit ? norm_key(raw, hash_bytes) : 0;
             const uint64_t b = bucket_of(K, g, mult);
             const uint32_t d0 = j < lit ? dir[b] : 0u, d1 = j < lit ? dir[b + 1] : 0u;
             st_b[bi] = d0;
@@ -692,6 +723,7 @@ void probe_rows_kernel(
             if ((int)lane >= d) inc += y;
         }
         const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        ev_w += total;
         // same wave writes and reads these slots: LDS ops of one wave complete in order.
         // Event ev of hash m reads entries[st_m + ev - pre_m] = entries[base_m + ev] (u32
         // arithmetic wraps consistently).
@@ -736,6 +768,9 @@ void probe_rows_kernel(
         __builtin_amdgcn_wave_barrier();
       }
     }
+    if (q_unsorted && __any(uns) && lane == 0) atomicOr(q_unsorted, 1u);
+    if (events && blockIdx.y == 0 && lane == 0 && ev_w)
+        atomicAdd(&events[1 + (blockIdx.x & 63)], ev_w);
     __syncthreads();
     // candidates of this row: popcount per word -> block scan -> append
     uint32_t mycnt = 0;
@@ -1049,8 +1084,9 @@ hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint
                               unsigned long long *events, uint32_t *unsorted, hipStream_t st)
 {
     uint64_t n = (uint64_t)n_qry * stride;
-    if (n) hipLaunchKernelGGL(probe_count_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0,
-                              st, d_qry, d_qry_len, stride, n_qry, hash_bytes, g, dir, events,
+    const uint64_t threads = (n + kPC - 1) / kPC;
+    if (n) hipLaunchKernelGGL(probe_count_kernel, dim3((uint32_t)((threads + 255) / 256)), dim3(256),
+                              0, st, d_qry, d_qry_len, stride, n_qry, hash_bytes, g, dir, events,
                               unsorted);
     return hipGetLastError();
 }
@@ -1061,7 +1097,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
-                             const uint32_t *d_qry_it_len, hipStream_t st)
+                             const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
+                             unsigned long long *events, hipStream_t st)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -1078,7 +1115,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                        d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref, \
                        d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
                        (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg, \
-                       d_qry_it_len)
+                       d_qry_it_len, q_unsorted, events)
     if (cnt.c16) FPM_PROBE(uint16_t);
     else FPM_PROBE(uint32_t);
 #undef FPM_PROBE

@@ -2070,7 +2070,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                            (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
     // the side fill of query rows [fill_from, q1): from the current point of `st`
     uint32_t fill_from = 0;
-    auto launch_fill_rows = [&](uint32_t q1) -> int {
+    // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
+    // start) and submits the fill after later work on `st`
+    auto launch_fill_rows = [&](uint32_t q1, bool record_in = true) -> int {
         const uint32_t q0 = fill_from;
         const uint64_t off = (uint64_t)q0 * n_ref;
         PairFill fill;
@@ -2087,11 +2089,25 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             c.denom = (char *)cnt.denom + cb;
         }
         HIP_TRY(ensure_aux(ctx));
-        HIP_TRY(hipEventRecord(ctx->ev_in, st));
+        if (record_in) HIP_TRY(hipEventRecord(ctx->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
+        // which fill: the flattened one runs ~35 % faster alone but slows a rank kernel
+        // beside it more (C2, 1e8 cells / 2.3e8 events: rank 0.66 -> 0.70 ms while the fill
+        // shrank 0.63 -> 0.57, step +0.03 ms; C4, 2.5e9 cells: 14.1 -> 12.8-13.3 ms, N = 8
+        // rank share 2.67 -> 2.20 ms).  The fill is the long pole when its cells outweigh the
+        // posting events (the rank kernel's work): flattened when the cells written (both
+        // grids with a transpose) times 1.6 exceed the events (C2: 2.3 events per cell);
+        // FPM_FILL_ROWS=1 / FPM_FILL_FLAT=1 force either (A/B)
+        static const int kFillFlat = [] {
+            const char *r = getenv("FPM_FILL_ROWS"), *f = getenv("FPM_FILL_FLAT");
+            return r && r[0] == '1' ? 0 : f && f[0] == '1' ? 1 : -1;
+        }();
+        const long double cells_w = (long double)n_pairs * (want_mir ? 2 : 1);
+        const bool flat = kFillFlat >= 0 ? kFillFlat == 1
+                                         : cells_w * 1.6L > (long double)ctx->last_events;
         HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len + q0, q1 - q0, sketch_size, c, fill,
-                                 ctx->aux));
+                                 ctx->aux, flat));
         if (want_mir && q1 == n_qry) {
             // the transposed grid: the ref rows as queries against the query rows
             PairFill mf = fill;
@@ -2099,7 +2115,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             mf.pval = fin->mir.pval;
             mf.pass = fin->mir.pass;
             HIP_TRY(launch_dist_fill(d_qry_len, n_qry, d_ref_len, n_ref, sketch_size, fin->mir.cnt,
-                                     mf, ctx->aux));
+                                     mf, ctx->aux, flat));
         }
         tl.done();
         HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
@@ -2125,6 +2141,26 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const uint32_t *dir = nullptr, *entries = nullptr;
         uint64_t ev = 0;
         bool all_sorted = true;
+        // A resident sorted set against another block of sorted rows (the C4 block pairs, the
+        // CLI's query blocks): no probe count.  The count pass reads every query hash's
+        // bucket bounds at random (~0.27 ms for 2.2e7 hashes at N = 8, as long as the index
+        // rebuild), and the probe reads them again; instead the probe reports the row's
+        // posting events and whether the query rows are sorted, and the candidate compare is
+        // chosen after it (rank kernel, or the literal walk for unsorted rows: the candidates
+        // are the same).  Taken in the forced sparse mode, and in AUTO when the set's own
+        // density (its self events per row) says the block is far from the dense regime;
+        // FPM_PROBE_COUNT=1 forces the count (A/B).
+        static const bool kForceCount = [] {
+            const char *v = getenv("FPM_PROBE_COUNT");
+            return v && v[0] == '1';
+        }();
+        const long double ev_est =
+            rs ? (long double)rs->self_events * n_qry / std::max<uint32_t>(1, rs->n_ref) : 0.0L;
+        const bool skip_count = rs && !self_set && !rs->deduped && !rs->ref_unsorted &&
+                                hash_bytes == 8 && !kForceCount &&
+                                (ctx->dist_mode == FPM_DIST_SPARSE ||
+                                 (ctx->dist_mode == FPM_DIST_AUTO &&
+                                  ev_est * 16.0L <= (long double)n_pairs * sketch_size));
         if (rs && self_set && !rs->deduped) {
             // the resident set against itself: its posting events and sortedness are the
             // index build's (sum_b |b|^2, the reference flag), no probe count
@@ -2134,6 +2170,13 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             ev = rs->self_events;
             all_sorted = !rs->ref_unsorted;
             HIP_TRY(hipMemsetAsync(ctr, 0, 67 * 8, st));   // the candidate counter among them
+        } else if (skip_count) {
+            geom = rs->geom;
+            dir = (const uint32_t *)rs->slot[4].p;
+            entries = (const uint32_t *)rs->slot[5].p;
+            ev = (uint64_t)ev_est;          // replaced by the probe's own count
+            all_sorted = true;              // verified by the probe
+            HIP_TRY(hipMemsetAsync(ctr, 0, 67 * 8, st));
         } else if (rs) {
             // resident index: count this block's posting events (and its sortedness)
             geom = rs->geom;
@@ -2235,13 +2278,15 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                             ((long double)ev * 4.0L <= (long double)n_pairs * sketch_size &&
                              (all_sorted || 2 * ev <= n_pairs));
         if (sparse) {
-            const uint64_t cap = std::max<uint64_t>(1, std::min<uint64_t>(ev, n_pairs));
+            // without a count the candidates are bounded by the pairs only
+            const uint64_t cap = std::max<uint64_t>(1, skip_count ? n_pairs
+                                                                  : std::min<uint64_t>(ev, n_pairs));
             void *cand, *row_seg;
             HIP_TRY(scratch(ctx, 8, cap * 8, &cand));
             HIP_TRY(scratch(ctx, 9, (size_t)n_qry * 8, &row_seg));
             const uint64_t lcap = std::max(ref_stride, qry_stride);
-            const bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
-                                    lcap <= 2048;
+            bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
+                              lcap <= 2048;
             // one sorted set against itself: (numer, denom) of sorted distinct lists is
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
@@ -2269,10 +2314,30 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, dir, entries, d_ref_len, sketch_size, sym,
                                           !fill_cnt, self_set, cnt, (uint64_t *)cand, n_cand,
-                                          (uint64_t *)row_seg, p_qry_it, st));
+                                          (uint64_t *)row_seg, p_qry_it,
+                                          skip_count ? unsorted : nullptr,
+                                          skip_count ? events : nullptr, st));
                 tl.done();
             }
+            if (skip_count) {
+                if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
+                ctx->last_events = ctx->host_counters[0];
+                if (((const uint32_t *)(ctx->host_counters + 66))[0] != 0) {
+                    all_sorted = false;         // unsorted query rows: the literal walk
+                    rows_merge = false;
+                }
+            }
             uint32_t *cnum = nullptr, *cden = nullptr;
+            // After the host read of the probe's counters the GPU is idle: the fill, submitted
+            // first, would take every CU before the rank kernel's workgroups arrive (rank +
+            // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
+            // ends (ev_in recorded here) but is submitted after the candidate compare.
+            const bool defer_fill = skip_count && rows_merge && fin && !fin->prefilled &&
+                                    !fill_pending && !ctx->fill_serial && !ctx->cmp;
+            if (defer_fill) {
+                HIP_TRY(ensure_aux(ctx));
+                HIP_TRY(hipEventRecord(ctx->ev_in, st));
+            }
             if (fin && fin->prefilled) {
                 if (rows_merge) {
                     void *cres;
@@ -2281,7 +2346,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     cden = cnum + cap;
                 }
             } else if (fin) {
-                if (!fill_pending)
+                if (!fill_pending && !defer_fill)
                     if (int rc = launch_fill()) return rc;   // the rows not filled yet
                 if (rows_merge) {
                     void *cres;
@@ -2318,6 +2383,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     HIP_TRY(hipStreamWaitEvent(st, ctx->ev_cmp1, 0));
                 }
             }
+            if (defer_fill)
+                if (int rc = launch_fill_rows(n_qry, false)) return rc;
             if (fin && fin->prefilled) {
                 // the walk kernel wrote numer / denom only; distance / p-value / pass of the
                 // candidates and the empty pairs overwrite the prefill, so after it

@@ -162,9 +162,11 @@ struct PairFill {
     uint8_t *pass = nullptr;
     double max_dist = -1, max_pvalue = -1;
 };
+// flat: the fill over the flattened grid (line-aligned wave stores, ~6.5 TB/s alone), else
+// row-aligned workgroups (~4.8 TB/s alone, gentler on a latency-bound kernel beside it)
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
-                            hipStream_t st);
+                            hipStream_t st, bool flat = true);
 // (d_ref_len == d_qry_len == nullptr: every list taken as non-empty, fpm_dist_prefill_dev)
 // distance 0 / p-value 1 / pass for the pairs of two empty lists (after such a prefill)
 hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
@@ -178,7 +180,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              const uint32_t *d_ref_len, uint32_t S, bool sym, bool defaults,
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
-                             const uint32_t *d_qry_it_len, hipStream_t st);
+                             const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
+                             unsigned long long *events, hipStream_t st);
 // (d_qry_it_len non-null: the probed query rows are launch_dedup_rows copies of length
 // d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)
 // (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are

@@ -758,3 +758,59 @@ def test_pvalue_asymptotic_branches_on_device(ctx, oracle):
         np.testing.assert_allclose(pv, exp, rtol=RTOL, atol=0)
         for b in bufs + outs:
             b.free()
+
+
+def test_refset_unsorted_query_block(ctx, oracle):
+    """A resident set of sorted sketches against a block of UNSORTED query lists in the
+    sparse mode: the probe runs without a count pass, finds the query rows out of order and
+    the candidates take the literal walk (the reference's own walk on unsorted lists) instead
+    of the rank kernel.  Every cell equals the oracle's grid; the same block with its lists
+    sorted takes the rank kernel and matches too."""
+    import ctypes as C
+    import fpmash
+    from fpmash import datagen
+    rng = np.random.default_rng(41)
+    seqs = datagen.family_dna(6, 10, 1500, sub_rate=(0.0, 0.1), seed=43)
+    lists = oracle.sketch_batch(oracle.params(k=21, s=300), seqs)
+    refs = lists[:30]
+    S, k, space = 300, 21, 4.0 ** 21
+    for shuffled in (True, False):
+        qrys = []
+        for x in lists[30:]:
+            y = np.array(x, dtype=np.uint64)
+            if shuffled:
+                rng.shuffle(y)
+            qrys.append(y)
+        rl = [int(len(x)) * 5 + 900 for x in refs]
+        ql = [int(len(x)) * 5 + 900 for x in qrys]
+        w = max(len(x) for x in lists)
+        R, rlen = fpmash._dense(refs, w, np.uint64)
+        Q, qlen = fpmash._dense(qrys, w, np.uint64)
+        L = fpmash.lib()
+        bufs = [fpmash.DeviceBuffer.from_array(ctx, np.ascontiguousarray(a))
+                for a in (R, rlen, np.array(rl, np.uint64), Q, qlen, np.array(ql, np.uint64))]
+        nr, nq = len(refs), len(qrys)
+        outs = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (4, 4, 8, 8, 1)]
+        ctx.set_dist_mode(2)
+        h = C.c_void_p()
+        try:
+            fpmash._check(L.fpm_refset_create_dev(ctx.h, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, w,
+                                                  nr, 8, S, C.byref(h)))
+            fpmash._check(L.fpm_refset_dist_dev(h, bufs[3].ptr, bufs[4].ptr, bufs[5].ptr, w, nq,
+                                                S, 4, k, space, 1.0, 1.0,
+                                                *[b.ptr for b in outs], None))
+            ctx.synchronize()
+            # 1: the literal walk of the candidates, 2: the rank kernel
+            assert ctx.last_dist_stats()["sparse"] == (1 if shuffled else 2)
+        finally:
+            ctx.set_dist_mode(0)
+            if h.value:
+                L.fpm_refset_free(h)
+        types = (np.uint32, np.uint32, np.float64, np.float64, np.uint8)
+        got = [b.to_array(t, nr * nq) for b, t in zip(outs, types)]
+        nu, de, di, pv = oracle.dist_grid(refs, rl, qrys, ql, S, k, space, use64=True)
+        assert np.array_equal(got[0], nu.ravel()) and np.array_equal(got[1], de.ravel())
+        np.testing.assert_allclose(got[2], di.ravel(), rtol=RTOL, atol=0)
+        np.testing.assert_allclose(got[3], pv.ravel(), rtol=RTOL, atol=0)
+        for b in bufs + outs:
+            b.free()

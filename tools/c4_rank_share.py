@@ -107,6 +107,7 @@ def main():
     dist()
     ctx.synchronize()
     ctx.set_timing(False)
+    last = ctx.last_dist_stats()       # the step's last dist call (its largest job)
     kern = {}
     for kid, name in fpmash.KERNEL_NAMES.items():
         tot, cnt = ctx.kernel_time(kid)
@@ -117,7 +118,8 @@ def main():
     print(json.dumps({"emulated_ws": a.ws, "emulated_rank": a.rank, "n": n,
                       "jobs": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                                for j in jobs],
-                      "cells_written": cells, "sketch_shard_ms": sk_ms, "dist_ms": di_ms,
+                      "cells_written": cells, "last_call_stats": last,
+                      "sketch_shard_ms": sk_ms, "dist_ms": di_ms,
                       "rank_step_ms_excl_gather": sk_ms + di_ms, "dist_kernels": kern,
                       "note": "all-gather of the 400 MB sketch rows not included"}))
     for rs in refsets.values():

@@ -5,6 +5,7 @@
 #include "../../fp-mash_amd/csrc/dist.hip"
 
 #include <stdio.h>
+#include <stdlib.h>
 #include <vector>
 
 using namespace fpm;
@@ -20,9 +21,36 @@ __global__ __launch_bounds__(256) void bare17(double *di, double *pv, uint8_t *p
     *(uint32_t *)(pa + c) = 0x01010101u;
 }
 
-int main()
+// the fill with flat indexing: workgroup k takes cells [1024 k, 1024 k + 1024) of the whole
+// grid (rows found per lane), so every wave store is line-aligned and no workgroup is partial
+__global__ __launch_bounds__(256) void flat_fill(const uint32_t *__restrict__ ref_len, uint32_t n_ref,
+                                                 const uint32_t *__restrict__ qry_len, uint64_t cells,
+                                                 uint32_t S, PairFill fill)
 {
-    const uint32_t n = 10000;
+    const uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (o >= cells) return;
+    const uint32_t q = (uint32_t)(o / n_ref), r = (uint32_t)(o - (uint64_t)q * n_ref);
+    const uint32_t lq = qry_len[q];
+    const uint4 rl = *(const uint4 *)(ref_len + r);
+    const uint32_t d[4] = {rl.x + lq, rl.y + lq, rl.z + lq, rl.w + lq};
+    double dv[4], pv[4];
+    uint32_t pa = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        dv[u] = d[u] == 0 ? 0.0 : 1.0;
+        pv[u] = 1.0;
+        pa |= 1u << (8 * u);
+    }
+    *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
+    *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
+    *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
+    *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
+    *(uint32_t *)(fill.pass + o) = pa;
+}
+
+int main(int argc, char **argv)
+{
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 10000;
     const uint64_t cells = (uint64_t)n * n;
     std::vector<uint32_t> len(n, 1000);
     uint32_t *d_len;
@@ -52,6 +80,9 @@ int main()
         printf("{\"variant\": \"%s\", \"ms\": %.4f, \"GBps\": %.1f}\n", name, best, 17.0 * cells / best / 1e6);
     };
     run("dist_fill_kernel", [&] { launch_dist_fill(d_len, n, d_len, n, 1000, Counts{}, f, 0); });
+    // no length loads (the prefill form: every list non-empty, constant cells)
+    run("dist_fill_kernel_no_lengths", [&] { launch_dist_fill(nullptr, n, nullptr, n, 1000, Counts{}, f, 0); });
+    run("flat_fill", [&] { hipLaunchKernelGGL(flat_fill, dim3((uint32_t)((cells / 4 + 255) / 256)), dim3(256), 0, 0, d_len, n, d_len, cells, 1000, f); });
     run("bare_17B_stores", [&] { hipLaunchKernelGGL(bare17, dim3((uint32_t)((cells / 4 + 255) / 256)), dim3(256), 0, 0, di, pv, pa, cells); });
     return 0;
 }

@@ -37,6 +37,7 @@ GROUPS = [
     ("dist_cand_finalize_kernel", "dist finalize (dense / candidate cells)"),
     ("probe_rows_kernel", "probe_rows_kernel"),
     ("dist_fill_kernel", "dist_fill_kernel"),
+    ("dist_fill_flat_kernel", "dist_fill_kernel"),
     ("idx_", "dist index build"),
     ("scan_", "dist index build"),
     ("probe_count_kernel", "dist index build"),

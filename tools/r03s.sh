@@ -1,0 +1,13 @@
+set -o pipefail
+cd /root/repo
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r03s
+timeout -k 10 600 python -u -m pytest tests/ -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/r03s/pytest.log 2>&1 || { tail -30 gpurun_out/r03s/pytest.log; exit 1; }
+tail -1 gpurun_out/r03s/pytest.log
+for a in "2 0" "4 0" "8 0" "8 7"; do
+  set -- $a
+  timeout -k 10 240 python3 tools/c4_rank_share.py --ws $1 --rank $2 > gpurun_out/r03s/c4_rank_share_ws$1_rank$2.json 2>/dev/null || exit 1
+  python3 -c "
+import json; d=json.load(open('gpurun_out/r03s/c4_rank_share_ws$1_rank$2.json'))
+print('ws $1 rank $2', round(d['rank_step_ms_excl_gather'],3), round(d['dist_ms'],3), {k[:14]:v['total_ms'] for k,v in d['dist_kernels'].items()})"
+done
