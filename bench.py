@@ -109,6 +109,9 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the one-genome-over-all-GPUs sketch leg (RCCL min-merge)")
     ap.add_argument("--split-bases", type=int, default=1_000_000_000)
+    ap.add_argument("--pipeline", action="store_true",
+                    help="C2 steps overlapped two deep: the next batch's sketch kernels on a "
+                         "second stream beside this batch's dist (double-buffered sketch rows)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
     return ap.parse_args()
@@ -1138,14 +1141,61 @@ def main():
                              1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
                              d_pass.ptr, st))
 
-    for _ in range(args.warmup):
-        step()
+    # --pipeline (A/B, off): K steps = K sketches + K dists, overlapped two deep: batch i + 1's
+    # sketch kernels run on a second stream while batch i's dist runs on the context stream
+    # (the sketch rows double-buffered; a buffer is re-sketched only after the dist that read
+    # it).  Measured slower on one MI355X (tools/pipe_ab.sh: 1.389 vs 1.355 ms per step): the
+    # VALU-bound sketch beside the latency-bound index / probe / rank kernels costs them more
+    # than the 0.16 ms it hides
+    run_steps = lambda k: [step() for _ in range(k)]   # noqa: E731
+    if args.pipeline and not prefill:
+        import ctypes as C
+        hip = C.CDLL("libamdhip64.so")
+        job2 = ctx.sketch_job(P, seqs)
+        d_rows2, d_cnt2, _, _ = job2.device_output()
+        bufs = [(job, d_rows, d_cnt), (job2, d_rows2, d_cnt2)]
+
+        def hip_ok(rc):
+            if rc != 0:
+                raise RuntimeError(f"HIP error {rc}")
+        ss = C.c_void_p()
+        hip_ok(hip.hipSetDevice(local))
+        hip_ok(hip.hipStreamCreateWithFlags(C.byref(ss), 1))   # hipStreamNonBlocking
+        ev_sk = [C.c_void_p(), C.c_void_p()]
+        ev_di = [C.c_void_p(), C.c_void_p()]
+        for e in ev_sk + ev_di:
+            hip_ok(hip.hipEventCreateWithFlags(C.byref(e), 2))  # hipEventDisableTiming
+        stp = C.c_void_p(st)
+
+        def run_steps(k):
+            used = [False, False]
+            if k:
+                bufs[0][0].run(ss.value)
+                hip_ok(hip.hipEventRecord(ev_sk[0], ss))
+            for i in range(k):
+                b = i & 1
+                if i + 1 < k:
+                    nb = 1 - b
+                    if used[nb]:
+                        hip_ok(hip.hipStreamWaitEvent(ss, ev_di[nb], 0))
+                    bufs[nb][0].run(ss.value)
+                    hip_ok(hip.hipEventRecord(ev_sk[nb], ss))
+                hip_ok(hip.hipStreamWaitEvent(stp, ev_sk[b], 0))
+                _, rows, cnts = bufs[b]
+                fpmash._check(L.fpm_dist_dev16(ctx.h, rows, cnts, d_len.ptr, stride, n, rows, cnts,
+                                               d_len.ptr, stride, n, 8, args.s, args.k,
+                                               4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
+                                               d_dist.ptr, d_pval.ptr, d_pass.ptr, st))
+                hip_ok(hip.hipEventRecord(ev_di[b], stp))
+                used[b] = True
+            hip_ok(hip.hipStreamSynchronize(ss))
+
+    run_steps(args.warmup)
     ctx.synchronize()
     grp.barrier()
     ctx.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     ctx.synchronize()
     t1 = time.perf_counter()
     grp.barrier()
