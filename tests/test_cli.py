@@ -265,6 +265,38 @@ def test_sketch_c2_10k_msh_byte_identical(tmp_path, oracle):
 
 
 @pytest.mark.gpu
+def test_c1_two_files_sketch_then_dist(tmp_path, oracle):
+    """Config C1 end to end: two FASTA files of one 2,000 bp record each
+    (uniform ACGT, seed 1, lyn2vec headers), `sketch -k 21 -s 1000 a.fa b.fa -o ab` (default
+    concatenated mode: one sketch per file, named by the file, commented by its first record)
+    then `dist ab.msh ab.msh`: the .msh equals the oracle's sketches encoded by the pinned
+    writer, byte for byte, and the four dist lines equal the oracle's (query-major, %g)."""
+    from fpmash import datagen
+    rng = np.random.default_rng(1)
+    seqs = [bytes(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 2000)]) for _ in range(2)]
+    ids = datagen.lyn2vec_ids(2)
+    for name, s, i in zip(("a.fa", "b.fa"), seqs, ids):
+        (tmp_path / name).write_bytes(datagen.fasta_bytes([s], [i]))
+    run(["sketch", "-k", "21", "-s", "1000", "a.fa", "b.fa", "-o", "ab"], cwd=tmp_path)
+    got = (tmp_path / "ab.msh").read_bytes()
+    exp_h = oracle.sketch_batch(oracle.params(k=21, s=1000), seqs)
+    refs = [dict(name=f.encode(), comment=b"T00000" + i.encode() + b" G00000" + i.encode(),
+                 length=len(s), hashes=h) for f, s, i, h in zip(("a.fa", "b.fa"), seqs, ids, exp_h)]
+    hdr = dict(kmer=21, windowSize=0, sketchSize=1000, concatenated=True, noncanonical=False,
+               preserveCase=False, error=0.0, seed=42, alphabet=b"ACGT")
+    assert got == mshfmt.write_msh(hdr, refs)
+    out = run(["dist", "ab.msh", "ab.msh"], cwd=tmp_path).stdout.decode().splitlines()
+    exp = []
+    for qn, qs, qh in zip(("a.fa", "b.fa"), seqs, exp_h):
+        for rn, rs, rh in zip(("a.fa", "b.fa"), seqs, exp_h):
+            nu, de = oracle.compare(rh, qh, 1000, use64=True)
+            d = oracle.distance(nu, de, 21)
+            pv = oracle.pvalue(nu, len(rs), len(qs), 4.0 ** 21, de)
+            exp.append(f"{rn}\t{qn}\t{d:g}\t{pv:g}\t{nu}/{de}")
+    assert out == exp
+
+
+@pytest.mark.gpu
 def test_dist_genomes_golden():
     """mash/test/ref/genomes.dist: distance, p-value and shared-hash fields."""
     lines = open(os.path.join(GOLDEN, "genomes.dist")).read().splitlines()
