@@ -1121,17 +1121,19 @@ def main():
     d_len = fpmash.DeviceBuffer.from_array(ctx, lengths)
     st = ctx.stream
 
-    # FPM_BENCH_PREFILL=1: the no-shared-hash cells prefilled beside the sketch kernels
-    # (fpm_dist_prefill_dev); same-box A/B: 1.49-1.50 ms either way (the sketch kernel then
-    # stretches 0.17 -> 0.37 ms), so the one-call form is the default
-    prefill = os.environ.get("FPM_BENCH_PREFILL", "0") != "0"
+    # FPM_BENCH_PREFILL=f: the no-shared-hash cells of the first f of the query rows
+    # prefilled beside the sketch kernels (fpm_dist_prefill_dev), the rest filled by the dist
+    # call beside the candidate compare (f = 1: the whole grid beside the sketch)
+    pre_frac = float(os.environ.get("FPM_BENCH_PREFILL", "0"))
+    n_pre = n if pre_frac >= 1 else min(n, int(n * pre_frac) // 16 * 16)
+    prefill = n_pre > 0
 
     def step():
         if prefill:
             # the grid's no-shared-hash distance / p-value / pass cells need no list: written
             # on the side stream while the sketches are computed (fpm_dist_prefill_dev)
-            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n, 1.0, 1.0, d_dist.ptr, d_pval.ptr,
-                                                 d_pass.ptr, None))
+            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n_pre, 1.0, 1.0, d_dist.ptr,
+                                                 d_pval.ptr, d_pass.ptr, None))
         job.run(st)
         # compare + distance + p-value + pass (the candidates and empty pairs rewritten after
         # the prefill)

@@ -110,6 +110,7 @@ struct fpm_ctx {
     hipEvent_t ev_cmp0 = nullptr, ev_cmp1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
     hipEvent_t ev_prefill = nullptr;       // end of the last fpm_dist_prefill_dev
+    uint32_t prefill_rows = 0, prefill_nref = 0;   // the grid rows / columns it wrote
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
     static constexpr size_t kRingBytes = 8u << 20;
@@ -1855,8 +1856,11 @@ struct DistFinal {
     double *dist, *pval;
     uint8_t *pass;
     // the caller ran fpm_dist_prefill_dev on these buffers (ctx->ev_prefill marks its end):
-    // no fill here, the empty pairs are fixed up and every rewrite waits for the prefill
+    // no fill here, the empty pairs are fixed up and every rewrite waits for the prefill.
+    // pre_rows < n_qry: only query rows [0, pre_rows) were prefilled (beside the sketch
+    // kernels); the other rows are filled here, beside the candidate compare
     bool prefilled = false;
+    uint32_t pre_rows = 0;
     // the transposed grid too (fpm_refset_dist_mirror_dev): filled beside the primary grid and
     // its candidate cells scattered by the candidate finalize; compare_impl sets *mirrored
     // when it wrote it (the sorted sparse path), else dist_dev_impl computes it by a second,
@@ -2069,7 +2073,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                           (want_mir ||
                            (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
     // the side fill of query rows [fill_from, q1): from the current point of `st`
-    uint32_t fill_from = 0;
+    uint32_t fill_from = fin && fin->prefilled ? std::min(fin->pre_rows, n_qry) : 0;
+    // every row prefilled: no fill in this call
+    const bool pre_all = fin && fin->prefilled && fill_from == n_qry;
     // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
     // start) and submits the fill after later work on `st`
     auto launch_fill_rows = [&](uint32_t q1, bool record_in = true) -> int {
@@ -2332,13 +2338,13 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // first, would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
             // ends (ev_in recorded here) but is submitted after the candidate compare.
-            const bool defer_fill = skip_count && rows_merge && fin && !fin->prefilled &&
+            const bool defer_fill = skip_count && rows_merge && fin && !pre_all &&
                                     !fill_pending && !ctx->fill_serial && !ctx->cmp;
             if (defer_fill) {
                 HIP_TRY(ensure_aux(ctx));
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
             }
-            if (fin && fin->prefilled) {
+            if (fin && pre_all) {
                 if (rows_merge) {
                     void *cres;
                     HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
@@ -2387,7 +2393,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 if (int rc = launch_fill_rows(n_qry, false)) return rc;
             if (fin && fin->prefilled) {
                 // the walk kernel wrote numer / denom only; distance / p-value / pass of the
-                // candidates and the empty pairs overwrite the prefill, so after it
+                // candidates and the empty pairs overwrite the prefill, so after it (the rows
+                // filled by this call handle their empty pairs themselves)
                 PairFill fx;
                 fx.dist = fin->dist;
                 fx.pval = fin->pval;
@@ -2395,10 +2402,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 fx.max_dist = fin->max_dist;
                 fx.max_pvalue = fin->max_pvalue;
                 HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
-                HIP_TRY(launch_dist_empty_fixup(d_ref_len, n_ref, d_qry_len, n_qry, fx, st));
-            } else if (fin && cnum) {
-                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+                HIP_TRY(launch_dist_empty_fixup(d_ref_len, n_ref, d_qry_len,
+                                                std::min(fin->pre_rows, n_qry), fx, st));
             }
+            if (fin && !pre_all && cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             if (fin) {
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
                 MirrorOut mir{};
@@ -2474,9 +2481,15 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
     if (prefilled && !ctx->ev_prefill)
         return fail(FPM_EINVAL, std::string(who) + ": no fpm_dist_prefill_dev on this context");
+    if (prefilled && (ctx->prefill_nref != n_ref || ctx->prefill_rows > n_qry))
+        return fail(FPM_EINVAL, std::string(who) + ": the last fpm_dist_prefill_dev wrote " +
+                                    std::to_string(ctx->prefill_rows) + " x " +
+                                    std::to_string(ctx->prefill_nref) + " cells, not rows of this " +
+                                    std::to_string(n_qry) + " x " + std::to_string(n_ref) + " grid");
     DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
                   d_dist, d_pvalue, d_pass};
     fin.prefilled = prefilled;
+    fin.pre_rows = prefilled ? ctx->prefill_rows : 0;
     bool finalized = false, mirrored = false;
     if (mirror) {
         fin.mir = *mirror;
@@ -2562,6 +2575,8 @@ int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double ma
     HIP_TRY(launch_dist_fill(nullptr, n_ref, nullptr, n_qry, 0, Counts{}, fill, st));
     tl.done();
     HIP_TRY(hipEventRecord(ctx->ev_prefill, st));
+    ctx->prefill_rows = n_qry;
+    ctx->prefill_nref = n_ref;
     return FPM_OK;
 }
 

@@ -267,7 +267,11 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
  * cell of the n_qry x n_ref grid without reading any list (NULL stream: the context's side
  * stream), and fpm_dist_dev16_prefilled then computes everything else: every cell's counts,
  * the pairs of two empty lists, and the cells of the pairs that share hashes (those rewrites
- * wait for the prefill; the rest of the call does not).  Same results as fpm_dist_dev16. */
+ * wait for the prefill; the rest of the call does not).  Same results as fpm_dist_dev16.
+ * A partial prefill: the last fpm_dist_prefill_dev on the context wrote the first n_pre
+ * query rows of this grid (its n_qry = n_pre <= this call's n_qry, its n_ref = this call's;
+ * FPM_EINVAL otherwise), and the call fills rows [n_pre, n_qry) itself, beside the candidate
+ * compare — so the prefill can be sized to end with the sketch kernels it overlaps. */
 int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double max_dist,
                          double max_pvalue, double *d_dist, double *d_pvalue, uint8_t *d_pass,
                          void *stream);

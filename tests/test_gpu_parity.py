@@ -560,11 +560,14 @@ def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
     dL = up(lens)
     dqL = dL if self_set else up(qlens)
     res = []
-    for pre in (False, True):
+    # prefilled rows: none (fpm_dist_dev16), all, and partial prefills (the call fills the
+    # other rows beside its compare; 37 leaves the rest unaligned for 16-B stores); the empty
+    # lists sit in the last query rows (self set) or the first (the reversed query set)
+    for pre in (0, nq, 37, nq // 2 // 16 * 16):
         outs = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (2, 2, 8, 8, 1)]
         bufs.extend(outs)
         if pre:
-            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr, nq, maxd, maxp, outs[2].ptr,
+            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr, pre, maxd, maxp, outs[2].ptr,
                                                  outs[3].ptr, outs[4].ptr, None))
         f = L.fpm_dist_dev16_prefilled if pre else L.fpm_dist_dev16
         fpmash._check(f(ctx.h, dR, drl, dL, w, nr, dQ, dql, dqL, w, nq, 8, 500, 21, 4.0 ** 21,
@@ -573,8 +576,15 @@ def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
         res.append([o.to_array(t, nr * nq) for o, t in zip(outs, (np.uint16, np.uint16,
                                                                    np.float64, np.float64,
                                                                    np.uint8))])
-    for a, b in zip(res[0], res[1]):
-        assert np.array_equal(a, b)
+    for other in res[1:]:
+        for a, b in zip(res[0], other):
+            assert np.array_equal(a, b)
+    # a prefill of another grid shape (fewer columns: within the buffers) is refused
+    fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr - 1, nq, maxd, maxp, outs[2].ptr,
+                                         outs[3].ptr, outs[4].ptr, None))
+    assert L.fpm_dist_dev16_prefilled(ctx.h, dR, drl, dL, w, nr, dQ, dql, dqL, w, nq, 8, 500, 21,
+                                      4.0 ** 21, maxd, maxp, *[o.ptr for o in outs], None) != 0
+    ctx.synchronize()
     nu, de, di, pv = oracle.dist_grid(sk, list(lens), qsk, list(qlens), 500, 21, 4.0 ** 21)
     assert np.array_equal(res[1][0], nu) and np.array_equal(res[1][1], de)
     ok = (res[1][0] > 0)
