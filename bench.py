@@ -1121,10 +1121,16 @@ def main():
     d_len = fpmash.DeviceBuffer.from_array(ctx, lengths)
     st = ctx.stream
 
-    # FPM_BENCH_PREFILL=f: the no-shared-hash cells of the first f of the query rows
-    # prefilled beside the sketch kernels (fpm_dist_prefill_dev), the rest filled by the dist
-    # call beside the candidate compare (f = 1: the whole grid beside the sketch)
-    pre_frac = float(os.environ.get("FPM_BENCH_PREFILL", "0"))
+    # The grid's no-shared-hash cells (distance 1, p-value 1, pass: no list needed) of the
+    # first f of the query rows are prefilled beside the sketch kernels (fpm_dist_prefill_dev),
+    # the rest by the dist call beside the candidate compare.  Same-box sweep
+    # (profiles/r03/s3/prefill_frac_ab*.txt, ms per step): f = 0 (the whole fill beside the
+    # compare) 1.338-1.359, 0.3 1.314, 0.45 1.295, 0.55 1.290-1.295, 0.6 1.285-1.289,
+    # 0.65 1.282-1.287, 0.75 1.289-1.297, 0.85 1.306-1.310, 1 1.324-1.329: the prefill
+    # stretches the sketch 0.16 -> 0.21 ms and, past the sketch, the latency-bound index
+    # build (0.15 -> 0.20 ms at 0.6, 0.30 at 1), while the compare beside the rest of the fill
+    # drops 0.65 -> 0.48 ms (0.42 alone).  FPM_BENCH_PREFILL=f overrides (0: one call)
+    pre_frac = float(os.environ.get("FPM_BENCH_PREFILL", "0.6"))
     n_pre = n if pre_frac >= 1 else min(n, int(n * pre_frac) // 16 * 16)
     prefill = n_pre > 0
 
@@ -1219,6 +1225,12 @@ def main():
         tot, cnt = ctx.kernel_time(kid)
         if cnt:
             ktimes[name] = {"total_ms": tot, "launches": cnt, "avg_ms": tot / cnt}
+            if kid == fpmash.K_FILL and prefill and cnt == 2 * n_timed:
+                # the prefill beside the sketch + the rest beside the compare: one step's
+                # grid in two launches, timed (and priced below) per step
+                ktimes[name]["avg_ms"] = tot / n_timed
+                ktimes[name]["launches_per_step"] = 2
+                ktimes[name]["prefill_rows"] = n_pre
     ctx.reset_timing()
 
     # sanity: shared-hash counts present (family structure) and no empty sketches
@@ -1291,9 +1303,11 @@ def main():
     for name, (b, _) in alg.items():
         if name in ktimes:
             gbs = b / (ktimes[name]["avg_ms"] * 1e-3) / 1e9
+            tb = traffic.get(name, {}).get("traffic_bytes")
+            lps = ktimes[name].get("launches_per_step", 1)   # PMC bytes are per launch
             per_kernel_roof[name] = {"avg_ms": ktimes[name]["avg_ms"], "alg_GBps": gbs,
                                      "frac_hbm": gbs / HBM_PEAK_GBS,
-                                     "traffic_bytes": traffic.get(name, {}).get("traffic_bytes")}
+                                     "traffic_bytes": tb * lps if tb is not None else None}
 
     sk_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_SKETCH, fpmash.K_MERGE)]
     di_names = [fpmash.KERNEL_NAMES[k_] for k_ in (fpmash.K_INDEX, fpmash.K_PROBE,
@@ -1354,6 +1368,7 @@ def main():
                              "u16 numer/denom + distance + FP64 p-value + pass), per GPU"),
                 "n_seqs_per_gpu": n, "seq_len": args.seq_len, "k": args.k, "s": args.s,
                 "pairs_per_gpu": n_pairs, "parallelism": f"independent batch per GPU x{ws}",
+                "prefill_rows": n_pre,   # grid rows filled beside the sketch kernels
             },
             "kernel_timing_steps": n_timed,
             "sketch": {"bases_per_s": bases_step / (sk_ms * 1e-3) if sk_ms else None,
