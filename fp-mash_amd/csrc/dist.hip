@@ -909,7 +909,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
 // workgroups put every wave store off the 64-B line grid whenever n_ref is not a multiple of
 // 1024, and left a partial workgroup per row: 4.8 -> 6.5 TB/s at n_ref = 10,000, 4.1 -> 5.8 at
 // 21,876, 5.6 -> 6.6 at 50,000 (tools/micro/fill_real.hip, one MI355X).
-template <typename C>
+template <typename C, bool STRIDE>
 __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
     uint64_t cells, double inv_n, uint32_t S, C *__restrict__ numer, C *__restrict__ denom,
@@ -917,8 +917,11 @@ __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
 {
     const bool keep1 = !(fill.max_dist >= 0 && 1.0 > fill.max_dist);   // distance 0 always kept
     const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
-    const uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
-    if (o >= cells) return;
+    // one pass per thread normally (STRIDE = false: the loop below runs once; as a loop the
+    // kernel measured slower beside the sketch kernels); a capped grid (a prefill that holds
+    // only a few wave slots beside them) strides over the rest
+    for (uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; o < cells;
+         o += (uint64_t)gridDim.x * 1024) {
     uint32_t q = (uint32_t)((double)o * inv_n);
     int64_t rr = (int64_t)(o - (uint64_t)q * n_ref);
     if (rr < 0) { q--; rr += n_ref; }
@@ -947,6 +950,8 @@ __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
     *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
     *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
     if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+    if (!STRIDE) break;
+    }
 }
 
 // After fpm_dist_prefill_dev (every cell written as a pair of non-empty lists sharing no
@@ -980,7 +985,7 @@ hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
 
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
-                            hipStream_t st, bool flat)
+                            hipStream_t st, bool flat, uint32_t grid_cap)
 {
     void *d_numer = cnt.numer, *d_denom = cnt.denom;
     if (!n_ref || !n_qry) return hipSuccess;
@@ -1001,17 +1006,23 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
     const uint32_t grid = (uint32_t)(kGridCap && blocks > kGridCap ? kGridCap : blocks);
     const uint64_t cells = (uint64_t)n_ref * n_qry;
     if (flat && vec && !kGridCap && cells < (1ULL << 50)) {
-        const uint64_t fb = (cells / 4 + 255) / 256;
-        if (fb >= (1ULL << 31)) return hipErrorInvalidValue;
+        uint64_t fb = (cells / 4 + 255) / 256;
+        if (fb >= (1ULL << 31) && !grid_cap) return hipErrorInvalidValue;
         const double inv_n = 1.0 / (double)n_ref;
-        if (cnt.c16)
-            hipLaunchKernelGGL(dist_fill_flat_kernel<uint16_t>, dim3((uint32_t)fb), dim3(256), 0, st,
-                               d_ref_len, n_ref, d_qry_len, cells, inv_n, S, (uint16_t *)d_numer,
-                               (uint16_t *)d_denom, fill);
-        else
-            hipLaunchKernelGGL(dist_fill_flat_kernel<uint32_t>, dim3((uint32_t)fb), dim3(256), 0, st,
-                               d_ref_len, n_ref, d_qry_len, cells, inv_n, S, (uint32_t *)d_numer,
-                               (uint32_t *)d_denom, fill);
+        const bool stride = grid_cap && fb > grid_cap;
+        if (stride) fb = grid_cap;
+#define FPM_FLAT(C_, ST_)                                                                          \
+    hipLaunchKernelGGL((dist_fill_flat_kernel<C_, ST_>), dim3((uint32_t)fb), dim3(256), 0, st,    \
+                       d_ref_len, n_ref, d_qry_len, cells, inv_n, S, (C_ *)d_numer, (C_ *)d_denom, \
+                       fill)
+        if (cnt.c16) {
+            if (stride) FPM_FLAT(uint16_t, true);
+            else FPM_FLAT(uint16_t, false);
+        } else {
+            if (stride) FPM_FLAT(uint32_t, true);
+            else FPM_FLAT(uint32_t, false);
+        }
+#undef FPM_FLAT
         return hipGetLastError();
     }
 #define FPM_FILL(V, C)                                                                         \

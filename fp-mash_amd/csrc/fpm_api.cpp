@@ -2571,8 +2571,15 @@ int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double ma
     fill.pass = d_pass;
     fill.max_dist = max_dist;
     fill.max_pvalue = max_pvalue;
+    // FPM_PREFILL_GRID=n: the flattened prefill on n workgroups striding over the grid (few
+    // wave slots held beside the sketch kernels) instead of one pass per thread (A/B)
+    static const uint32_t kPrefillGrid = [] {
+        const char *v = getenv("FPM_PREFILL_GRID");
+        return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
+    }();
     TimedLaunch tl(ctx, FPM_K_FILL, st);
-    HIP_TRY(launch_dist_fill(nullptr, n_ref, nullptr, n_qry, 0, Counts{}, fill, st));
+    HIP_TRY(launch_dist_fill(nullptr, n_ref, nullptr, n_qry, 0, Counts{}, fill, st, true,
+                             kPrefillGrid));
     tl.done();
     HIP_TRY(hipEventRecord(ctx->ev_prefill, st));
     ctx->prefill_rows = n_qry;

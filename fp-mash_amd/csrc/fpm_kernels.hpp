@@ -166,7 +166,7 @@ struct PairFill {
 // row-aligned workgroups (~4.8 TB/s alone, gentler on a latency-bound kernel beside it)
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
-                            hipStream_t st, bool flat = true);
+                            hipStream_t st, bool flat = true, uint32_t grid_cap = 0);
 // (d_ref_len == d_qry_len == nullptr: every list taken as non-empty, fpm_dist_prefill_dev)
 // distance 0 / p-value 1 / pass for the pairs of two empty lists (after such a prefill)
 hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
