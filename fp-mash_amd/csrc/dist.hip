@@ -274,6 +274,18 @@ constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest
 #ifndef FPM_RANK_LOGB
 #define FPM_RANK_LOGB 12             // log2 buckets for CAP 1024 (CAP 2048: one more)
 #endif
+#ifndef FPM_RANK_LO32
+#define FPM_RANK_LO32 0              // 1: B as 32-bit keys + the 32 bits below them (A/B)
+#endif
+#ifndef FPM_RANK_SELF
+#define FPM_RANK_SELF 0              // 1: the pair (q, q) of a set against itself not probed (A/B)
+#endif
+#ifndef FPM_RANK_LDS_ORDER
+#define FPM_RANK_LDS_ORDER 1         // 1: K32 at LDS offset 0 (ds_read2 offsets fold the probe's q) (A/B)
+#endif
+#ifndef FPM_RANK_LDS_PAD
+#define FPM_RANK_LDS_PAD 0           // bytes of unused LDS per workgroup: fewer workgroups per CU (A/B)
+#endif
 
 // One chunk of 64 A elements against B (one per lane): j = #{B < a} and the lanes whose a
 // is in B (a wave mask).
@@ -343,13 +355,43 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     }
 }
 
+// NP > 0 with B held as (key, low) halves: K32[p] = v >> kshift (distinct, ordering B exactly)
+// and Blo[p] = the kshift bits below the key, so v = K32 << kshift | Blo.  An A value below
+// 2^bits (not `over`) splits the same way; p = lo + #{keys < ka} as in rank_chunk, a key equal
+// to ka can only sit at p (the keys are distinct and ascending), and then the low halves
+// settle the order and the equality: one 32-bit read of Blo[p] instead of the 64-bit Bs[p].
+template <int NP>
+__device__ __forceinline__ uint64_t rank_chunk_lo(const uint32_t *K32, const uint32_t *Blo,
+                                                  const uint16_t *Bkt, uint32_t shift,
+                                                  uint32_t kshift, uint32_t lomask, uint32_t top,
+                                                  uint32_t lb, uint64_t a, uint32_t &j)
+{
+    const uint64_t t = a >> shift;
+    const bool over = t > (uint64_t)top;
+    const uint32_t lo = Bkt[over ? top + 1 : (uint32_t)t];
+    const uint32_t ka = (uint32_t)(a >> kshift), al = (uint32_t)a & lomask;
+    uint32_t p = lo;
+    bool keq = false;
+#pragma unroll
+    for (int q = 0; q < NP; q++) {
+        const uint32_t k = K32[lo + q];
+        p += k < ka ? 1u : 0u;
+        keq |= k == ka;
+    }
+    const uint32_t bl = Blo[p];
+    const bool hit = keq && !over && p < lb;
+    j = p + (hit && bl < al ? 1u : 0u);
+    return __builtin_amdgcn_ballot_w64(hit && bl == al);
+}
+
 template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
-    const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
-    uint32_t n_ref, const uint64_t *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, uint32_t sym, C *__restrict__ numer,
-    C *__restrict__ denom, uint32_t *__restrict__ cnum, uint32_t *__restrict__ cden)
+    uint32_t q_lo, const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len,
+    uint64_t ref_stride, uint32_t n_ref, const uint64_t *__restrict__ qry,
+    const uint32_t *__restrict__ qry_len, uint64_t qry_stride, uint32_t S, uint32_t sym,
+    C *__restrict__ numer, C *__restrict__ denom, uint32_t *__restrict__ cnum,
+    uint32_t *__restrict__ cden)
 {
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? FPM_RANK_LOGB : FPM_RANK_LOGB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
@@ -357,12 +399,40 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // (Sizing them by the launch instead — 20.3 KB at s = 1000, 8 workgroups per CU — put a
     // runtime base add on every probe read: the kernel ran 0.645 -> 0.70 ms beside the fill
     // at 6, 7 or 8 workgroups per CU alike, same-box A/B r03o.)
+#if FPM_RANK_LO32
+    // the 64-bit values while the row is set up (and for rows on the NP = 0 loop), then the
+    // same bytes as key / low halves (rank_chunk_lo): 4 KB less LDS per workgroup
+    __shared__ union {
+        uint64_t v[CAP + kRankProbeMax];
+        struct { uint32_t k[CAP + kRankProbeMax], lo[CAP + kRankProbeMax]; } h;
+    } sB;
+    uint64_t *const Bs = sB.v;
+    uint32_t *const K32 = sB.h.k;
+    uint32_t *const Blo = sB.h.lo;
+#elif FPM_RANK_LDS_ORDER
+    // one block with the keys first: the NP key reads K32[lo + q] are ds_read2_b32 pairs
+    // whose 8-bit dword offsets then hold q (the allocator put K32 after Bs and Bkt, at
+    // 16 KB: one address add per key read)
+    __shared__ struct {
+        uint32_t k[CAP + kRankProbeMax];
+        uint64_t v[CAP + kRankProbeMax];
+    } sKB;
+    uint32_t *const K32 = sKB.k;
+    uint64_t *const Bs = sKB.v;
+#else
     __shared__ uint64_t Bs[CAP + kRankProbeMax];
     __shared__ uint32_t K32[CAP + kRankProbeMax];      // 32-bit keys of B (rank_chunk)
+#endif
     __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
     __shared__ uint32_t s_maxn, s_keydup;
-    const uint32_t q = xcd_row(blockIdx.x, n_qry);
-    if (q >= n_qry) return;
+#if FPM_RANK_LDS_PAD
+    __shared__ uint32_t s_pad[FPM_RANK_LDS_PAD / 4];
+    if (threadIdx.x == 1023u) s_pad[blockIdx.x % (FPM_RANK_LDS_PAD / 4)] = 0;   // kept, never run
+#endif
+    // rows [q_lo, q_lo + n_qry) of the grid (a part of the rows, whose probe ran before)
+    const uint32_t qr = xcd_row(blockIdx.x, n_qry);
+    if (qr >= n_qry) return;
+    const uint32_t q = q_lo + qr;
     const uint64_t seg = row_seg[q];
     const uint32_t n = (uint32_t)(seg & 0xFFFFFF);
     if (n == 0) return;
@@ -391,7 +461,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // sentinels past the end: no A value is below them
     if (threadIdx.x < kRankProbeMax) {
         Bs[lb + threadIdx.x] = ~0ULL;
-        K32[lb + threadIdx.x] = 0xFFFFFFFFu;
+        if (!FPM_RANK_LO32) K32[lb + threadIdx.x] = 0xFFFFFFFFu;
     }
     __syncthreads();
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
@@ -410,7 +480,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
         if (j < lb) {
             const uint32_t k = (uint32_t)(v >> kshift);
-            K32[j] = k;
+            if (!FPM_RANK_LO32) K32[j] = k;   // (LO32: written over Bs once np is known)
             dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
         }
         const uint32_t bj = j < lb ? (uint32_t)(v >> shift) : top + 1;
@@ -436,6 +506,30 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t np = s_keydup ? 0u
                       : maxn <= 2 ? 2u : maxn <= 3 ? 3u : maxn <= 4 ? 4u
                       : maxn <= (uint32_t)kRankProbeMax ? (uint32_t)kRankProbeMax : 0u;
+#if FPM_RANK_LO32
+    const uint32_t lomask = kshift >= 32 ? 0xFFFFFFFFu : (1u << kshift) - 1u;
+    if (np) {
+        // Bs -> (K32, Blo) in place: every thread's values into registers, then written back
+        // as halves (the sentinels: key 0xFFFFFFFF)
+        constexpr int kConv = (CAP + kRankProbeMax + 64 * kRankWaves - 1) / (64 * kRankWaves);
+        uint64_t v[kConv];
+#pragma unroll
+        for (int u = 0; u < kConv; u++) {
+            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
+            v[u] = t < lb + kRankProbeMax ? Bs[t] : 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < kConv; u++) {
+            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
+            if (t < lb + kRankProbeMax) {
+                K32[t] = t < lb ? (uint32_t)(v[u] >> kshift) : 0xFFFFFFFFu;
+                Blo[t] = (uint32_t)v[u] & lomask;
+            }
+        }
+        __syncthreads();
+    }
+#endif
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
@@ -567,7 +661,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             const uint32_t nch = (la + kChunk - 1) / kChunk;
             const uint32_t ngr = (nch + kGroup - 1) / kGroup;
             uint32_t shared_below = 0, cnt = 0;
-            for (uint32_t gi = 0; gi < ngr; gi++) {
+            // a row against itself (sym: the same buffers) shares every value and U(c) = i:
+            // numer = min(la, S), and denom follows from shared = la below
+            const bool self_pair = FPM_RANK_SELF && sym && (uint32_t)(o - pair_row) == q;
+            if (self_pair) {
+                shared_below = la;
+                cnt = la < S ? la : S;
+            }
+            for (uint32_t gi = 0; gi < (self_pair ? 0u : ngr); gi++) {
                 if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
                 const uint32_t g0 = gi * kGroup;
                 const uint32_t u_last = rank_group(probe, g0, la, cur, shared_below, cnt);
@@ -599,9 +700,19 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint16_t *bk_ = Bkt;
     const uint64_t *bs_ = Bs;
     const uint32_t *k_ = K32;
+#if FPM_RANK_LO32
+    const uint32_t *lo_ = Blo;
+#define FPM_RANK_NP(NP_) \
+    run([&](uint64_t a, uint32_t &j) { \
+        if constexpr (NP_ > 0) \
+            return rank_chunk_lo<NP_>(k_, lo_, bk_, shift, kshift, lomask, top, lb, a, j); \
+        else \
+            return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+#else
 #define FPM_RANK_NP(NP_) \
     run([&](uint64_t a, uint32_t &j) { \
         return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+#endif
     switch (np) {
     case 2: FPM_RANK_NP(2); break;
     case 3: FPM_RANK_NP(3); break;
@@ -618,17 +729,17 @@ static hipError_t merge_rows_c(const uint64_t *d_cand, const uint64_t *row_seg, 
                                uint64_t ref_stride, uint32_t n_ref, const uint64_t *d_qry,
                                const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t S,
                                bool sym, C *d_numer, C *d_denom, uint32_t *d_cnum,
-                               uint32_t *d_cden, hipStream_t st)
+                               uint32_t *d_cden, hipStream_t st, uint32_t q_lo)
 {
     const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
     const uint64_t cap = std::max(ref_stride, qry_stride);
     if (cap <= 1024)
-        hipLaunchKernelGGL((rank_rows_kernel<1024, C>), g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
-                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
+        hipLaunchKernelGGL((rank_rows_kernel<1024, C>), g, b, 0, st, d_cand, row_seg, n_qry, q_lo,
+                           d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
                            (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else if (cap <= 2048)
-        hipLaunchKernelGGL((rank_rows_kernel<2048, C>), g, b, 0, st, d_cand, row_seg, n_qry, d_ref,
-                           d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
+        hipLaunchKernelGGL((rank_rows_kernel<2048, C>), g, b, 0, st, d_cand, row_seg, n_qry, q_lo,
+                           d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
                            (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else
         return hipErrorInvalidValue;
@@ -639,16 +750,16 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
                              uint64_t qry_stride, uint32_t S, bool sym, Counts cnt,
-                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st)
+                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st, uint32_t q_lo)
 {
     if (!n_qry) return hipSuccess;
     if (cnt.c16)
         return merge_rows_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
                             d_qry_len, qry_stride, S, sym, (uint16_t *)cnt.numer,
-                            (uint16_t *)cnt.denom, d_cnum, d_cden, st);
+                            (uint16_t *)cnt.denom, d_cnum, d_cden, st, q_lo);
     return merge_rows_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
                         d_qry_len, qry_stride, S, sym, (uint32_t *)cnt.numer,
-                        (uint32_t *)cnt.denom, d_cnum, d_cden, st);
+                        (uint32_t *)cnt.denom, d_cnum, d_cden, st, q_lo);
 }
 
 // ---- FP64 p-value (same algorithm as the oracle restatement)

@@ -649,7 +649,7 @@ __attribute__((amdgpu_waves_per_eu(FPM_PROBE_WPE)))
 #endif
 void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
-    uint32_t n_qry, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
+    uint32_t n_qry, uint32_t q_lo, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
     const uint32_t *__restrict__ dir, const uint32_t *__restrict__ entries,
     uint32_t chunk_refs, const uint32_t *__restrict__ ref_len, uint32_t S, uint32_t sym,
     uint32_t defaults, uint32_t vec_defaults, uint32_t self_set, C *__restrict__ numer,
@@ -666,8 +666,10 @@ void probe_rows_kernel(
     constexpr uint32_t kWin = 1024;
     __shared__ uint64_t w_tab[4][64];
     __shared__ uint8_t w_own[4][kWin];
-    const uint32_t q = xcd_row(blockIdx.x, n_qry);   // XCD-contiguous rows: shared buckets in L2
-    if (q >= n_qry) return;
+    // XCD-contiguous rows (shared buckets in L2) of rows [q_lo, q_lo + n_qry)
+    const uint32_t qr = xcd_row(blockIdx.x, n_qry);
+    if (qr >= n_qry) return;
+    const uint32_t q = q_lo + qr;
     const uint64_t mult = idx_mult(g);
     const uint32_t r0 = blockIdx.y * chunk_refs;
     const uint32_t r1 = min(n_ref, r0 + chunk_refs);
@@ -1098,7 +1100,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
-                             unsigned long long *events, hipStream_t st)
+                             unsigned long long *events, hipStream_t st, uint32_t q_lo)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -1112,7 +1114,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                                   al(cnt.numer) && al(cnt.denom);
 #define FPM_PROBE(C)                                                                            \
     hipLaunchKernelGGL(probe_rows_kernel<C>, dim3(xcd_grid(n_qry), nchunks), dim3(256), lds, st,  \
-                       d_qry, d_qry_len, stride, n_qry, n_ref, hash_bytes, g, dir, entries, cref, \
+                       d_qry, d_qry_len, stride, n_qry, q_lo, n_ref, hash_bytes, g, dir, entries, \
+                       cref,                                                                     \
                        d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
                        (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg, \
                        d_qry_it_len, q_unsorted, events)

@@ -110,6 +110,12 @@ struct fpm_ctx {
     hipEvent_t ev_cmp0 = nullptr, ev_cmp1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
     hipEvent_t ev_prefill = nullptr;       // end of the last fpm_dist_prefill_dev
+    // the candidate compare of row part i on its own stream once the probe of part i is done,
+    // beside the probe of part i + 1 (FPM_RANK_PARTS)
+    static constexpr int kMaxParts = 16;
+    hipStream_t rk = nullptr;
+    hipEvent_t ev_part[kMaxParts] = {};
+    hipEvent_t ev_rk = nullptr;
     uint32_t prefill_rows = 0, prefill_nref = 0;   // the grid rows / columns it wrote
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
@@ -482,6 +488,10 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
     if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
+    if (ctx->rk) (void)hipStreamDestroy(ctx->rk);
+    for (auto &e : ctx->ev_part)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->ev_rk) (void)hipEventDestroy(ctx->ev_rk);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -2315,7 +2325,53 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 if (qs > 0 && qs < n_qry)
                     if (int rc = launch_fill_rows(qs)) return rc;
             }
-            {
+            // FPM_RANK_PARTS=k: the query rows in k parts; the candidate compare of part i runs
+            // on its own stream once the probe of part i is done, beside the probe of part
+            // i + 1 (the probe waits on memory, the rank kernel on LDS).  Sorted rows known
+            // before the probe (no probe-reported sortedness), results per candidate slot.
+            static const int kRankParts = [] {
+                const char *v = getenv("FPM_RANK_PARTS");
+                const int p = v ? atoi(v) : 1;
+                return std::max(1, std::min(p, (int)fpm_ctx::kMaxParts));
+            }();
+            const int parts = rows_merge && !skip_count && fin && !ctx->cmp && !ctx->fill_serial &&
+                                      n_qry >= (uint32_t)kRankParts * 64
+                                  ? kRankParts
+                                  : 1;
+            if (parts > 1) {
+                if (!ctx->rk) {
+                    HIP_TRY(hipStreamCreateWithFlags(&ctx->rk, hipStreamNonBlocking));
+                    for (auto &e : ctx->ev_part)
+                        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rk, hipEventDisableTiming));
+                }
+                void *cres;
+                HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
+                uint32_t *pn = (uint32_t *)cres, *pd = pn + cap;
+                for (int i = 0; i < parts; i++) {
+                    const uint32_t lo = (uint32_t)((uint64_t)n_qry * i / parts);
+                    const uint32_t hi = (uint32_t)((uint64_t)n_qry * (i + 1) / parts);
+                    {
+                        TimedLaunch tl(ctx, FPM_K_PROBE, st);
+                        HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, hi - lo, n_ref,
+                                                  hash_bytes, geom, dir, entries, d_ref_len,
+                                                  sketch_size, sym, !fill_cnt, self_set, cnt,
+                                                  (uint64_t *)cand, n_cand, (uint64_t *)row_seg,
+                                                  p_qry_it, nullptr, nullptr, st, lo));
+                        tl.done();
+                    }
+                    HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
+                    HIP_TRY(hipStreamWaitEvent(ctx->rk, ctx->ev_part[i], 0));
+                    TimedLaunch tl(ctx, FPM_K_COMPARE, ctx->rk);
+                    HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg,
+                                              hi - lo, (const uint64_t *)d_ref, d_ref_len,
+                                              ref_stride, n_ref, (const uint64_t *)d_qry,
+                                              d_qry_len, qry_stride, sketch_size, sym, cnt, pn, pd,
+                                              ctx->rk, lo));
+                    tl.done();
+                }
+                HIP_TRY(hipEventRecord(ctx->ev_rk, ctx->rk));
+            } else {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, dir, entries, d_ref_len, sketch_size, sym,
@@ -2363,7 +2419,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             }
             if (fill_pending && (!cnum || ctx->fill_serial))
                 HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
-            {
+            if (parts > 1) {
+                // the parts' compares ran on ctx->rk (their results in the same slots)
+                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_rk, 0));
+            } else {
                 // FPM_FILL_CUS: the compare on the CUs the fill does not own
                 const bool on_cmp = ctx->cmp && rows_merge && fill_pending && cnum;
                 hipStream_t cs = on_cmp ? ctx->cmp : st;

@@ -181,7 +181,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
-                             unsigned long long *events, hipStream_t st);
+                             unsigned long long *events, hipStream_t st, uint32_t q_lo = 0);
+// (q_lo, n_qry: the query rows [q_lo, q_lo + n_qry) of the grid)
 // (d_qry_it_len non-null: the probed query rows are launch_dedup_rows copies of length
 // d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)
 // (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are
@@ -191,8 +192,9 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              const uint64_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
                              uint32_t n_ref, const uint64_t *d_qry, const uint32_t *d_qry_len,
                              uint64_t qry_stride, uint32_t S, bool sym, Counts cnt,
-                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st);
-// (d_cnum, d_cden non-null: results go to candidate slot c instead of the grid cells)
+                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st, uint32_t q_lo = 0);
+// (d_cnum, d_cden non-null: results go to candidate slot c instead of the grid cells;
+// q_lo, n_qry: the query rows [q_lo, q_lo + n_qry), whose probe has run)
 
 // -fp CFL text: newline index, then one lane per line (fingerprint.hip)
 uint32_t text_blocks(uint64_t len);
