@@ -599,9 +599,15 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, seq_len, np.uint64))
         outs = [{"p": [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]}]
     refsets = {}
-    phase = {"sketch": 0.0, "gather": 0.0, "dist": 0.0}
+    # multi-rank phases: the sketch, the all-gather window (this rank's own block against
+    # itself runs beside it: that job reads only local rows), the jobs after the gather
+    phase = ({"sketch": 0.0, "gather_beside_self_job": 0.0, "dist_after_gather": 0.0}
+             if ws > 1 else {"sketch": 0.0, "gather": 0.0, "dist": 0.0})
 
-    def gather():
+    def gather_start():
+        """The rank's rows and counts into the collective's buffers, then the all-gathers
+        launched asynchronously (RCCL on its own stream, or gloo threads); returns the
+        function that waits for them."""
         if on_dev:
             fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
             fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
@@ -609,21 +615,46 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
             fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
         ctx.synchronize()
-        all_gather_rows(loc_rows, n, ws, group=grp.nccl, bounds=bounds, out=g["rows"])
-        all_gather_rows(loc_cnt, n, ws, group=grp.nccl, bounds=bounds, out=g["cnt"])
-        if on_dev:
-            torch.cuda.synchronize(dev)
-        else:
-            fpmash._check(L.fpm_memcpy_h2d(ctx.h, R, g["rows"].data_ptr(), n * stride * 8))
-            fpmash._check(L.fpm_memcpy_h2d(ctx.h, C_, g["cnt"].data_ptr(), n * 4))
+        fin_rows = all_gather_rows(loc_rows, n, ws, group=grp.nccl, bounds=bounds,
+                                   out=g["rows"], async_op=True)
+        fin_cnt = all_gather_rows(loc_cnt, n, ws, group=grp.nccl, bounds=bounds, out=g["cnt"],
+                                  async_op=True)
 
-    def dist_share():
-        for rs in refsets.values():
-            fpmash._check(L.fpm_refset_reindex(rs, st))
+        def finish():
+            fin_rows()
+            fin_cnt()
+            if on_dev:
+                torch.cuda.synchronize(dev)
+            else:
+                fpmash._check(L.fpm_memcpy_h2d(ctx.h, R, g["rows"].data_ptr(), n * stride * 8))
+                fpmash._check(L.fpm_memcpy_h2d(ctx.h, C_, g["cnt"].data_ptr(), n * 4))
+        return finish
+
+    def gather():
+        gather_start()()
+
+    own = (lo, hi)
+
+    def job_query(j):
+        (ql, qh) = j["qry"]
+        if j["kind"] == "self":
+            # the own block's rows as the sketch left them (the refset's own pointers: the
+            # library's symmetric self path)
+            return (d_rows, d_cnt, Ln + ql * 8, stride, qh - ql)
+        return (R + ql * stride * 8, C_ + ql * 4, Ln + ql * 8, stride, qh - ql)
+
+    def dist_share(which="all"):
+        """which: "self" = the own block's index + its self job (local rows only), "rest" =
+        the other indexes + the mirror jobs (gathered rows), "all" = both."""
+        for key, rs in refsets.items():
+            if which == "all" or (which == "self") == (key == own):
+                fpmash._check(L.fpm_refset_reindex(rs, st))
         for j, o in zip(jobs, outs):
+            if which != "all" and (which == "self") != (j["kind"] == "self"):
+                continue
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
             rs = refsets[(rl, rh)]
-            q = (R + ql * stride * 8, C_ + ql * 4, Ln + ql * 8, stride, qh - ql)
+            q = job_query(j)
             if j["kind"] == "self":
                 fpmash._check(L.fpm_refset_dist_dev(rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
                                                     *[b.ptr for b in o["p"]], st))
@@ -639,10 +670,14 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             ctx.synchronize()
         t1 = time.perf_counter()
         if ws > 1:
-            gather()
+            finish = gather_start()
+            dist_share("self")          # beside the gather: local rows only
+            finish()
+            if timed:
+                ctx.synchronize()
         t2 = time.perf_counter()
         if ws > 1:
-            dist_share()
+            dist_share("rest")
         else:
             fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
                                          d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
@@ -650,9 +685,10 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         if timed:
             ctx.synchronize()
             t3 = time.perf_counter()
-            phase["sketch"] += t1 - t0
-            phase["gather"] += t2 - t1
-            phase["dist"] += t3 - t2
+            ks = list(phase)
+            phase[ks[0]] += t1 - t0
+            phase[ks[1]] += t2 - t1
+            phase[ks[2]] += t3 - t2
     if ws > 1:
         # the indexes live as long as the leg (rebuilt in every step by fpm_refset_reindex)
         job.run(st)
@@ -662,9 +698,13 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             rl, rh = j["ref"]
             if (rl, rh) not in refsets:
                 h = C.c_void_p()
-                fpmash._check(L.fpm_refset_create_dev(ctx.h, R + rl * stride * 8, C_ + rl * 4,
-                                                      Ln + rl * 8, stride, rh - rl, 8, s,
-                                                      C.byref(h)))
+                # the own block's index over the sketch output itself (no gathered copy
+                # needed: its self job runs while the gather is in flight); others over the
+                # gathered rows
+                rp, cp = (d_rows, d_cnt) if (rl, rh) == own else (R + rl * stride * 8,
+                                                                  C_ + rl * 4)
+                fpmash._check(L.fpm_refset_create_dev(ctx.h, rp, cp, Ln + rl * 8, stride,
+                                                      rh - rl, 8, s, C.byref(h)))
                 refsets[(rl, rh)] = h
     for _ in range(warmup):
         run(False)
@@ -1131,6 +1171,8 @@ def main():
     # build (0.15 -> 0.20 ms at 0.6, 0.30 at 1), while the compare beside the rest of the fill
     # drops 0.65 -> 0.48 ms (0.42 alone).  FPM_BENCH_PREFILL=f overrides (0: one call)
     pre_frac = float(os.environ.get("FPM_BENCH_PREFILL", "0.6"))
+    if args.pipeline:
+        pre_frac = 0.0      # --pipeline overlaps whole sketches with dists instead
     n_pre = n if pre_frac >= 1 else min(n, int(n * pre_frac) // 16 * 16)
     prefill = n_pre > 0
 
@@ -1156,7 +1198,7 @@ def main():
     # VALU-bound sketch beside the latency-bound index / probe / rank kernels costs them more
     # than the 0.16 ms it hides
     run_steps = lambda k: [step() for _ in range(k)]   # noqa: E731
-    if args.pipeline and not prefill:
+    if args.pipeline:
         import ctypes as C
         hip = C.CDLL("libamdhip64.so")
         job2 = ctx.sketch_job(P, seqs)

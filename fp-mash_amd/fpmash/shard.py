@@ -14,12 +14,15 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
     return n * rank // world, n * (rank + 1) // world
 
 
-def all_gather_rows(local, n_total: int, world: int, group=None, bounds=None, out=None):
+def all_gather_rows(local, n_total: int, world: int, group=None, bounds=None, out=None,
+                    async_op: bool = False):
     """Concatenate every rank's `local` rows (a [n_local, w] tensor, any dtype) in rank
     order.  Shards may differ in size (`bounds`: each rank's [lo, hi), default
     shard_range): each is padded to the largest before the collective and the padding is
     dropped afterwards.  `out`: a preallocated [n_total, w] tensor to write into (its storage
-    stays put across calls, so device pointers into it stay valid)."""
+    stays put across calls, so device pointers into it stay valid).  async_op: the
+    collective is only launched, and a function is returned that waits for it and returns
+    the rows (work on other streams can run meanwhile)."""
     import torch
     import torch.distributed as dist
 
@@ -30,12 +33,17 @@ def all_gather_rows(local, n_total: int, world: int, group=None, bounds=None, ou
     buf = torch.zeros(shape, dtype=local.dtype, device=local.device)
     buf[: local.shape[0]] = local
     parts = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(parts, buf, group=group)
-    pieces = [parts[r][: hi - lo] for r, (lo, hi) in enumerate(bounds)]
-    if out is None:
-        return torch.cat(pieces, dim=0)
-    torch.cat(pieces, dim=0, out=out)
-    return out
+    work = dist.all_gather(parts, buf, group=group, async_op=async_op)
+
+    def finish():
+        if work is not None:
+            work.wait()
+        pieces = [parts[r][: hi - lo] for r, (lo, hi) in enumerate(bounds)]
+        if out is None:
+            return torch.cat(pieces, dim=0)
+        torch.cat(pieces, dim=0, out=out)
+        return out
+    return finish if async_op else finish()
 
 
 def pair_block_jobs(bounds, rank: int):

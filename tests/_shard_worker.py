@@ -32,6 +32,14 @@ def main():
         cnt[i, 0] = len(h)
     g_rows = all_gather_rows(torch.from_numpy(rows.view(np.int64)), n, world).numpy().view(np.uint64)
     g_cnt = all_gather_rows(torch.from_numpy(cnt), n, world).numpy()[:, 0]
+    # the asynchronous form (bench.c4_leg: the own block's job runs while it is in flight)
+    # into a preallocated tensor, uneven bounds
+    bnd = [shard_range(n, world, r) for r in range(world)]
+    out = torch.empty((n, s), dtype=torch.int64)
+    fin = all_gather_rows(torch.from_numpy(rows.view(np.int64)), n, world, bounds=bnd, out=out,
+                          async_op=True)
+    assert callable(fin)
+    assert fin() is out and np.array_equal(out.numpy().view(np.uint64), g_rows)
     full = oracle.sketch_batch(P, seqs)
     for i, h in enumerate(full):
         assert g_cnt[i] == len(h) and np.array_equal(g_rows[i, :len(h)], h), (rank, i)
