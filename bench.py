@@ -663,8 +663,18 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
                     rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0, *[b.ptr for b in o["p"]],
                     *[b.ptr for b in o["m"]], st))
 
+    # one GPU: the grid's first rows prefilled beside the sketch kernels, as in the C2 step
+    # (FPM_C4_PREFILL = the fraction of the rows; the rest and every row's counts are
+    # written by the dist call's side fill)
+    c4_frac = float(os.environ.get("FPM_C4_PREFILL", "0")) if ws == 1 else 0.0
+    c4_pre = min(n, int(n * c4_frac) // 16 * 16)
+
     def run(timed):
         t0 = time.perf_counter()
+        if c4_pre:
+            p_ = outs[0]["p"]
+            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, c4_pre, 1.0, 1.0, p_[2].ptr,
+                                                 p_[3].ptr, p_[4].ptr, None))
         job.run(st)
         if timed:
             ctx.synchronize()
@@ -679,9 +689,10 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         if ws > 1:
             dist_share("rest")
         else:
-            fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
-                                         d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
-                                         1.0, 1.0, *[b.ptr for b in outs[0]["p"]], st))
+            dist16 = L.fpm_dist_dev16_prefilled if c4_pre else L.fpm_dist_dev16
+            fpmash._check(dist16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                 d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
+                                 1.0, 1.0, *[b.ptr for b in outs[0]["p"]], st))
         if timed:
             ctx.synchronize()
             t3 = time.perf_counter()
@@ -768,6 +779,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
                       f"rows (RCCL) + this rank's block pairs (each unordered pair compared once, "
                       f"grid + transpose written), {ws} GPU(s)",
             "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "prefill_rows": c4_pre,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
             "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,

@@ -978,21 +978,25 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
                 __builtin_nontemporal_store(u32x4{dn[0], dn[1], dn[2], dn[3]}, (u32x4 *)(denom + o));
             }
         }
-        __builtin_nontemporal_store(f64x2{dv[0], dv[1]}, (f64x2 *)(fill.dist + o));
-        __builtin_nontemporal_store(f64x2{dv[2], dv[3]}, (f64x2 *)(fill.dist + o + 2));
-        __builtin_nontemporal_store(f64x2{pv[0], pv[1]}, (f64x2 *)(fill.pval + o));
-        __builtin_nontemporal_store(f64x2{pv[2], pv[3]}, (f64x2 *)(fill.pval + o + 2));
-        if (fill.pass) __builtin_nontemporal_store(pa, (uint32_t *)(fill.pass + o));
+        if (fill.dist) {
+            __builtin_nontemporal_store(f64x2{dv[0], dv[1]}, (f64x2 *)(fill.dist + o));
+            __builtin_nontemporal_store(f64x2{dv[2], dv[3]}, (f64x2 *)(fill.dist + o + 2));
+            __builtin_nontemporal_store(f64x2{pv[0], pv[1]}, (f64x2 *)(fill.pval + o));
+            __builtin_nontemporal_store(f64x2{pv[2], pv[3]}, (f64x2 *)(fill.pval + o + 2));
+            if (fill.pass) __builtin_nontemporal_store(pa, (uint32_t *)(fill.pass + o));
+        }
 #else
         if (numer) {
             store_counts4(numer + o, 0, 0, 0, 0);
             store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
         }
-        *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
-        *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
-        *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
-        *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
-        if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+        if (fill.dist) {     // (null: the counts only, of rows a prefill wrote the rest of)
+            *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
+            *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
+            *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
+            *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
+            if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+        }
 #endif
         continue;
     }
@@ -1007,6 +1011,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
             numer[o] = 0;
             denom[o] = (C)(d < S ? d : S);
         }
+        if (!fill.dist) continue;
         fill.dist[o] = d == 0 ? 0.0 : 1.0;
         fill.pval[o] = ok ? 1.0 : 0.0;
         if (fill.pass) fill.pass[o] = ok && pkeep ? 1 : 0;
@@ -1056,11 +1061,13 @@ __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
         store_counts4(numer + o, 0, 0, 0, 0);
         store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
     }
-    *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
-    *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
-    *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
-    *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
-    if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+    if (fill.dist) {         // (null: the counts only, of rows a prefill wrote the rest of)
+        *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
+        *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
+        *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
+        *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
+        if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
+    }
     if (!STRIDE) break;
     }
 }

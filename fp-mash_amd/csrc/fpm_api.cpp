@@ -2079,13 +2079,16 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     // Measured (same box): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 % (the
     // heavier fill beside the rank kernel costs more than the probe saves), so by grid size.
     const bool want_mir = fin && fin->mir.dist && !self_set;
-    const bool fill_cnt = fin && !fin->prefilled &&
-                          (want_mir ||
-                           (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
     // the side fill of query rows [fill_from, q1): from the current point of `st`
     uint32_t fill_from = fin && fin->prefilled ? std::min(fin->pre_rows, n_qry) : 0;
     // every row prefilled: no fill in this call
     const bool pre_all = fin && fin->prefilled && fill_from == n_qry;
+    // (a partial prefill keeps the counts in the side fill: the prefilled rows then get a
+    // counts-only pass with the rest of the rows)
+    const bool fill_cnt = fin && !pre_all &&
+                          (want_mir ||
+                           (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
+    const uint32_t pre_cnt_rows = fill_cnt ? fill_from : 0;   // prefilled rows lacking counts
     // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
     // start) and submits the fill after later work on `st`
     auto launch_fill_rows = [&](uint32_t q1, bool record_in = true) -> int {
@@ -2108,6 +2111,18 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         if (record_in) HIP_TRY(hipEventRecord(ctx->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
+        if (pre_cnt_rows && q0 == pre_cnt_rows) {
+            // the numer / denom defaults of the prefilled rows [0, q0) (their distance /
+            // p-value / pass are the prefill's)
+            PairFill cf;
+            cf.dist = nullptr;
+            cf.pval = nullptr;
+            cf.pass = nullptr;
+            cf.max_dist = fin->max_dist;
+            cf.max_pvalue = fin->max_pvalue;
+            HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, q0, sketch_size, cnt, cf,
+                                     ctx->aux, true));
+        }
         // which fill: the flattened one runs ~35 % faster alone but slows a rank kernel
         // beside it more (C2, 1e8 cells / 2.3e8 events: rank 0.66 -> 0.70 ms while the fill
         // shrank 0.63 -> 0.57, step +0.03 ms; C4, 2.5e9 cells: 14.1 -> 12.8-13.3 ms, N = 8

@@ -529,14 +529,23 @@ def test_sketch_merge_dev_matches_whole(ctx, oracle, s):
         assert np.array_equal(out.to_array(np.uint64, s)[:n], exp)
 
 
+@pytest.mark.parametrize("fillcnt", [False, True])
 @pytest.mark.parametrize("self_set", [True, False])
 @pytest.mark.parametrize("maxd,maxp", [(-1.0, -1.0), (1.0, 1.0), (0.5, 1.0), (1.0, 1e-10)])
-def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
+def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp, fillcnt):
     """fpm_dist_prefill_dev (side stream, no list read) + fpm_dist_dev16_prefilled give the
     same five outputs as fpm_dist_dev16, empty lists and -d / -v filters included; the
-    counts and p-values also match the oracle."""
+    counts and p-values also match the oracle.  fillcnt: a context whose side fill writes the
+    numer / denom defaults (FPM_FILL_COUNTS=1, the large-grid default): a partial prefill
+    then takes a counts-only pass over its rows."""
     import fpmash
     from fpmash import datagen
+    if fillcnt:
+        os.environ["FPM_FILL_COUNTS"] = "1"
+        try:
+            ctx = fpmash.Context(0)
+        finally:
+            del os.environ["FPM_FILL_COUNTS"]
     P = fpmash.make_params(k=21, s=500)
     seqs = datagen.family_dna(8, 12, 1500, sub_rate=(0.0, 0.08), seed=31)
     seqs += [b"N" * 300, b"", b"ACGT" * 3]          # lists with no k-mer: empty sketches
@@ -591,6 +600,8 @@ def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp):
     assert np.allclose(res[1][3][ok], pv[ok], rtol=1e-12, atol=0)
     for b in bufs:
         b.free()
+    if fillcnt:
+        ctx.close()
 
 
 @pytest.mark.parametrize("mode", ["sorted", "fp", "dense"])
