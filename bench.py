@@ -665,8 +665,10 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
 
     # one GPU: the grid's first rows prefilled beside the sketch kernels, as in the C2 step
     # (FPM_C4_PREFILL = the fraction of the rows; the rest and every row's counts are
-    # written by the dist call's side fill)
-    c4_frac = float(os.environ.get("FPM_C4_PREFILL", "0")) if ws == 1 else 0.0
+    # written by the dist call's side fill).  Same box (profiles/r03/s3/c4_prefill_ab.txt,
+    # ms per step): 0 -> 13.14-13.81, 0.05 -> 12.52-12.66, 0.1 -> 12.47-12.66, 0.15 ->
+    # 12.60-13.58 (the sketch kernels stretch 0.78 -> 0.97-1.6 ms)
+    c4_frac = float(os.environ.get("FPM_C4_PREFILL", "0.1")) if ws == 1 else 0.0
     c4_pre = min(n, int(n * c4_frac) // 16 * 16)
 
     def run(timed):
