@@ -1190,12 +1190,34 @@ def main():
     n_pre = n if pre_frac >= 1 else min(n, int(n * pre_frac) // 16 * 16)
     prefill = n_pre > 0
 
+    # FPM_BENCH_PREFILL_PRIO=low|high (A/B): the prefill on a stream of the lowest / highest
+    # priority of its own (ordered after the previous step by an event) instead of the
+    # context's side stream
+    pre_prio = os.environ.get("FPM_BENCH_PREFILL_PRIO", "") if prefill else ""
+    if pre_prio:
+        import ctypes as C
+        hipl = C.CDLL("libamdhip64.so")
+        least, greatest = C.c_int(), C.c_int()
+        hipl.hipSetDevice(local)
+        hipl.hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest))
+        pre_st, pre_ev = C.c_void_p(), C.c_void_p()
+        if hipl.hipStreamCreateWithPriority(C.byref(pre_st), 1, least.value if pre_prio == "low"
+                                            else greatest.value) != 0 or \
+                hipl.hipEventCreateWithFlags(C.byref(pre_ev), 2) != 0:
+            raise RuntimeError("prefill stream")
+        st_p = C.c_void_p(st)
+
     def step():
         if prefill:
             # the grid's no-shared-hash distance / p-value / pass cells need no list: written
             # on the side stream while the sketches are computed (fpm_dist_prefill_dev)
+            ps = None
+            if pre_prio:
+                hipl.hipEventRecord(pre_ev, st_p)
+                hipl.hipStreamWaitEvent(pre_st, pre_ev, 0)
+                ps = pre_st.value
             fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n_pre, 1.0, 1.0, d_dist.ptr,
-                                                 d_pval.ptr, d_pass.ptr, None))
+                                                 d_pval.ptr, d_pass.ptr, ps))
         job.run(st)
         # compare + distance + p-value + pass (the candidates and empty pairs rewritten after
         # the prefill)
