@@ -1385,6 +1385,12 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
 // compare_grid_img_kernel (per tile): U staged in LDS, the 32 ref lists' values mapped by
 // a fixed-step lower bound, then both images in LDS and the literal walk of 1,024 pairs.
 constexpr int kImgTile = 32;
+#ifndef FPM_IMG_DW
+#define FPM_IMG_DW 0      // 1: the 3-step windows from two aligned dword reads per list (A/B)
+#endif
+#ifndef FPM_IMG_STEPS
+#define FPM_IMG_STEPS 1   // common from i + j - steps, not a per-step count (0: the count, A/B)
+#endif
 #ifndef FPM_IMG_BLK
 #define FPM_IMG_BLK 3     // walk steps per LDS window (4 merged into unaligned ds_read_b64: 27 vs 15 ms on C3)
 #endif
@@ -1659,7 +1665,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     // i* = min(i, la), j* = min(j, lb) the reference's denom (steps + remainders, capped
     // at S: CommandDistance.cpp:376-415) is min(S, i* + j* - common).  Per step: two
     // compares into lane masks, three masked increments, the window shifts.
-    uint32_t i = 0, j = 0, common = 0;
+    uint32_t i = 0, j = 0, common = 0, steps = 0;
 #ifdef FPM_IMG_NOWALK
     const uint32_t Swalk = 0;   // timing experiment: prologue only
 #else
@@ -1668,18 +1674,44 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     for (uint32_t d0 = 0; d0 < Swalk; d0 += BLK) {
         if (!__any((i < la) | (j < lb))) break;
         uint32_t a[BLK], b[BLK];
+        if constexpr (FPM_IMG_DW && BLK == 3) {
+            // the dwords holding positions i, i + 1, i + 2 (rows start dword-aligned, and
+            // Wp >= W + 4 keeps the second dword inside the row): two reads instead of three
+            const uint32_t *Aw = reinterpret_cast<const uint32_t *>(A);
+            const uint32_t *Bw = reinterpret_cast<const uint32_t *>(B);
+            const uint32_t a0 = Aw[i >> 1], a1 = Aw[(i >> 1) + 1];
+            const uint32_t b0 = Bw[j >> 1], b1 = Bw[(j >> 1) + 1];
+            const uint32_t sa = (i & 1) * 16, sb = (j & 1) * 16;
+            const uint32_t la2 = __builtin_amdgcn_alignbit(a1, a0, sa);
+            const uint32_t lb2 = __builtin_amdgcn_alignbit(b1, b0, sb);
+            a[0] = la2 & 0xFFFFu;
+            a[1] = la2 >> 16;
+            a[2] = (a1 >> sa) & 0xFFFFu;
+            b[0] = lb2 & 0xFFFFu;
+            b[1] = lb2 >> 16;
+            b[2] = (b1 >> sb) & 0xFFFFu;
+        } else {
 #pragma unroll
-        for (int u = 0; u < BLK; u++) {
-            a[u] = A[i + u];
-            b[u] = B[j + u];
+            for (int u = 0; u < BLK; u++) {
+                a[u] = A[i + u];
+                b[u] = B[j + u];
+            }
         }
 #pragma unroll
         for (int u = 0; u < BLK; u++) {
             if (d0 + u >= S) break;                    // uniform
+#if FPM_IMG_STEPS
+            // every step advances i, j or both (both exactly on an equal pair), so after n
+            // steps i + j = n + common: no per-step count of the equal pairs
+            const uint64_t ma = __builtin_amdgcn_ballot_w64(a[0] <= b[0]);
+            const uint64_t mb = __builtin_amdgcn_ballot_w64(b[0] <= a[0]);
+            steps++;
+#else
             const uint64_t mlt = __builtin_amdgcn_ballot_w64(a[0] < b[0]);
             const uint64_t mgt = __builtin_amdgcn_ballot_w64(b[0] < a[0]);
             const uint64_t ma = ~mgt, mb = ~mlt, meq = ~(mlt | mgt);
             common = add_mask(common, meq);
+#endif
             i = add_mask(i, ma);
             j = add_mask(j, mb);
 #pragma unroll
@@ -1690,6 +1722,10 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         }
     }
     IMG_STAMP(4);
+#if FPM_IMG_STEPS
+    common = i + j - steps;
+#endif
+    (void)steps;
     const uint32_t is = min(i, la), js = min(j, lb);
     const uint32_t d = min(S, is + js - common);
     const uint64_t o = (uint64_t)q * n_ref + r;
