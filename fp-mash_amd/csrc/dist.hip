@@ -1388,6 +1388,9 @@ constexpr int kImgTile = 32;
 #ifndef FPM_IMG_DW
 #define FPM_IMG_DW 0      // 1: the 3-step windows from two aligned dword reads per list (A/B)
 #endif
+#ifndef FPM_IMG_FULL
+#define FPM_IMG_FULL 1    // no per-block exhaustion test when no pair can end before S (0: A/B)
+#endif
 #ifndef FPM_IMG_STEPS
 #define FPM_IMG_STEPS 1   // common from i + j - steps, not a per-step count (0: the count, A/B)
 #endif
@@ -1671,8 +1674,16 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
 #else
     const uint32_t Swalk = S;
 #endif
+#if FPM_IMG_FULL
+    // both lists of a pair are exhausted after at least max(la, lb) steps (each step advances
+    // each index by at most one): when that is >= S on every lane the walk runs S steps and
+    // the per-block test below never fires (the C3 rows: W = S entries each)
+    const bool full = !__any(max(la, lb) < S);
+#else
+    const bool full = false;
+#endif
     for (uint32_t d0 = 0; d0 < Swalk; d0 += BLK) {
-        if (!__any((i < la) | (j < lb))) break;
+        if (!full && !__any((i < la) | (j < lb))) break;
         uint32_t a[BLK], b[BLK];
         if constexpr (FPM_IMG_DW && BLK == 3) {
             // the dwords holding positions i, i + 1, i + 2 (rows start dword-aligned, and
