@@ -15,6 +15,9 @@
 namespace fpm {
 
 constexpr int kBlock = 256;
+#ifndef FPM_SK_CMP64
+#define FPM_SK_CMP64 1     // canonical compare on 64-bit big-endian words (0: per-dword chain, A/B)
+#endif
 #ifndef FPM_SK_WPE
 #define FPM_SK_WPE 7       // waves per SIMD asked of the tile kernel for P <= 2048
 #endif
@@ -333,12 +336,30 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
                                                                      SR[(f >> 2) + m], f & 3)
                                         : 0u;
                     r[nw - 1] &= tail_mask;
+#if FPM_SK_CMP64
+                    // memcmp order = the big-endian order of the bytes: 64-bit big-endian words
+                    // (dwords past nw are 0 in both), compared most significant first with
+                    // lane masks (3 64-bit compares for k = 21 instead of a per-dword chain)
+                    constexpr int NQ = K ? ((K + 3) / 4 + 1) / 2 : 4;
+                    bool gt = false, eq = true;
+#pragma unroll
+                    for (int q = 0; q < NQ; q++) {
+                        const uint64_t fq = ((uint64_t)__builtin_bswap32(d[2 * q]) << 32) |
+                                            __builtin_bswap32(d[2 * q + 1]);
+                        const uint64_t rq = ((uint64_t)__builtin_bswap32(r[2 * q]) << 32) |
+                                            __builtin_bswap32(r[2 * q + 1]);
+                        gt = gt || (eq && fq > rq);
+                        eq = eq && fq == rq;
+                    }
+                    const int cmp = gt ? 1 : 0;
+#else
                     int cmp = 0;
 #pragma unroll
                     for (int m = 0; m < 8; m++) {
                         uint32_t fbe = __builtin_bswap32(d[m]), rbe = __builtin_bswap32(r[m]);
                         if (cmp == 0 && m < nw) cmp = (fbe > rbe) - (fbe < rbe);
                     }
+#endif
                     if (cmp > 0) {
 #pragma unroll
                         for (int m = 0; m < 8; m++) d[m] = r[m];
