@@ -265,7 +265,8 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
  * lists are (CommandDistance.cpp:404-419, 433-450 at common = 0), so
  * fpm_dist_prefill_dev writes those values (and the -d / -v pass flag at them) to every
  * cell of the n_qry x n_ref grid without reading any list (NULL stream: the context's side
- * stream), and fpm_dist_dev16_prefilled then computes everything else: every cell's counts,
+ * stream, ordered after the work already queued on the context's stream; a caller stream
+ * must itself be ordered after any earlier work on these buffers), and fpm_dist_dev16_prefilled then computes everything else: every cell's counts,
  * the pairs of two empty lists, and the cells of the pairs that share hashes (those rewrites
  * wait for the prefill; the rest of the call does not).  Same results as fpm_dist_dev16.
  * A partial prefill: the last fpm_dist_prefill_dev on the context wrote the first n_pre
