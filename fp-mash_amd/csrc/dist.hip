@@ -1388,6 +1388,9 @@ constexpr int kImgTile = 32;
 #ifndef FPM_IMG_DW
 #define FPM_IMG_DW 0      // 1: the 3-step windows from two aligned dword reads per list (A/B)
 #endif
+#ifndef FPM_IMG_AIL
+#define FPM_IMG_AIL 0     // 1: the 32 ref images interleaved per position in LDS (A/B)
+#endif
 #ifndef FPM_IMG_FULL
 #define FPM_IMG_FULL 1    // no per-block exhaustion test when no pair can end before S (0: A/B)
 #endif
@@ -1637,7 +1640,8 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         const uint32_t y = t + 1024u * k;
         if (y < nv) {
             const uint32_t l = y / W, e = y - l * W;
-            img[l * Wp + e] = (uint16_t)(res[k / 2] >> (16 * (k & 1)));
+            img[FPM_IMG_AIL ? e * kImgTile + l : l * Wp + e] =
+                (uint16_t)(res[k / 2] >> (16 * (k & 1)));
         }
     }
     for (uint32_t y = t; y < nv; y += 1024) {
@@ -1649,7 +1653,10 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         const uint32_t tw = Wp - W;
         for (uint32_t y = t; y < 2 * kImgTile * tw; y += 1024) {
             const uint32_t l = y / tw;
-            img[l * Wp + W + (y - l * tw)] = (uint16_t)(l < (uint32_t)kImgTile ? kInfA : kInfB);
+            if (FPM_IMG_AIL && l < (uint32_t)kImgTile)
+                img[(W + (y - l * tw)) * kImgTile + l] = (uint16_t)kInfA;
+            else
+                img[l * Wp + W + (y - l * tw)] = (uint16_t)(l < (uint32_t)kImgTile ? kInfA : kInfB);
         }
     }
     __syncthreads();
@@ -1658,7 +1665,12 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     const uint32_t r = r0 + (t & (kImgTile - 1)), q = q0 + t / kImgTile;
     if (r >= n_ref || q >= n_qry) return;
     const uint32_t la = ref_len[r], lb = qry_len[q];
-    const uint16_t *A = img + (t & (kImgTile - 1)) * Wp;
+    // ref images: rows of Wp, or (AIL) interleaved: position e of ref l at e * 32 + l, so the
+    // 32 ref rows that lanes read at their own walk positions fall into distinct LDS banks
+    // unless two positions of one 2-row pair collide (a row-major layout spreads them at
+    // random: ~3.7 conflict cycles per read in PMC)
+    const uint16_t *A = FPM_IMG_AIL ? img + (t & (kImgTile - 1)) : img + (t & (kImgTile - 1)) * Wp;
+    constexpr uint32_t kAs = FPM_IMG_AIL ? kImgTile : 1;   // A element stride
     const uint16_t *B = img + (kImgTile + t / kImgTile) * Wp;
     (void)lane;
     // Padded walk: past its first min(len, W) entries each image row holds a sentinel,
@@ -1685,7 +1697,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     for (uint32_t d0 = 0; d0 < Swalk; d0 += BLK) {
         if (!full && !__any((i < la) | (j < lb))) break;
         uint32_t a[BLK], b[BLK];
-        if constexpr (FPM_IMG_DW && BLK == 3) {
+        if constexpr (FPM_IMG_DW && !FPM_IMG_AIL && BLK == 3) {
             // the dwords holding positions i, i + 1, i + 2 (rows start dword-aligned, and
             // Wp >= W + 4 keeps the second dword inside the row): two reads instead of three
             const uint32_t *Aw = reinterpret_cast<const uint32_t *>(A);
@@ -1704,7 +1716,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         } else {
 #pragma unroll
             for (int u = 0; u < BLK; u++) {
-                a[u] = A[i + u];
+                a[u] = A[(i + u) * kAs];
                 b[u] = B[j + u];
             }
         }
