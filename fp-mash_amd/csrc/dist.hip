@@ -1389,7 +1389,7 @@ constexpr int kImgTile = 32;
 #define FPM_IMG_DW 0      // 1: the 3-step windows from two aligned dword reads per list (A/B)
 #endif
 #ifndef FPM_IMG_AIL
-#define FPM_IMG_AIL 0     // 1: the 32 ref images interleaved per position in LDS (A/B)
+#define FPM_IMG_AIL 1     // the 32 ref images interleaved per position in LDS (0: rows, A/B)
 #endif
 #ifndef FPM_IMG_FULL
 #define FPM_IMG_FULL 1    // no per-block exhaustion test when no pair can end before S (0: A/B)
