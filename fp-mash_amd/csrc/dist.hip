@@ -192,7 +192,6 @@ __global__ __launch_bounds__(256) void compare_grid_lds_kernel(
             const bool act = (d0 + u < S) & (i < la) & (j < lb);
             const bool lt = a[0] < b[0], gt = b[0] < a[0];
             const bool adv_a = act & !gt, adv_b = act & !lt;
-            common += (adv_a & adv_b) ? 1u : 0u;
             d += act ? 1u : 0u;
             i += adv_a ? 1u : 0u;
             j += adv_b ? 1u : 0u;
@@ -207,6 +206,9 @@ __global__ __launch_bounds__(256) void compare_grid_lds_kernel(
             }
         }
     }
+    // every active step advanced i, j or both (both exactly on an equal pair): the equal
+    // pairs come from the step count instead of a per-step count
+    common = i + j - d;
     if (d < S) {
         uint64_t dd = (uint64_t)d + (la - i) + (lb - j);
         d = dd > S ? S : (uint32_t)dd;
