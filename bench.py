@@ -1198,11 +1198,11 @@ def main():
         import ctypes as C
         hipl = C.CDLL("libamdhip64.so")
         least, greatest = C.c_int(), C.c_int()
-        hipl.hipSetDevice(local)
-        hipl.hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest))
         pre_st, pre_ev = C.c_void_p(), C.c_void_p()
-        if hipl.hipStreamCreateWithPriority(C.byref(pre_st), 1, least.value if pre_prio == "low"
-                                            else greatest.value) != 0 or \
+        if hipl.hipSetDevice(local) != 0 or \
+                hipl.hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest)) != 0 or \
+                hipl.hipStreamCreateWithPriority(C.byref(pre_st), 1, least.value if pre_prio == "low"
+                                                 else greatest.value) != 0 or \
                 hipl.hipEventCreateWithFlags(C.byref(pre_ev), 2) != 0:
             raise RuntimeError("prefill stream")
         st_p = C.c_void_p(st)
@@ -1213,8 +1213,9 @@ def main():
             # on the side stream while the sketches are computed (fpm_dist_prefill_dev)
             ps = None
             if pre_prio:
-                hipl.hipEventRecord(pre_ev, st_p)
-                hipl.hipStreamWaitEvent(pre_st, pre_ev, 0)
+                if hipl.hipEventRecord(pre_ev, st_p) != 0 or \
+                        hipl.hipStreamWaitEvent(pre_st, pre_ev, 0) != 0:
+                    raise RuntimeError("prefill stream ordering")
                 ps = pre_st.value
             fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n_pre, 1.0, 1.0, d_dist.ptr,
                                                  d_pval.ptr, d_pass.ptr, ps))
