@@ -116,6 +116,12 @@ struct fpm_ctx {
     hipStream_t rk = nullptr;
     hipEvent_t ev_part[kMaxParts] = {};
     hipEvent_t ev_rk = nullptr;
+    // long groups' selections on a side stream beside the next batch of tiles
+    // (fpm_sketch_run, FPM_SEL_OVERLAP)
+    static constexpr int kSelBatches = 4;
+    hipStream_t sel_st = nullptr;
+    hipEvent_t ev_sel[kSelBatches] = {};
+    hipEvent_t ev_sel_done = nullptr;
     uint32_t prefill_rows = 0, prefill_nref = 0;   // the grid rows / columns it wrote
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
@@ -492,6 +498,10 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     for (auto &e : ctx->ev_part)
         if (e) (void)hipEventDestroy(e);
     if (ctx->ev_rk) (void)hipEventDestroy(ctx->ev_rk);
+    if (ctx->sel_st) (void)hipStreamDestroy(ctx->sel_st);
+    for (auto &e : ctx->ev_sel)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->ev_sel_done) (void)hipEventDestroy(ctx->ev_sel_done);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -685,6 +695,9 @@ struct fpm_sketch_job {
     std::vector<uint8_t> fround_small;
     uint32_t n_ssel = 0;                      // sample selections (first n_ssel of d_sel)
     std::vector<uint32_t> ssel_begin, sel_begin;   // d_sel offsets of each level
+    // one level of main selections whose inputs come from the tiles in launch order: the
+    // last tile position (in d_tiles) each selection reads, non-decreasing (else empty)
+    std::vector<uint32_t> sel_ready;
     // fallback merge plans (rows >= n_rows live in d_fb_rows, allocated on first use)
     std::vector<std::array<uint32_t, 3>> fplan, sfplan;
     uint32_t n_fb_rows = 0;
@@ -1051,9 +1064,32 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         !order_by_class(stiles, sby_class, sclass_begin))
         return fail(FPM_EINVAL, "internal: tile exceeds capacity");
 
+    // the main selections' readiness in tile launch order (single level only)
+    std::vector<uint32_t> sel_ready;
+    if (sel_lv.size() == 1 && !sel_lv[0].empty()) {
+        std::vector<uint32_t> pos_of_row(n_rows, 0xFFFFFFFFu);
+        for (size_t t = 0; t < by_class.size(); t++)
+            if (by_class[t].out_row < n_rows) pos_of_row[by_class[t].out_row] = (uint32_t)t;
+        bool ok = true;
+        uint32_t prev = 0;
+        for (const SelDesc &d : sel_lv[0]) {
+            uint32_t last = 0;
+            for (uint32_t i = 0; i < d.n_rows && ok; i++) {
+                const uint32_t pr = pos_of_row[sel_rows[d.row_begin + i]];
+                if (pr == 0xFFFFFFFFu) ok = false;
+                else last = std::max(last, pr);
+            }
+            if (!ok || last < prev) { ok = false; break; }
+            sel_ready.push_back(last);
+            prev = last;
+        }
+        if (!ok) sel_ready.clear();
+    }
+
     auto *job = new fpm_sketch_job();
     job->ctx = ctx;
     job->kp = kp;
+    job->sel_ready.swap(sel_ready);
     job->n_groups = n_groups;
     job->n_rows = n_core;
     job->n_fb_rows = n_rows - n_core;
@@ -1231,8 +1267,54 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
                                         job->kp.s, job->d_thr, st));
     }
-    if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
-    if (job->n_sel) {
+    // FPM_SEL_OVERLAP=1: the main tiles in kSelBatches launches; after each, the selections
+    // of the groups whose tiles are all done start on a side stream beside the next batch
+    static const bool kSelOverlap = [] {
+        const char *v = getenv("FPM_SEL_OVERLAP");
+        return v && atoi(v) != 0;
+    }();
+    const bool overlap = kSelOverlap && job->n_sel && !job->sel_ready.empty() &&
+                         job->sel_ready.size() == job->n_sel && job->n_tiles >= 4096;
+    if (overlap) {
+        if (!ctx->sel_st) {
+            HIP_TRY(hipStreamCreateWithFlags(&ctx->sel_st, hipStreamNonBlocking));
+            for (auto &e : ctx->ev_sel) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_sel_done, hipEventDisableTiming));
+        }
+        const uint32_t nt = (uint32_t)job->n_tiles, sb = job->sel_begin[0];
+        uint32_t next = 0;   // next selection to launch
+        for (int k = 0; k < fpm_ctx::kSelBatches; k++) {
+            const uint32_t t0 = (uint32_t)((uint64_t)nt * k / fpm_ctx::kSelBatches);
+            const uint32_t t1 = (uint32_t)((uint64_t)nt * (k + 1) / fpm_ctx::kSelBatches);
+            for (int c = 0; c < kTileClasses; c++) {
+                const uint32_t b = std::max(job->class_begin[c], t0);
+                const uint32_t e = std::min(job->class_begin[c + 1], t1);
+                if (b >= e) continue;
+                TimedLaunch tl(ctx, FPM_K_SKETCH, st);
+                HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_tiles + b, e - b, job->kp,
+                                            job->d_thr, job->d_rows, job->d_count, st));
+                tl.done();
+            }
+            uint32_t upto = next;
+            while (upto < job->n_sel && job->sel_ready[upto] < t1) upto++;
+            if (upto > next) {
+                HIP_TRY(hipEventRecord(ctx->ev_sel[k], st));
+                HIP_TRY(hipStreamWaitEvent(ctx->sel_st, ctx->ev_sel[k], 0));
+                TimedLaunch tl(ctx, FPM_K_MERGE, ctx->sel_st);
+                HIP_TRY(launch_group_select(job->d_sel + sb + next, upto - next, job->d_sel_rows,
+                                            job->d_rows, job->d_count, job->kp.s, job->d_thr,
+                                            fail_main, ctx->sel_st));
+                tl.done();
+                next = upto;
+            }
+        }
+        if (next != job->n_sel) return fail(FPM_EINVAL, "internal: selection overlap left groups");
+        HIP_TRY(hipEventRecord(ctx->ev_sel_done, ctx->sel_st));
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_sel_done, 0));
+        HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, st));
+    } else if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
+    if (job->n_sel && !overlap) {
         for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
             const uint32_t b = job->sel_begin[l], n = job->sel_begin[l + 1] - b;
             TimedLaunch tl(ctx, FPM_K_MERGE, st);
