@@ -109,11 +109,14 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the one-genome-over-all-GPUs sketch leg (RCCL min-merge)")
     ap.add_argument("--split-bases", type=int, default=1_000_000_000)
-    ap.add_argument("--pipeline", action="store_true",
-                    help="C2 steps overlapped two deep: the next batch's sketch kernels on a "
-                         "second stream beside this batch's dist (double-buffered sketch rows)")
+    ap.add_argument("--no-full-grid", action="store_true",
+                    help="skip the comparison run of the C2 step with the full five-array dist "
+                         "output (fpm_dist_dev16)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
+    ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
+                    help="side file for the full result (per-kernel tables, leg counters, CLI "
+                         "phases); '' = none.  The printed line keeps the headline numbers")
     return ap.parse_args()
 
 
@@ -123,7 +126,8 @@ def parse_args_for_test(**kw):
                            k=21, s=1000, no_cpu_baseline=True, cpu_seconds=8.0,
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
                            no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True,
-                           no_split=True, split_bases=1_000_000_000)
+                           no_split=True, split_bases=1_000_000_000, detail="",
+                           no_full_grid=True)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -366,16 +370,37 @@ def sample_rows(n, m, salt=0):
     return np.sort(rng.choice(n, size=m, replace=False)) if m else np.zeros(0, np.int64)
 
 
-def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
-    """device (numer u16, denom u16, distance, p-value, pass) rows vs the oracle's grid of the
-    same query rows: counts and pass flags exact, distance and p-value within rtol 1e-12
-    (the north-star tolerance)"""
-    nu_o, de_o, di_o, pv_o = (x.reshape(len(rows), n_ref) for x in exp)
+def expanded_rows(outs, n_ref, rows, max_dist=1.0, max_pvalue=1.0):
+    """rows [r] of a device dist grid as the five per-cell arrays [len(rows), n_ref]: either
+    five device buffers (numer u16, denom u16, distance, p-value, pass: the full output) or
+    the compact output (numer u16, denom u16, fpmash.CellList), expanded by
+    fpmash.expand_compact's rule for the cells not listed"""
     nu = fetch_rows(outs[0], np.uint16, n_ref, rows)
     de = fetch_rows(outs[1], np.uint16, n_ref, rows)
-    di = fetch_rows(outs[2], np.float64, n_ref, rows)
-    pv = fetch_rows(outs[3], np.float64, n_ref, rows)
-    pa = fetch_rows(outs[4], np.uint8, n_ref, rows)
+    if len(outs) == 5:
+        return (nu, de, fetch_rows(outs[2], np.float64, n_ref, rows),
+                fetch_rows(outs[3], np.float64, n_ref, rows),
+                fetch_rows(outs[4], np.uint8, n_ref, rows))
+    listed = outs[2].fetch()
+    pos = np.full(int(max(rows)) + 1 if len(rows) else 1, -1, np.int64)
+    pos[np.asarray(rows, np.int64)] = np.arange(len(rows))
+    q = listed["qry"].astype(np.int64)
+    keep = q < len(pos)
+    keep[keep] = pos[q[keep]] >= 0
+    sub = {k: v[keep] for k, v in listed.items()}
+    sub["qry"] = pos[q[keep]].astype(np.uint32)
+    e = fpmash.expand_compact(nu.reshape(-1), de.reshape(-1), sub, n_ref, max_dist, max_pvalue)
+    shp = (len(rows), n_ref)
+    return (nu, de, e["distance"].reshape(shp), e["pvalue"].reshape(shp),
+            e["pass"].reshape(shp).astype(np.uint8))
+
+
+def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
+    """device rows (full or compact output, expanded_rows) vs the oracle's grid of the same
+    query rows: counts and pass flags exact, distance and p-value within rtol 1e-12 (the
+    north-star tolerance)"""
+    nu_o, de_o, di_o, pv_o = (x.reshape(len(rows), n_ref) for x in exp)
+    nu, de, di, pv, pa = expanded_rows(outs, n_ref, rows, max_dist, max_pvalue)
     exp_pass = (di_o <= max_dist) & (pv_o <= max_pvalue)
     counts_ok = bool(np.array_equal(nu, nu_o) and np.array_equal(de, de_o))
     dist_ok = bool(np.allclose(di, di_o, rtol=1e-12, atol=0))
@@ -532,6 +557,15 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
             "counts_equal_dense_walk": same_as_dense, "parity": par}
 
 
+def compact_out(ctx, cells):
+    """device buffers of one grid's compact dist output: u16 numer, u16 denom and the list of
+    the cells with numer > 0 (room for 1/64 of the cells, at least 2^20 entries: the
+    family-structured C2 / C4 grids share hashes in 1 % / 0.2 % of their pairs; an overflow is
+    detected and raised after the run)"""
+    return [fpmash.DeviceBuffer(ctx, cells * 2), fpmash.DeviceBuffer(ctx, cells * 2),
+            fpmash.CellList(ctx, min(cells, max(1 << 20, cells // 64)))]
+
+
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
            steps=3, warmup=1, parity=True):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
@@ -545,10 +579,11 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
          blocks is compared on one rank and written twice (the grid and its transpose:
          sorted sketches give symmetric results), so each rank indexes only its own block
          (plus, for even N, one more block), compares ~n^2 / 2N pairs and writes ~n^2 / N
-         cells: shared-hash counts, distance, FP64 p-value, pass flags, left in HBM (the
-         indexes are rebuilt inside the step).
+         cells, left in HBM in the compact output of SURVEY §8(b)/(d): u16 numer / denom of
+         every cell + distance / FP64 p-value / pass of the cells with numer > 0 (the indexes
+         are rebuilt inside the step).
     With one rank there is no gather and the whole grid is the library's symmetric self
-    path (fpm_dist_dev16 with the queries = the references)."""
+    path (fpm_dist_list_dev with the queries = the references)."""
     import ctypes as C
     from fpmash.shard import all_gather_rows, pair_block_jobs, shard_range
     fams = n // members
@@ -591,13 +626,13 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         for j in jobs:
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
             cells = (rh - rl) * (qh - ql)
-            o = {"p": [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]}
+            o = {"p": compact_out(ctx, cells)}
             if j["kind"] == "mirror":
-                o["m"] = [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]
+                o["m"] = compact_out(ctx, cells)
             outs.append(o)
     else:
         d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, seq_len, np.uint64))
-        outs = [{"p": [fpmash.DeviceBuffer(ctx, n_loc * n * b) for b in (2, 2, 8, 8, 1)]}]
+        outs = [{"p": compact_out(ctx, n_loc * n)}]
     refsets = {}
     # multi-rank phases: the sketch, the all-gather window (this rank's own block against
     # itself runs beside it: that job reads only local rows), the jobs after the gather
@@ -655,28 +690,18 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
             rs = refsets[(rl, rh)]
             q = job_query(j)
+            p_ = o["p"]
             if j["kind"] == "self":
-                fpmash._check(L.fpm_refset_dist_dev(rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
-                                                    *[b.ptr for b in o["p"]], st))
+                fpmash._check(L.fpm_refset_dist_list_dev(rs, *q, s, k, 4.0 ** k, 1.0, 1.0,
+                                                         p_[0].ptr, p_[1].ptr, p_[2].ref, st))
             else:
-                fpmash._check(L.fpm_refset_dist_mirror_dev(
-                    rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0, *[b.ptr for b in o["p"]],
-                    *[b.ptr for b in o["m"]], st))
-
-    # one GPU: the grid's first rows prefilled beside the sketch kernels, as in the C2 step
-    # (FPM_C4_PREFILL = the fraction of the rows; the rest and every row's counts are
-    # written by the dist call's side fill).  Same box (profiles/r03/s3/c4_prefill_ab.txt,
-    # ms per step): 0 -> 13.14-13.81, 0.05 -> 12.52-12.66, 0.1 -> 12.47-12.66, 0.15 ->
-    # 12.60-13.58 (the sketch kernels stretch 0.78 -> 0.97-1.6 ms)
-    c4_frac = float(os.environ.get("FPM_C4_PREFILL", "0.1")) if ws == 1 else 0.0
-    c4_pre = min(n, int(n * c4_frac) // 16 * 16)
+                m_ = o["m"]
+                fpmash._check(L.fpm_refset_dist_mirror_list_dev(
+                    rs, *q, s, k, 4.0 ** k, 1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref,
+                    m_[0].ptr, m_[1].ptr, m_[2].ref, st))
 
     def run(timed):
         t0 = time.perf_counter()
-        if c4_pre:
-            p_ = outs[0]["p"]
-            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, c4_pre, 1.0, 1.0, p_[2].ptr,
-                                                 p_[3].ptr, p_[4].ptr, None))
         job.run(st)
         if timed:
             ctx.synchronize()
@@ -691,10 +716,10 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         if ws > 1:
             dist_share("rest")
         else:
-            dist16 = L.fpm_dist_dev16_prefilled if c4_pre else L.fpm_dist_dev16
-            fpmash._check(dist16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
-                                 d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
-                                 1.0, 1.0, *[b.ptr for b in outs[0]["p"]], st))
+            p_ = outs[0]["p"]
+            fpmash._check(L.fpm_dist_list_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                              d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
+                                              1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref, st))
         if timed:
             ctx.synchronize()
             t3 = time.perf_counter()
@@ -730,6 +755,15 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     el = time.perf_counter() - t0
     grp.barrier()
     el = grp.max(el)
+    listed = 0
+    for o in outs:
+        for key in ("p", "m"):
+            if key in o:
+                c_ = o[key][2].count()
+                if c_ > o[key][2].cap:
+                    raise RuntimeError(f"C4 cell list overflow: {c_} > {o[key][2].cap}")
+                listed += c_
+    listed = grp.sum(listed)
     dst = ctx.last_dist_stats()
     cand = grp.sum(dst["candidates"])
     run(True)                                   # one more step, phase-timed (not in el)
@@ -781,7 +815,8 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
                       f"rows (RCCL) + this rank's block pairs (each unordered pair compared once, "
                       f"grid + transpose written), {ws} GPU(s)",
             "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
-            "prefill_rows": c4_pre,
+            "output": "u16 numer/denom per pair + listed pairs with numer > 0 (SURVEY 8(d))",
+            "listed_pairs_all_ranks": listed,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
             "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
@@ -919,6 +954,8 @@ def cli_leg(args, seqs, cpu=None, check=True):
                                       "text, endl per line (extrapolated from 40 rows)": t_txt,
                                       "combined as": "load + max(compare, text)"}
                 res["speedup_dist"] = cw["dist_s"] / t_dist
+                # the north-star figure: sketch + dist of C2, CPU same work / GPU wall
+                res["speedup_sketch_plus_dist"] = (cw["sketch_s"] + cw["dist_s"]) / (t_sketch + t_dist)
             res["parity"] = {"msh_byte_identical": bool(msh_ok),
                              "dist_text_rows_checked": len(rows), "dist_text_exact": bool(text_ok),
                              "ok": bool(msh_ok and text_ok), "check_s": time.perf_counter() - t_c}
@@ -1150,6 +1187,95 @@ def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, s
     return out
 
 
+MAX_LINE_BYTES = 8192     # the driver parses one JSON line of about this size at most
+
+
+def write_detail(detail, path):
+    """The full result (every leg's counters, per-kernel tables, CLI phases) as a side file;
+    the printed line keeps only the headline numbers.  Returns the path written, or None."""
+    if path == "":
+        return None
+    try:
+        os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(detail, f, indent=1)
+        return os.path.relpath(os.path.abspath(path), ROOT)
+    except OSError:
+        return None
+
+
+def _r(x, nd=4):
+    """a number rounded to nd significant digits (None passes through)"""
+    if x is None or isinstance(x, bool):
+        return x
+    if isinstance(x, int):
+        return x
+    try:
+        return float(f"{float(x):.{nd}g}")
+    except (TypeError, ValueError):
+        return None
+
+
+def _ok(part):
+    return None if not part else bool(part.get("ok"))
+
+
+def compact_line(d, detail_path=None):
+    """The one JSON line bench.py prints: the contract's fields, `roofline`, `cpu_baseline`,
+    parity as booleans and one or two numbers per leg (well under MAX_LINE_BYTES; the
+    detail goes to the side file)."""
+    g = lambda o, *ks: (o or {}).get(ks[0]) if len(ks) == 1 else g((o or {}).get(ks[0]), *ks[1:])  # noqa: E731
+    roof = d.get("roofline") or {}
+    cpu = d.get("cpu_baseline")
+    par = d.get("parity") or {}
+    line = {k: d.get(k) for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup",
+                                  "ms_per_step", "higher_is_better", "scaling", "vs_baseline",
+                                  "dtype", "data")}
+    line["config"] = d.get("config")
+    line["roofline"] = {k: (_r(roof.get(k)) if isinstance(roof.get(k), float) else roof.get(k))
+                        for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
+                                  "avg_launch_ms", "alg_bytes_per_launch", "valu_issue_frac")}
+    if roof.get("wave_state_frac"):
+        line["roofline"]["wave_state_frac"] = {k: _r(v, 3) for k, v in
+                                               roof["wave_state_frac"].items()}
+    line["cpu_baseline"] = None if not cpu else {
+        "value": cpu.get("value"), "unit": cpu.get("unit"), "cores": cpu.get("cores"),
+        "kind": cpu.get("kind"), "sample": cpu.get("sample"), "cpu_model": cpu.get("cpu_model")}
+    line["parity"] = {"c2": _ok(par.get("c2")), "c3_fp": _ok(par.get("c3_fp")),
+                      "c4": _ok(par.get("c4")), "c5": _ok(par.get("c5")),
+                      "split": _ok(par.get("split")), "cli": _ok(par.get("cli")),
+                      "all_ok": par.get("all_ok")}
+    c3, c4, c5 = d.get("c3_fp"), d.get("c4_dist"), d.get("c5_sketch")
+    sp, cli = d.get("split_sketch"), d.get("cli")
+    legs = {
+        "sketch_bases_per_s": _r(g(d, "sketch", "bases_per_s")),
+        "sketch_device_ms": _r(g(d, "sketch", "device_ms_per_step")),
+        "dist_mpairs_per_s": _r(g(d, "dist", "mpairs_per_s")),
+        "dist_device_ms": _r(g(d, "dist", "device_ms_per_step")),
+        "dist_path": g(d, "dist", "path"),
+        "c2_full_grid_ms": _r(g(d, "config", "full_grid_ms_per_step")),
+        "fp_text_lines_per_s": _r(g(d, "fp_text", "lines_per_s_device")),
+        "c3_dist_ms": _r(g(c3, "dist_ms")), "c3_parse_device_ms": _r(g(c3, "parse_device_ms")),
+        "c4_ms_per_step": _r(g(c4, "ms_per_step")), "c4_mpairs_per_s": _r(g(c4, "mpairs_per_s")),
+        "c4_output": g(c4, "output"),
+        "c5_ms_per_step": _r(g(c5, "ms_per_step")), "c5_bases_per_s": _r(g(c5, "bases_per_s")),
+        "split_ms_per_step": _r(g(sp, "ms_per_step")),
+        "cli_sketch_wall_s": _r(g(cli, "cli_sketch_wall_s")),
+        "cli_dist_wall_s": _r(g(cli, "cli_dist_wall_s")),
+        "cli_speedup_sketch": _r(g(cli, "speedup_sketch"), 3),
+        "cli_speedup_dist": _r(g(cli, "speedup_dist"), 3),
+        "cli_speedup_sketch_plus_dist": _r(g(cli, "speedup_sketch_plus_dist"), 3),
+    }
+    line["legs"] = {k: v for k, v in legs.items() if v is not None}
+    line["detail"] = detail_path
+    s = json.dumps(line)
+    if len(s) > MAX_LINE_BYTES:                 # never let the line outgrow the parser
+        line["cpu_baseline"] = line["cpu_baseline"] and {
+            k: v for k, v in line["cpu_baseline"].items() if k != "sample"}
+        line["legs"] = {k: v for k, v in line["legs"].items() if isinstance(v, (int, float))}
+    return line
+
+
 def main():
     args = parse()
     ws, rank, local = dist_env()
@@ -1165,117 +1291,28 @@ def main():
     d_rows, d_cnt, ng, stride = job.device_output()
     L = fpmash.lib()
     n_pairs = n * n
-    # u16 numer / denom cells (fpm_dist_dev16: counts <= s = 1000)
+    # The dist output: u16 numer / denom for every cell (4 B per pair) +
+    # the list of cells that share hashes (numer > 0) with distance / FP64 p-value / pass
+    # (fpm_dist_list_dev).  Every other cell's distance / p-value / pass is closed-form
+    # (CommandDistance.cpp:404-408, 435-437 at common = 0); the parity check expands sampled
+    # rows to all five values.  Family-structured C2: ~1 % of the pairs share hashes.
     d_numer = fpmash.DeviceBuffer(ctx, n_pairs * 2)
     d_denom = fpmash.DeviceBuffer(ctx, n_pairs * 2)
-    d_dist = fpmash.DeviceBuffer(ctx, n_pairs * 8)
-    d_pval = fpmash.DeviceBuffer(ctx, n_pairs * 8)
-    d_pass = fpmash.DeviceBuffer(ctx, n_pairs)
+    cells = fpmash.CellList(ctx, max(1 << 20, n_pairs // 25))
     lengths = np.full(n, args.seq_len, dtype=np.uint64)
     d_len = fpmash.DeviceBuffer.from_array(ctx, lengths)
     st = ctx.stream
 
-    # The grid's no-shared-hash cells (distance 1, p-value 1, pass: no list needed) of the
-    # first f of the query rows are prefilled beside the sketch kernels (fpm_dist_prefill_dev),
-    # the rest by the dist call beside the candidate compare.  Same-box sweep
-    # (profiles/r03/s3/prefill_frac_ab*.txt, ms per step): f = 0 (the whole fill beside the
-    # compare) 1.338-1.359, 0.3 1.314, 0.45 1.295, 0.55 1.290-1.295, 0.6 1.285-1.289,
-    # 0.65 1.282-1.287, 0.75 1.289-1.297, 0.85 1.306-1.310, 1 1.324-1.329: the prefill
-    # stretches the sketch 0.16 -> 0.21 ms and, past the sketch, the latency-bound index
-    # build (0.15 -> 0.20 ms at 0.6, 0.30 at 1), while the compare beside the rest of the fill
-    # drops 0.65 -> 0.48 ms (0.42 alone).  FPM_BENCH_PREFILL=f overrides (0: one call)
-    pre_frac = float(os.environ.get("FPM_BENCH_PREFILL", "0.6"))
-    if args.pipeline:
-        pre_frac = 0.0      # --pipeline overlaps whole sketches with dists instead
-    n_pre = n if pre_frac >= 1 else min(n, int(n * pre_frac) // 16 * 16)
-    prefill = n_pre > 0
-
-    # FPM_BENCH_PREFILL_PRIO=low|high (A/B): the prefill on a stream of the lowest / highest
-    # priority of its own (ordered after the previous step by an event) instead of the
-    # context's side stream
-    pre_prio = os.environ.get("FPM_BENCH_PREFILL_PRIO", "") if prefill else ""
-    if pre_prio:
-        import ctypes as C
-        hipl = C.CDLL("libamdhip64.so")
-        least, greatest = C.c_int(), C.c_int()
-        pre_st, pre_ev = C.c_void_p(), C.c_void_p()
-        if hipl.hipSetDevice(local) != 0 or \
-                hipl.hipDeviceGetStreamPriorityRange(C.byref(least), C.byref(greatest)) != 0 or \
-                hipl.hipStreamCreateWithPriority(C.byref(pre_st), 1, least.value if pre_prio == "low"
-                                                 else greatest.value) != 0 or \
-                hipl.hipEventCreateWithFlags(C.byref(pre_ev), 2) != 0:
-            raise RuntimeError("prefill stream")
-        st_p = C.c_void_p(st)
-
     def step():
-        if prefill:
-            # the grid's no-shared-hash distance / p-value / pass cells need no list: written
-            # on the side stream while the sketches are computed (fpm_dist_prefill_dev)
-            ps = None
-            if pre_prio:
-                if hipl.hipEventRecord(pre_ev, st_p) != 0 or \
-                        hipl.hipStreamWaitEvent(pre_st, pre_ev, 0) != 0:
-                    raise RuntimeError("prefill stream ordering")
-                ps = pre_st.value
-            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, n, n_pre, 1.0, 1.0, d_dist.ptr,
-                                                 d_pval.ptr, d_pass.ptr, ps))
         job.run(st)
-        # compare + distance + p-value + pass (the candidates and empty pairs rewritten after
-        # the prefill)
-        dist16 = L.fpm_dist_dev16_prefilled if prefill else L.fpm_dist_dev16
-        fpmash._check(dist16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows, d_cnt,
-                             d_len.ptr, stride, n, 8, args.s, args.k, 4.0 ** args.k,
-                             1.0, 1.0, d_numer.ptr, d_denom.ptr, d_dist.ptr, d_pval.ptr,
-                             d_pass.ptr, st))
+        fpmash._check(L.fpm_dist_list_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                          d_cnt, d_len.ptr, stride, n, 8, args.s, args.k,
+                                          4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
+                                          cells.ref, st))
 
-    # --pipeline (A/B, off): K steps = K sketches + K dists, overlapped two deep: batch i + 1's
-    # sketch kernels run on a second stream while batch i's dist runs on the context stream
-    # (the sketch rows double-buffered; a buffer is re-sketched only after the dist that read
-    # it).  Measured slower on one MI355X (tools/pipe_ab.sh: 1.389 vs 1.355 ms per step): the
-    # VALU-bound sketch beside the latency-bound index / probe / rank kernels costs them more
-    # than the 0.16 ms it hides
-    run_steps = lambda k: [step() for _ in range(k)]   # noqa: E731
-    if args.pipeline:
-        import ctypes as C
-        hip = C.CDLL("libamdhip64.so")
-        job2 = ctx.sketch_job(P, seqs)
-        d_rows2, d_cnt2, _, _ = job2.device_output()
-        bufs = [(job, d_rows, d_cnt), (job2, d_rows2, d_cnt2)]
-
-        def hip_ok(rc):
-            if rc != 0:
-                raise RuntimeError(f"HIP error {rc}")
-        ss = C.c_void_p()
-        hip_ok(hip.hipSetDevice(local))
-        hip_ok(hip.hipStreamCreateWithFlags(C.byref(ss), 1))   # hipStreamNonBlocking
-        ev_sk = [C.c_void_p(), C.c_void_p()]
-        ev_di = [C.c_void_p(), C.c_void_p()]
-        for e in ev_sk + ev_di:
-            hip_ok(hip.hipEventCreateWithFlags(C.byref(e), 2))  # hipEventDisableTiming
-        stp = C.c_void_p(st)
-
-        def run_steps(k):
-            used = [False, False]
-            if k:
-                bufs[0][0].run(ss.value)
-                hip_ok(hip.hipEventRecord(ev_sk[0], ss))
-            for i in range(k):
-                b = i & 1
-                if i + 1 < k:
-                    nb = 1 - b
-                    if used[nb]:
-                        hip_ok(hip.hipStreamWaitEvent(ss, ev_di[nb], 0))
-                    bufs[nb][0].run(ss.value)
-                    hip_ok(hip.hipEventRecord(ev_sk[nb], ss))
-                hip_ok(hip.hipStreamWaitEvent(stp, ev_sk[b], 0))
-                _, rows, cnts = bufs[b]
-                fpmash._check(L.fpm_dist_dev16(ctx.h, rows, cnts, d_len.ptr, stride, n, rows, cnts,
-                                               d_len.ptr, stride, n, 8, args.s, args.k,
-                                               4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
-                                               d_dist.ptr, d_pval.ptr, d_pass.ptr, st))
-                hip_ok(hip.hipEventRecord(ev_di[b], stp))
-                used[b] = True
-            hip_ok(hip.hipStreamSynchronize(ss))
+    def run_steps(k):
+        for _ in range(k):
+            step()
 
     run_steps(args.warmup)
     ctx.synchronize()
@@ -1287,6 +1324,34 @@ def main():
     t1 = time.perf_counter()
     grp.barrier()
     elapsed = grp.max(t1 - t0)
+    n_listed = cells.count()
+    if n_listed > cells.cap:
+        raise RuntimeError(f"C2 cell list overflow: {n_listed} cells > {cells.cap}")
+
+    # the same step with the full five-array output (fpm_dist_dev16: distance / p-value / pass
+    # written for every cell, 21 B per pair), for comparison with rounds 1-3: not `value`
+    full_ms = None
+    if not args.no_full_grid:
+        d_dist = fpmash.DeviceBuffer(ctx, n_pairs * 8)
+        d_pval = fpmash.DeviceBuffer(ctx, n_pairs * 8)
+        d_pass = fpmash.DeviceBuffer(ctx, n_pairs)
+
+        def full_step():
+            job.run(st)
+            fpmash._check(L.fpm_dist_dev16(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                           d_cnt, d_len.ptr, stride, n, 8, args.s, args.k,
+                                           4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
+                                           d_dist.ptr, d_pval.ptr, d_pass.ptr, st))
+        for _ in range(args.warmup):
+            full_step()
+        ctx.synchronize()
+        t0f = time.perf_counter()
+        for _ in range(args.steps):
+            full_step()
+        ctx.synchronize()
+        full_ms = (time.perf_counter() - t0f) / args.steps * 1e3
+        for b in (d_dist, d_pval, d_pass):
+            b.free()
 
     # per-kernel times: HIP events around every launch, in separate steps after the timed
     # region (the event records add markers between launches, so they stay out of it)
@@ -1304,12 +1369,6 @@ def main():
         tot, cnt = ctx.kernel_time(kid)
         if cnt:
             ktimes[name] = {"total_ms": tot, "launches": cnt, "avg_ms": tot / cnt}
-            if kid == fpmash.K_FILL and prefill and cnt == 2 * n_timed:
-                # the prefill beside the sketch + the rest beside the compare: one step's
-                # grid in two launches, timed (and priced below) per step
-                ktimes[name]["avg_ms"] = tot / n_timed
-                ktimes[name]["launches_per_step"] = 2
-                ktimes[name]["prefill_rows"] = n_pre
     ctx.reset_timing()
 
     # sanity: shared-hash counts present (family structure) and no empty sketches
@@ -1318,7 +1377,7 @@ def main():
     numer_sample = d_numer.to_array(np.uint16, min(n_pairs, 1 << 20))
     c2par = None
     if rank == 0 and not args.no_parity:
-        c2par = c2_parity(job, seqs, (d_numer, d_denom, d_dist, d_pval, d_pass), args)
+        c2par = c2_parity(job, seqs, (d_numer, d_denom, cells), args)
 
     bases_rank = n * args.seq_len
     total_bases = grp.sum(bases_rank) * args.steps
@@ -1337,28 +1396,26 @@ def main():
                               "ref + query sketches read once (8 B per hash)"),
     }
     if dstats["sparse"]:
-        # fused sparse dist: the probe writes every cell's final values, the candidate
-        # finalize rewrites the candidate cells (and their mirrors on the symmetric path)
+        # sparse dist, compact output: the probe writes every cell's u16 numer / denom
+        # defaults; the candidate kernel scatters the candidates' counts (and their mirrors on
+        # the symmetric path) and lists the cells with numer > 0
         n_cand = dstats["candidates"]
-        cells = 2 * n_cand - n if dstats["sparse"] == 2 else n_cand
-        alg[N[fpmash.K_FILL]] = (n_pairs * (8 + 8 + 1),
-                                 "distance/p-value/pass (17 B/pair) written")
+        ccells = 2 * n_cand - n if dstats["sparse"] == 2 else n_cand
         alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * (2 + 2),
                                   "query sketch hashes read + u16 numer/denom defaults (4 B/pair) "
                                   "written")
-        alg[N[fpmash.K_FINALIZE]] = (n_cand * (8 + 4 + 4) + cells * (2 + 2 + 8 + 8 + 1),
-                                     "candidate + its numer/denom read, distance/p-value/pass "
-                                     "written per candidate cell (mirrors included)")
+        alg[N[fpmash.K_FINALIZE]] = (n_cand * (8 + 4 + 4) + ccells * (2 + 2) + n_listed * 25,
+                                     "candidate + its counts read, counts scattered per candidate "
+                                     "cell (mirrors included), 25 B per listed cell")
     else:
-        alg[N[fpmash.K_PROBE]] = (n_hash * 8 + n_pairs * 4,
-                                  "query sketch hashes read + u16 numer/denom (4 B/pair) written")
-        alg[N[fpmash.K_FINALIZE]] = (n_pairs * (2 + 2 + 8 + 8 + 1),
-                                     "numer+denom read, distance+p-value+pass written per pair")
+        alg[N[fpmash.K_COMPARE]] = (2 * n_hash * 8 + n_pairs * 4,
+                                    "ref + query sketches read + u16 numer/denom (4 B/pair) written")
+        alg[N[fpmash.K_FINALIZE]] = (n_pairs * (2 + 2) + n_listed * 25,
+                                     "numer/denom read, 25 B per listed cell written")
     traffic = {}
     if os.path.exists(PMC_TRAFFIC):
         traffic = json.load(open(PMC_TRAFFIC)).get("kernels", {})
-    # the dominant kernel: the longest single launch (the fill's per-step time is split over
-    # two launches, prefill beside the sketch + the rest beside the compare: 0.31 ms each)
+    # the dominant kernel: the longest single launch
     dom = max(ktimes, key=lambda k_: ktimes[k_]["total_ms"] / ktimes[k_]["launches"])
     achieved = alg[dom][0] / (ktimes[dom]["avg_ms"] * 1e-3) / 1e9 if dom in alg else None
     roof = {
@@ -1404,8 +1461,9 @@ def main():
     c4 = None
     if not args.no_c4:
         job.free()                       # the C2 batch's buffers make room for C4's grid
-        for b in (d_numer, d_denom, d_dist, d_pval, d_pass):
+        for b in (d_numer, d_denom):
             b.free()
+        cells.free()
         c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
                     parity=not args.no_parity)
 
@@ -1431,7 +1489,7 @@ def main():
         cli = cli_leg(args, seqs, cpu, check=not args.no_parity)
 
     if rank == 0:
-        line = {
+        detail = {
             "metric": METRIC,
             "value": value,
             "unit": "bases/s",
@@ -1446,11 +1504,15 @@ def main():
             "data": "synthetic (family-structured lyn2vec-generate-shaped DNA, seeded per rank)",
             "config": {
                 "workload": (f"C2 step: sketch -i k={args.k} s={args.s} of {n} x {args.seq_len} bp "
-                             f"+ all-vs-all dist of the {n} sketches ({n_pairs:.3g} pairs, "
-                             "u16 numer/denom + distance + FP64 p-value + pass), per GPU"),
+                             f"+ all-vs-all dist of the {n} sketches ({n_pairs:.3g} pairs), per GPU; "
+                             "dist output per SURVEY 8(b)/(d): u16 numer/denom of every pair + "
+                             "distance/FP64 p-value/pass listed for the pairs with numer > 0 "
+                             "(all other pairs: distance 1, p-value 1 by CommandDistance.cpp:"
+                             "404-408, 435-437)"),
                 "n_seqs_per_gpu": n, "seq_len": args.seq_len, "k": args.k, "s": args.s,
                 "pairs_per_gpu": n_pairs, "parallelism": f"independent batch per GPU x{ws}",
-                "prefill_rows": n_pre,   # grid rows filled beside the sketch kernels
+                "listed_pairs_per_gpu": n_listed,
+                "full_grid_ms_per_step": full_ms,   # distance/p-value/pass written for every pair
             },
             "kernel_timing_steps": n_timed,
             "sketch": {"bases_per_s": bases_step / (sk_ms * 1e-3) if sk_ms else None,
@@ -1474,7 +1536,8 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity_summary(c2par, c3, c4, c5, cli, split),
         }
-        print(json.dumps(line))
+        path = write_detail(detail, args.detail)
+        print(json.dumps(compact_line(detail, path)))
     job.free()
     ctx.close()
 

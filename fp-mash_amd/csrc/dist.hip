@@ -29,9 +29,7 @@
 namespace fpm {
 
 constexpr int kTile = 16;   // 16 x 16 pairs per 256-lane workgroup
-#ifndef FPM_WALK_BLK
-#define FPM_WALK_BLK 4
-#endif
+constexpr int kWalkBlk = 4;   // steps per LDS window of the u32 / u64 dense walk
 
 // The literal walk of compareSketches for one pair (CommandDistance.cpp:376-400),
 // with the remainder rule (:402-415).
@@ -259,35 +257,9 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //  * when max(|A|, |B|) >= S, denom is S whatever #shared is, and no A element after the
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
-#ifndef FPM_RANK_WAVES
-#define FPM_RANK_WAVES 4
-#endif
-constexpr int kRankWaves = FPM_RANK_WAVES;
+constexpr int kRankWaves = 4;        // waves per query row (2 and 8 measured slower)
 constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest unrolled probe
-#ifndef FPM_RANK_EXP
-#define FPM_RANK_EXP 0               // measurement builds: 1 = A loads only, 2 = row setup only
-#endif
-#ifndef FPM_RANK_LAYOUT
-#define FPM_RANK_LAYOUT 0            // 1: lane l ranks A[i0 + l], A[i0 + 64 + l] (A/B)
-#endif
-#ifndef FPM_RANK_KEQ
-#define FPM_RANK_KEQ 0               // 1: the 64-bit confirm read only on an equal 32-bit key (A/B)
-#endif
-#ifndef FPM_RANK_LOGB
-#define FPM_RANK_LOGB 12             // log2 buckets for CAP 1024 (CAP 2048: one more)
-#endif
-#ifndef FPM_RANK_LO32
-#define FPM_RANK_LO32 0              // 1: B as 32-bit keys + the 32 bits below them (A/B)
-#endif
-#ifndef FPM_RANK_SELF
-#define FPM_RANK_SELF 0              // 1: the pair (q, q) of a set against itself not probed (A/B)
-#endif
-#ifndef FPM_RANK_LDS_ORDER
-#define FPM_RANK_LDS_ORDER 1         // 1: K32 at LDS offset 0 (ds_read2 offsets fold the probe's q) (A/B)
-#endif
-#ifndef FPM_RANK_LDS_PAD
-#define FPM_RANK_LDS_PAD 0           // bytes of unused LDS per workgroup: fewer workgroups per CU (A/B)
-#endif
+constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one more)
 
 // One chunk of 64 A elements against B (one per lane): j = #{B < a} and the lanes whose a
 // is in B (a wave mask).
@@ -314,35 +286,11 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     if constexpr (NP > 0) {
         const uint32_t ka = (uint32_t)(a >> kshift);
         uint32_t p = lo;
-#if FPM_RANK_KEQ
-        // the 64-bit confirm read only where a's key is one of B's (the keys are distinct and
-        // order B: a key below ka is a value below a, a key above it a value above; only an
-        // equal key leaves a's order and equality to the full values)
-        bool keq = false;
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-            const uint32_t k = K32[lo + q];
-            p += k < ka ? 1u : 0u;
-            keq |= k == ka;
-        }
-        keq = keq && !over;
-        j = p;
-        bool eq = false;
-        if (__builtin_amdgcn_ballot_w64(keq)) {
-            if (keq) {
-                const uint64_t v = Bs[p];
-                j = p + (v < a ? 1u : 0u);
-                eq = v == a;
-            }
-        }
-        return __builtin_amdgcn_ballot_w64(eq);
-#else
 #pragma unroll
         for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
         const uint64_t v = Bs[p];
         j = p + (v < a ? 1u : 0u);
         return __builtin_amdgcn_ballot_w64(v == a) & ~__builtin_amdgcn_ballot_w64(over);
-#endif
     } else {
         uint32_t jj = lo;
         uint64_t eqm = 0;
@@ -357,35 +305,6 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     }
 }
 
-// NP > 0 with B held as (key, low) halves: K32[p] = v >> kshift (distinct, ordering B exactly)
-// and Blo[p] = the kshift bits below the key, so v = K32 << kshift | Blo.  An A value below
-// 2^bits (not `over`) splits the same way; p = lo + #{keys < ka} as in rank_chunk, a key equal
-// to ka can only sit at p (the keys are distinct and ascending), and then the low halves
-// settle the order and the equality: one 32-bit read of Blo[p] instead of the 64-bit Bs[p].
-template <int NP>
-__device__ __forceinline__ uint64_t rank_chunk_lo(const uint32_t *K32, const uint32_t *Blo,
-                                                  const uint16_t *Bkt, uint32_t shift,
-                                                  uint32_t kshift, uint32_t lomask, uint32_t top,
-                                                  uint32_t lb, uint64_t a, uint32_t &j)
-{
-    const uint64_t t = a >> shift;
-    const bool over = t > (uint64_t)top;
-    const uint32_t lo = Bkt[over ? top + 1 : (uint32_t)t];
-    const uint32_t ka = (uint32_t)(a >> kshift), al = (uint32_t)a & lomask;
-    uint32_t p = lo;
-    bool keq = false;
-#pragma unroll
-    for (int q = 0; q < NP; q++) {
-        const uint32_t k = K32[lo + q];
-        p += k < ka ? 1u : 0u;
-        keq |= k == ka;
-    }
-    const uint32_t bl = Blo[p];
-    const bool hit = keq && !over && p < lb;
-    j = p + (hit && bl < al ? 1u : 0u);
-    return __builtin_amdgcn_ballot_w64(hit && bl == al);
-}
-
 template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
@@ -395,23 +314,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     C *__restrict__ numer, C *__restrict__ denom, uint32_t *__restrict__ cnum,
     uint32_t *__restrict__ cden)
 {
-    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? FPM_RANK_LOGB : FPM_RANK_LOGB + 1;
+    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? kRankLogB : kRankLogB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
     // fixed-size LDS arrays: their compile-time offsets fold into the ds_read instructions.
     // (Sizing them by the launch instead — 20.3 KB at s = 1000, 8 workgroups per CU — put a
     // runtime base add on every probe read: the kernel ran 0.645 -> 0.70 ms beside the fill
     // at 6, 7 or 8 workgroups per CU alike, same-box A/B r03o.)
-#if FPM_RANK_LO32
-    // the 64-bit values while the row is set up (and for rows on the NP = 0 loop), then the
-    // same bytes as key / low halves (rank_chunk_lo): 4 KB less LDS per workgroup
-    __shared__ union {
-        uint64_t v[CAP + kRankProbeMax];
-        struct { uint32_t k[CAP + kRankProbeMax], lo[CAP + kRankProbeMax]; } h;
-    } sB;
-    uint64_t *const Bs = sB.v;
-    uint32_t *const K32 = sB.h.k;
-    uint32_t *const Blo = sB.h.lo;
-#elif FPM_RANK_LDS_ORDER
     // one block with the keys first: the NP key reads K32[lo + q] are ds_read2_b32 pairs
     // whose 8-bit dword offsets then hold q (the allocator put K32 after Bs and Bkt, at
     // 16 KB: one address add per key read)
@@ -421,16 +329,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     } sKB;
     uint32_t *const K32 = sKB.k;
     uint64_t *const Bs = sKB.v;
-#else
-    __shared__ uint64_t Bs[CAP + kRankProbeMax];
-    __shared__ uint32_t K32[CAP + kRankProbeMax];      // 32-bit keys of B (rank_chunk)
-#endif
     __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
     __shared__ uint32_t s_maxn, s_keydup;
-#if FPM_RANK_LDS_PAD
-    __shared__ uint32_t s_pad[FPM_RANK_LDS_PAD / 4];
-    if (threadIdx.x == 1023u) s_pad[blockIdx.x % (FPM_RANK_LDS_PAD / 4)] = 0;   // kept, never run
-#endif
     // rows [q_lo, q_lo + n_qry) of the grid (a part of the rows, whose probe ran before)
     const uint32_t qr = xcd_row(blockIdx.x, n_qry);
     if (qr >= n_qry) return;
@@ -463,7 +363,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // sentinels past the end: no A value is below them
     if (threadIdx.x < kRankProbeMax) {
         Bs[lb + threadIdx.x] = ~0ULL;
-        if (!FPM_RANK_LO32) K32[lb + threadIdx.x] = 0xFFFFFFFFu;
+        K32[lb + threadIdx.x] = 0xFFFFFFFFu;
     }
     __syncthreads();
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
@@ -482,7 +382,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
         if (j < lb) {
             const uint32_t k = (uint32_t)(v >> kshift);
-            if (!FPM_RANK_LO32) K32[j] = k;   // (LO32: written over Bs once np is known)
+            K32[j] = k;
             dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
         }
         const uint32_t bj = j < lb ? (uint32_t)(v >> shift) : top + 1;
@@ -500,38 +400,11 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     if (lane == 0 && mx) atomicMax(&s_maxn, mx);
     __syncthreads();
     const uint32_t maxn = s_maxn;
-#if FPM_RANK_EXP == 2
-    if (maxn < 1000000) return;      // measurement: the per-row setup only
-#endif
     // probe width (row-uniform): unrolled reads for buckets of up to 2 / 3 / 4 / 8 values;
     // 0 = the clamped loop (a crowded bucket, or keys that do not order the row)
     const uint32_t np = s_keydup ? 0u
                       : maxn <= 2 ? 2u : maxn <= 3 ? 3u : maxn <= 4 ? 4u
                       : maxn <= (uint32_t)kRankProbeMax ? (uint32_t)kRankProbeMax : 0u;
-#if FPM_RANK_LO32
-    const uint32_t lomask = kshift >= 32 ? 0xFFFFFFFFu : (1u << kshift) - 1u;
-    if (np) {
-        // Bs -> (K32, Blo) in place: every thread's values into registers, then written back
-        // as halves (the sentinels: key 0xFFFFFFFF)
-        constexpr int kConv = (CAP + kRankProbeMax + 64 * kRankWaves - 1) / (64 * kRankWaves);
-        uint64_t v[kConv];
-#pragma unroll
-        for (int u = 0; u < kConv; u++) {
-            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            v[u] = t < lb + kRankProbeMax ? Bs[t] : 0;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < kConv; u++) {
-            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            if (t < lb + kRankProbeMax) {
-                K32[t] = t < lb ? (uint32_t)(v[u] >> kshift) : 0xFFFFFFFFu;
-                Blo[t] = (uint32_t)v[u] & lomask;
-            }
-        }
-        __syncthreads();
-    }
-#endif
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
@@ -541,10 +414,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // Three register groups: `cur` (being ranked), `nxt` (this candidate's next group,
     // issued before `cur` is ranked) and `pf` (the next candidate's first group, issued when
     // a candidate starts); the groups after an early exit are never loaded.
-#ifndef FPM_RANK_GROUP
-#define FPM_RANK_GROUP 1
-#endif
-    constexpr int kGroup = FPM_RANK_GROUP;
+    constexpr int kGroup = 1;      // chunks per load group (2 and 4 measured slower)
     constexpr uint32_t kChunk = 128;
     struct Row { __amdgpu_buffer_rsrc_t rsrc; uint32_t la; uint64_t o; };
     auto open_row = [&](uint64_t o) -> Row {
@@ -565,20 +435,10 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
-#if FPM_RANK_LAYOUT == 1
-            // lane l: A[i0 + l] and A[i0 + 64 + l] (8-B loads; consecutive lanes probe
-            // neighbouring B positions: fewer LDS bank conflicts than pairs per lane)
-            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
-            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
-                                                                 0, 0);
-            dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
-            dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
-#else
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(R.rsrc, (t * kChunk + 2 * lane) * 8u,
                                                                  0, 0);
             dst[u].e0 = ((uint64_t)v[1] << 32) | v[0];
             dst[u].e1 = ((uint64_t)v[3] << 32) | v[2];
-#endif
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -591,32 +451,18 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                           uint32_t &shared_below, uint32_t &cnt) -> uint32_t {
         uint32_t j0[kGroup], j1[kGroup];
         uint64_t m0[kGroup], m1[kGroup];
-#if FPM_RANK_EXP == 1
-        // measurement: loads only (no LDS probes)
-#pragma unroll
-        for (int g = 0; g < kGroup; g++) {
-            m0[g] = __builtin_amdgcn_ballot_w64(cur[g].e0 & 1); j0[g] = (uint32_t)cur[g].e0 & 7;
-            m1[g] = __builtin_amdgcn_ballot_w64(cur[g].e1 & 1); j1[g] = (uint32_t)cur[g].e1 & 7;
-        }
-#else
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
             m0[g] = probe(cur[g].e0, j0[g]);
             m1[g] = probe(cur[g].e1, j1[g]);
         }
-#endif
         uint32_t u_last = 0;
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
             const int rem = (int)la - (int)i0;
-#if FPM_RANK_LAYOUT == 1
-            // lane l holds i0 + l (e0) and i0 + 64 + l (e1)
-            const int r0 = rem, r1 = rem - 64;               // lanes whose e0 / e1 are valid
-#else
             // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
             const int r0 = (rem + 1) >> 1, r1 = rem >> 1;   // lanes whose e0 / e1 are valid
-#endif
             const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
             const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
@@ -624,26 +470,16 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
-#if FPM_RANK_LAYOUT == 1
-            const uint32_t k0 = shared_below + b0;
-            const uint32_t k1 = shared_below + (uint32_t)__popcll(a0) + b1;
-            const uint32_t u0 = i0 + lane + j0[g] - k0, u1 = i0 + 64 + lane + j1[g] - k1;
-#else
             const uint32_t k0 = shared_below + b0 + b1;
             const uint32_t k1 = k0 + (uint32_t)((a0 >> lane) & 1);
             const uint32_t i = i0 + 2 * lane;
             const uint32_t u0 = i + j0[g] - k0, u1 = i + 1 + j1[g] - k1;   // union ranks
-#endif
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
             shared_below += __popcll(a0) + __popcll(a1);
             if (g == kGroup - 1) {
                 const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
-#if FPM_RANK_LAYOUT == 1
-                u_last = (uint32_t)__builtin_amdgcn_readlane((int)(e >= 64 ? u1 : u0), (int)(e & 63));
-#else
                 u_last = (uint32_t)__builtin_amdgcn_readlane((int)((e & 1) ? u1 : u0), (int)(e >> 1));
-#endif
             }
         }
         return u_last;
@@ -663,14 +499,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             const uint32_t nch = (la + kChunk - 1) / kChunk;
             const uint32_t ngr = (nch + kGroup - 1) / kGroup;
             uint32_t shared_below = 0, cnt = 0;
-            // a row against itself (sym: the same buffers) shares every value and U(c) = i:
-            // numer = min(la, S), and denom follows from shared = la below
-            const bool self_pair = FPM_RANK_SELF && sym && (uint32_t)(o - pair_row) == q;
-            if (self_pair) {
-                shared_below = la;
-                cnt = la < S ? la : S;
-            }
-            for (uint32_t gi = 0; gi < (self_pair ? 0u : ngr); gi++) {
+            for (uint32_t gi = 0; gi < ngr; gi++) {
                 if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
                 const uint32_t g0 = gi * kGroup;
                 const uint32_t u_last = rank_group(probe, g0, la, cur, shared_below, cnt);
@@ -702,19 +531,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint16_t *bk_ = Bkt;
     const uint64_t *bs_ = Bs;
     const uint32_t *k_ = K32;
-#if FPM_RANK_LO32
-    const uint32_t *lo_ = Blo;
-#define FPM_RANK_NP(NP_) \
-    run([&](uint64_t a, uint32_t &j) { \
-        if constexpr (NP_ > 0) \
-            return rank_chunk_lo<NP_>(k_, lo_, bk_, shift, kshift, lomask, top, lb, a, j); \
-        else \
-            return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
-#else
 #define FPM_RANK_NP(NP_) \
     run([&](uint64_t a, uint32_t &j) { \
         return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
-#endif
     switch (np) {
     case 2: FPM_RANK_NP(2); break;
     case 3: FPM_RANK_NP(3); break;
@@ -930,9 +749,6 @@ __global__ __launch_bounds__(256) void dist_finalize_kernel(
 // VEC (n_ref % 4 == 0, so a row starts 4-cell aligned): each lane writes 4 consecutive
 // cells with 16-B stores (1 KiB per wave store; the pass bytes as one dword).
 constexpr uint32_t kFillCells = 1024;
-#ifndef FPM_FILL_NT
-#define FPM_FILL_NT 0     // 1: the fill's stores non-temporal (A/B)
-#endif
 template <bool VEC, typename C>
 __global__ __launch_bounds__(256) void dist_fill_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
@@ -943,15 +759,13 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
     const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
     for (uint32_t t = blockIdx.x; t < ntask; t += gridDim.x) {
     const uint32_t q = t / nrb, rb = t - q * nrb;
-    // no lengths (fpm_dist_prefill_dev): every list taken as non-empty (the empty pairs are
-    // fixed up by dist_empty_fixup_kernel once the lengths exist)
-    const uint32_t lq = qry_len ? qry_len[q] : 1u;
+    const uint32_t lq = qry_len[q];
     const uint64_t row = (uint64_t)q * n_ref;
     if (VEC) {
         const uint32_t r = rb * kFillCells + threadIdx.x * 4;
         if (r >= n_ref) continue;
         const uint64_t o = row + r;
-        const uint4 rl = ref_len ? *(const uint4 *)(ref_len + r) : make_uint4(0, 0, 0, 0);
+        const uint4 rl = *(const uint4 *)(ref_len + r);
         const uint32_t d[4] = {rl.x + lq, rl.y + lq, rl.z + lq, rl.w + lq};  // <= 2 stride
         uint32_t dn[4], pa = 0;
         double dv[4], pv[4];
@@ -966,40 +780,17 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         // plain stores: non-temporal ones (nt) let the candidate compare beside run 15%
         // faster but slowed this stream by 20% (step 1.99 -> 2.14 ms); 16-B write-through
         // (sc1) buffer stores slowed it 1.9x (0.9 -> 1.67 ms beside the compare)
-#if FPM_FILL_NT
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        typedef double f64x2 __attribute__((ext_vector_type(2)));
-        if (numer) {
-            if constexpr (sizeof(C) == 2) {
-                __builtin_nontemporal_store(u32x2{0u, 0u}, (u32x2 *)(numer + o));
-                __builtin_nontemporal_store(u32x2{dn[0] | (dn[1] << 16), dn[2] | (dn[3] << 16)},
-                                            (u32x2 *)(denom + o));
-            } else {
-                __builtin_nontemporal_store(u32x4{0u, 0u, 0u, 0u}, (u32x4 *)(numer + o));
-                __builtin_nontemporal_store(u32x4{dn[0], dn[1], dn[2], dn[3]}, (u32x4 *)(denom + o));
-            }
-        }
-        if (fill.dist) {
-            __builtin_nontemporal_store(f64x2{dv[0], dv[1]}, (f64x2 *)(fill.dist + o));
-            __builtin_nontemporal_store(f64x2{dv[2], dv[3]}, (f64x2 *)(fill.dist + o + 2));
-            __builtin_nontemporal_store(f64x2{pv[0], pv[1]}, (f64x2 *)(fill.pval + o));
-            __builtin_nontemporal_store(f64x2{pv[2], pv[3]}, (f64x2 *)(fill.pval + o + 2));
-            if (fill.pass) __builtin_nontemporal_store(pa, (uint32_t *)(fill.pass + o));
-        }
-#else
         if (numer) {
             store_counts4(numer + o, 0, 0, 0, 0);
             store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
         }
-        if (fill.dist) {     // (null: the counts only, of rows a prefill wrote the rest of)
+        if (fill.dist) {     // (null: the counts only, the compact output)
             *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
             *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
             *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
             *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
             if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
         }
-#endif
         continue;
     }
 #pragma unroll
@@ -1007,7 +798,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
         const uint32_t r = rb * kFillCells + u * 256 + threadIdx.x;
         if (r >= n_ref) break;
         const uint64_t o = row + r;
-        const uint32_t d = (ref_len ? ref_len[r] : 0u) + lq;   // both <= stride, no overflow
+        const uint32_t d = ref_len[r] + lq;   // both <= stride, no overflow
         const bool ok = d == 0 || keep1;
         if (numer) {
             numer[o] = 0;
@@ -1027,7 +818,7 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
 // workgroups put every wave store off the 64-B line grid whenever n_ref is not a multiple of
 // 1024, and left a partial workgroup per row: 4.8 -> 6.5 TB/s at n_ref = 10,000, 4.1 -> 5.8 at
 // 21,876, 5.6 -> 6.6 at 50,000 (tools/micro/fill_real.hip, one MI355X).
-template <typename C, bool STRIDE>
+template <typename C>
 __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
     uint64_t cells, double inv_n, uint32_t S, C *__restrict__ numer, C *__restrict__ denom,
@@ -1035,19 +826,16 @@ __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
 {
     const bool keep1 = !(fill.max_dist >= 0 && 1.0 > fill.max_dist);   // distance 0 always kept
     const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
-    // one pass per thread normally (STRIDE = false: the loop below runs once; as a loop the
-    // kernel measured slower beside the sketch kernels); a capped grid (a prefill that holds
-    // only a few wave slots beside them) strides over the rest
-    for (uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4; o < cells;
-         o += (uint64_t)gridDim.x * 1024) {
+    // one pass per thread (a grid-stride loop measured slower)
+    const uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+    if (o >= cells) return;
     uint32_t q = (uint32_t)((double)o * inv_n);
     int64_t rr = (int64_t)(o - (uint64_t)q * n_ref);
     if (rr < 0) { q--; rr += n_ref; }
     else if (rr >= (int64_t)n_ref) { q++; rr -= n_ref; }
     const uint32_t r = (uint32_t)rr;
-    // no lengths (fpm_dist_prefill_dev): every list taken as non-empty
-    const uint32_t lq = qry_len ? qry_len[q] : 1u;
-    const uint4 rl = ref_len ? *(const uint4 *)(ref_len + r) : make_uint4(0, 0, 0, 0);
+    const uint32_t lq = qry_len[q];
+    const uint4 rl = *(const uint4 *)(ref_len + r);
     const uint32_t d[4] = {rl.x + lq, rl.y + lq, rl.z + lq, rl.w + lq};  // <= 2 stride
     uint32_t dn[4], pa = 0;
     double dv[4], pv[4];
@@ -1063,49 +851,18 @@ __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
         store_counts4(numer + o, 0, 0, 0, 0);
         store_counts4(denom + o, dn[0], dn[1], dn[2], dn[3]);
     }
-    if (fill.dist) {         // (null: the counts only, of rows a prefill wrote the rest of)
+    if (fill.dist) {         // (null: the counts only, the compact output)
         *(double2 *)(fill.dist + o) = make_double2(dv[0], dv[1]);
         *(double2 *)(fill.dist + o + 2) = make_double2(dv[2], dv[3]);
         *(double2 *)(fill.pval + o) = make_double2(pv[0], pv[1]);
         *(double2 *)(fill.pval + o + 2) = make_double2(pv[2], pv[3]);
         if (fill.pass) *(uint32_t *)(fill.pass + o) = pa;
     }
-    if (!STRIDE) break;
-    }
-}
-
-// After fpm_dist_prefill_dev (every cell written as a pair of non-empty lists sharing no
-// hash): the pairs of two empty lists get distance 0 (numer == denom == 0), p-value 1 and
-// the -d / -v filter at those values.  One thread per query row; only empty rows loop.
-__global__ __launch_bounds__(256) void dist_empty_fixup_kernel(
-    const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
-    uint32_t n_qry, PairFill fill)
-{
-    const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= n_qry || qry_len[q] != 0) return;
-    const bool pkeep = !(fill.max_pvalue >= 0 && 1.0 > fill.max_pvalue);
-    const uint64_t row = (uint64_t)q * n_ref;
-    for (uint32_t r = 0; r < n_ref; r++)
-        if (ref_len[r] == 0) {
-            fill.dist[row + r] = 0.0;
-            fill.pval[row + r] = 1.0;
-            if (fill.pass) fill.pass[row + r] = pkeep ? 1 : 0;
-        }
-}
-
-hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
-                                   const uint32_t *d_qry_len, uint32_t n_qry,
-                                   const PairFill &fill, hipStream_t st)
-{
-    if (!n_ref || !n_qry) return hipSuccess;
-    hipLaunchKernelGGL(dist_empty_fixup_kernel, dim3((n_qry + 255) / 256), dim3(256), 0, st,
-                       d_ref_len, n_ref, d_qry_len, n_qry, fill);
-    return hipGetLastError();
 }
 
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
-                            hipStream_t st, bool flat, uint32_t grid_cap)
+                            hipStream_t st, bool flat)
 {
     void *d_numer = cnt.numer, *d_denom = cnt.denom;
     if (!n_ref || !n_qry) return hipSuccess;
@@ -1114,34 +871,24 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
     if (blocks >= (1ULL << 31)) return hipErrorInvalidValue;
     // 16-B stores need 16-B aligned rows of every output (the pass row as 4-B aligned)
     const auto al = [](const void *p, uintptr_t a) { return ((uintptr_t)p & (a - 1)) == 0; };
-    const bool vec = n_ref % 4 == 0 && (!d_ref_len || al(d_ref_len, 16)) && al(d_numer, 16) &&
+    // (null outputs are aligned)
+    const bool vec = n_ref % 4 == 0 && al(d_ref_len, 16) && al(d_numer, 16) &&
                      al(d_denom, 16) && al(fill.dist, 16) && al(fill.pval, 16) &&
                      al(fill.pass, 4);
     // the full grid: short workgroups hand their slots back to the candidate compare running
-    // beside; a capped grid-stride fill (256-4096 workgroups) held them and measured slower
-    static const uint64_t kGridCap = [] {
-        const char *v = getenv("FPM_FILL_GRID");   // A/B: cap the grid (grid-stride loop)
-        return v ? strtoull(v, nullptr, 10) : 0ULL;
-    }();
-    const uint32_t grid = (uint32_t)(kGridCap && blocks > kGridCap ? kGridCap : blocks);
+    // beside (a capped grid-stride fill of 256-4096 workgroups held them and measured slower)
+    const uint32_t grid = (uint32_t)blocks;
     const uint64_t cells = (uint64_t)n_ref * n_qry;
-    if (flat && vec && !kGridCap && cells < (1ULL << 50)) {
-        uint64_t fb = (cells / 4 + 255) / 256;
-        if (fb >= (1ULL << 31) && !grid_cap) return hipErrorInvalidValue;
+    if (flat && vec && cells < (1ULL << 50)) {
+        const uint64_t fb = (cells / 4 + 255) / 256;
+        if (fb >= (1ULL << 31)) return hipErrorInvalidValue;
         const double inv_n = 1.0 / (double)n_ref;
-        const bool stride = grid_cap && fb > grid_cap;
-        if (stride) fb = grid_cap;
-#define FPM_FLAT(C_, ST_)                                                                          \
-    hipLaunchKernelGGL((dist_fill_flat_kernel<C_, ST_>), dim3((uint32_t)fb), dim3(256), 0, st,    \
+#define FPM_FLAT(C_)                                                                               \
+    hipLaunchKernelGGL((dist_fill_flat_kernel<C_>), dim3((uint32_t)fb), dim3(256), 0, st,          \
                        d_ref_len, n_ref, d_qry_len, cells, inv_n, S, (C_ *)d_numer, (C_ *)d_denom, \
                        fill)
-        if (cnt.c16) {
-            if (stride) FPM_FLAT(uint16_t, true);
-            else FPM_FLAT(uint16_t, false);
-        } else {
-            if (stride) FPM_FLAT(uint32_t, true);
-            else FPM_FLAT(uint32_t, false);
-        }
+        if (cnt.c16) FPM_FLAT(uint16_t);
+        else FPM_FLAT(uint32_t);
 #undef FPM_FLAT
         return hipGetLastError();
     }
@@ -1258,6 +1005,177 @@ hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long
     return hipGetLastError();
 }
 
+// ---- Compact output: dense numer / denom cells plus a list of the
+// cells that share hashes (numer > 0) with their distance / p-value / pass.  Every other cell
+// has closed-form values (CommandDistance.cpp:404-419, 433-450 at common = 0), so nothing is
+// written for it beyond its counts.
+
+// distance, p-value and -d / -v pass of one cell (finalize_cell's arithmetic, by value)
+__device__ __forceinline__ void cell_values(uint32_t c, uint32_t d, uint64_t len_ref,
+                                            uint64_t len_qry, uint32_t kmer_size,
+                                            double kmer_space, double max_dist, double max_pvalue,
+                                            double &dv, double &pv, bool &ok)
+{
+    if (c == d) dv = 0.0;
+    else if (c == 0) dv = 1.0;
+    else {
+        double jac = (double)c / (double)d;
+        dv = -log(2.0 * jac / (1.0 + jac)) / (double)kmer_size;
+        if (dv > 1.0) dv = 1.0;
+    }
+    ok = !(max_dist >= 0 && dv > max_dist);
+    pv = 0.0;
+    if (ok) {
+        pv = pvalue_dev(c, len_ref, len_qry, kmer_space, d);
+        ok = !(max_pvalue >= 0 && pv > max_pvalue);
+    }
+}
+
+// Append this lane's entry when `want`: one atomic per wave reserves the wave's run of slots
+// (entries past the capacity are counted but not written).  Called by every active lane.
+__device__ __forceinline__ void list_append(const CellList &L, bool want, uint32_t q, uint32_t r,
+                                            double dv, double pv, bool ok)
+{
+    const uint64_t m = __builtin_amdgcn_ballot_w64(want);
+    if (!m) return;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(L.count, (unsigned long long)__popcll(m));
+    base = ((unsigned long long)(uint32_t)__shfl((int)(uint32_t)(base >> 32), (int)leader, 64) << 32) |
+           (uint32_t)__shfl((int)(uint32_t)base, (int)leader, 64);
+    if (!want) return;
+    const uint64_t i = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (i >= L.cap) return;
+    L.qry[i] = q;
+    L.ref[i] = r;
+    L.dist[i] = dv;
+    L.pval[i] = pv;
+    if (L.pass) L.pass[i] = ok ? 1 : 0;
+}
+
+// The candidate cells of the sparse path in compact form: scatter each candidate's
+// (numer, denom) to its cell (and, with `sym`, to its mirror (r, q); with a transposed grid,
+// to that grid's cell), then list the cells whose numer > 0.  cnum == nullptr: the walk kernel
+// wrote the counts in place; they are read from the grid.
+template <typename C>
+__global__ __launch_bounds__(256) void dist_cand_list_kernel(
+    const uint64_t *__restrict__ cand, const unsigned long long *__restrict__ n_cand,
+    uint32_t sym, const uint32_t *__restrict__ cnum, const uint32_t *__restrict__ cden,
+    C *__restrict__ numer, C *__restrict__ denom, const uint64_t *__restrict__ ref_length,
+    const uint64_t *__restrict__ qry_length, uint32_t n_ref, uint32_t kmer_size,
+    double kmer_space, double max_dist, double max_pvalue, CellList L, Counts mcnt,
+    uint32_t m_nqry, CellList ML)
+{
+    const uint64_t n = *n_cand;
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < n;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t o = cand[c];
+        const uint32_t q = (uint32_t)(o / n_ref), r = (uint32_t)(o - (uint64_t)q * n_ref);
+        uint32_t nm, dn;
+        if (cnum) {
+            nm = cnum[c];
+            dn = cden[c];
+            numer[o] = (C)nm;
+            denom[o] = (C)dn;
+        } else {
+            nm = numer[o];
+            dn = denom[o];
+        }
+        const bool mirror_cell = sym && r != q;
+        if (mirror_cell) {
+            const uint64_t o2 = (uint64_t)r * n_ref + q;
+            numer[o2] = (C)nm;
+            denom[o2] = (C)dn;
+        }
+        if (mcnt.numer) {
+            const uint64_t o2 = (uint64_t)r * m_nqry + q;
+            ((C *)mcnt.numer)[o2] = (C)nm;
+            ((C *)mcnt.denom)[o2] = (C)dn;
+        }
+        double dv = 1.0, pv = 1.0;
+        bool ok = false;
+        if (nm > 0)
+            cell_values(nm, dn, ref_length[r], qry_length[q], kmer_size, kmer_space, max_dist,
+                        max_pvalue, dv, pv, ok);
+        // sorted distinct lists: the pair seen from the other side has the same counts, and
+        // distance and p-value are symmetric in the two lengths (pValue's r is)
+        list_append(L, nm > 0, q, r, dv, pv, ok);
+        list_append(L, nm > 0 && mirror_cell, r, q, dv, pv, ok);
+        if (mcnt.numer) list_append(ML, nm > 0, r, q, dv, pv, ok);
+    }
+}
+
+// The dense path in compact form: every cell's counts are in the grid; list those with
+// numer > 0 (4 cells per lane).
+template <typename C>
+__global__ __launch_bounds__(256) void dist_grid_list_kernel(
+    const C *__restrict__ numer, const C *__restrict__ denom, uint32_t n_ref, uint64_t n_pairs,
+    const uint64_t *__restrict__ ref_length, const uint64_t *__restrict__ qry_length,
+    uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue, CellList L)
+{
+    for (uint64_t o0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; o0 < n_pairs;
+         o0 += (uint64_t)gridDim.x * blockDim.x * 4) {
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t o = o0 + u;
+            const uint32_t c = o < n_pairs ? (uint32_t)numer[o] : 0u;
+            double dv = 1.0, pv = 1.0;
+            bool ok = false;
+            uint32_t q = 0, r = 0;
+            if (c > 0) {
+                q = (uint32_t)(o / n_ref);
+                r = (uint32_t)(o - (uint64_t)q * n_ref);
+                cell_values(c, denom[o], ref_length[r], qry_length[q], kmer_size, kmer_space,
+                            max_dist, max_pvalue, dv, pv, ok);
+            }
+            list_append(L, c > 0, q, r, dv, pv, ok);
+        }
+    }
+}
+
+hipError_t launch_dist_cand_list(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                 uint64_t cap, bool sym, const uint32_t *d_cnum,
+                                 const uint32_t *d_cden, Counts cnt, const uint64_t *d_ref_length,
+                                 const uint64_t *d_qry_length, uint32_t n_ref, uint32_t kmer_size,
+                                 double kmer_space, double max_dist, double max_pvalue,
+                                 const CellList &list, Counts mcnt, uint32_t m_nqry,
+                                 const CellList &mlist, hipStream_t st)
+{
+    if (!cap) return hipSuccess;
+    if (mcnt.numer && (!mcnt.denom || mcnt.c16 != cnt.c16 || !d_cnum || !mlist.count))
+        return hipErrorInvalidValue;
+    const uint64_t blocks = std::min<uint64_t>((cap + 255) / 256, 4096);
+#define FPM_CLIST(C)                                                                          \
+    hipLaunchKernelGGL(dist_cand_list_kernel<C>, dim3((uint32_t)blocks), dim3(256), 0, st,      \
+                       d_cand, d_n_cand, (uint32_t)sym, d_cnum, d_cden, (C *)cnt.numer,        \
+                       (C *)cnt.denom, d_ref_length, d_qry_length, n_ref, kmer_size,           \
+                       kmer_space, max_dist, max_pvalue, list, mcnt, m_nqry, mlist)
+    if (cnt.c16) FPM_CLIST(uint16_t);
+    else FPM_CLIST(uint32_t);
+#undef FPM_CLIST
+    return hipGetLastError();
+}
+
+hipError_t launch_dist_grid_list(Counts cnt, uint32_t n_ref, uint32_t n_qry,
+                                 const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+                                 uint32_t kmer_size, double kmer_space, double max_dist,
+                                 double max_pvalue, const CellList &list, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)n_ref * n_qry;
+    if (!n) return hipSuccess;
+    const uint64_t blocks = std::min<uint64_t>((n / 4 + 255) / 256 + 1, 1u << 20);
+#define FPM_GLIST(C)                                                                          \
+    hipLaunchKernelGGL(dist_grid_list_kernel<C>, dim3((uint32_t)blocks), dim3(256), 0, st,      \
+                       (const C *)cnt.numer, (const C *)cnt.denom, n_ref, n, d_ref_length,     \
+                       d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue, list)
+    if (cnt.c16) FPM_GLIST(uint16_t);
+    else FPM_GLIST(uint32_t);
+#undef FPM_GLIST
+    return hipGetLastError();
+}
+
 // triangle -fp's compareFingerprints (CommandTriangle.cpp:255-302): positional compare of
 // two lists over min(len) entries.  The fork reads the hash64 half of a u32 union whose
 // upper bits are uninitialised (:279); here u32 values are zero-extended, so a match is
@@ -1323,7 +1241,7 @@ static hipError_t compare_grid_c(const void *d_ref, const uint32_t *d_ref_len, u
     {
         constexpr size_t kMaxLds = 156 * 1024;
         const uint64_t W = std::min<uint64_t>({(uint64_t)sketch_size, std::max(ref_stride, qry_stride)});
-        constexpr int kBlk = FPM_WALK_BLK;
+        constexpr int kBlk = kWalkBlk;
         const size_t lds = (size_t)2 * kTile * ((W + kBlk + 3) & ~3ull) * hash_bytes;
         if (W > 0 && lds <= kMaxLds && (hash_bytes == 4 || hash_bytes == 8)) {
             const void *fn = hash_bytes == 8 ? (const void *)compare_grid_lds_kernel<uint64_t, kBlk, C>
@@ -1387,21 +1305,7 @@ hipError_t launch_compare_grid(const void *d_ref, const uint32_t *d_ref_len, uin
 // compare_grid_img_kernel (per tile): U staged in LDS, the 32 ref lists' values mapped by
 // a fixed-step lower bound, then both images in LDS and the literal walk of 1,024 pairs.
 constexpr int kImgTile = 32;
-#ifndef FPM_IMG_DW
-#define FPM_IMG_DW 0      // 1: the 3-step windows from two aligned dword reads per list (A/B)
-#endif
-#ifndef FPM_IMG_AIL
-#define FPM_IMG_AIL 1     // the 32 ref images interleaved per position in LDS (0: rows, A/B)
-#endif
-#ifndef FPM_IMG_FULL
-#define FPM_IMG_FULL 1    // no per-block exhaustion test when no pair can end before S (0: A/B)
-#endif
-#ifndef FPM_IMG_STEPS
-#define FPM_IMG_STEPS 1   // common from i + j - steps, not a per-step count (0: the count, A/B)
-#endif
-#ifndef FPM_IMG_BLK
-#define FPM_IMG_BLK 3     // walk steps per LDS window (4 merged into unaligned ds_read_b64: 27 vs 15 ms on C3)
-#endif
+constexpr int kImgBlk3 = 3;   // walk steps per LDS window (4, merged into unaligned ds_read_b64: 27 vs 15 ms on C3)
 constexpr uint32_t kImgMaxW = 1023;          // 2 * 32 * W + 1 < 2^16
 constexpr uint32_t kImgNP = 32768;           // pow2 >= 32 * kImgMaxW
 constexpr uint32_t kInfA = 0xFFFF, kInfB = 0xFFFE;
@@ -1521,22 +1425,6 @@ __host__ __device__ __forceinline__ uint32_t img_row_u16(uint32_t W, uint32_t bl
     return 2 * (((W + blk + 1) / 2) | 1u);
 }
 
-#ifdef FPM_IMG_PHASES
-// timing experiment: per-phase s_memtime deltas of thread 0, summed over workgroups
-__device__ unsigned long long g_img_ph[8];
-#define IMG_STAMP(k)                                                                   \
-    if (t == 0) {                                                                      \
-        const uint64_t now = __builtin_amdgcn_s_memtime();                             \
-        if (k) atomicAdd(&g_img_ph[k - 1], (unsigned long long)(now - ph_last));       \
-        ph_last = now;                                                                 \
-    }
-extern "C" int fpm_debug_img_phases(unsigned long long *out)
-{
-    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_img_ph), sizeof(g_img_ph));
-}
-#else
-#define IMG_STAMP(k)
-#endif
 
 template <int BLK, typename C>
 __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
@@ -1552,13 +1440,9 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     const uint32_t Wp = img_row_u16(W, BLK);
     const uint32_t t = threadIdx.x, r0 = blockIdx.x * kImgTile, qb = blockIdx.y,
                    q0 = qb * kImgTile;
-#ifdef FPM_IMG_PHASES
-    uint64_t ph_last = 0;
-#endif
     const uint32_t us = usize[2 * qb], maxb = usize[2 * qb + 1];
     const uint32_t nv = kImgTile * W;
     uint32_t *dirL = lds32 + kImgNP;
-    IMG_STAMP(0);
     {   // U: every thread's 16-B loads in flight before its LDS stores
         constexpr int kUV = kImgNP / 4096;
         const uint32_t *src = ublk + (uint64_t)qb * kImgBlk;
@@ -1577,7 +1461,6 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         }
     }
     __syncthreads();
-    IMG_STAMP(1);
     uint32_t P = 1;
     while (P <= maxb) P <<= 1;
     // the 32 ref lists' first W values: entry t + 1024 k.  Groups of 8, the next group's
@@ -1635,14 +1518,13 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         okc = okn;
     }
     __syncthreads();
-    IMG_STAMP(2);
     // images: ref lists 0..31, query lists 32..63, rows of Wp u16
 #pragma unroll
     for (int k = 0; k < kPer; k++) {
         const uint32_t y = t + 1024u * k;
         if (y < nv) {
             const uint32_t l = y / W, e = y - l * W;
-            img[FPM_IMG_AIL ? e * kImgTile + l : l * Wp + e] =
+            img[e * kImgTile + l] =
                 (uint16_t)(res[k / 2] >> (16 * (k & 1)));
         }
     }
@@ -1655,24 +1537,23 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
         const uint32_t tw = Wp - W;
         for (uint32_t y = t; y < 2 * kImgTile * tw; y += 1024) {
             const uint32_t l = y / tw;
-            if (FPM_IMG_AIL && l < (uint32_t)kImgTile)
+            if (l < (uint32_t)kImgTile)
                 img[(W + (y - l * tw)) * kImgTile + l] = (uint16_t)kInfA;
             else
                 img[l * Wp + W + (y - l * tw)] = (uint16_t)(l < (uint32_t)kImgTile ? kInfA : kInfB);
         }
     }
     __syncthreads();
-    IMG_STAMP(3);
     const uint32_t lane = t & 63;
     const uint32_t r = r0 + (t & (kImgTile - 1)), q = q0 + t / kImgTile;
     if (r >= n_ref || q >= n_qry) return;
     const uint32_t la = ref_len[r], lb = qry_len[q];
-    // ref images: rows of Wp, or (AIL) interleaved: position e of ref l at e * 32 + l, so the
-    // 32 ref rows that lanes read at their own walk positions fall into distinct LDS banks
-    // unless two positions of one 2-row pair collide (a row-major layout spreads them at
-    // random: ~3.7 conflict cycles per read in PMC)
-    const uint16_t *A = FPM_IMG_AIL ? img + (t & (kImgTile - 1)) : img + (t & (kImgTile - 1)) * Wp;
-    constexpr uint32_t kAs = FPM_IMG_AIL ? kImgTile : 1;   // A element stride
+    // ref images interleaved: position e of ref l at e * 32 + l, so the 32 ref rows that lanes
+    // read at their own walk positions fall into distinct LDS banks unless two positions of
+    // one 2-row pair collide (a row-major layout spreads them at random: ~3.7 conflict cycles
+    // per read in PMC)
+    const uint16_t *A = img + (t & (kImgTile - 1));
+    constexpr uint32_t kAs = kImgTile;   // A element stride
     const uint16_t *B = img + (kImgTile + t / kImgTile) * Wp;
     (void)lane;
     // Padded walk: past its first min(len, W) entries each image row holds a sentinel,
@@ -1683,60 +1564,26 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     // at S: CommandDistance.cpp:376-415) is min(S, i* + j* - common).  Per step: two
     // compares into lane masks, three masked increments, the window shifts.
     uint32_t i = 0, j = 0, common = 0, steps = 0;
-#ifdef FPM_IMG_NOWALK
-    const uint32_t Swalk = 0;   // timing experiment: prologue only
-#else
-    const uint32_t Swalk = S;
-#endif
-#if FPM_IMG_FULL
     // both lists of a pair are exhausted after at least max(la, lb) steps (each step advances
     // each index by at most one): when that is >= S on every lane the walk runs S steps and
     // the per-block test below never fires (the C3 rows: W = S entries each)
     const bool full = !__any(max(la, lb) < S);
-#else
-    const bool full = false;
-#endif
-    for (uint32_t d0 = 0; d0 < Swalk; d0 += BLK) {
+    for (uint32_t d0 = 0; d0 < S; d0 += BLK) {
         if (!full && !__any((i < la) | (j < lb))) break;
         uint32_t a[BLK], b[BLK];
-        if constexpr (FPM_IMG_DW && !FPM_IMG_AIL && BLK == 3) {
-            // the dwords holding positions i, i + 1, i + 2 (rows start dword-aligned, and
-            // Wp >= W + 4 keeps the second dword inside the row): two reads instead of three
-            const uint32_t *Aw = reinterpret_cast<const uint32_t *>(A);
-            const uint32_t *Bw = reinterpret_cast<const uint32_t *>(B);
-            const uint32_t a0 = Aw[i >> 1], a1 = Aw[(i >> 1) + 1];
-            const uint32_t b0 = Bw[j >> 1], b1 = Bw[(j >> 1) + 1];
-            const uint32_t sa = (i & 1) * 16, sb = (j & 1) * 16;
-            const uint32_t la2 = __builtin_amdgcn_alignbit(a1, a0, sa);
-            const uint32_t lb2 = __builtin_amdgcn_alignbit(b1, b0, sb);
-            a[0] = la2 & 0xFFFFu;
-            a[1] = la2 >> 16;
-            a[2] = (a1 >> sa) & 0xFFFFu;
-            b[0] = lb2 & 0xFFFFu;
-            b[1] = lb2 >> 16;
-            b[2] = (b1 >> sb) & 0xFFFFu;
-        } else {
 #pragma unroll
-            for (int u = 0; u < BLK; u++) {
-                a[u] = A[(i + u) * kAs];
-                b[u] = B[j + u];
-            }
+        for (int u = 0; u < BLK; u++) {
+            a[u] = A[(i + u) * kAs];
+            b[u] = B[j + u];
         }
 #pragma unroll
         for (int u = 0; u < BLK; u++) {
             if (d0 + u >= S) break;                    // uniform
-#if FPM_IMG_STEPS
             // every step advances i, j or both (both exactly on an equal pair), so after n
             // steps i + j = n + common: no per-step count of the equal pairs
             const uint64_t ma = __builtin_amdgcn_ballot_w64(a[0] <= b[0]);
             const uint64_t mb = __builtin_amdgcn_ballot_w64(b[0] <= a[0]);
             steps++;
-#else
-            const uint64_t mlt = __builtin_amdgcn_ballot_w64(a[0] < b[0]);
-            const uint64_t mgt = __builtin_amdgcn_ballot_w64(b[0] < a[0]);
-            const uint64_t ma = ~mgt, mb = ~mlt, meq = ~(mlt | mgt);
-            common = add_mask(common, meq);
-#endif
             i = add_mask(i, ma);
             j = add_mask(j, mb);
 #pragma unroll
@@ -1746,11 +1593,7 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
             }
         }
     }
-    IMG_STAMP(4);
-#if FPM_IMG_STEPS
     common = i + j - steps;
-#endif
-    (void)steps;
     const uint32_t is = min(i, la), js = min(j, lb);
     const uint32_t d = min(S, is + js - common);
     const uint64_t o = (uint64_t)q * n_ref + r;
@@ -1783,7 +1626,7 @@ static hipError_t compare_grid_img_c(const uint32_t *ref, const uint32_t *ref_le
                                      uint32_t S, void *ublk_p, void *bimg_p, C *numer, C *denom,
                                      hipStream_t st)
 {
-    constexpr int kBlk = FPM_IMG_BLK;
+    constexpr int kBlk = kImgBlk3;
     const uint32_t W = (uint32_t)std::min<uint64_t>(S, std::max(ref_stride, qry_stride));
     const uint32_t nqb = (n_qry + kImgTile - 1) / kImgTile, nrb = (n_ref + kImgTile - 1) / kImgTile;
     const uint32_t Wimg = (W + 7) & ~7u, Wp = img_row_u16(W, kBlk);

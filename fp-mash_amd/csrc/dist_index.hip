@@ -31,15 +31,10 @@
 
 namespace fpm {
 
-constexpr uint32_t kParts = 1u << kIdxL1;
-#ifndef FPM_PROBE_NT
-#define FPM_PROBE_NT 1   // the probe's default cells with non-temporal stores (0: plain, A/B;
-                         // C2 probe 0.381 -> 0.335 ms: the 0.4 GB of defaults no longer evict
-                         // the posting lists the event loop reads from L2)
-#endif
-#ifndef PROBE_KU
+constexpr uint32_t kParts = 1u << kIdxL1;    // level-1 partitions (top 10 key bits)
+// posting events in flight per lane in the probe (4: 0.307 ms, 12 without the 8-wave cap
+// 0.339 ms, against 0.298-0.301 ms at 8)
 #define PROBE_KU 8
-#endif    // level-1 partitions (top 10 key bits)
 
 __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_bytes, uint64_t idx)
 {
@@ -637,16 +632,10 @@ __global__ void sum64_kernel(unsigned long long *events)
 // a wave scan flattens the 64 buckets into one event range, and the lanes then read
 // consecutive entries of that range (coalesced).  The owner hash of each event comes from
 // a per-wave byte map filled by the lanes for 1024-event windows (one LDS read per event).
-// 8 waves per SIMD (FPM_PROBE_WPE=0 drops the attribute, A/B): the kernel waits on its
+// 8 waves per SIMD (without the attribute: 7): the kernel waits on its
 // event loads most of the time, and at 105 SGPRs the compiler's own allocation left 7
-#ifndef FPM_PROBE_WPE
-#define FPM_PROBE_WPE 8
-#endif
 template <typename C>
-__global__ __launch_bounds__(256)
-#if FPM_PROBE_WPE
-__attribute__((amdgpu_waves_per_eu(FPM_PROBE_WPE)))
-#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8)))
 void probe_rows_kernel(
     const void *__restrict__ qry, const uint32_t *__restrict__ qry_len, uint64_t stride,
     uint32_t n_qry, uint32_t q_lo, uint32_t n_ref, uint32_t hash_bytes, IdxGeom g,
@@ -811,8 +800,9 @@ void probe_rows_kernel(
                 const uint64_t o = pair_row + r;
                 const uint4 rl = *(const uint4 *)(ref_len + r);
                 const uint32_t d0 = rl.x + lq, d1 = rl.y + lq, d2 = rl.z + lq, d3 = rl.w + lq;
-#if FPM_PROBE_NT
-                // non-temporal: the row's defaults are not read again by this kernel
+                // non-temporal: the row's defaults are not read again by this kernel (C2 probe
+                // 0.381 -> 0.335 ms: the 0.4 GB of defaults no longer evict the posting lists
+                // the event loop reads from L2)
                 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
                 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                 if constexpr (sizeof(C) == 2) {
@@ -825,10 +815,6 @@ void probe_rows_kernel(
                     __builtin_nontemporal_store(u32x4{min(d0, S), min(d1, S), min(d2, S), min(d3, S)},
                                                 (u32x4 *)(denom + o));
                 }
-#else
-                store_counts4(numer + o, 0, 0, 0, 0);
-                store_counts4(denom + o, min(d0, S), min(d1, S), min(d2, S), min(d3, S));
-#endif
             }
         } else {
             for (uint32_t r = r0 + threadIdx.x; r < r1; r += 256) {

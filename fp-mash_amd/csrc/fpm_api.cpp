@@ -48,13 +48,8 @@ const char kComplAZ[26] = {'T', 'V', 'G', 'H', 'N', 'N', 'C', 'D', 'N', 'N', 'M'
 // Tile sizing: small records are packed up to kPackKmers k-mer starts per tile,
 // long records are cut into kChunkKmers-start chunks (k-1 bytes of halo).
 constexpr uint32_t kPackKmers = 2048;
-// FPM_CHUNK_KMERS=2048 cuts long records into 2048-start chunks (the P = 2048 tile kernel:
-// 7 waves per SIMD against 4 for P = 4096) -- an A/B switch for the C5 shape
-static const uint32_t kChunkKmers = [] {
-    const char *v = getenv("FPM_CHUNK_KMERS");
-    const uint32_t c = v ? (uint32_t)atoi(v) : 4096u;
-    return (c == 1024 || c == 2048 || c == 4096 || c == 8192) ? c : 4096u;
-}();
+// (2048-start chunks: the tile kernel 1.3 ms faster on C5, the group selection 1.3 ms slower)
+constexpr uint32_t kChunkKmers = 4096;
 
 int tile_class(uint32_t nstarts)
 {
@@ -85,16 +80,6 @@ struct fpm_ctx {
     unsigned long long *dev_counters = nullptr;    // its device-side address
     unsigned long long pub_seq = 0;                // last sequence number published into it
     int dist_mode = FPM_DIST_AUTO;
-    // dense walk of u32 lists on 16-bit rank images (FPM_DENSE_IMG=0 turns it off, A/B)
-    bool dense_img = true;
-    // FPM_FILL_SERIAL=1 runs the sparse dist's fill before the candidate compare instead of
-    // beside it (measurement only: per-kernel times without the overlap)
-    bool fill_serial = false;
-    // FPM_FILL_EARLY=1 (A/B): the fill starts on the side stream with the index build instead
-    // of after the probe
-    bool fill_early = false;
-    bool fill_pre_probe = false;   // FPM_FILL_AT=probe: the side fill starts with the probe
-    double fill_split = 0;         // FPM_FILL_SPLIT=f: that fraction of rows beside the probe
     int fill_counts = -1;      // the side-stream fill also writes the numer / denom defaults
                                // (-1: for grids of >= 2^28 pairs; FPM_FILL_COUNTS=0/1 forces)
     int last_sparse = 0;
@@ -102,27 +87,9 @@ struct fpm_ctx {
     const unsigned long long *last_cand_dev = nullptr;   // the last sparse call's counter
     hipStream_t last_cand_stream = nullptr;
     // side stream for the sparse dist's fill (a pure write stream that runs beside the
-    // latency-bound index build and probe); ev_in / ev_fill order it against `stream`
+    // latency-bound candidate compare); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
-    // FPM_FILL_CUS=n (A/B): the side fill on n CUs of its own (CU-masked aux stream) and the
-    // candidate compare on the others (cmp, the complementary mask)
-    hipStream_t cmp = nullptr;
-    hipEvent_t ev_cmp0 = nullptr, ev_cmp1 = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
-    hipEvent_t ev_prefill = nullptr;       // end of the last fpm_dist_prefill_dev
-    // the candidate compare of row part i on its own stream once the probe of part i is done,
-    // beside the probe of part i + 1 (FPM_RANK_PARTS)
-    static constexpr int kMaxParts = 16;
-    hipStream_t rk = nullptr;
-    hipEvent_t ev_part[kMaxParts] = {};
-    hipEvent_t ev_rk = nullptr;
-    // long groups' selections on a side stream beside the next batch of tiles
-    // (fpm_sketch_run, FPM_SEL_OVERLAP)
-    static constexpr int kSelBatches = 4;
-    hipStream_t sel_st = nullptr;
-    hipEvent_t ev_sel[kSelBatches] = {};
-    hipEvent_t ev_sel_done = nullptr;
-    uint32_t prefill_rows = 0, prefill_nref = 0;   // the grid rows / columns it wrote
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
     static constexpr size_t kRingBytes = 8u << 20;
@@ -275,11 +242,7 @@ static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
 // buffers back with munmap) the kernel driver evicts and restores the process's GPU queues,
 // which stalled whatever ran on the GPU for ~20-30 ms (tools/micro/fp_clock.hip: a ticker
 // wave on its own stream saw a 26 ms gap next to the -fp text fetch into freshly malloc'd
-// arrays).  FPM_PAGEABLE_DIRECT=1 restores the direct copies (A/B).
-static const bool g_pageable_direct = [] {
-    const char *v = getenv("FPM_PAGEABLE_DIRECT");
-    return v && v[0] == '1';
-}();
+// arrays).
 
 static bool host_pinned(const void *p)
 {
@@ -295,7 +258,7 @@ static bool host_pinned(const void *p)
 static hipError_t copy_out(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!bytes) return hipSuccess;
-    if (g_pageable_direct || bytes < (64u << 10) || host_pinned(dst))
+    if (bytes < (64u << 10) || host_pinned(dst))
         return copy_sync(ctx, dst, src, bytes, hipMemcpyDeviceToHost);
     return d2h_staged(ctx, dst, src, bytes);
 }
@@ -304,7 +267,7 @@ static hipError_t copy_out(fpm_ctx *ctx, void *dst, const void *src, size_t byte
 static hipError_t copy_in(fpm_ctx *ctx, void *dst, const void *src, size_t bytes)
 {
     if (!bytes) return hipSuccess;
-    if (g_pageable_direct || host_pinned(src)) return copy_sync(ctx, dst, src, bytes, hipMemcpyHostToDevice);
+    if (host_pinned(src)) return copy_sync(ctx, dst, src, bytes, hipMemcpyHostToDevice);
     return h2d_staged(ctx, dst, src, bytes);
 }
 
@@ -312,30 +275,9 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
 {
     if (ctx->aux) return hipSuccess;
     // default priority: a low-priority side stream (or a high-priority main one) measured
-    // slower, the fill then trails the candidate compare instead of sharing its CUs
-    static const int kFillCus = [] {
-        const char *v = getenv("FPM_FILL_CUS");
-        return v ? atoi(v) : 0;
-    }();
-    hipError_t e = hipSuccess;
-    int ncu = 0;
-    if (kFillCus > 0) e = hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    if (e == hipSuccess && kFillCus > 0 && kFillCus < ncu) {
-        // the fill's CUs spread evenly over the CU index space (over the XCDs / shader arrays)
-        std::vector<uint32_t> m((ncu + 31) / 32, 0), c((ncu + 31) / 32, 0);
-        for (int i = 0; i < kFillCus; i++) {
-            const int b = (int)((int64_t)i * ncu / kFillCus);
-            m[b / 32] |= 1u << (b % 32);
-        }
-        for (int b = 0; b < ncu; b++)
-            if (!(m[b / 32] >> (b % 32) & 1)) c[b / 32] |= 1u << (b % 32);
-        e = hipExtStreamCreateWithCUMask(&ctx->aux, (uint32_t)m.size(), m.data());
-        if (e == hipSuccess) e = hipExtStreamCreateWithCUMask(&ctx->cmp, (uint32_t)c.size(), c.data());
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_cmp0, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_cmp1, hipEventDisableTiming);
-    } else if (e == hipSuccess) {
-        e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
-    }
+    // slower, the fill then trails the candidate compare instead of sharing its CUs; so did
+    // CU-masked streams splitting the CUs between the fill and the compare
+    hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming);
     return e;
@@ -462,12 +404,7 @@ int fpm_ctx_create(int device, fpm_ctx **out)
                                     ", fpmash kernels are built for gfx950 only");
     fpm_ctx *ctx = new fpm_ctx();
     ctx->device = device;
-    if (const char *v = getenv("FPM_DENSE_IMG")) ctx->dense_img = atoi(v) != 0;
-    if (const char *v = getenv("FPM_FILL_SERIAL")) ctx->fill_serial = atoi(v) != 0;
-    if (const char *v = getenv("FPM_FILL_EARLY")) ctx->fill_early = atoi(v) != 0;
     if (const char *v = getenv("FPM_FILL_COUNTS")) ctx->fill_counts = atoi(v) != 0 ? 1 : 0;
-    if (const char *v = getenv("FPM_FILL_AT")) ctx->fill_pre_probe = strcmp(v, "probe") == 0;
-    if (const char *v = getenv("FPM_FILL_SPLIT")) ctx->fill_split = atof(v);
     hipError_t e = hipSetDevice(device);
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -488,20 +425,8 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->host_counters) (void)hipHostFree(ctx->host_counters);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
-    if (ctx->cmp) (void)hipStreamDestroy(ctx->cmp);
-    if (ctx->ev_cmp0) (void)hipEventDestroy(ctx->ev_cmp0);
-    if (ctx->ev_cmp1) (void)hipEventDestroy(ctx->ev_cmp1);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
-    if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
-    if (ctx->rk) (void)hipStreamDestroy(ctx->rk);
-    for (auto &e : ctx->ev_part)
-        if (e) (void)hipEventDestroy(e);
-    if (ctx->ev_rk) (void)hipEventDestroy(ctx->ev_rk);
-    if (ctx->sel_st) (void)hipStreamDestroy(ctx->sel_st);
-    for (auto &e : ctx->ev_sel)
-        if (e) (void)hipEventDestroy(e);
-    if (ctx->ev_sel_done) (void)hipEventDestroy(ctx->ev_sel_done);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -695,9 +620,6 @@ struct fpm_sketch_job {
     std::vector<uint8_t> fround_small;
     uint32_t n_ssel = 0;                      // sample selections (first n_ssel of d_sel)
     std::vector<uint32_t> ssel_begin, sel_begin;   // d_sel offsets of each level
-    // one level of main selections whose inputs come from the tiles in launch order: the
-    // last tile position (in d_tiles) each selection reads, non-decreasing (else empty)
-    std::vector<uint32_t> sel_ready;
     // fallback merge plans (rows >= n_rows live in d_fb_rows, allocated on first use)
     std::vector<std::array<uint32_t, 3>> fplan, sfplan;
     uint32_t n_fb_rows = 0;
@@ -948,17 +870,13 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     for (uint32_t g = 0; g < n_groups; g++)
         if (slot_of[g]) srow[slot_of[g] - 1] = slists[g].size() == 1 ? slists[g][0] : 0;
     // sampled groups select their sketch (and their sample's) with group_select_kernel; their
-    // lists leave the merge plans for fallback plans (FPM_GROUP_SELECT=0: merges only, A/B).
+    // lists leave the merge plans for fallback plans (pairwise merges only: C5 17.6 vs 2.6 ms).
     // A group with more keys than one workgroup should read (~2^19: a 1 Gb genome's sample
     // holds 62 M) is split into chunks of rows selected in parallel, then the chunks' sketches
     // are selected again (a tree of levels, one launch per level).
     std::vector<uint32_t> sel_rows;
     std::vector<std::vector<SelDesc>> ssel_lv, sel_lv;
-    static const bool kSelEnv = [] {
-        const char *v = getenv("FPM_GROUP_SELECT");
-        return !v || atoi(v) != 0;
-    }();
-    const bool use_sel = kSelEnv && (uint64_t)s + s / 8 + 64 <= group_select_cap();
+    const bool use_sel = (uint64_t)s + s / 8 + 64 <= group_select_cap();
     auto build_sel = [&](const std::vector<uint32_t> &rows0, uint32_t final_row, uint32_t slot,
                          std::vector<std::vector<SelDesc>> &lv) {
         constexpr uint64_t kKeysPerWG = 1u << 19;
@@ -1064,32 +982,9 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         !order_by_class(stiles, sby_class, sclass_begin))
         return fail(FPM_EINVAL, "internal: tile exceeds capacity");
 
-    // the main selections' readiness in tile launch order (single level only)
-    std::vector<uint32_t> sel_ready;
-    if (sel_lv.size() == 1 && !sel_lv[0].empty()) {
-        std::vector<uint32_t> pos_of_row(n_rows, 0xFFFFFFFFu);
-        for (size_t t = 0; t < by_class.size(); t++)
-            if (by_class[t].out_row < n_rows) pos_of_row[by_class[t].out_row] = (uint32_t)t;
-        bool ok = true;
-        uint32_t prev = 0;
-        for (const SelDesc &d : sel_lv[0]) {
-            uint32_t last = 0;
-            for (uint32_t i = 0; i < d.n_rows && ok; i++) {
-                const uint32_t pr = pos_of_row[sel_rows[d.row_begin + i]];
-                if (pr == 0xFFFFFFFFu) ok = false;
-                else last = std::max(last, pr);
-            }
-            if (!ok || last < prev) { ok = false; break; }
-            sel_ready.push_back(last);
-            prev = last;
-        }
-        if (!ok) sel_ready.clear();
-    }
-
     auto *job = new fpm_sketch_job();
     job->ctx = ctx;
     job->kp = kp;
-    job->sel_ready.swap(sel_ready);
     job->n_groups = n_groups;
     job->n_rows = n_core;
     job->n_fb_rows = n_rows - n_core;
@@ -1267,54 +1162,10 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
                                         job->kp.s, job->d_thr, st));
     }
-    // FPM_SEL_OVERLAP=1: the main tiles in kSelBatches launches; after each, the selections
-    // of the groups whose tiles are all done start on a side stream beside the next batch
-    static const bool kSelOverlap = [] {
-        const char *v = getenv("FPM_SEL_OVERLAP");
-        return v && atoi(v) != 0;
-    }();
-    const bool overlap = kSelOverlap && job->n_sel && !job->sel_ready.empty() &&
-                         job->sel_ready.size() == job->n_sel && job->n_tiles >= 4096;
-    if (overlap) {
-        if (!ctx->sel_st) {
-            HIP_TRY(hipStreamCreateWithFlags(&ctx->sel_st, hipStreamNonBlocking));
-            for (auto &e : ctx->ev_sel) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_sel_done, hipEventDisableTiming));
-        }
-        const uint32_t nt = (uint32_t)job->n_tiles, sb = job->sel_begin[0];
-        uint32_t next = 0;   // next selection to launch
-        for (int k = 0; k < fpm_ctx::kSelBatches; k++) {
-            const uint32_t t0 = (uint32_t)((uint64_t)nt * k / fpm_ctx::kSelBatches);
-            const uint32_t t1 = (uint32_t)((uint64_t)nt * (k + 1) / fpm_ctx::kSelBatches);
-            for (int c = 0; c < kTileClasses; c++) {
-                const uint32_t b = std::max(job->class_begin[c], t0);
-                const uint32_t e = std::min(job->class_begin[c + 1], t1);
-                if (b >= e) continue;
-                TimedLaunch tl(ctx, FPM_K_SKETCH, st);
-                HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_tiles + b, e - b, job->kp,
-                                            job->d_thr, job->d_rows, job->d_count, st));
-                tl.done();
-            }
-            uint32_t upto = next;
-            while (upto < job->n_sel && job->sel_ready[upto] < t1) upto++;
-            if (upto > next) {
-                HIP_TRY(hipEventRecord(ctx->ev_sel[k], st));
-                HIP_TRY(hipStreamWaitEvent(ctx->sel_st, ctx->ev_sel[k], 0));
-                TimedLaunch tl(ctx, FPM_K_MERGE, ctx->sel_st);
-                HIP_TRY(launch_group_select(job->d_sel + sb + next, upto - next, job->d_sel_rows,
-                                            job->d_rows, job->d_count, job->kp.s, job->d_thr,
-                                            fail_main, ctx->sel_st));
-                tl.done();
-                next = upto;
-            }
-        }
-        if (next != job->n_sel) return fail(FPM_EINVAL, "internal: selection overlap left groups");
-        HIP_TRY(hipEventRecord(ctx->ev_sel_done, ctx->sel_st));
-        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_sel_done, 0));
-        HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),
-                               hipMemcpyDeviceToHost, st));
-    } else if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
-    if (job->n_sel && !overlap) {
+    // (the selections of each batch of genomes on a side stream beside the next batch's
+    // tiles measured a wash on C5: the 120 KB-LDS selection workgroups take the tiles' CUs)
+    if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
+    if (job->n_sel) {
         for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
             const uint32_t b = job->sel_begin[l], n = job->sel_begin[l + 1] - b;
             TimedLaunch tl(ctx, FPM_K_MERGE, st);
@@ -1938,27 +1789,31 @@ extern "C" {
 
 }  // extern "C"
 
-// distance / p-value outputs of fpm_dist_dev, handed to compare_impl so the sparse path
-// can finalize in place: the probe writes every cell's no-shared-hash values and a
-// candidate kernel rewrites the candidates (no dense pass re-reading numer / denom)
+// One grid's outputs: the counts, and either the full per-cell distance / p-value / pass
+// (fpm_dist_dev*) or the compact list of the cells with numer > 0 (fpm_dist_list_dev*).
+struct DistOut {
+    Counts cnt;
+    double *dist = nullptr, *pval = nullptr;
+    uint8_t *pass = nullptr;
+    CellList list{};
+};
+
+// The outputs handed to compare_impl, so the sparse path can finalize in place: the probe (or
+// the side fill) writes every cell's no-shared-hash values and a candidate kernel rewrites
+// (or lists) the candidates, with no dense pass re-reading the grid.
 struct DistFinal {
     const uint64_t *ref_length, *qry_length;
     uint32_t kmer_size;
     double kmer_space, max_dist, max_pvalue;
-    double *dist, *pval;
-    uint8_t *pass;
-    // the caller ran fpm_dist_prefill_dev on these buffers (ctx->ev_prefill marks its end):
-    // no fill here, the empty pairs are fixed up and every rewrite waits for the prefill.
-    // pre_rows < n_qry: only query rows [0, pre_rows) were prefilled (beside the sketch
-    // kernels); the other rows are filled here, beside the candidate compare
-    bool prefilled = false;
-    uint32_t pre_rows = 0;
-    // the transposed grid too (fpm_refset_dist_mirror_dev): filled beside the primary grid and
+    DistOut prim;
+    // the transposed grid too (fpm_refset_dist_mirror_dev*): filled beside the primary grid and
     // its candidate cells scattered by the candidate finalize; compare_impl sets *mirrored
     // when it wrote it (the sorted sparse path), else dist_dev_impl computes it by a second,
     // swapped call
-    MirrorOut mir{};
+    DistOut mir;
     bool *mirrored = nullptr;
+    bool compact() const { return prim.list.count != nullptr; }
+    bool has_mirror() const { return mir.cnt.numer != nullptr; }
 };
 
 // bucket index geometry for E entries over n_ref rows: ~2.4 entries per bucket (2^nbits >=
@@ -2126,8 +1981,8 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
 }
 
 // The grid compare: dense walk, or bucket index + probe + candidate kernel (sparse).
-// With `fin`, a sparse run also finalizes and sets *finalized.  With `rs`, the references
-// are that resident set and its index is reused (not rebuilt).
+// With `fin`, a sparse run also finalizes (full outputs, or the compact list) and sets
+// *finalized.  With `rs`, the references are that resident set and its index is reused.
 static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                         uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                         const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
@@ -2153,92 +2008,55 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (rs && !rs->sparse_ok) try_sparse = false;
     const bool self_set = d_ref == d_qry && d_ref_len == d_qry_len && ref_stride == qry_stride &&
                           n_ref == n_qry;
+    const bool compact = fin && fin->compact();
+    const bool want_mir = fin && fin->has_mirror() && !self_set;
+    // The side-stream fill writes every cell's no-shared-hash values (full output: distance /
+    // p-value / pass, 17 B per cell), and with fill_cnt the numer / denom defaults too, which
+    // the probe then leaves out: the probe (event reads, latency-bound, slowed ~3x by any write
+    // stream beside it) gets shorter and the bytes move beside the rank kernel.  Measured
+    // (same box, full output): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 %, so
+    // by grid size.  A transposed grid's defaults are written by the fill only.  The compact
+    // output needs a fill only for the counts.
+    const bool fill_cnt = fin && (want_mir || (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28)
+                                                                     : ctx->fill_counts != 0));
+    const bool need_fill = fin && (!compact || fill_cnt);
     bool fill_pending = false;
-    // the fill of every cell's no-shared-hash values on the side stream (see below); with
-    // fill_cnt it writes the numer / denom defaults too and the probe writes none: the probe
-    // (event reads, latency-bound, slowed ~3x by any write stream beside it) gets shorter and
-    // the bytes move to the fill beside the rank kernel.
-    // Measured (same box): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 % (the
-    // heavier fill beside the rank kernel costs more than the probe saves), so by grid size.
-    const bool want_mir = fin && fin->mir.dist && !self_set;
-    // the side fill of query rows [fill_from, q1): from the current point of `st`
-    uint32_t fill_from = fin && fin->prefilled ? std::min(fin->pre_rows, n_qry) : 0;
-    // every row prefilled: no fill in this call
-    const bool pre_all = fin && fin->prefilled && fill_from == n_qry;
-    // (a partial prefill keeps the counts in the side fill: the prefilled rows then get a
-    // counts-only pass with the rest of the rows)
-    const bool fill_cnt = fin && !pre_all &&
-                          (want_mir ||
-                           (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28) : ctx->fill_counts != 0));
-    const uint32_t pre_cnt_rows = fill_cnt ? fill_from : 0;   // prefilled rows lacking counts
     // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
     // start) and submits the fill after later work on `st`
-    auto launch_fill_rows = [&](uint32_t q1, bool record_in = true) -> int {
-        const uint32_t q0 = fill_from;
-        const uint64_t off = (uint64_t)q0 * n_ref;
+    auto launch_fill = [&](bool record_in) -> int {
         PairFill fill;
-        fill.dist = fin->dist + off;
-        fill.pval = fin->pval + off;
-        fill.pass = fin->pass + off;
+        fill.dist = compact ? nullptr : fin->prim.dist;
+        fill.pval = compact ? nullptr : fin->prim.pval;
+        fill.pass = compact ? nullptr : fin->prim.pass;
         fill.max_dist = fin->max_dist;
         fill.max_pvalue = fin->max_pvalue;
-        Counts c{};
-        if (fill_cnt) {
-            const uint64_t cb = off * (cnt.c16 ? 2 : 4);
-            c = cnt;
-            c.numer = (char *)cnt.numer + cb;
-            c.denom = (char *)cnt.denom + cb;
-        }
         HIP_TRY(ensure_aux(ctx));
         if (record_in) HIP_TRY(hipEventRecord(ctx->ev_in, st));
         HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
         TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
-        if (pre_cnt_rows && q0 == pre_cnt_rows) {
-            // the numer / denom defaults of the prefilled rows [0, q0) (their distance /
-            // p-value / pass are the prefill's)
-            PairFill cf;
-            cf.dist = nullptr;
-            cf.pval = nullptr;
-            cf.pass = nullptr;
-            cf.max_dist = fin->max_dist;
-            cf.max_pvalue = fin->max_pvalue;
-            HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, q0, sketch_size, cnt, cf,
-                                     ctx->aux, true));
-        }
-        // which fill: the flattened one runs ~35 % faster alone but slows a rank kernel
-        // beside it more (C2, 1e8 cells / 2.3e8 events: rank 0.66 -> 0.70 ms while the fill
-        // shrank 0.63 -> 0.57, step +0.03 ms; C4, 2.5e9 cells: 14.1 -> 12.8-13.3 ms, N = 8
-        // rank share 2.67 -> 2.20 ms).  The fill is the long pole when its cells outweigh the
-        // posting events (the rank kernel's work): flattened when the cells written (both
-        // grids with a transpose) times 1.6 exceed the events (C2: 2.3 events per cell);
-        // FPM_FILL_ROWS=1 / FPM_FILL_FLAT=1 force either (A/B)
-        static const int kFillFlat = [] {
-            const char *r = getenv("FPM_FILL_ROWS"), *f = getenv("FPM_FILL_FLAT");
-            return r && r[0] == '1' ? 0 : f && f[0] == '1' ? 1 : -1;
-        }();
+        // the flattened fill runs ~35 % faster alone but slows a rank kernel beside it more
+        // (C2, 1e8 cells / 2.3e8 events: rank 0.66 -> 0.70 ms while the fill shrank 0.63 ->
+        // 0.57; C4, 2.5e9 cells: 14.1 -> 12.8-13.3 ms).  The fill is the long pole when its
+        // cells outweigh the posting events (the rank kernel's work): flattened when the cells
+        // written (both grids with a transpose) times 1.6 exceed the events
         const long double cells_w = (long double)n_pairs * (want_mir ? 2 : 1);
-        const bool flat = kFillFlat >= 0 ? kFillFlat == 1
-                                         : cells_w * 1.6L > (long double)ctx->last_events;
-        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len + q0, q1 - q0, sketch_size, c, fill,
-                                 ctx->aux, flat));
-        if (want_mir && q1 == n_qry) {
+        const bool flat = cells_w * 1.6L > (long double)ctx->last_events;
+        HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size,
+                                 fill_cnt ? cnt : Counts{}, fill, ctx->aux, flat));
+        if (want_mir) {
             // the transposed grid: the ref rows as queries against the query rows
             PairFill mf = fill;
-            mf.dist = fin->mir.dist;
-            mf.pval = fin->mir.pval;
-            mf.pass = fin->mir.pass;
-            HIP_TRY(launch_dist_fill(d_qry_len, n_qry, d_ref_len, n_ref, sketch_size, fin->mir.cnt,
-                                     mf, ctx->aux, flat));
+            mf.dist = compact ? nullptr : fin->mir.dist;
+            mf.pval = compact ? nullptr : fin->mir.pval;
+            mf.pass = compact ? nullptr : fin->mir.pass;
+            HIP_TRY(launch_dist_fill(d_qry_len, n_qry, d_ref_len, n_ref, sketch_size,
+                                     fin->mir.cnt, mf, ctx->aux, flat));
         }
         tl.done();
         HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
-        fill_from = q1;
-        fill_pending = q1 == n_qry;
+        fill_pending = true;
         return FPM_OK;
     };
-    auto launch_fill = [&]() -> int { return launch_fill_rows(n_qry); };
-    if (try_sparse && fin && ctx->fill_early && !fin->prefilled)
-        if (int rc = launch_fill()) return rc;
     if (try_sparse) {
         const uint64_t NB = 1ULL << geom.nbits;
         void *ctr;
@@ -2261,16 +2079,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         // posting events and whether the query rows are sorted, and the candidate compare is
         // chosen after it (rank kernel, or the literal walk for unsorted rows: the candidates
         // are the same).  Taken in the forced sparse mode, and in AUTO when the set's own
-        // density (its self events per row) says the block is far from the dense regime;
-        // FPM_PROBE_COUNT=1 forces the count (A/B).
-        static const bool kForceCount = [] {
-            const char *v = getenv("FPM_PROBE_COUNT");
-            return v && v[0] == '1';
-        }();
+        // density (its self events per row) says the block is far from the dense regime.
         const long double ev_est =
             rs ? (long double)rs->self_events * n_qry / std::max<uint32_t>(1, rs->n_ref) : 0.0L;
         const bool skip_count = rs && !self_set && !rs->deduped && !rs->ref_unsorted &&
-                                hash_bytes == 8 && !kForceCount &&
+                                hash_bytes == 8 &&
                                 (ctx->dist_mode == FPM_DIST_SPARSE ||
                                  (ctx->dist_mode == FPM_DIST_AUTO &&
                                   ev_est * 16.0L <= (long double)n_pairs * sketch_size));
@@ -2404,71 +2217,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
             const bool sym = rows_merge && self_set;
-            // a transposed grid is written from the rank kernel's candidate results (sorted
-            // distinct lists: symmetric); its fill needs the whole-grid form (no split)
-            // with `fin`: every cell's no-shared-hash values, written on the side stream
-            // beside the candidate compare (it needs only the list lengths; beside the
-            // index build or the probe it slowed both, they move as many bytes as it does).
-            // The rank kernel then leaves the grid alone (results per candidate slot), and the
-            // candidate finalize, after the fill, scatters them; the literal walk writes cells
-            // in place, so it waits for the fill instead.
-            if (fin && !fin->prefilled && ctx->fill_pre_probe && !fill_pending)
-                if (int rc = launch_fill()) return rc;
-            // FPM_FILL_SPLIT=f: the first f of the query rows filled beside the probe, the rest
-            // beside the candidate compare (rows in multiples of 8: 16-B aligned row starts)
-            if (fin && !fin->prefilled && ctx->fill_split > 0 && !fill_pending && fill_from == 0 &&
-                !want_mir) {
-                const uint32_t qs = (uint32_t)(n_qry * ctx->fill_split) & ~7u;
-                if (qs > 0 && qs < n_qry)
-                    if (int rc = launch_fill_rows(qs)) return rc;
-            }
-            // FPM_RANK_PARTS=k: the query rows in k parts; the candidate compare of part i runs
-            // on its own stream once the probe of part i is done, beside the probe of part
-            // i + 1 (the probe waits on memory, the rank kernel on LDS).  Sorted rows known
-            // before the probe (no probe-reported sortedness), results per candidate slot.
-            static const int kRankParts = [] {
-                const char *v = getenv("FPM_RANK_PARTS");
-                const int p = v ? atoi(v) : 1;
-                return std::max(1, std::min(p, (int)fpm_ctx::kMaxParts));
-            }();
-            const int parts = rows_merge && !skip_count && fin && !ctx->cmp && !ctx->fill_serial &&
-                                      n_qry >= (uint32_t)kRankParts * 64
-                                  ? kRankParts
-                                  : 1;
-            if (parts > 1) {
-                if (!ctx->rk) {
-                    HIP_TRY(hipStreamCreateWithFlags(&ctx->rk, hipStreamNonBlocking));
-                    for (auto &e : ctx->ev_part)
-                        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-                    HIP_TRY(hipEventCreateWithFlags(&ctx->ev_rk, hipEventDisableTiming));
-                }
-                void *cres;
-                HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
-                uint32_t *pn = (uint32_t *)cres, *pd = pn + cap;
-                for (int i = 0; i < parts; i++) {
-                    const uint32_t lo = (uint32_t)((uint64_t)n_qry * i / parts);
-                    const uint32_t hi = (uint32_t)((uint64_t)n_qry * (i + 1) / parts);
-                    {
-                        TimedLaunch tl(ctx, FPM_K_PROBE, st);
-                        HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, hi - lo, n_ref,
-                                                  hash_bytes, geom, dir, entries, d_ref_len,
-                                                  sketch_size, sym, !fill_cnt, self_set, cnt,
-                                                  (uint64_t *)cand, n_cand, (uint64_t *)row_seg,
-                                                  p_qry_it, nullptr, nullptr, st, lo));
-                        tl.done();
-                    }
-                    HIP_TRY(hipEventRecord(ctx->ev_part[i], st));
-                    HIP_TRY(hipStreamWaitEvent(ctx->rk, ctx->ev_part[i], 0));
-                    TimedLaunch tl(ctx, FPM_K_COMPARE, ctx->rk);
-                    HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg,
-                                              hi - lo, (const uint64_t *)d_ref, d_ref_len,
-                                              ref_stride, n_ref, (const uint64_t *)d_qry,
-                                              d_qry_len, qry_stride, sketch_size, sym, cnt, pn, pd,
-                                              ctx->rk, lo));
-                    tl.done();
-                }
-                HIP_TRY(hipEventRecord(ctx->ev_rk, ctx->rk));
-            } else {
+            {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, dir, entries, d_ref_len, sketch_size, sym,
@@ -2486,97 +2235,75 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     rows_merge = false;
                 }
             }
+            // The rank kernel keeps its results in per-candidate slots (cnum / cden) and leaves
+            // the grid alone, so the fill (needing only the list lengths) runs beside it on the
+            // side stream, and the candidate finalize scatters the results after both.  The
+            // literal walk writes cells in place, so it waits for the fill instead.  (Beside the
+            // index build or the probe the fill slowed both: they move as many bytes as it does.)
             uint32_t *cnum = nullptr, *cden = nullptr;
-            // After the host read of the probe's counters the GPU is idle: the fill, submitted
-            // first, would take every CU before the rank kernel's workgroups arrive (rank +
+            if (fin && rows_merge) {
+                void *cres;
+                HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
+                cnum = (uint32_t *)cres;
+                cden = cnum + cap;
+            }
+            // After the host read of the probe's counters the GPU is idle: a fill submitted
+            // first would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
             // ends (ev_in recorded here) but is submitted after the candidate compare.
-            const bool defer_fill = skip_count && rows_merge && fin && !pre_all &&
-                                    !fill_pending && !ctx->fill_serial && !ctx->cmp;
+            const bool defer_fill = need_fill && skip_count && rows_merge;
             if (defer_fill) {
                 HIP_TRY(ensure_aux(ctx));
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
+            } else if (need_fill) {
+                if (int rc = launch_fill(true)) return rc;
             }
-            if (fin && pre_all) {
-                if (rows_merge) {
-                    void *cres;
-                    HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
-                    cnum = (uint32_t *)cres;
-                    cden = cnum + cap;
-                }
-            } else if (fin) {
-                if (!fill_pending && !defer_fill)
-                    if (int rc = launch_fill()) return rc;   // the rows not filled yet
-                if (rows_merge) {
-                    void *cres;
-                    HIP_TRY(scratch(ctx, 3, cap * 8, &cres));
-                    cnum = (uint32_t *)cres;
-                    cden = cnum + cap;
-                }
-            }
-            if (fill_pending && (!cnum || ctx->fill_serial))
-                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
-            if (parts > 1) {
-                // the parts' compares ran on ctx->rk (their results in the same slots)
-                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_rk, 0));
-            } else {
-                // FPM_FILL_CUS: the compare on the CUs the fill does not own
-                const bool on_cmp = ctx->cmp && rows_merge && fill_pending && cnum;
-                hipStream_t cs = on_cmp ? ctx->cmp : st;
-                if (on_cmp) {
-                    HIP_TRY(hipEventRecord(ctx->ev_cmp0, st));
-                    HIP_TRY(hipStreamWaitEvent(cs, ctx->ev_cmp0, 0));
-                }
-                TimedLaunch tl(ctx, FPM_K_COMPARE, cs);
+            if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+            {
+                TimedLaunch tl(ctx, FPM_K_COMPARE, st);
                 if (rows_merge)
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
-                                              sketch_size, sym, cnt, cnum, cden,
-                                              cs));
+                                              sketch_size, sym, cnt, cnum, cden, st));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                                                    qry_stride, hash_bytes, sketch_size, cnt,
                                                    st));
                 tl.done();
-                if (on_cmp) {
-                    HIP_TRY(hipEventRecord(ctx->ev_cmp1, cs));
-                    HIP_TRY(hipStreamWaitEvent(st, ctx->ev_cmp1, 0));
-                }
             }
             if (defer_fill)
-                if (int rc = launch_fill_rows(n_qry, false)) return rc;
-            if (fin && fin->prefilled) {
-                // the walk kernel wrote numer / denom only; distance / p-value / pass of the
-                // candidates and the empty pairs overwrite the prefill, so after it (the rows
-                // filled by this call handle their empty pairs themselves)
-                PairFill fx;
-                fx.dist = fin->dist;
-                fx.pval = fin->pval;
-                fx.pass = fin->pass;
-                fx.max_dist = fin->max_dist;
-                fx.max_pvalue = fin->max_pvalue;
-                HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
-                HIP_TRY(launch_dist_empty_fixup(d_ref_len, n_ref, d_qry_len,
-                                                std::min(fin->pre_rows, n_qry), fx, st));
-            }
-            if (fin && !pre_all && cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+                if (int rc = launch_fill(false)) return rc;
+            if (fill_pending && cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             if (fin) {
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
-                MirrorOut mir{};
-                if (want_mir && cnum && fill_pending) {
-                    mir = fin->mir;
-                    mir.n_qry = n_qry;
-                }
-                HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
-                                                  cden, cnt, fin->ref_length,
-                                                  fin->qry_length,
+                if (compact) {
+                    const CellList none{};
+                    HIP_TRY(launch_dist_cand_list((const uint64_t *)cand, n_cand, cap, sym, cnum,
+                                                  cden, cnt, fin->ref_length, fin->qry_length,
                                                   n_ref, fin->kmer_size, fin->kmer_space,
-                                                  fin->max_dist, fin->max_pvalue, fin->dist,
-                                                  fin->pval, fin->pass, mir, st));
+                                                  fin->max_dist, fin->max_pvalue, fin->prim.list,
+                                                  want_mir && cnum ? fin->mir.cnt : Counts{}, n_qry,
+                                                  want_mir && cnum ? fin->mir.list : none, st));
+                } else {
+                    MirrorOut mir{};
+                    if (want_mir && cnum) {
+                        mir.cnt = fin->mir.cnt;
+                        mir.dist = fin->mir.dist;
+                        mir.pval = fin->mir.pval;
+                        mir.pass = fin->mir.pass;
+                        mir.n_qry = n_qry;
+                    }
+                    HIP_TRY(launch_dist_cand_finalize((const uint64_t *)cand, n_cand, cap, sym, cnum,
+                                                      cden, cnt, fin->ref_length,
+                                                      fin->qry_length, n_ref, fin->kmer_size,
+                                                      fin->kmer_space, fin->max_dist,
+                                                      fin->max_pvalue, fin->prim.dist,
+                                                      fin->prim.pval, fin->prim.pass, mir, st));
+                }
                 tl.done();
-                if (mir.dist && fin->mirrored) *fin->mirrored = true;
+                if (want_mir && cnum && fin->mirrored) *fin->mirrored = true;
                 *finalized = true;
             }
             ctx->last_sparse = rows_merge ? 2 : 1;
@@ -2586,8 +2313,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             return FPM_OK;
         }
     }
-    if (fill_pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));   // dense after all
-    if (ctx->dense_img && compare_grid_img_ok(hash_bytes, sketch_size, ref_stride, qry_stride)) {
+    if (compare_grid_img_ok(hash_bytes, sketch_size, ref_stride, qry_stride)) {
         size_t ub, bb;
         compare_grid_img_scratch(n_qry, sketch_size, ref_stride, qry_stride, &ub, &bb);
         void *ublk, *bimg;
@@ -2622,37 +2348,37 @@ int fpm_compare_grid_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
 
 }  // extern "C"
 
-// compare + finalize on device buffers (fpm_dist_dev / fpm_dist_dev16)
+// compare + finalize on device buffers (fpm_dist_dev* and fpm_dist_list_dev*)
 static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                          const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
                          const void *d_qry, const uint32_t *d_qry_len,
                          const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
                          uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
-                         double kmer_space, double max_dist, double max_pvalue, Counts cnt,
-                         double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream,
-                         const char *who, fpm_refset *rs = nullptr, bool prefilled = false,
-                         const MirrorOut *mirror = nullptr)
+                         double kmer_space, double max_dist, double max_pvalue, const DistOut &out,
+                         void *stream, const char *who, fpm_refset *rs = nullptr,
+                         const DistOut *mirror = nullptr)
 {
-    if (!d_ref_length || !d_qry_length || !d_dist || !d_pvalue)
-        return fail(FPM_EINVAL, std::string(who) + ": lengths, distance and p-value buffers required");
-    if (prefilled && !ctx->ev_prefill)
-        return fail(FPM_EINVAL, std::string(who) + ": no fpm_dist_prefill_dev on this context");
-    if (prefilled && (ctx->prefill_nref != n_ref || ctx->prefill_rows > n_qry))
-        return fail(FPM_EINVAL, std::string(who) + ": the last fpm_dist_prefill_dev wrote " +
-                                    std::to_string(ctx->prefill_rows) + " x " +
-                                    std::to_string(ctx->prefill_nref) + " cells, not rows of this " +
-                                    std::to_string(n_qry) + " x " + std::to_string(n_ref) + " grid");
-    DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue,
-                  d_dist, d_pvalue, d_pass};
-    fin.prefilled = prefilled;
-    fin.pre_rows = prefilled ? ctx->prefill_rows : 0;
+    const bool compact = out.list.count != nullptr;
+    if (!d_ref_length || !d_qry_length)
+        return fail(FPM_EINVAL, std::string(who) + ": lengths required");
+    if (!out.cnt.numer || !out.cnt.denom)
+        return fail(FPM_EINVAL, std::string(who) + ": numer / denom buffers required");
+    if (compact ? (!out.list.qry || !out.list.ref || !out.list.dist || !out.list.pval)
+                : (!out.dist || !out.pval))
+        return fail(FPM_EINVAL, std::string(who) +
+                                    (compact ? ": list qry / ref / distance / p-value buffers required"
+                                             : ": distance and p-value buffers required"));
+    hipStream_t st = pick_stream(ctx, stream);
+    if (compact) HIP_TRY(hipMemsetAsync(out.list.count, 0, 8, st));
+    DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue, out};
     bool finalized = false, mirrored = false;
     if (mirror) {
         fin.mir = *mirror;
         fin.mirrored = &mirrored;
+        if (compact) HIP_TRY(hipMemsetAsync(mirror->list.count, 0, 8, st));
     }
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
-                              qry_stride, n_qry, hash_bytes, sketch_size, cnt, stream, &fin,
+                              qry_stride, n_qry, hash_bytes, sketch_size, out.cnt, stream, &fin,
                               &finalized, rs))
         return rc;
     // the transposed grid, when the compare could not scatter it (dense path, unsorted lists:
@@ -2661,17 +2387,45 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
         if (!mirror || mirrored) return FPM_OK;
         return dist_dev_impl(ctx, d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, d_ref,
                              d_ref_len, d_ref_length, ref_stride, n_ref, hash_bytes, sketch_size,
-                             kmer_size, kmer_space, max_dist, max_pvalue, mirror->cnt,
-                             mirror->dist, mirror->pval, mirror->pass, stream, who);
+                             kmer_size, kmer_space, max_dist, max_pvalue, *mirror, stream, who);
     };
     if (finalized) return mirror_swapped();
-    hipStream_t st = pick_stream(ctx, stream);
-    if (prefilled) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));   // rewrites every cell
     TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
-    HIP_TRY(launch_dist_finalize(cnt, d_ref_length, d_qry_length, n_ref, n_qry, kmer_size,
-                                 kmer_space, max_dist, max_pvalue, d_dist, d_pvalue, d_pass, st));
+    if (compact)
+        HIP_TRY(launch_dist_grid_list(out.cnt, n_ref, n_qry, d_ref_length, d_qry_length, kmer_size,
+                                      kmer_space, max_dist, max_pvalue, out.list, st));
+    else
+        HIP_TRY(launch_dist_finalize(out.cnt, d_ref_length, d_qry_length, n_ref, n_qry, kmer_size,
+                                     kmer_space, max_dist, max_pvalue, out.dist, out.pval,
+                                     out.pass, st));
     tl.done();
     return mirror_swapped();
+}
+
+static DistOut full_out(void *numer, void *denom, bool c16, double *dist, double *pval,
+                        uint8_t *pass)
+{
+    DistOut o;
+    o.cnt = Counts{numer, denom, c16};
+    o.dist = dist;
+    o.pval = pval;
+    o.pass = pass;
+    return o;
+}
+
+static int list_out(void *numer, void *denom, bool c16, const fpm_cell_list *l, DistOut &o,
+                    const char *who)
+{
+    if (!l || !l->count) return fail(FPM_EINVAL, std::string(who) + ": cell list with a count required");
+    o.cnt = Counts{numer, denom, c16};
+    o.list.qry = l->qry;
+    o.list.ref = l->ref;
+    o.list.dist = l->dist;
+    o.list.pval = l->pvalue;
+    o.list.pass = l->pass;
+    o.list.count = (unsigned long long *)l->count;
+    o.list.cap = l->cap;
+    return FPM_OK;
 }
 
 extern "C" {
@@ -2686,8 +2440,9 @@ int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
 {
     return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
                          d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
-                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, false},
-                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev");
+                         kmer_space, max_dist, max_pvalue,
+                         full_out(d_numer, d_denom, false, d_dist, d_pvalue, d_pass), stream,
+                         "fpm_dist_dev");
 }
 
 int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
@@ -2702,63 +2457,27 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
         return fail(FPM_EINVAL, "fpm_dist_dev16: sketch_size must be <= 65535 (u16 counts)");
     return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
                          d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
-                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, true},
-                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev16");
+                         kmer_space, max_dist, max_pvalue,
+                         full_out(d_numer, d_denom, true, d_dist, d_pvalue, d_pass), stream,
+                         "fpm_dist_dev16");
 }
 
-int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double max_dist,
-                         double max_pvalue, double *d_dist, double *d_pvalue, uint8_t *d_pass,
-                         void *stream)
+int fpm_dist_list_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                      const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                      const void *d_qry, const uint32_t *d_qry_len, const uint64_t *d_qry_length,
+                      uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
+                      uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                      double max_dist, double max_pvalue, uint16_t *d_numer, uint16_t *d_denom,
+                      const fpm_cell_list *list, void *stream)
 {
     if (int rc = set_device(ctx)) return rc;
-    if (!d_dist || !d_pvalue) return fail(FPM_EINVAL, "fpm_dist_prefill_dev: null output");
-    HIP_TRY(ensure_aux(ctx));
-    if (!ctx->ev_prefill) HIP_TRY(hipEventCreateWithFlags(&ctx->ev_prefill, hipEventDisableTiming));
-    hipStream_t st = stream ? (hipStream_t)stream : ctx->aux;
-    if (!stream) {
-        // the side stream starts after the work already queued on the context's stream (an
-        // earlier call's rewrites of the same cells)
-        HIP_TRY(hipEventRecord(ctx->ev_in, ctx->stream));
-        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_in, 0));
-    }
-    PairFill fill;
-    fill.dist = d_dist;
-    fill.pval = d_pvalue;
-    fill.pass = d_pass;
-    fill.max_dist = max_dist;
-    fill.max_pvalue = max_pvalue;
-    // FPM_PREFILL_GRID=n: the flattened prefill on n workgroups striding over the grid (few
-    // wave slots held beside the sketch kernels) instead of one pass per thread (A/B)
-    static const uint32_t kPrefillGrid = [] {
-        const char *v = getenv("FPM_PREFILL_GRID");
-        return v ? (uint32_t)strtoul(v, nullptr, 10) : 0u;
-    }();
-    TimedLaunch tl(ctx, FPM_K_FILL, st);
-    HIP_TRY(launch_dist_fill(nullptr, n_ref, nullptr, n_qry, 0, Counts{}, fill, st, true,
-                             kPrefillGrid));
-    tl.done();
-    HIP_TRY(hipEventRecord(ctx->ev_prefill, st));
-    ctx->prefill_rows = n_qry;
-    ctx->prefill_nref = n_ref;
-    return FPM_OK;
-}
-
-int fpm_dist_dev16_prefilled(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
-                             const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
-                             const void *d_qry, const uint32_t *d_qry_len,
-                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
-                             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
-                             double kmer_space, double max_dist, double max_pvalue,
-                             uint16_t *d_numer, uint16_t *d_denom, double *d_dist,
-                             double *d_pvalue, uint8_t *d_pass, void *stream)
-{
     if (sketch_size > 65535)
-        return fail(FPM_EINVAL, "fpm_dist_dev16_prefilled: sketch_size must be <= 65535");
+        return fail(FPM_EINVAL, "fpm_dist_list_dev: sketch_size must be <= 65535 (u16 counts)");
+    DistOut o;
+    if (int rc = list_out(d_numer, d_denom, true, list, o, "fpm_dist_list_dev")) return rc;
     return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
                          d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
-                         kmer_space, max_dist, max_pvalue, Counts{d_numer, d_denom, true},
-                         d_dist, d_pvalue, d_pass, stream, "fpm_dist_dev16_prefilled", nullptr,
-                         true);
+                         kmer_space, max_dist, max_pvalue, o, stream, "fpm_dist_list_dev");
 }
 
 int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,
@@ -2925,6 +2644,18 @@ int fpm_refset_create(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len,
     return FPM_OK;
 }
 
+static int refset_check(fpm_refset *rs, uint32_t sketch_size, uint32_t count_bytes,
+                        const char *who)
+{
+    if (!rs) return fail(FPM_EINVAL, std::string(who) + ": null set");
+    if (sketch_size != rs->sketch_size)
+        return fail(FPM_EINVAL, std::string(who) + ": sketch_size differs from the set's");
+    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
+    if (count_bytes == 2 && sketch_size > 65535)
+        return fail(FPM_EINVAL, std::string(who) + ": u16 counts need sketch_size <= 65535");
+    return set_device(rs->ctx);
+}
+
 int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
                         const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
                         uint32_t sketch_size, uint32_t count_bytes, uint32_t kmer_size,
@@ -2932,17 +2663,36 @@ int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry
                         void *d_denom, double *d_dist, double *d_pvalue, uint8_t *d_pass,
                         void *stream)
 {
-    if (!rs) return fail(FPM_EINVAL, "refset_dist: null set");
-    if (sketch_size != rs->sketch_size)
-        return fail(FPM_EINVAL, "refset_dist: sketch_size differs from the set's");
-    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
-    if (count_bytes == 2 && sketch_size > 65535)
-        return fail(FPM_EINVAL, "refset_dist: u16 counts need sketch_size <= 65535");
+    if (int rc = refset_check(rs, sketch_size, count_bytes, "fpm_refset_dist_dev")) return rc;
     return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
                          d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
                          sketch_size, kmer_size, kmer_space, max_dist, max_pvalue,
-                         Counts{d_numer, d_denom, count_bytes == 2}, d_dist, d_pvalue, d_pass,
+                         full_out(d_numer, d_denom, count_bytes == 2, d_dist, d_pvalue, d_pass),
                          stream, "fpm_refset_dist_dev", rs);
+}
+
+int fpm_refset_dist_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                             uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                             double max_dist, double max_pvalue, uint16_t *d_numer,
+                             uint16_t *d_denom, const fpm_cell_list *list, void *stream)
+{
+    if (int rc = refset_check(rs, sketch_size, 2, "fpm_refset_dist_list_dev")) return rc;
+    DistOut o;
+    if (int rc = list_out(d_numer, d_denom, true, list, o, "fpm_refset_dist_list_dev")) return rc;
+    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
+                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
+                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue, o, stream,
+                         "fpm_refset_dist_list_dev", rs);
+}
+
+static int mirror_check(fpm_refset *rs, const void *d_qry, const char *who)
+{
+    if (d_qry == rs->ref)
+        return fail(FPM_EINVAL, std::string(who) + ": the query rows are the reference rows "
+                                                   "(use the non-mirror call: that grid is its "
+                                                   "own transpose)");
+    return FPM_OK;
 }
 
 int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
@@ -2953,28 +2703,38 @@ int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t
                                uint8_t *d_pass, void *m_numer, void *m_denom, double *m_dist,
                                double *m_pvalue, uint8_t *m_pass, void *stream)
 {
-    if (!rs) return fail(FPM_EINVAL, "refset_dist_mirror: null set");
-    if (sketch_size != rs->sketch_size)
-        return fail(FPM_EINVAL, "refset_dist_mirror: sketch_size differs from the set's");
-    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
-    if (count_bytes == 2 && sketch_size > 65535)
-        return fail(FPM_EINVAL, "refset_dist_mirror: u16 counts need sketch_size <= 65535");
+    const char *who = "fpm_refset_dist_mirror_dev";
+    if (int rc = refset_check(rs, sketch_size, count_bytes, who)) return rc;
     if (!m_numer || !m_denom || !m_dist || !m_pvalue)
         return fail(FPM_EINVAL, "refset_dist_mirror: mirror numer / denom / distance / p-value required");
-    if (d_qry == rs->ref)
-        return fail(FPM_EINVAL, "refset_dist_mirror: the query rows are the reference rows "
-                                "(use fpm_refset_dist_dev: that grid is its own transpose)");
-    MirrorOut mir;
-    mir.cnt = Counts{m_numer, m_denom, count_bytes == 2};
-    mir.dist = m_dist;
-    mir.pval = m_pvalue;
-    mir.pass = m_pass;
-    mir.n_qry = n_qry;
+    if (int rc = mirror_check(rs, d_qry, who)) return rc;
+    const DistOut mir = full_out(m_numer, m_denom, count_bytes == 2, m_dist, m_pvalue, m_pass);
     return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
                          d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
                          sketch_size, kmer_size, kmer_space, max_dist, max_pvalue,
-                         Counts{d_numer, d_denom, count_bytes == 2}, d_dist, d_pvalue, d_pass,
-                         stream, "fpm_refset_dist_mirror_dev", rs, false, &mir);
+                         full_out(d_numer, d_denom, count_bytes == 2, d_dist, d_pvalue, d_pass),
+                         stream, who, rs, &mir);
+}
+
+int fpm_refset_dist_mirror_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                                    const uint64_t *d_qry_length, uint64_t qry_stride,
+                                    uint32_t n_qry, uint32_t sketch_size, uint32_t kmer_size,
+                                    double kmer_space, double max_dist, double max_pvalue,
+                                    uint16_t *d_numer, uint16_t *d_denom,
+                                    const fpm_cell_list *list, uint16_t *m_numer,
+                                    uint16_t *m_denom, const fpm_cell_list *m_list, void *stream)
+{
+    const char *who = "fpm_refset_dist_mirror_list_dev";
+    if (int rc = refset_check(rs, sketch_size, 2, who)) return rc;
+    if (int rc = mirror_check(rs, d_qry, who)) return rc;
+    DistOut o, m;
+    if (int rc = list_out(d_numer, d_denom, true, list, o, who)) return rc;
+    if (int rc = list_out(m_numer, m_denom, true, m_list, m, who)) return rc;
+    if (!m_numer || !m_denom) return fail(FPM_EINVAL, std::string(who) + ": mirror numer / denom required");
+    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
+                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
+                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue, o, stream, who,
+                         rs, &m);
 }
 
 int fpm_refset_reindex(fpm_refset *rs, void *stream)

@@ -163,15 +163,11 @@ struct PairFill {
     double max_dist = -1, max_pvalue = -1;
 };
 // flat: the fill over the flattened grid (line-aligned wave stores, ~6.5 TB/s alone), else
-// row-aligned workgroups (~4.8 TB/s alone, gentler on a latency-bound kernel beside it)
+// row-aligned workgroups (~4.8 TB/s alone, gentler on a latency-bound kernel beside it).
+// fill.dist == nullptr: the numer / denom defaults only (the compact output)
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
-                            hipStream_t st, bool flat = true, uint32_t grid_cap = 0);
-// (d_ref_len == d_qry_len == nullptr: every list taken as non-empty, fpm_dist_prefill_dev)
-// distance 0 / p-value 1 / pass for the pairs of two empty lists (after such a prefill)
-hipError_t launch_dist_empty_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
-                                   const uint32_t *d_qry_len, uint32_t n_qry,
-                                   const PairFill &fill, hipStream_t st);
+                            hipStream_t st, bool flat = true);
 // `defaults`: also write (0, min(S, la+lb)) to every numer / denom cell of the row (off
 // when launch_dist_fill already did)
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
@@ -269,5 +265,30 @@ hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const 
                                 double kmer_space, double max_dist, double max_pvalue,
                                 double *d_dist, double *d_pvalue, uint8_t *d_pass,
                                 hipStream_t st);
+
+// The compact dist output's list of cells with numer > 0 (fpm_dist_list_dev): entry i =
+// (qry[i], ref[i]) with its distance / p-value / pass; *count (device) counts every entry,
+// those at index >= cap are not written.
+struct CellList {
+    uint32_t *qry = nullptr, *ref = nullptr;
+    double *dist = nullptr, *pval = nullptr;
+    uint8_t *pass = nullptr;
+    unsigned long long *count = nullptr;
+    uint64_t cap = 0;
+};
+// candidates: scatter (numer, denom) (mirror cell with `sym`; transposed grid mcnt with its own
+// list mlist) and list the cells with numer > 0; d_cnum == nullptr: counts read from the grid
+hipError_t launch_dist_cand_list(const uint64_t *d_cand, const unsigned long long *d_n_cand,
+                                 uint64_t cap, bool sym, const uint32_t *d_cnum,
+                                 const uint32_t *d_cden, Counts cnt, const uint64_t *d_ref_length,
+                                 const uint64_t *d_qry_length, uint32_t n_ref, uint32_t kmer_size,
+                                 double kmer_space, double max_dist, double max_pvalue,
+                                 const CellList &list, Counts mcnt, uint32_t m_nqry,
+                                 const CellList &mlist, hipStream_t st);
+// every cell of a computed grid with numer > 0 into the list
+hipError_t launch_dist_grid_list(Counts cnt, uint32_t n_ref, uint32_t n_qry,
+                                 const uint64_t *d_ref_length, const uint64_t *d_qry_length,
+                                 uint32_t kmer_size, double kmer_space, double max_dist,
+                                 double max_pvalue, const CellList &list, hipStream_t st);
 
 }  // namespace fpm

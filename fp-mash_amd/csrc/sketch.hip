@@ -15,12 +15,7 @@
 namespace fpm {
 
 constexpr int kBlock = 256;
-#ifndef FPM_SK_CMP64
-#define FPM_SK_CMP64 1     // canonical compare on 64-bit big-endian words (0: per-dword chain, A/B)
-#endif
-#ifndef FPM_SK_WPE
-#define FPM_SK_WPE 7       // waves per SIMD asked of the tile kernel for P <= 2048
-#endif
+constexpr int kSkWpe = 7;   // waves per SIMD asked of the tile kernel for P <= 2048
 constexpr int kWaves = kBlock / 64;
 
 // Phase timestamps of the tile kernel for tools/micro/sketch_phases.hip (which defines
@@ -336,7 +331,6 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
                                                                      SR[(f >> 2) + m], f & 3)
                                         : 0u;
                     r[nw - 1] &= tail_mask;
-#if FPM_SK_CMP64
                     // memcmp order = the big-endian order of the bytes: 64-bit big-endian words
                     // (dwords past nw are 0 in both), compared most significant first with
                     // lane masks (3 64-bit compares for k = 21 instead of a per-dword chain)
@@ -352,14 +346,6 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
                         eq = eq && fq == rq;
                     }
                     const int cmp = gt ? 1 : 0;
-#else
-                    int cmp = 0;
-#pragma unroll
-                    for (int m = 0; m < 8; m++) {
-                        uint32_t fbe = __builtin_bswap32(d[m]), rbe = __builtin_bswap32(r[m]);
-                        if (cmp == 0 && m < nw) cmp = (fbe > rbe) - (fbe < rbe);
-                    }
-#endif
                     if (cmp > 0) {
 #pragma unroll
                         for (int m = 0; m < 8; m++) d[m] = r[m];
@@ -378,7 +364,7 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
 }
 
 template <int P, int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? FPM_SK_WPE : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
 {
@@ -922,14 +908,8 @@ __global__ __launch_bounds__(kMBlock) void merge_lds_kernel(const MergeDesc *__r
 // fixed 16 KiB of LDS instead of 1,024 threads and s * 8 bytes (80 KiB at s = 10,000, two
 // merges per CU), so up to 8 merges share a CU.  A list longer than kSCap is searched in global
 // memory instead (same results; the host's size estimate only steers speed).
-#ifndef FPM_SBLOCK
-#define FPM_SBLOCK 256
-#endif
-#ifndef FPM_SCAP
-#define FPM_SCAP 2048
-#endif
-constexpr int kSBlock = FPM_SBLOCK, kSWaves = kSBlock / 64;
-constexpr uint32_t kSCap = FPM_SCAP;
+constexpr int kSBlock = 256, kSWaves = kSBlock / 64;
+constexpr uint32_t kSCap = 2048;
 uint32_t merge_small_cap() { return kSCap; }
 
 __device__ __forceinline__ uint32_t block_exscan_s(uint32_t v, uint32_t *tmp, uint32_t *total)

@@ -93,12 +93,9 @@ SYMBOLS = [
     ("fpm_dist_dev16", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
                                  C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
                                  C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
-    ("fpm_dist_prefill_dev", C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_double, C.c_double, vp,
-                                       vp, vp, vp]),
-    ("fpm_dist_dev16_prefilled", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp,
-                                           C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32,
-                                           C.c_uint32, C.c_double, C.c_double, C.c_double, vp,
-                                           vp, vp, vp, vp, vp]),
+    ("fpm_dist_list_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp,
+                                    C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
+                                    C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
     ("fpm_fp_positional_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p,
                                          C.c_uint64, C.c_uint32, C.c_uint32, C.c_double,
                                          C.c_double, u32p, u32p, f64p, f64p, u8p]),
@@ -116,6 +113,12 @@ SYMBOLS = [
                                              C.c_uint32, C.c_uint32, C.c_double, C.c_double,
                                              C.c_double, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                              vp]),
+    ("fpm_refset_dist_list_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32,
+                                           C.c_uint32, C.c_double, C.c_double, C.c_double, vp,
+                                           vp, vp, vp]),
+    ("fpm_refset_dist_mirror_list_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32,
+                                                  C.c_uint32, C.c_uint32, C.c_double, C.c_double,
+                                                  C.c_double, vp, vp, vp, vp, vp, vp, vp]),
     ("fpm_refset_reindex", C.c_int, [vp, vp]),
     ("fpm_ctx_index_rebuilds", C.c_int, [vp, u64p]),
     ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
@@ -131,6 +134,12 @@ SYMBOLS = [
     ("fpm_host_alloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
     ("fpm_host_free", C.c_int, [vp, vp]),
 ]
+
+
+class CellListStruct(C.Structure):
+    """fpm_cell_list (include/fpmash.h): device arrays of the compact dist output's list"""
+    _fields_ = [("qry", vp), ("ref", vp), ("dist", vp), ("pvalue", vp), ("pass_", vp),
+                ("cap", C.c_uint64), ("count", vp)]
 
 
 class FpmError(RuntimeError):
@@ -244,6 +253,68 @@ class DeviceBuffer:
             self.free()
         except Exception:
             pass
+
+
+class CellList:
+    """Device buffers of a compact dist output's cell list (fpm_cell_list) with room for
+    `cap` entries.  .struct is what the *_list_dev calls take (by reference)."""
+
+    def __init__(self, ctx, cap):
+        self.ctx, self.cap = ctx, int(max(cap, 1))
+        self.bufs = [DeviceBuffer(ctx, self.cap * b) for b in (4, 4, 8, 8, 1)] + \
+            [DeviceBuffer(ctx, 8)]
+        q, r, d, p, a, c = (b.ptr for b in self.bufs)
+        self.struct = CellListStruct(q, r, d, p, a, self.cap, c)
+
+    @property
+    def ref(self):
+        return C.byref(self.struct)
+
+    def count(self):
+        """cells with numer > 0 the last call listed (may exceed cap: then re-run larger)"""
+        return int(self.bufs[5].to_array(np.uint64, 1)[0])
+
+    def fetch(self):
+        """-> dict of the listed cells' qry, ref, distance, pvalue, pass (host arrays)"""
+        n = self.count()
+        if n > self.cap:
+            raise FpmError(FPM_ENOMEM, f"cell list holds {self.cap} entries, {n} needed")
+        m = max(n, 1)
+        out = {k: b.to_array(t, m)[:n] for k, b, t in zip(
+            ("qry", "ref", "distance", "pvalue", "pass"), self.bufs[:5],
+            (np.uint32, np.uint32, np.float64, np.float64, np.uint8))}
+        out["pass"] = out["pass"].astype(bool)
+        return out
+
+    def free(self):
+        for b in self.bufs:
+            b.free()
+
+
+def expand_compact(numer, denom, listed, n_ref, max_dist=-1.0, max_pvalue=-1.0):
+    """The five per-cell outputs of a compact result (fpm_dist_list_dev: counts of every
+    cell + the list of cells with numer > 0), by the rule include/fpmash.h states: an unlisted
+    cell has distance 0 if denom == 0 else 1, p-value 1, and the -d / -v filters at those
+    values (CommandDistance.cpp:404-408, 435-437 at common = 0).  numer / denom: flat
+    query-major arrays; listed: CellList.fetch()."""
+    numer = np.asarray(numer)
+    denom = np.asarray(denom)
+    dist = np.where(denom == 0, 0.0, 1.0)
+    pval = np.ones(len(numer), np.float64)
+    ok = np.ones(len(numer), bool)
+    if max_dist >= 0:
+        ok &= dist <= max_dist
+    if max_pvalue >= 0:
+        ok &= 1.0 <= max_pvalue
+    idx = listed["qry"].astype(np.int64) * n_ref + listed["ref"].astype(np.int64)
+    if len(idx) and np.any(numer[idx] == 0):
+        raise AssertionError("a listed cell has numer 0")
+    if int(np.count_nonzero(numer)) != len(idx) or len(np.unique(idx)) != len(idx):
+        raise AssertionError("the list is not exactly the cells with numer > 0")
+    dist[idx] = listed["distance"]
+    pval[idx] = listed["pvalue"]
+    ok[idx] = listed["pass"]
+    return {"numer": numer, "denom": denom, "distance": dist, "pvalue": pval, "pass": ok}
 
 
 class SketchJob:
@@ -522,6 +593,52 @@ class Context:
                 b.free()
         return {"numer": res[0], "denom": res[1], "distance": res[2], "pvalue": res[3],
                 "pass": res[4].astype(bool)}
+
+    def dist_list(self, ref_lists, qry_lists, sketch_size, use64=True, k=21, kmer_space=None,
+                  ref_lengths=None, qry_lengths=None, max_dist=-1.0, max_pvalue=-1.0, cap=None,
+                  expand=True):
+        """dist() through fpm_dist_list_dev (the compact output: u16 counts + the list of
+        cells with numer > 0).  expand=True: the five per-cell arrays (expand_compact), else
+        (numer, denom, listed)."""
+        dt = np.uint64 if use64 else np.uint32
+        w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
+        R, rl = _dense(ref_lists, w, dt)
+        Q, ql = (R, rl) if qry_lists is ref_lists else _dense(qry_lists, w, dt)
+        nr, nq = len(ref_lists), len(qry_lists)
+        n = nr * nq
+        if kmer_space is None:
+            kmer_space = 4.0 ** k
+        bufs = []
+
+        def up(a):
+            b = DeviceBuffer.from_array(self, a)
+            bufs.append(b)
+            return b.ptr
+        lst = None
+        try:
+            dR, drl = up(R), up(rl)
+            dQ, dql = (dR, drl) if qry_lists is ref_lists else (up(Q), up(ql))
+            drL = up(np.ascontiguousarray(ref_lengths, dtype=np.uint64))
+            dqL = drL if qry_lists is ref_lists and qry_lengths is ref_lengths else \
+                up(np.ascontiguousarray(qry_lengths, dtype=np.uint64))
+            outs = [DeviceBuffer(self, max(n, 1) * 2) for _ in range(2)]
+            bufs += outs
+            lst = CellList(self, cap if cap is not None else max(n, 1))
+            _check(lib().fpm_dist_list_dev(self.h, dR, drl, drL, w, nr, dQ, dql, dqL, w, nq,
+                                           8 if use64 else 4, sketch_size, k, kmer_space,
+                                           max_dist, max_pvalue, outs[0].ptr, outs[1].ptr,
+                                           lst.ref, None))
+            self.synchronize()
+            nu, de = (o.to_array(np.uint16, n) for o in outs)
+            listed = lst.fetch()
+        finally:
+            for b in bufs:
+                b.free()
+            if lst is not None:
+                lst.free()
+        if not expand:
+            return nu, de, listed
+        return expand_compact(nu, de, listed, nr, max_dist, max_pvalue)
 
     def refset(self, ref_lists, sketch_size, use64=True, ref_lengths=None, width=None):
         """A resident reference set (fpm_refset_create): rows uploaded and indexed once."""

@@ -260,30 +260,32 @@ int fpm_dist_dev16(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
                    uint32_t kmer_size, double kmer_space, double max_dist, double max_pvalue,
                    uint16_t *d_numer, uint16_t *d_denom, double *d_dist, double *d_pvalue,
                    uint8_t *d_pass, void *stream);
-/* The same in two parts, so the output grid's bulk overlaps the sketching of the lists: a
- * pair of non-empty lists that share no hash has distance 1 and p-value 1 whatever the
- * lists are (CommandDistance.cpp:404-419, 433-450 at common = 0), so
- * fpm_dist_prefill_dev writes those values (and the -d / -v pass flag at them) to every
- * cell of the n_qry x n_ref grid without reading any list (NULL stream: the context's side
- * stream, ordered after the work already queued on the context's stream; a caller stream
- * must itself be ordered after any earlier work on these buffers), and fpm_dist_dev16_prefilled then computes everything else: every cell's counts,
- * the pairs of two empty lists, and the cells of the pairs that share hashes (those rewrites
- * wait for the prefill; the rest of the call does not).  Same results as fpm_dist_dev16.
- * A partial prefill: the last fpm_dist_prefill_dev on the context wrote the first n_pre
- * query rows of this grid (its n_qry = n_pre <= this call's n_qry, its n_ref = this call's;
- * FPM_EINVAL otherwise), and the call fills rows [n_pre, n_qry) itself, beside the candidate
- * compare — so the prefill can be sized to end with the sketch kernels it overlaps. */
-int fpm_dist_prefill_dev(fpm_ctx *ctx, uint32_t n_ref, uint32_t n_qry, double max_dist,
-                         double max_pvalue, double *d_dist, double *d_pvalue, uint8_t *d_pass,
-                         void *stream);
-int fpm_dist_dev16_prefilled(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
-                             const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
-                             const void *d_qry, const uint32_t *d_qry_len,
-                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
-                             uint32_t hash_bytes, uint32_t sketch_size, uint32_t kmer_size,
-                             double kmer_space, double max_dist, double max_pvalue,
-                             uint16_t *d_numer, uint16_t *d_denom, double *d_dist,
-                             double *d_pvalue, uint8_t *d_pass, void *stream);
+/* ---- compact dist output (the grid as u16 numer / denom) ----------
+ * compareSketches' (numer, denom) for every cell of the n_qry x n_ref grid as u16 cells (4 B
+ * per pair, query-major), and distance / p-value / pass only for the cells that share hashes
+ * (numer > 0): an unordered list, each such cell exactly once.  A cell not in the list has
+ * numer 0, and compareSketches / pValue give it closed-form values (CommandDistance.cpp:
+ * 404-408 and 435-437 at common = 0): distance 0 when denom == 0 (two empty lists), else 1;
+ * p-value 1; pass = (max_dist < 0 || distance <= max_dist) && (max_pvalue < 0 || 1 <=
+ * max_pvalue).  Listed cells hold what fpm_dist_dev16 writes for them.
+ * The list lives in caller device memory: entry i is (qry[i], ref[i], dist[i], pvalue[i],
+ * pass[i]) (pass may be NULL).  *count is a DEVICE u64 the call resets and then sets to the
+ * number of cells with numer > 0; entries at index >= cap are not written, so a caller that
+ * reads *count > cap after the stream work repeats the call with cap >= *count. */
+typedef struct fpm_cell_list {
+    uint32_t *qry, *ref;
+    double *dist, *pvalue;
+    uint8_t *pass;
+    uint64_t cap;
+    uint64_t *count;
+} fpm_cell_list;
+int fpm_dist_list_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,
+                      const uint64_t *d_ref_length, uint64_t ref_stride, uint32_t n_ref,
+                      const void *d_qry, const uint32_t *d_qry_len, const uint64_t *d_qry_length,
+                      uint64_t qry_stride, uint32_t n_qry, uint32_t hash_bytes,
+                      uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                      double max_dist, double max_pvalue, uint16_t *d_numer, uint16_t *d_denom,
+                      const fpm_cell_list *list, void *stream);
 /* host-buffer convenience: compare + finalize */
 int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
              uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,
@@ -334,6 +336,20 @@ int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t
                                double *m_pvalue, uint8_t *m_pass, void *stream);
 /* Rebuild the set's bucket index from its (device, borrowed) rows in place, e.g. after the
  * rows were rewritten by a new sketch run; no reallocation when the geometry is unchanged. */
+/* The compact output (fpm_dist_list_dev) against a resident set, and with its transposed grid
+ * (m_numer / m_denom cell (r, q) at r * n_qry + q, m_list its own list of cells). */
+int fpm_refset_dist_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                             const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                             uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                             double max_dist, double max_pvalue, uint16_t *d_numer,
+                             uint16_t *d_denom, const fpm_cell_list *list, void *stream);
+int fpm_refset_dist_mirror_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                                    const uint64_t *d_qry_length, uint64_t qry_stride,
+                                    uint32_t n_qry, uint32_t sketch_size, uint32_t kmer_size,
+                                    double kmer_space, double max_dist, double max_pvalue,
+                                    uint16_t *d_numer, uint16_t *d_denom,
+                                    const fpm_cell_list *list, uint16_t *m_numer,
+                                    uint16_t *m_denom, const fpm_cell_list *m_list, void *stream);
 int fpm_refset_reindex(fpm_refset *rs, void *stream);
 int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
                     const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,

@@ -96,3 +96,30 @@ def test_c5_genome_deterministic():
     a = bench.c5_genome(7, 1001)
     assert a == bench.c5_genome(7, 1001) and a != bench.c5_genome(8, 1001)
     assert len(a) == 1001 and set(a) <= set(b"ACGT")
+
+
+def test_headline_line_fits_driver_parser():
+    """The printed line is built from the full result by compact_line and stays under the
+    driver's parse limit (round 3's 26.8 KB line was not parsed).  Canned input: the full
+    result of the round-3 bench, which carries every leg."""
+    import json
+    import bench
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    full = json.load(open(os.path.join(root, "profiles", "r03", "bench_r03_head_final.json")))
+    line = bench.compact_line(full, "gpurun_out/bench_detail.json")
+    s = json.dumps(line)
+    assert len(s) < bench.MAX_LINE_BYTES
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "dtype",
+              "config", "roofline", "cpu_baseline", "parity", "higher_is_better", "scaling",
+              "vs_baseline", "data"):
+        assert k in line, k
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in line["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    assert line["parity"]["all_ok"] is True
+    assert all(isinstance(v, (bool, type(None))) for v in line["parity"].values())
+    assert line["legs"]["c4_ms_per_step"] > 0 and line["legs"]["cli_dist_wall_s"] > 0
+    # a pathological detail (huge strings) still yields a parseable line
+    full["cpu_baseline"]["sample"] = "x" * 20000
+    assert len(json.dumps(bench.compact_line(full))) < bench.MAX_LINE_BYTES

@@ -530,88 +530,103 @@ def test_sketch_merge_dev_matches_whole(ctx, oracle, s):
 
 
 @pytest.mark.parametrize("fillcnt", [False, True])
-@pytest.mark.parametrize("self_set", [True, False])
-@pytest.mark.parametrize("maxd,maxp", [(-1.0, -1.0), (1.0, 1.0), (0.5, 1.0), (1.0, 1e-10)])
-def test_dist_prefilled_equals_dist16(ctx, oracle, self_set, maxd, maxp, fillcnt):
-    """fpm_dist_prefill_dev (side stream, no list read) + fpm_dist_dev16_prefilled give the
-    same five outputs as fpm_dist_dev16, empty lists and -d / -v filters included; the
-    counts and p-values also match the oracle.  fillcnt: a context whose side fill writes the
-    numer / denom defaults (FPM_FILL_COUNTS=1, the large-grid default): a partial prefill
-    then takes a counts-only pass over its rows."""
+@pytest.mark.parametrize("data", ["self", "other", "fp"])
+@pytest.mark.parametrize("maxd,maxp", [(-1.0, -1.0), (0.5, 1.0), (1.0, 1e-10)])
+def test_dist_list_equals_dist16(ctx, oracle, data, maxd, maxp, fillcnt, dist_mode):
+    """The compact output (fpm_dist_list_dev: u16 counts of every cell + the list of cells
+    with numer > 0) expands, by the rule include/fpmash.h states for unlisted cells, to the
+    five arrays fpm_dist_dev16 writes; counts and p-values also match the oracle.  Sorted
+    sketches against themselves (the symmetric path) and against another set, unsorted -fp
+    lists, empty lists, the -d / -v filters, every dist mode, and a context whose side fill
+    writes the counts (FPM_FILL_COUNTS=1, the large-grid default)."""
     import fpmash
     from fpmash import datagen
     if fillcnt:
         os.environ["FPM_FILL_COUNTS"] = "1"
         try:
             ctx = fpmash.Context(0)
+            ctx.set_dist_mode({"auto": 0, "dense": 1, "sparse": 2}[dist_mode])
         finally:
             del os.environ["FPM_FILL_COUNTS"]
-    P = fpmash.make_params(k=21, s=500)
-    seqs = datagen.family_dna(8, 12, 1500, sub_rate=(0.0, 0.08), seed=31)
-    seqs += [b"N" * 300, b"", b"ACGT" * 3]          # lists with no k-mer: empty sketches
-    sk = ctx.sketch(P, seqs)
-    qsk = sk if self_set else sk[::-1][:60]
-    w = 500
-    R, rl = fpmash._dense(sk, w, np.uint64)
-    Q, ql = (R, rl) if self_set else fpmash._dense(qsk, w, np.uint64)
-    nr, nq = len(sk), len(qsk)
-    L = fpmash.lib()
-    bufs = []
-
-    def up(a):
-        b = fpmash.DeviceBuffer.from_array(ctx, a)
-        bufs.append(b)
-        return b.ptr
-    dR, drl = up(R), up(rl)
-    dQ, dql = (dR, drl) if self_set else (up(Q), up(ql))
-    lens = np.array([len(x) for x in seqs], np.uint64)
-    qlens = lens if self_set else lens[::-1][:60].copy()
-    dL = up(lens)
-    dqL = dL if self_set else up(qlens)
-    res = []
-    # prefilled rows: none (fpm_dist_dev16), all, and partial prefills (the call fills the
-    # other rows beside its compare; 37 leaves the rest unaligned for 16-B stores); the empty
-    # lists sit in the last query rows (self set) or the first (the reversed query set)
-    for pre in (0, nq, 37, nq // 2 // 16 * 16):
-        outs = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (2, 2, 8, 8, 1)]
-        bufs.extend(outs)
-        if pre:
-            fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr, pre, maxd, maxp, outs[2].ptr,
-                                                 outs[3].ptr, outs[4].ptr, None))
-        f = L.fpm_dist_dev16_prefilled if pre else L.fpm_dist_dev16
-        fpmash._check(f(ctx.h, dR, drl, dL, w, nr, dQ, dql, dqL, w, nq, 8, 500, 21, 4.0 ** 21,
-                        maxd, maxp, *[o.ptr for o in outs], None))
-        ctx.synchronize()
-        res.append([o.to_array(t, nr * nq) for o, t in zip(outs, (np.uint16, np.uint16,
-                                                                   np.float64, np.float64,
-                                                                   np.uint8))])
-    for other in res[1:]:
-        for a, b in zip(res[0], other):
-            assert np.array_equal(a, b)
-    # a prefill of another grid shape (fewer columns: within the buffers) is refused
-    fpmash._check(L.fpm_dist_prefill_dev(ctx.h, nr - 1, nq, maxd, maxp, outs[2].ptr,
-                                         outs[3].ptr, outs[4].ptr, None))
-    assert L.fpm_dist_dev16_prefilled(ctx.h, dR, drl, dL, w, nr, dQ, dql, dqL, w, nq, 8, 500, 21,
-                                      4.0 ** 21, maxd, maxp, *[o.ptr for o in outs], None) != 0
-    ctx.synchronize()
-    nu, de, di, pv = oracle.dist_grid(sk, list(lens), qsk, list(qlens), 500, 21, 4.0 ** 21)
-    assert np.array_equal(res[1][0], nu) and np.array_equal(res[1][1], de)
-    ok = (res[1][0] > 0)
-    assert np.allclose(res[1][3][ok], pv[ok], rtol=1e-12, atol=0)
-    for b in bufs:
-        b.free()
+    if data == "fp":
+        rng = np.random.default_rng(41)
+        sk = [rng.integers(0, 60, size=int(rng.integers(0, 400))).astype(np.uint32)
+              for _ in range(90)]
+        sk[3] = sk[3][:0]
+        qsk = sk[::-1][:50]
+        S, k, space, use64 = 300, 1, 10.0, False
+        lens = np.array([len(x) * 3 + 7 for x in sk], np.uint64)
+        qlens = lens[::-1][:50].copy()
+    else:
+        P = fpmash.make_params(k=21, s=500)
+        seqs = datagen.family_dna(8, 12, 1500, sub_rate=(0.0, 0.08), seed=31)
+        seqs += [b"N" * 300, b"", b"ACGT" * 3]          # lists with no k-mer: empty sketches
+        sk = ctx.sketch(P, seqs)
+        qsk = sk if data == "self" else sk[::-1][:60]
+        S, k, space, use64 = 500, 21, 4.0 ** 21, True
+        lens = np.array([len(x) for x in seqs], np.uint64)
+        qlens = lens if data == "self" else lens[::-1][:60].copy()
+    full = ctx.dist16(sk, qsk, S, use64=use64, k=k, kmer_space=space, ref_lengths=lens,
+                      qry_lengths=qlens, max_dist=maxd, max_pvalue=maxp)
+    comp = ctx.dist_list(sk, qsk, S, use64=use64, k=k, kmer_space=space, ref_lengths=lens,
+                         qry_lengths=qlens, max_dist=maxd, max_pvalue=maxp)
+    for key in ("numer", "denom", "distance", "pass"):
+        assert np.array_equal(comp[key], full[key]), key
+    dok = full["distance"] <= maxd if maxd >= 0 else np.ones(len(full["distance"]), bool)
+    assert np.array_equal(comp["pvalue"][dok], full["pvalue"][dok])
+    nu, de, di, pv = oracle.dist_grid(sk, list(lens), qsk, list(qlens), S, k, space, use64=use64)
+    assert np.array_equal(comp["numer"], nu) and np.array_equal(comp["denom"], de)
+    assert np.allclose(comp["distance"], di, rtol=1e-12, atol=0)
+    assert np.allclose(comp["pvalue"][dok], pv[dok], rtol=1e-12, atol=0)
+    assert (comp["numer"] > 0).any() and (comp["numer"] == 0).any()
     if fillcnt:
         ctx.close()
 
 
+def test_dist_list_capacity(ctx, oracle):
+    """A list too small for the cells with numer > 0: the count reports every cell, only
+    `cap` entries are written (no write past the buffers), and the binding refuses to fetch;
+    a re-run with cap = count lists them all."""
+    import fpmash
+    from fpmash import datagen
+    P = fpmash.make_params(k=21, s=400)
+    seqs = datagen.family_dna(4, 10, 1200, sub_rate=(0.0, 0.05), seed=8)
+    sk = ctx.sketch(P, seqs)
+    lens = [len(x) for x in seqs]
+    nu, de, listed = ctx.dist_list(sk, sk, 400, ref_lengths=lens, qry_lengths=lens,
+                                   expand=False)
+    n = int((nu > 0).sum())
+    assert len(listed["qry"]) == n and n > 50
+    with pytest.raises(fpmash.FpmError):
+        ctx.dist_list(sk, sk, 400, ref_lengths=lens, qry_lengths=lens, cap=17)
+    # the count of a short list is still the full count
+    lst = fpmash.CellList(ctx, 17)
+    R, rl = fpmash._dense(sk, 400, np.uint64)
+    bufs = [fpmash.DeviceBuffer.from_array(ctx, a) for a in (R, rl, np.array(lens, np.uint64))]
+    out = [fpmash.DeviceBuffer(ctx, len(sk) ** 2 * 2) for _ in range(2)]
+    L = fpmash.lib()
+    fpmash._check(L.fpm_dist_list_dev(ctx.h, bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, 400, len(sk),
+                                      bufs[0].ptr, bufs[1].ptr, bufs[2].ptr, 400, len(sk), 8, 400,
+                                      21, 4.0 ** 21, -1.0, -1.0, out[0].ptr, out[1].ptr, lst.ref,
+                                      None))
+    ctx.synchronize()
+    assert lst.count() == n
+    for b in bufs + out:
+        b.free()
+    lst.free()
+
+
+@pytest.mark.parametrize("compact", [False, True])
 @pytest.mark.parametrize("mode", ["sorted", "fp", "dense"])
-def test_refset_mirror_matches_oracle(ctx, oracle, mode):
+def test_refset_mirror_matches_oracle(ctx, oracle, mode, compact):
     """fpm_refset_dist_mirror_dev (the block pairs of the sharded C4 all-vs-all): the grid
     (queries x refs) and its transpose (refs as queries x the query rows as refs) both equal
     the oracle's grids of the two orientations; sorted u64 sketches take the sparse path that
     scatters the candidate results to both grids, unsorted -fp u32 lists (not symmetric under
     the literal walk) and a forced dense walk compute the transpose by the swapped call.
-    Empty lists and the -d / -v filters included."""
+    Empty lists and the -d / -v filters included.  compact: fpm_refset_dist_mirror_list_dev
+    (u16 counts of both grids + one list of numer > 0 cells per grid), expanded by the rule
+    for unlisted cells."""
     import ctypes as C
     import fpmash
     from fpmash import datagen
@@ -643,9 +658,11 @@ def test_refset_mirror_matches_oracle(ctx, oracle, mode):
     dR, drl, dRL = up(R), up(rlen), up(np.array(rl, np.uint64))
     dQ, dql, dQL = up(Q), up(qlen), up(np.array(ql, np.uint64))
     nr, nq = len(refs), len(qrys)
-    prim = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (4, 4, 8, 8, 1)]
-    mirr = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (4, 4, 8, 8, 1)]
+    cb = 2 if compact else 4
+    prim = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (cb, cb, 8, 8, 1)]
+    mirr = [fpmash.DeviceBuffer(ctx, nr * nq * b) for b in (cb, cb, 8, 8, 1)]
     keep += prim + mirr
+    lists_ = [fpmash.CellList(ctx, nr * nq), fpmash.CellList(ctx, nr * nq)]
     # the grids are small (AUTO would walk them densely): force the index path for the
     # sorted and -fp cases
     ctx.set_dist_mode(1 if mode == "dense" else 2)
@@ -656,13 +673,25 @@ def test_refset_mirror_matches_oracle(ctx, oracle, mode):
         for rep in range(2):                            # a second call after a reindex
             if rep:
                 fpmash._check(L.fpm_refset_reindex(h, None))
-            fpmash._check(L.fpm_refset_dist_mirror_dev(h, dQ, dql, dQL, w, nq, S, 4, k, space,
-                                                       0.9, 0.5, *[b.ptr for b in prim],
-                                                       *[b.ptr for b in mirr], None))
-            ctx.synchronize()
-            types = (np.uint32, np.uint32, np.float64, np.float64, np.uint8)
-            got_p = [b.to_array(t, nr * nq) for b, t in zip(prim, types)]
-            got_m = [b.to_array(t, nr * nq) for b, t in zip(mirr, types)]
+            if compact:
+                fpmash._check(L.fpm_refset_dist_mirror_list_dev(
+                    h, dQ, dql, dQL, w, nq, S, k, space, 0.9, 0.5, prim[0].ptr, prim[1].ptr,
+                    lists_[0].ref, mirr[0].ptr, mirr[1].ptr, lists_[1].ref, None))
+                ctx.synchronize()
+                got_p, got_m = [
+                    [e[x] for x in ("numer", "denom", "distance", "pvalue", "pass")] for e in (
+                        fpmash.expand_compact(bb[0].to_array(np.uint16, nr * nq),
+                                              bb[1].to_array(np.uint16, nr * nq), lst.fetch(),
+                                              n_r, 0.9, 0.5)
+                        for bb, lst, n_r in ((prim, lists_[0], nr), (mirr, lists_[1], nq)))]
+            else:
+                fpmash._check(L.fpm_refset_dist_mirror_dev(h, dQ, dql, dQL, w, nq, S, 4, k, space,
+                                                           0.9, 0.5, *[b.ptr for b in prim],
+                                                           *[b.ptr for b in mirr], None))
+                ctx.synchronize()
+                types = (np.uint32, np.uint32, np.float64, np.float64, np.uint8)
+                got_p = [b.to_array(t, nr * nq) for b, t in zip(prim, types)]
+                got_m = [b.to_array(t, nr * nq) for b, t in zip(mirr, types)]
             for got, (a, al, b, bl) in ((got_p, (refs, rl, qrys, ql)),
                                         (got_m, (qrys, ql, refs, rl))):
                 nu, de, di, pv = oracle.dist_grid(a, al, b, bl, S, k, space, use64=use64)
@@ -679,6 +708,8 @@ def test_refset_mirror_matches_oracle(ctx, oracle, mode):
         ctx.set_dist_mode(0)
         for b in keep:
             b.free()
+        for lst in lists_:
+            lst.free()
 
 
 def test_index_one_pass_holds_sketch_partitions(ctx, oracle):

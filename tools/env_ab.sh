@@ -1,6 +1,6 @@
 #!/bin/bash
-# tools/env_ab.sh "VAR=VAL[,VAR=VAL]" ... — same-box A/B of runtime switches (FPM_FILL_EARLY,
-# FPM_DENSE_IMG, ...) on the C2 step: each setting ("base" = none) runs twice, alternating,
+# tools/env_ab.sh "VAR=VAL[,VAR=VAL]" ... — same-box A/B of runtime switches (FPM_FILL_COUNTS,
+# FPM_IDX_ONEPASS, ...) on the C2 step: each setting ("base" = none) runs twice, alternating,
 # 20 timed steps each; one line per run: setting, ms/step, per-kernel averages.
 # AB_LEG=c4: the C4 leg instead (50k-sketch all-vs-all, 3 timed steps), its ms/step;
 # AB_LEG=c5: the C5 leg (tools/leg_run.py --leg c5: 1,000 x 5 Mb, one timed step).
