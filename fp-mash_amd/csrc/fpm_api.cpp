@@ -1913,7 +1913,8 @@ struct fpm_refset {
     // per-query-block host buffers (fpm_refset_dist): pinned staging + device copies
     void *h_stage = nullptr;
     size_t h_stage_bytes = 0;
-    fpm_ctx::Slot qslot[10];
+    fpm_ctx::Slot qslot[16];
+    uint64_t list_cap = 0;        // entries the device list slots (qslot 10-15) hold
 };
 
 static hipError_t slot_buf(fpm_ctx::Slot &s, size_t bytes, void **out)
@@ -2671,19 +2672,35 @@ int fpm_refset_dist_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry
                          stream, "fpm_refset_dist_dev", rs);
 }
 
+}  // extern "C"
+
+static int refset_list_impl(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
+                            const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
+                            uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                            double max_dist, double max_pvalue, uint32_t count_bytes,
+                            void *d_numer, void *d_denom, const fpm_cell_list *list, void *stream,
+                            const char *who)
+{
+    if (int rc = refset_check(rs, sketch_size, count_bytes, who)) return rc;
+    DistOut o;
+    if (int rc = list_out(d_numer, d_denom, count_bytes == 2, list, o, who)) return rc;
+    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
+                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
+                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue, o, stream, who,
+                         rs);
+}
+
+extern "C" {
+
 int fpm_refset_dist_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
                              const uint64_t *d_qry_length, uint64_t qry_stride, uint32_t n_qry,
                              uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
                              double max_dist, double max_pvalue, uint16_t *d_numer,
                              uint16_t *d_denom, const fpm_cell_list *list, void *stream)
 {
-    if (int rc = refset_check(rs, sketch_size, 2, "fpm_refset_dist_list_dev")) return rc;
-    DistOut o;
-    if (int rc = list_out(d_numer, d_denom, true, list, o, "fpm_refset_dist_list_dev")) return rc;
-    return dist_dev_impl(rs->ctx, rs->ref, rs->ref_len, rs->ref_length, rs->ref_stride, rs->n_ref,
-                         d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, rs->hash_bytes,
-                         sketch_size, kmer_size, kmer_space, max_dist, max_pvalue, o, stream,
-                         "fpm_refset_dist_list_dev", rs);
+    return refset_list_impl(rs, d_qry, d_qry_len, d_qry_length, qry_stride, n_qry, sketch_size,
+                            kmer_size, kmer_space, max_dist, max_pvalue, 2, d_numer, d_denom,
+                            list, stream, "fpm_refset_dist_list_dev");
 }
 
 static int mirror_check(fpm_refset *rs, const void *d_qry, const char *who)
@@ -2787,6 +2804,80 @@ int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
     if (out_pvalue) HIP_TRY(copy_out(ctx, out_pvalue, pv, np * 8));
     if (out_pass) HIP_TRY(copy_out(ctx, out_pass, pa, np));
     return FPM_OK;
+}
+
+int fpm_refset_dist_list(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
+                         const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                         double max_dist, double max_pvalue, uint32_t count_bytes,
+                         void *out_numer, void *out_denom, uint32_t *l_qry, uint32_t *l_ref,
+                         double *l_dist, double *l_pvalue, uint8_t *l_pass, uint64_t cap,
+                         uint64_t *n_listed)
+{
+    if (!rs) return fail(FPM_EINVAL, "refset_dist_list: null set");
+    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
+    if (!n_listed) return fail(FPM_EINVAL, "refset_dist_list: null n_listed");
+    *n_listed = 0;
+    fpm_ctx *ctx = rs->ctx;
+    if (int rc = set_device(ctx)) return rc;
+    const uint64_t np = (uint64_t)rs->n_ref * n_qry;
+    if (np == 0) return FPM_OK;
+    hipStream_t st = ctx->stream;
+    void *q, *ql, *qL, *nu, *de;
+    const size_t qb = std::max<size_t>(16, (size_t)n_qry * qry_stride * rs->hash_bytes);
+    HIP_TRY(slot_buf(rs->qslot[0], qb, &q));
+    HIP_TRY(slot_buf(rs->qslot[1], (size_t)n_qry * 4, &ql));
+    HIP_TRY(slot_buf(rs->qslot[2], (size_t)n_qry * 8, &qL));
+    HIP_TRY(slot_buf(rs->qslot[3], np * count_bytes, &nu));
+    HIP_TRY(slot_buf(rs->qslot[4], np * count_bytes, &de));
+    HIP_TRY(hipStreamSynchronize(st));            // the query slots are free to overwrite
+    HIP_TRY(copy_in(ctx, q, qry, (size_t)n_qry * qry_stride * rs->hash_bytes));
+    HIP_TRY(copy_in(ctx, ql, qry_len, (size_t)n_qry * 4));
+    if (qry_length)
+        HIP_TRY(copy_in(ctx, qL, qry_length, (size_t)n_qry * 8));
+    else
+        HIP_TRY(hipMemsetAsync(qL, 0, (size_t)n_qry * 8, st));
+    // the device list: grown (and the call repeated) when the cells sharing hashes outnumber it
+    uint64_t want = std::max<uint64_t>(rs->list_cap, std::max<uint64_t>(4096, np / 32));
+    for (;;) {
+        fpm_cell_list L{};
+        void *p[6];
+        const size_t eb[6] = {4, 4, 8, 8, 1, 0};
+        for (int i = 0; i < 5; i++) HIP_TRY(slot_buf(rs->qslot[10 + i], want * eb[i], &p[i]));
+        HIP_TRY(slot_buf(rs->qslot[15], 8, &p[5]));
+        rs->list_cap = want;
+        L.qry = (uint32_t *)p[0];
+        L.ref = (uint32_t *)p[1];
+        L.dist = (double *)p[2];
+        L.pvalue = (double *)p[3];
+        L.pass = (uint8_t *)p[4];
+        L.cap = want;
+        L.count = (uint64_t *)p[5];
+        if (int rc = refset_list_impl(rs, q, (const uint32_t *)ql, (const uint64_t *)qL,
+                                      qry_stride, n_qry, sketch_size, kmer_size, kmer_space,
+                                      max_dist, max_pvalue, count_bytes, nu, de, &L, st,
+                                      "fpm_refset_dist_list"))
+            return rc;
+        uint64_t cnt = 0;
+        HIP_TRY(hipMemcpyAsync(&cnt, L.count, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (cnt > want) {
+            want = cnt + cnt / 8;
+            continue;
+        }
+        *n_listed = cnt;
+        const uint64_t m = std::min<uint64_t>(cnt, cap);
+        if (out_numer) HIP_TRY(copy_out(ctx, out_numer, nu, np * count_bytes));
+        if (out_denom) HIP_TRY(copy_out(ctx, out_denom, de, np * count_bytes));
+        if (m) {
+            if (l_qry) HIP_TRY(copy_out(ctx, l_qry, L.qry, m * 4));
+            if (l_ref) HIP_TRY(copy_out(ctx, l_ref, L.ref, m * 4));
+            if (l_dist) HIP_TRY(copy_out(ctx, l_dist, L.dist, m * 8));
+            if (l_pvalue) HIP_TRY(copy_out(ctx, l_pvalue, L.pvalue, m * 8));
+            if (l_pass) HIP_TRY(copy_out(ctx, l_pass, L.pass, m));
+        }
+        return FPM_OK;
+    }
 }
 
 void fpm_refset_free(fpm_refset *rs)

@@ -124,6 +124,10 @@ SYMBOLS = [
     ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),
+    ("fpm_refset_dist_list", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
+                                       C.c_uint32, C.c_double, C.c_double, C.c_double,
+                                       C.c_uint32, vp, vp, u32p, u32p, f64p, f64p, u8p,
+                                       C.c_uint64, u64p]),
     ("fpm_refset_free", None, [vp]),
     ("fpm_sketch_merge_dev", C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, vp, vp, vp]),
     ("fpm_seq_parse", C.c_int, [vp, C.POINTER(C.c_char_p), u64p, C.c_uint32, C.POINTER(vp),

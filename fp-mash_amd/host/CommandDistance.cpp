@@ -24,6 +24,7 @@
 #include <thread>
 
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -107,6 +108,66 @@ inline char *uTo(char *p, uint64_t x)
     memcpy(p, t + 20 - n, n);
     return p + n;
 }
+
+// Output into a shared mapping of the stdout file: windows of 1 GiB mapped on first use, the
+// file extended (ftruncate) before each block's pieces are copied in.  Page faults of a
+// mapping run in parallel, where write() / pwrite() to one file serialise on its inode lock.
+class MappedOut {
+  public:
+    bool open(int ofd)
+    {
+        char path[64];
+        snprintf(path, sizeof path, "/proc/self/fd/%d", ofd);
+        fd_ = ::open(path, O_RDWR);   // the same file, opened for reading too (mmap needs it)
+        return fd_ >= 0;
+    }
+    bool extend(off_t size) { return ftruncate(fd_, size) == 0; }
+    void put(off_t at, const char *src, size_t n)
+    {
+        while (n) {
+            const size_t w = (size_t)at / kWin, off = (size_t)at % kWin;
+            const size_t c = std::min(n, kWin - off);
+            char *base = window(w);
+            // populate the range's pages writable in one call (MADV_POPULATE_WRITE, Linux >=
+            // 5.14; where the kernel lacks it the copy takes the faults)
+            const uintptr_t a0 = (uintptr_t)(base + off) & ~(uintptr_t)4095;
+            const uintptr_t a1 = (uintptr_t)(base + off + c);
+            (void)madvise((void *)a0, a1 - a0, 23);
+            memcpy(base + off, src, c);
+            at += (off_t)c;
+            src += c;
+            n -= c;
+        }
+    }
+    void close()
+    {
+        for (char *p : wins_)
+            if (p) munmap(p, kWin);
+        wins_.clear();
+        if (fd_ >= 0) ::close(fd_);
+        fd_ = -1;
+    }
+
+  private:
+    static constexpr size_t kWin = size_t(1) << 30;
+    char *window(size_t w)
+    {
+        std::lock_guard<std::mutex> g(mu_);
+        if (wins_.size() <= w) wins_.resize(w + 1, nullptr);
+        if (!wins_[w]) {
+            void *p = mmap(nullptr, kWin, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, (off_t)(w * kWin));
+            if (p == MAP_FAILED) {
+                std::cerr << "ERROR: mapping the distance output failed." << std::endl;
+                fatalExit();
+            }
+            wins_[w] = (char *)p;
+        }
+        return wins_[w];
+    }
+    int fd_ = -1;
+    std::mutex mu_;
+    std::vector<char *> wins_;
+};
 
 }  // namespace
 
@@ -238,9 +299,8 @@ int CommandDistance::run() const
     for (uint64_t i = 0; i < nR; i++) width = std::max<uint64_t>(width, sketchRef.getReference(i).hashes.size());
     for (uint64_t i = 0; i < nQ; i++) width = std::max<uint64_t>(width, sketchQuery.getReference(i).hashes.size());
     const int nDev = nR && nQ ? deviceCount() : 0;
-    // 1 M pairs per block: 29 MB of pinned results per slot (16 M-pair slots made pinning and
-    // unpinning ~1.4 GB cost ~0.6 s of the C2 command; C2 `dist` wall: 4 M 1.27 s, 2 M 1.15 s,
-    // 1 M 1.06-1.09 s, 512 K 1.50 s)
+    // 1 M pairs per block (16 M-pair slots made pinning and unpinning the slots cost ~0.6 s of
+    // the C2 command; C2 `dist` wall: 4 M 1.27 s, 2 M 1.15 s, 1 M 1.06-1.09 s, 512 K 1.50 s)
     uint64_t blockPairs = 1ULL << 20;
     if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
     const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
@@ -248,10 +308,21 @@ int CommandDistance::run() const
     const int nSlots = std::max(2, 2 * nDev + 1);
     const int nFmt = std::max(1, std::min(parameters.parallelism > 1 ? parameters.parallelism
                                           : (int)std::thread::hardware_concurrency(), 64));
+    // A block's results in the compact form (fpm_refset_dist_list): u16 numer / denom of
+    // every pair, and distance / p-value / pass of the pairs that share hashes (numer > 0); a
+    // pair sharing none has distance 1 (0 for two empty sketches) and p-value 1
+    // (CommandDistance.cpp:404-408, 435-437), its line needs nothing else.  4 B per pair over
+    // PCIe instead of 21.
+    // u16 counts (every count is <= the sketch size), u32 past 65535
+    const uint32_t cb = sketchSize <= 65535 ? 2 : 4;
     struct Slot {
-        uint32_t *nu = nullptr, *de = nullptr;
-        double *di = nullptr, *pv = nullptr;
-        uint8_t *pa = nullptr;
+        void *nu = nullptr, *de = nullptr;
+        uint32_t *lq = nullptr, *lr = nullptr;
+        double *ld = nullptr, *lp = nullptr;
+        uint8_t *la = nullptr;
+        uint64_t cap = 0, nl = 0;           // listed cells: room, count
+        std::vector<uint32_t> rowStart;     // per query row of the block: its listed cells,
+        std::vector<uint32_t> byRow;        // ordered by reference (indexes into l*)
         int dev = 0;
         uint64_t b = ~0ULL;                 // block held
         std::vector<std::string> text;      // formatted pieces
@@ -264,19 +335,29 @@ int CommandDistance::run() const
     uint64_t written = 0;                   // blocks already written out
     std::deque<std::function<void()>> tasks;
     bool stop = false;
+    auto allocList = [&](Slot &sl, uint64_t cap) {
+        fpm_ctx *c = device(0);
+        for (void *p : {(void *)sl.lq, (void *)sl.lr, (void *)sl.ld, (void *)sl.lp, (void *)sl.la})
+            if (p) fpm_host_free(c, p);
+        sl.cap = cap;
+        check(fpm_host_alloc(c, (void **)&sl.lq, cap * 4), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.lr, cap * 4), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.ld, cap * 8), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.lp, cap * 8), "pinned buffers");
+        check(fpm_host_alloc(c, (void **)&sl.la, cap), "pinned buffers");
+    };
     // pinned result buffers (page locking costs ~0.6 ms per MB): one thread per slot, beside
-    // the row packing and the reference sets
+    // the row packing and the reference sets.  The list starts at 1/16 of the block's pairs
+    // and grows when a block lists more.
     std::vector<std::thread> pinner;
     for (int i = 0; i < nSlots && nBlocks; i++)
         pinner.emplace_back([&, i] {
             Slot &sl = slots[i];
             const uint64_t np = block * nR;
             fpm_ctx *c = device(0);
-            check(fpm_host_alloc(c, (void **)&sl.nu, np * 4), "pinned buffers");
-            check(fpm_host_alloc(c, (void **)&sl.de, np * 4), "pinned buffers");
-            check(fpm_host_alloc(c, (void **)&sl.di, np * 8), "pinned buffers");
-            check(fpm_host_alloc(c, (void **)&sl.pv, np * 8), "pinned buffers");
-            check(fpm_host_alloc(c, (void **)&sl.pa, np), "pinned buffers");
+            check(fpm_host_alloc(c, &sl.nu, np * cb), "pinned buffers");
+            check(fpm_host_alloc(c, &sl.de, np * cb), "pinned buffers");
+            allocList(sl, std::max<uint64_t>(4096, np / 16));
         });
     std::unique_ptr<HostRows<uint8_t>> R, Qown;
     std::vector<uint32_t> rl, qlOwn;
@@ -290,8 +371,8 @@ int CommandDistance::run() const
     // The grid in query blocks (CommandDistance.cpp:224-261 chunks it for the pool): every
     // device holds the reference set with its index built once (fpm_refset_create) and takes
     // blocks in turn; results land in pinned buffers; formatter threads (-p) turn each block
-    // into text pieces, which this thread writes strictly in block order (writeOutput,
-    // :276-333, consumes the pool's outputs in order).
+    // into text pieces, which are written strictly in block order (writeOutput, :276-333,
+    // consumes the pool's outputs in order).
     std::vector<fpm_refset *> sets(nDev, nullptr);
     for (int d = 0; d < nDev; d++)
         check(fpm_refset_create(device(d), R->data(), rl.data(), rL.data(), width, (uint32_t)nR,
@@ -306,6 +387,9 @@ int CommandDistance::run() const
         refTag[j] = rr.name;
         if (comment) { refTag[j].push_back(':'); refTag[j] += rr.comment; }
     }
+    // the -d / -v filters at the values of a pair sharing no hash (compareSketches, :421-429)
+    const bool passNone = !(distanceMax >= 0 && 1.0 > distanceMax) && !(pValueMax >= 0 && 1.0 > pValueMax);
+    const bool passEmpty = !(pValueMax >= 0 && 1.0 > pValueMax);   // distance 0: two empty sketches
     auto format = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, std::string &dst) {
         char line[512];
         Out o;
@@ -322,12 +406,27 @@ int CommandDistance::run() const
                 if (comment) { qtail.push_back(':'); qtail += qr.comment; }
                 qtail.push_back('\t');
             }
+            uint32_t cur = sl.rowStart[qi];   // the row's listed cells, in reference order
             for (uint64_t j = 0; j < nR; j++) {
                 const uint64_t k = qi * nR + j;
+                const uint32_t nm = cb == 2 ? ((const uint16_t *)sl.nu)[k] : ((const uint32_t *)sl.nu)[k];
+                const uint32_t dn = cb == 2 ? ((const uint16_t *)sl.de)[k] : ((const uint32_t *)sl.de)[k];
+                double di, pv;
+                bool pa;
+                if (nm == 0) {
+                    di = dn == 0 ? 0.0 : 1.0;
+                    pv = 1.0;
+                    pa = dn == 0 ? passEmpty : passNone;
+                } else {
+                    const uint32_t e = sl.byRow[cur++];
+                    di = sl.ld[e];
+                    pv = sl.lp[e];
+                    pa = sl.la[e] != 0;
+                }
                 if (table) {
                     o.put('\t');
-                    if (sl.pa[k]) o.num(sl.di[k]);
-                } else if (sl.pa[k]) {
+                    if (pa) o.num(di);
+                } else if (pa) {
                     const std::string &tag = refTag[j];
                     if (tag.size() + qtail.size() + kLineNums <= sizeof(line)) {
                         // one append per line: the line is assembled in a stack buffer
@@ -336,26 +435,26 @@ int CommandDistance::run() const
                         p += tag.size();
                         memcpy(p, qtail.data(), qtail.size());
                         p += qtail.size();
-                        p = numTo(p, sl.di[k]);
+                        p = numTo(p, di);
                         *p++ = '\t';
-                        p = numTo(p, sl.pv[k]);
+                        p = numTo(p, pv);
                         *p++ = '\t';
-                        p = uTo(p, sl.nu[k]);
+                        p = uTo(p, nm);
                         *p++ = '/';
-                        p = uTo(p, sl.de[k]);
+                        p = uTo(p, dn);
                         *p++ = '\n';
                         o.buf.append(line, (size_t)(p - line));
                         continue;
                     }
                     o.put(tag);
                     o.put(qtail);
-                    o.num(sl.di[k]);
+                    o.num(di);
                     o.put('\t');
-                    o.num(sl.pv[k]);
+                    o.num(pv);
                     o.put('\t');
-                    o.u(sl.nu[k]);
+                    o.u(nm);
                     o.put('/');
-                    o.u(sl.de[k]);
+                    o.u(dn);
                     o.put('\n');
                 }
             }
@@ -392,11 +491,31 @@ int CommandDistance::run() const
                     cv.wait(lk, [&] { return written + nSlots > b; });
                 }
                 const uint64_t q0 = b * block, nq = std::min(block, nQ - q0);
-                check(fpm_refset_dist(sets[d], Q + q0 * width * hb, ql.data() + q0,
-                                      qL.data() + q0, width, (uint32_t)nq, (uint32_t)sketchSize,
-                                      (uint32_t)sketchRef.getKmerSize(), sketchRef.getKmerSpace(),
-                                      distanceMax, pValueMax, sl.nu, sl.de, sl.di, sl.pv, sl.pa),
-                      "dist");
+                for (;;) {
+                    check(fpm_refset_dist_list(sets[d], Q + q0 * width * hb, ql.data() + q0,
+                                               qL.data() + q0, width, (uint32_t)nq,
+                                               (uint32_t)sketchSize,
+                                               (uint32_t)sketchRef.getKmerSize(),
+                                               sketchRef.getKmerSpace(), distanceMax, pValueMax,
+                                               cb, sl.nu, sl.de, sl.lq, sl.lr, sl.ld, sl.lp, sl.la,
+                                               sl.cap, &sl.nl),
+                          "dist");
+                    if (sl.nl <= sl.cap) break;
+                    allocList(sl, sl.nl + sl.nl / 4);      // more pairs share hashes: room
+                }
+                // the listed cells by query row, each row's in reference order (the device
+                // lists them unordered)
+                sl.rowStart.assign(nq + 1, 0);
+                for (uint64_t e = 0; e < sl.nl; e++) sl.rowStart[sl.lq[e] + 1]++;
+                for (uint64_t i = 0; i < nq; i++) sl.rowStart[i + 1] += sl.rowStart[i];
+                sl.byRow.resize(sl.nl);
+                {
+                    std::vector<uint32_t> fill(sl.rowStart.begin(), sl.rowStart.end() - 1);
+                    for (uint64_t e = 0; e < sl.nl; e++) sl.byRow[fill[sl.lq[e]]++] = (uint32_t)e;
+                }
+                for (uint64_t i = 0; i < nq; i++)
+                    std::sort(sl.byRow.begin() + sl.rowStart[i], sl.byRow.begin() + sl.rowStart[i + 1],
+                              [&](uint32_t x, uint32_t y) { return sl.lr[x] < sl.lr[y]; });
                 // pieces of ~1 M pairs (at least one query row) for the formatter threads
                 const uint64_t per = std::max<uint64_t>(1, (1ULL << 20) / nR);
                 const uint64_t parts = (nq + per - 1) / per;
@@ -424,8 +543,10 @@ int CommandDistance::run() const
                 cv.notify_all();
             }
         });
-    // stdout a regular file (not O_APPEND): the pieces of a block go out as pwrite()s at their
-    // offsets from the formatter threads; otherwise (pipes, terminals) this thread writes them
+    // stdout a regular file (not O_APPEND): the pieces of a block are copied into a shared
+    // mapping of the file at their offsets by the formatter threads (write() / pwrite() to one
+    // file hold its inode lock: 4.1 GB of C2 text went out one writer at a time); the file is
+    // extended block by block.  Otherwise (pipes, terminals) this thread writes the pieces.
     out.flush();
     fflush(stdout);
     const int ofd = fileno(stdout);
@@ -434,6 +555,9 @@ int CommandDistance::run() const
     off_t opos = -1;
     const bool direct = nBlocks && fstat(ofd, &ost) == 0 && S_ISREG(ost.st_mode) && ofl >= 0 &&
                         !(ofl & O_APPEND) && (opos = lseek(ofd, 0, SEEK_CUR)) >= 0;
+    MappedOut mapped;
+    const char *wm = getenv("FPMASH_DIST_WRITE");   // A/B: "pwrite" keeps the pwrite path
+    const bool useMap = direct && !(wm && strcmp(wm, "pwrite") == 0) && mapped.open(ofd);
     std::atomic<bool> writeFailed{false};
     double waitMs = 0, writeMs = 0;
     for (uint64_t b = 0; b < nBlocks; b++) {
@@ -448,16 +572,24 @@ int CommandDistance::run() const
         auto t1 = std::chrono::steady_clock::now();
         if (direct) {
             int left = (int)pieces.size();
+            off_t end = opos;
+            for (auto &t : pieces) end += (off_t)t.size();
+            if (useMap && !mapped.extend(end)) writeFailed = true;
             {
                 std::lock_guard<std::mutex> lk(mu);
                 for (auto &t : pieces) {
                     const off_t at = opos;
                     opos += (off_t)t.size();
                     tasks.emplace_front([&, at, piece = &t] {
-                        for (size_t q = 0; q < piece->size();) {
-                            const ssize_t w = pwrite(ofd, piece->data() + q, piece->size() - q, at + (off_t)q);
-                            if (w <= 0) { writeFailed = true; break; }
-                            q += (size_t)w;
+                        if (useMap) {
+                            if (!writeFailed) mapped.put(at, piece->data(), piece->size());
+                        } else {
+                            for (size_t q = 0; q < piece->size();) {
+                                const ssize_t w = pwrite(ofd, piece->data() + q, piece->size() - q,
+                                                         at + (off_t)q);
+                                if (w <= 0) { writeFailed = true; break; }
+                                q += (size_t)w;
+                            }
                         }
                         std::lock_guard<std::mutex> lk2(mu);
                         --left;
@@ -483,14 +615,16 @@ int CommandDistance::run() const
         }
         cv.notify_all();
     }
+    if (useMap) mapped.close();
     if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
     if (writeFailed) {
         std::cerr << "ERROR: writing the distance output failed." << std::endl;
         fatalExit();
     }
     if (timingOn())
-        fprintf(stderr, "[fpmash] writer: waited %.1f ms for blocks, wrote for %.1f ms\n", waitMs,
-                writeMs);
+        fprintf(stderr, "[fpmash] writer waiting for blocks: %.1f ms\n[fpmash] writer copying "
+                        "pieces out (%s): %.1f ms\n", waitMs,
+                useMap ? "mapped file" : direct ? "pwrite" : "stdout", writeMs);
     phaseMark("blocks computed, formatted and written");
     for (auto &t : gpu) t.join();
     {
@@ -499,11 +633,15 @@ int CommandDistance::run() const
     }
     cv.notify_all();
     for (auto &t : fmt) t.join();
-    for (auto &sl : slots)
-        for (void *ptr : {(void *)sl.nu, (void *)sl.de, (void *)sl.di, (void *)sl.pv,
-                          (void *)sl.pa})
-            if (ptr) fpm_host_free(device(0), ptr);
-    for (auto *rs : sets) fpm_refset_free(rs);
+    if (cleanExit()) {
+        // (the process otherwise leaves by _exit once the output is flushed: unpinning the
+        // slots cost ~50 ms of the C2 command)
+        for (auto &sl : slots)
+            for (void *ptr : {sl.nu, sl.de, (void *)sl.lq, (void *)sl.lr,
+                              (void *)sl.ld, (void *)sl.lp, (void *)sl.la})
+                if (ptr) fpm_host_free(device(0), ptr);
+        for (auto *rs : sets) fpm_refset_free(rs);
+    }
     out.flush();
     fflush(stdout);
     if (warningCount > 0 && !parameters.reads)

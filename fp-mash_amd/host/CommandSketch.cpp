@@ -1,6 +1,7 @@
 // CommandSketch.cpp — `fpmash sketch` (CommandSketch.cpp:19-122): same options,
 // messages and .msh output; sketching runs on the MI355X.
 #include "Command.h"
+#include "Timing.h"
 #include "Device.h"
 #include "Sketch.h"
 
@@ -71,8 +72,7 @@ int CommandSketch::run() const
     if (!hasSuffix(prefix, suffixSketch)) prefix += suffixSketch;
     std::cerr << "Writing to " << prefix << "..." << std::endl;
     sketch.writeToMsh(prefix);
-    const char *clean = getenv("FPMASH_CLEAN_EXIT");
-    if (!(clean && *clean && *clean != '0')) (void)owned.release();
+    if (!cleanExit()) (void)owned.release();
     return 0;
 }
 

@@ -18,6 +18,17 @@ inline bool timingOn()
     return on;
 }
 
+// FPMASH_CLEAN_EXIT=1: the full teardown at exit (contexts, pinned buffers); otherwise a
+// command leaves by _exit once its outputs are flushed (main.cpp)
+inline bool cleanExit()
+{
+    static const bool on = [] {
+        const char *v = getenv("FPMASH_CLEAN_EXIT");
+        return v && *v && *v != '0';
+    }();
+    return on;
+}
+
 // prints the time since the previous mark (or since the first call) under `what`
 inline void phaseMark(const char *what)
 {

@@ -24,8 +24,7 @@ int main(int argc, const char **argv)
     // without the HIP runtime's teardown (context, stream and code-object release run from
     // atexit and the library destructors), which the kernel driver does with the process
     // anyway.  FPMASH_CLEAN_EXIT=1 keeps the full teardown.
-    const char *clean = getenv("FPMASH_CLEAN_EXIT");
-    if (!(clean && *clean && *clean != '0')) {
+    if (!fpmhost::cleanExit()) {
         std::cout.flush();
         std::cerr.flush();
         fflush(nullptr);

@@ -356,6 +356,18 @@ int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
                     uint32_t sketch_size, uint32_t kmer_size, double kmer_space, double max_dist,
                     double max_pvalue, uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
                     double *out_pvalue, uint8_t *out_pass);
+/* The compact output of one host query block (fpm_refset_dist_list_dev with host buffers):
+ * out_numer / out_denom (n_qry x n_ref cells of count_bytes = 2 (u16, sketch_size <= 65535)
+ * or 4 (u32), query-major, may be NULL) and the cells with numer > 0 (l_* arrays of cap
+ * entries, any may be NULL).  *n_listed = the number of such cells; only the first
+ * min(*n_listed, cap) are copied (the device list grows as needed). */
+int fpm_refset_dist_list(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
+                         const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
+                         uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
+                         double max_dist, double max_pvalue, uint32_t count_bytes,
+                         void *out_numer, void *out_denom, uint32_t *l_qry, uint32_t *l_ref,
+                         double *l_dist, double *l_pvalue, uint8_t *l_pass, uint64_t cap,
+                         uint64_t *n_listed);
 void fpm_refset_free(fpm_refset *rs);
 
 /* pinned (page-locked) host memory for staging buffers of the host-buffer calls */
