@@ -767,6 +767,18 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     dst = ctx.last_dist_stats()
     cand = grp.sum(dst["candidates"])
     run(True)                                   # one more step, phase-timed (not in el)
+    # and one with per-kernel HIP events (the event records add markers between launches)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    run(False)
+    ctx.synchronize()
+    ctx.set_timing(False)
+    kt = {}
+    for kid, name in fpmash.KERNEL_NAMES.items():
+        tot, cnt_ = ctx.kernel_time(kid)
+        if cnt_:
+            kt[name] = {"ms": tot, "launches": cnt_}
+    ctx.reset_timing()
     par = None
     if parity and (rank == 0 or parity == "all"):
         # the CPU leg's checker: sampled rows of each of this rank's grids (and their
@@ -819,6 +831,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "listed_pairs_all_ranks": listed,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
+            "kernels_rank0": kt,
             "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
             "jobs_rank0": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                            for j in jobs], "cells_rank0": cells,

@@ -1468,14 +1468,29 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     uint32_t n_ref, const uint32_t *__restrict__ qry_len, uint32_t n_qry,
     const uint32_t *__restrict__ ublk, const uint32_t *__restrict__ usize,
     const uint16_t *__restrict__ bimg, uint32_t Wimg, uint32_t S, uint32_t W,
-    C *__restrict__ numer, C *__restrict__ denom)
+    uint32_t nrb, C *__restrict__ numer, C *__restrict__ denom)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds32[];
     uint16_t *img = reinterpret_cast<uint16_t *>(lds32);
     constexpr int kPer = (kImgTile * kImgMaxW + 1023) / 1024;   // ref values per thread (<= 32)
     const uint32_t Wp = img_row_u16(W, BLK);
-    const uint32_t t = threadIdx.x, r0 = blockIdx.x * kImgTile, qb = blockIdx.y,
-                   q0 = qb * kImgTile;
+    // XCD-aware tiles: workgroup b runs on XCD b % 8, and each XCD owns a fixed range of ~nrb / 8
+    // ref blocks, which it sweeps for one query block after another: its ref rows (~2.5 MB at
+    // C3's 5,000 x 1,000 u32) stay in the XCD's 4 MB L2 for every query block, and a query
+    // block's union and images are fetched once per XCD (row-major tiles re-read every ref block
+    // from the fabric once per query block: 7.6 GB per C3 launch)
+    uint32_t rb, qb;
+    {
+        const uint32_t x = blockIdx.x % kXcds, k = blockIdx.x / kXcds;
+        const uint32_t per = (nrb + kXcds - 1) / kXcds;          // ref blocks per XCD (max)
+        const uint32_t lo = x * per, hi = min(nrb, lo + per);
+        if (lo >= hi) return;
+        const uint32_t mine = hi - lo;
+        qb = k / per;
+        rb = lo + (k - qb * per);
+        if (k - qb * per >= mine || qb >= (n_qry + kImgTile - 1) / kImgTile) return;
+    }
+    const uint32_t t = threadIdx.x, r0 = rb * kImgTile, q0 = qb * kImgTile;
     const uint32_t us = usize[2 * qb], maxb = usize[2 * qb + 1];
     const uint32_t nv = kImgTile * W;
     uint32_t *dirL = lds32 + kImgNP;
@@ -1678,9 +1693,12 @@ static hipError_t compare_grid_img_c(const uint32_t *ref, const uint32_t *ref_le
         return e;
     hipLaunchKernelGGL(qblock_union_kernel, dim3(nqb), dim3(1024), lds_u, st, qry, qry_len,
                        qry_stride, n_qry, W, Wimg, ublk, usize, bimg);
-    hipLaunchKernelGGL((compare_grid_img_kernel<kBlk, C>), dim3(nrb, nqb), dim3(1024), lds_t, st,
-                       ref, ref_len, ref_stride, n_ref, qry_len, n_qry, (const uint32_t *)ublk,
-                       (const uint32_t *)usize, (const uint16_t *)bimg, Wimg, S, W, numer, denom);
+    // a 1-D grid of kXcds x (ref blocks per XCD x query blocks) tiles (the kernel's tile map)
+    const uint32_t per = (nrb + kXcds - 1) / kXcds;
+    hipLaunchKernelGGL((compare_grid_img_kernel<kBlk, C>), dim3(kXcds * per * nqb, 1), dim3(1024),
+                       lds_t, st, ref, ref_len, ref_stride, n_ref, qry_len, n_qry,
+                       (const uint32_t *)ublk, (const uint32_t *)usize, (const uint16_t *)bimg,
+                       Wimg, S, W, nrb, numer, denom);
     return hipGetLastError();
 }
 

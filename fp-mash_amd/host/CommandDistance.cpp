@@ -109,9 +109,14 @@ inline char *uTo(char *p, uint64_t x)
     return p + n;
 }
 
-// Output into a shared mapping of the stdout file: windows of 1 GiB mapped on first use, the
-// file extended (ftruncate) before each block's pieces are copied in.  Page faults of a
-// mapping run in parallel, where write() / pwrite() to one file serialise on its inode lock.
+// Output into a shared mapping of the stdout file: windows of 1 GiB mapped on first use.  The
+// file's pages are allocated ahead of the copies by a thread of its own (fallocate in 64 MB
+// steps, up to kAhead past the last block handed out; the excess is cut at the end): pages
+// first touched through the mapping cost a fault each, and faults on one tmpfs file
+// serialise (4 GB into /dev/shm on the MI355X box: 3.5 GB/s faulting, 8-9 GB/s into
+// fallocated pages, 5.6-6.1 GB/s by one pwrite stream: tools/micro/write_rate.cpp).  Page
+// faults of a mapping run in parallel, where write() / pwrite() to one file serialise on its
+// inode lock.
 class MappedOut {
   public:
     bool open(int ofd)
@@ -119,17 +124,29 @@ class MappedOut {
         char path[64];
         snprintf(path, sizeof path, "/proc/self/fd/%d", ofd);
         fd_ = ::open(path, O_RDWR);   // the same file, opened for reading too (mmap needs it)
-        return fd_ >= 0;
+        if (fd_ < 0) return false;
+        struct stat st {};
+        if (fstat(fd_, &st) == 0) size_ = want_ = st.st_size;
+        alloc_ = std::thread([this] { allocate(); });
+        return true;
     }
-    bool extend(off_t size) { return ftruncate(fd_, size) == 0; }
+    // the file allocated up to `upto` (waits for the allocator thread), and asked ahead
+    bool extend(off_t upto)
+    {
+        std::unique_lock<std::mutex> lk(amu_);
+        want_ = std::max(want_, upto + kAhead);
+        acv_.notify_all();
+        acv_.wait(lk, [&] { return size_ >= upto || failed_; });
+        return !failed_;
+    }
     void put(off_t at, const char *src, size_t n)
     {
         while (n) {
             const size_t w = (size_t)at / kWin, off = (size_t)at % kWin;
             const size_t c = std::min(n, kWin - off);
             char *base = window(w);
-            // populate the range's pages writable in one call (MADV_POPULATE_WRITE, Linux >=
-            // 5.14; where the kernel lacks it the copy takes the faults)
+            // map the range's (allocated) pages writable in one call (MADV_POPULATE_WRITE,
+            // Linux >= 5.14; where the kernel lacks it the copy takes the faults)
             const uintptr_t a0 = (uintptr_t)(base + off) & ~(uintptr_t)4095;
             const uintptr_t a1 = (uintptr_t)(base + off + c);
             (void)madvise((void *)a0, a1 - a0, 23);
@@ -139,17 +156,46 @@ class MappedOut {
             n -= c;
         }
     }
-    void close()
+    // unmap, and cut the file to the bytes written (drops the pages allocated ahead)
+    bool close(off_t final_size)
     {
+        {
+            std::lock_guard<std::mutex> lk(amu_);
+            stop_ = true;
+        }
+        acv_.notify_all();
+        if (alloc_.joinable()) alloc_.join();
         for (char *p : wins_)
             if (p) munmap(p, kWin);
         wins_.clear();
-        if (fd_ >= 0) ::close(fd_);
+        const bool ok = !failed_ && ftruncate(fd_, final_size) == 0;
+        ::close(fd_);
         fd_ = -1;
+        return ok;
     }
 
   private:
     static constexpr size_t kWin = size_t(1) << 30;
+    static constexpr off_t kStep = off_t(64) << 20, kAhead = off_t(512) << 20;
+    void allocate()
+    {
+        std::unique_lock<std::mutex> lk(amu_);
+        for (;;) {
+            acv_.wait(lk, [&] { return stop_ || want_ > size_; });
+            if (stop_) return;
+            const off_t at = size_, n = std::min(kStep, want_ - size_);
+            lk.unlock();
+            const bool ok = fallocate(fd_, 0, at, n) == 0 || ftruncate(fd_, at + n) == 0;
+            lk.lock();
+            if (!ok) {
+                failed_ = true;
+                acv_.notify_all();
+                return;
+            }
+            size_ = at + n;
+            acv_.notify_all();
+        }
+    }
     char *window(size_t w)
     {
         std::lock_guard<std::mutex> g(mu_);
@@ -167,6 +213,11 @@ class MappedOut {
     int fd_ = -1;
     std::mutex mu_;
     std::vector<char *> wins_;
+    std::thread alloc_;
+    std::mutex amu_;
+    std::condition_variable acv_;
+    off_t size_ = 0, want_ = 0;   // allocated, asked for
+    bool stop_ = false, failed_ = false;
 };
 
 }  // namespace
@@ -478,6 +529,7 @@ int CommandDistance::run() const
             }
         });
     std::atomic<uint64_t> next{0};
+    std::atomic<uint64_t> devUs{0};         // device calls + the listed cells' row order
     std::vector<std::thread> gpu;
     for (int d = 0; d < nDev; d++)
         gpu.emplace_back([&, d] {
@@ -491,6 +543,7 @@ int CommandDistance::run() const
                     cv.wait(lk, [&] { return written + nSlots > b; });
                 }
                 const uint64_t q0 = b * block, nq = std::min(block, nQ - q0);
+                const auto tb0 = std::chrono::steady_clock::now();
                 for (;;) {
                     check(fpm_refset_dist_list(sets[d], Q + q0 * width * hb, ql.data() + q0,
                                                qL.data() + q0, width, (uint32_t)nq,
@@ -516,6 +569,8 @@ int CommandDistance::run() const
                 for (uint64_t i = 0; i < nq; i++)
                     std::sort(sl.byRow.begin() + sl.rowStart[i], sl.byRow.begin() + sl.rowStart[i + 1],
                               [&](uint32_t x, uint32_t y) { return sl.lr[x] < sl.lr[y]; });
+                devUs += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+                             std::chrono::steady_clock::now() - tb0).count();
                 // pieces of ~1 M pairs (at least one query row) for the formatter threads
                 const uint64_t per = std::max<uint64_t>(1, (1ULL << 20) / nR);
                 const uint64_t parts = (nq + per - 1) / per;
@@ -615,7 +670,7 @@ int CommandDistance::run() const
         }
         cv.notify_all();
     }
-    if (useMap) mapped.close();
+    if (useMap && !mapped.close(opos)) writeFailed = true;
     if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
     if (writeFailed) {
         std::cerr << "ERROR: writing the distance output failed." << std::endl;
@@ -625,6 +680,9 @@ int CommandDistance::run() const
         fprintf(stderr, "[fpmash] writer waiting for blocks: %.1f ms\n[fpmash] writer copying "
                         "pieces out (%s): %.1f ms\n", waitMs,
                 useMap ? "mapped file" : direct ? "pwrite" : "stdout", writeMs);
+    if (timingOn())
+        fprintf(stderr, "[fpmash] device blocks (compare + fetch + row order, summed): %.1f ms\n",
+                devUs.load() / 1e3);
     phaseMark("blocks computed, formatted and written");
     for (auto &t : gpu) t.join();
     {
