@@ -100,10 +100,10 @@ static bool readFile(const std::string &path, std::string &out)
 
 // The .msh inputs are opened several times (parameters of the first file, the per-file
 // compatibility test, the load: Sketch.cpp:257-336): keep the last image read, keyed by path,
-// size and modification time, until its load (loadMsh) has parsed it.  Main thread only (no
-// locking): every caller is on the command's main thread.
-static std::string g_mshPath, g_mshData;
-static struct stat g_mshSt {};
+// size and modification time, until its load (loadMsh) has parsed it.  One cache per thread
+// (thread_local): a Sketch loaded on another thread reads and caches on its own.
+static thread_local std::string g_mshPath, g_mshData;
+static thread_local struct stat g_mshSt {};
 
 static void releaseMshCache()
 {

@@ -150,6 +150,21 @@ def pvalue_asymp_table():
         for j in range(0, 10):
             for r in (1.0 - 1e-7, 1.0 - 1e-6, 1.0 - 2e-6):
                 row(n - j, n, r)
+    # the incomplete gamma's switch at X = shape + 1: below it the upper Q of the
+    # large-a branch is 1 - P from the series, the cancellation is largest where P is; rows
+    # with X just below, at and just above the switch, for both branches
+    for n in (100001, 1000000):
+        for j in range(0, 9):
+            x = n - j
+            a, b = float(x), float(n - x + 1)
+            N = a + (b - 1) / 2
+            for X in (b + 1 - 1e-6, b + 0.5, b + 1 + 1e-6):
+                row(x, n, float(mp.exp(-mp.mpf(X) / N)))
+        for x in range(1, 10):
+            a, b = float(x), float(n - x + 1)
+            N = b + (a - 1) / 2
+            for X in (a + 1 - 1e-6, a + 0.5, a + 1 + 1e-6):
+                row(x, n, float(-mp.expm1(-mp.mpf(X) / N)))
     return rows
 
 

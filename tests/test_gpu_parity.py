@@ -737,6 +737,38 @@ def test_index_one_pass_holds_sketch_partitions(ctx, oracle):
     assert np.array_equal(got_nu, nu) and np.array_equal(got_de, de)
 
 
+def test_index_one_pass_overflow_rebuilds(ctx, oracle):
+    """Skewed keys: 600 sorted sketches that all hold the same 400 values (plus
+    their own) put ~2.4e5 entries into the level-1 partition of those values, past its
+    one-pass slot; the build flags the overflow and the exact two-pass build replaces it
+    (ctx.index_rebuilds() goes up), and the sparse grid still equals the oracle."""
+    import fpmash
+    rng = np.random.default_rng(77)
+    # the shared values span one level-1 partition (keys scale to the largest, ~2^62: a
+    # partition is 2^52 wide) but many of its buckets (~1,800 entries each, not one bucket of
+    # 240,000: the probe reads every entry of a hash's bucket)
+    common = np.unique(rng.integers(1, 1 << 52, size=400, dtype=np.uint64))
+    lists = []
+    for _ in range(600):
+        own = rng.integers(1 << 52, 1 << 62, size=int(rng.integers(50, 200)), dtype=np.uint64)
+        lists.append(np.unique(np.concatenate([common, own])))
+    L = [len(x) * 3 for x in lists]
+    before = ctx.index_rebuilds()
+    ctx.set_dist_mode(fpmash.DIST_SPARSE)
+    try:
+        d = ctx.dist(lists, lists, 500, ref_lengths=L, qry_lengths=L)
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+    assert ctx.index_rebuilds() > before
+    rows = list(range(0, 600, 37))
+    nu, de, di, pv = oracle.dist_grid(lists, L, [lists[r] for r in rows], [L[r] for r in rows],
+                                      500, 21, 4.0 ** 21)
+    n = len(lists)
+    got = np.concatenate([d["numer"][r * n:(r + 1) * n] for r in rows])
+    gde = np.concatenate([d["denom"][r * n:(r + 1) * n] for r in rows])
+    assert np.array_equal(got, nu) and np.array_equal(gde, de)
+
+
 def test_index_exact_build_forced():
     """FPM_IDX_ONEPASS=0 (read at library load: a child process) forces the exact two-pass
     index build; the sorted and the -fp dist grids still equal the oracle."""

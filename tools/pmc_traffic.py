@@ -35,6 +35,9 @@ GROUPS = [
     ("compare_grid_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
     ("dist_finalize_kernel", "dist finalize (dense / candidate cells)"),
     ("dist_cand_finalize_kernel", "dist finalize (dense / candidate cells)"),
+    ("dist_cand_list_kernel", "dist finalize (dense / candidate cells)"),
+    ("dist_grid_list_kernel", "dist finalize (dense / candidate cells)"),
+    ("qblock_union_kernel", "candidate compare (rank_rows/walk_cand/compare_grid)"),
     ("probe_rows_kernel", "probe_rows_kernel"),
     ("dist_fill_kernel", "dist_fill_kernel"),
     ("dist_fill_flat_kernel", "dist_fill_kernel"),
