@@ -492,12 +492,13 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
     d_rl = fpmash.DeviceBuffer.from_array(ctx, rl)
     d_rL = fpmash.DeviceBuffer.from_array(ctx, rL)
     np_ = n * n
-    outs = [fpmash.DeviceBuffer(ctx, np_ * b) for b in (2, 2, 8, 8, 1)]
+    # the compact output: u16 counts of every pair + the pairs with numer > 0
+    outs = compact_out(ctx, np_)
 
     def run():
-        fpmash._check(L.fpm_dist_dev16(ctx.h, d_R.ptr, d_rl.ptr, d_rL.ptr, w, n, d_R.ptr, d_rl.ptr,
-                                     d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
-                                     *[o.ptr for o in outs], ctx.stream))
+        fpmash._check(L.fpm_dist_list_dev(ctx.h, d_R.ptr, d_rl.ptr, d_rL.ptr, w, n, d_R.ptr,
+                                          d_rl.ptr, d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
+                                          outs[0].ptr, outs[1].ptr, outs[2].ref, ctx.stream))
     run()
     ctx.synchronize()
     t0 = time.perf_counter()
@@ -505,6 +506,8 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
         run()
     ctx.synchronize()
     dist_ms = (time.perf_counter() - t0) / reps * 1e3
+    if outs[2].count() > outs[2].cap:
+        raise RuntimeError(f"C3 cell list overflow: {outs[2].count()} > {outs[2].cap}")
     st = ctx.last_dist_stats()
     numer = outs[0].to_array(np.uint16, np_)
     denom = outs[1].to_array(np.uint16, np_)
@@ -531,9 +534,10 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
             lists = [x if cut is None else x[:cut] for x in rows]
             if cut is not None:
                 d_rl2 = fpmash.DeviceBuffer.from_array(ctx, np.minimum(rl, cut).astype(np.uint32))
-                fpmash._check(L.fpm_dist_dev16(ctx.h, d_R.ptr, d_rl2.ptr, d_rL.ptr, w, n, d_R.ptr,
-                                             d_rl2.ptr, d_rL.ptr, w, n, 4, s, 1, 10.0, 1.0, 1.0,
-                                             *[o.ptr for o in outs], ctx.stream))
+                fpmash._check(L.fpm_dist_list_dev(ctx.h, d_R.ptr, d_rl2.ptr, d_rL.ptr, w, n,
+                                                  d_R.ptr, d_rl2.ptr, d_rL.ptr, w, n, 4, s, 1,
+                                                  10.0, 1.0, 1.0, outs[0].ptr, outs[1].ptr,
+                                                  outs[2].ref, ctx.stream))
                 ctx.synchronize()
                 d_rl2.free()
             g = O.dist_grid(lists, list(rL), [lists[int(q)] for q in qrows],
@@ -543,7 +547,8 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
         par["check_s"] = time.perf_counter() - t0
     for b in [d_R, d_rl, d_rL] + outs:
         b.free()
-    return {"config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
+    return {"output": "u16 numer/denom per pair + listed pairs with numer > 0 (SURVEY 8(d))",
+            "config": f"C3: {n_seqs} x 2000 bp -> CFL k-finger text in {len(files)} files "
                       f"({n_lines} lines, {sum(map(len, files)) / 1e6:.0f} MB), sketch -fp per file "
                       f"+ dist -fp {n} x {n} (s={s}, unsorted u32 walk)",
             "references": n, "lines": n_lines,
@@ -559,11 +564,11 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
 
 def compact_out(ctx, cells):
     """device buffers of one grid's compact dist output: u16 numer, u16 denom and the list of
-    the cells with numer > 0 (room for 1/64 of the cells, at least 2^20 entries: the
-    family-structured C2 / C4 grids share hashes in 1 % / 0.2 % of their pairs; an overflow is
-    detected and raised after the run)"""
+    the cells with numer > 0 (room for 1/16 of the cells, 2^20 to 2^26 entries: the
+    family-structured C2 / C4 grids share hashes in 1 % / 0.2 % of their pairs, C3's k-finger
+    lists in ~4 %; an overflow is detected and raised after the run)"""
     return [fpmash.DeviceBuffer(ctx, cells * 2), fpmash.DeviceBuffer(ctx, cells * 2),
-            fpmash.CellList(ctx, min(cells, max(1 << 20, cells // 64)))]
+            fpmash.CellList(ctx, min(cells, max(1 << 20, min(1 << 26, cells // 16))))]
 
 
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
