@@ -524,3 +524,54 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file,
     got = text.decode().splitlines()
     assert len(got) == len(exp) == len(refs) ** 2
     assert got == exp
+
+
+def _bgzf(data: bytes, block=65280) -> bytes:
+    """BGZF (SAM spec 4.1): raw-deflate blocks of <= 64 KiB, each a gzip member whose extra
+    field 'BC' holds the member's size - 1, then the 28-byte empty EOF member."""
+    import struct
+    import zlib
+    out = []
+    for i in range(0, len(data), block):
+        raw = data[i:i + block]
+        c = zlib.compressobj(6, zlib.DEFLATED, -15)
+        d = c.compress(raw) + c.flush()
+        bsize = 18 + len(d) + 8
+        out.append(b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" +
+                   struct.pack("<H", bsize - 1) + d +
+                   struct.pack("<II", zlib.crc32(raw) & 0xffffffff, len(raw)))
+    out.append(bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000"))
+    return b"".join(out)
+
+
+def test_seqload_gzip_forms(tmp_path):
+    """loadSequenceFile (host/SeqReader.cpp, through bin/seqload) inflates like zlib's gzread,
+    which the reference's kseq reads through (Sketch.cpp:38): plain text, one gzip member,
+    several members, BGZF (members inflated on several threads), a member followed by
+    non-gzip bytes (ignored, as gz_look does), and a truncated member (what inflates)."""
+    import gzip
+    import random
+    seqload = os.path.join(ROOT, "fp-mash_amd", "bin", "seqload")
+    rng = random.Random(5)
+    text = b"".join(b">r%d c\n" % i + bytes(rng.choice(b"ACGTN") for _ in range(rng.randint(0, 3000)))
+                    + b"\n" for i in range(400))
+    cases = {
+        "plain.fa": text,
+        "one.fa.gz": gzip.compress(text),
+        "multi.fa.gz": gzip.compress(text[:1000]) + gzip.compress(text[1000:5000]) +
+                       gzip.compress(b"") + gzip.compress(text[5000:]),
+        "bgzf.fa.gz": _bgzf(text, block=4000),
+        "tail.fa.gz": gzip.compress(text) + b"not gzip trailing bytes",
+    }
+    for name, blob in cases.items():
+        (tmp_path / name).write_bytes(blob)
+        p = subprocess.run([seqload, str(tmp_path / name)], capture_output=True)
+        assert p.returncode == 0, name
+        assert p.stdout == text, name
+    # a truncated member: gzread returns what inflates and then end of file (no error), so the
+    # reference's kseq reads the partial text; libdeflate refuses it and the loader falls back
+    import zlib
+    cut = gzip.compress(text)[:-100]
+    (tmp_path / "cut.fa.gz").write_bytes(cut)
+    p = subprocess.run([seqload, str(tmp_path / "cut.fa.gz")], capture_output=True)
+    assert p.returncode == 0 and p.stdout == zlib.decompressobj(16 + 15).decompress(cut)

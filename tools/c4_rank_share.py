@@ -7,7 +7,8 @@ A rank of a ws-GPU C4 run (bench.c4_leg) sketches its contiguous block of famili
 every rank's sketch rows through the all-gather, and runs its block pairs of the all-vs-all
 grid (fpmash.shard.pair_block_jobs): the index of its own block (and, for even ws, one more)
 rebuilt, its own block on the symmetric self path, and the other block pairs as a grid + its
-transpose (fpm_refset_dist_mirror_dev).  Here the gathered rows come from one sketch job of all
+transpose (fpm_refset_dist_mirror_list_dev: the compact output, u16 counts + the cells with
+numer > 0; --full: the five arrays per cell).  Here the gathered rows come from one sketch job of all
 n sequences on device 0, and the rank's own work is timed: its block's sketch job and its
 dist share (the same calls c4_leg makes).  The all-gather (N x s x 8 B = 400 MB over xGMI) is
 not in the number.  One JSON line.
@@ -35,7 +36,10 @@ def main():
     ap.add_argument("--rank", type=int, default=0)
     ap.add_argument("--n", type=int, default=50_000)
     ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--full", action="store_true", help="the full five-array output")
     a = ap.parse_args()
+    sys.path.insert(0, ROOT)
+    from bench import compact_out
     members, s, k, seq_len = 100, 1000, 21, 2000
     fams = a.n // members
     n = fams * members
@@ -61,9 +65,11 @@ def main():
     for j in jobs:
         (rl, rh), (ql, qh) = j["ref"], j["qry"]
         cells = (rh - rl) * (qh - ql)
-        o = {"p": [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]}
+        mk = (lambda c: [fpmash.DeviceBuffer(ctx, c * b) for b in (2, 2, 8, 8, 1)]) if a.full \
+            else (lambda c: compact_out(ctx, c))
+        o = {"p": mk(cells)}
         if j["kind"] == "mirror":
-            o["m"] = [fpmash.DeviceBuffer(ctx, cells * b) for b in (2, 2, 8, 8, 1)]
+            o["m"] = mk(cells)
         outs.append(o)
         if (rl, rh) not in refsets:
             h = C.c_void_p()
@@ -73,22 +79,37 @@ def main():
 
     def dist():
         if a.ws == 1:
-            fpmash._check(L.fpm_dist_dev16(ctx.h, R, C_, Ln, stride, n, R, C_, Ln, stride, n, 8, s,
-                                         k, 4.0 ** k, 1.0, 1.0, *[b.ptr for b in outs[0]["p"]],
-                                         st))
+            p_ = outs[0]["p"]
+            if a.full:
+                fpmash._check(L.fpm_dist_dev16(ctx.h, R, C_, Ln, stride, n, R, C_, Ln, stride, n,
+                                               8, s, k, 4.0 ** k, 1.0, 1.0, *[b.ptr for b in p_],
+                                               st))
+            else:
+                fpmash._check(L.fpm_dist_list_dev(ctx.h, R, C_, Ln, stride, n, R, C_, Ln, stride,
+                                                  n, 8, s, k, 4.0 ** k, 1.0, 1.0, p_[0].ptr,
+                                                  p_[1].ptr, p_[2].ref, st))
             return
         for rs in refsets.values():
             fpmash._check(L.fpm_refset_reindex(rs, st))
         for j, o in zip(jobs, outs):
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
             q = (R + ql * stride * 8, C_ + ql * 4, Ln + ql * 8, stride, qh - ql)
-            if j["kind"] == "self":
-                fpmash._check(L.fpm_refset_dist_dev(refsets[(rl, rh)], *q, s, 2, k, 4.0 ** k,
-                                                    1.0, 1.0, *[b.ptr for b in o["p"]], st))
+            rs, p_ = refsets[(rl, rh)], o["p"]
+            if a.full and j["kind"] == "self":
+                fpmash._check(L.fpm_refset_dist_dev(rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
+                                                    *[b.ptr for b in p_], st))
+            elif a.full:
+                fpmash._check(L.fpm_refset_dist_mirror_dev(rs, *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
+                                                           *[b.ptr for b in p_],
+                                                           *[b.ptr for b in o["m"]], st))
+            elif j["kind"] == "self":
+                fpmash._check(L.fpm_refset_dist_list_dev(rs, *q, s, k, 4.0 ** k, 1.0, 1.0,
+                                                         p_[0].ptr, p_[1].ptr, p_[2].ref, st))
             else:
-                fpmash._check(L.fpm_refset_dist_mirror_dev(
-                    refsets[(rl, rh)], *q, s, 2, k, 4.0 ** k, 1.0, 1.0,
-                    *[b.ptr for b in o["p"]], *[b.ptr for b in o["m"]], st))
+                m_ = o["m"]
+                fpmash._check(L.fpm_refset_dist_mirror_list_dev(
+                    rs, *q, s, k, 4.0 ** k, 1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref,
+                    m_[0].ptr, m_[1].ptr, m_[2].ref, st))
 
     def timed(fn):
         for _ in range(2):
@@ -116,6 +137,7 @@ def main():
     cells = sum((j["ref"][1] - j["ref"][0]) * (j["qry"][1] - j["qry"][0]) *
                 (2 if j["kind"] == "mirror" else 1) for j in jobs)
     print(json.dumps({"emulated_ws": a.ws, "emulated_rank": a.rank, "n": n,
+                      "output": "full" if a.full else "compact",
                       "jobs": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                                for j in jobs],
                       "cells_written": cells, "last_call_stats": last,
