@@ -1,6 +1,7 @@
 #!/bin/bash
 # tools/gpu_r04b.sh — round-4 measurement pass: CLI write-mode A/B, C3 / C4 legs with kernel
-# times, C4 rank shares at N = 2 / 4 / 8 (compact output), new GPU tests.
+# times, C4 rank shares at N = 2 / 4 / 8 (compact output), new GPU tests, the C3 XCD-tile A/B
+# (fp-mash_amd/lib/libfpmash_prexcd.so: dist.hip before the change, tools/build_variant.sh).
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r04b; mkdir -p $O
@@ -18,6 +19,10 @@ for ws in 2 4 8; do
     || { tail -20 $O/share_ws$ws.err; exit 1; }
   python3 -c "import json; d=json.load(open('$O/share_ws$ws.json')); print($ws, round(d['rank_step_ms_excl_gather'],3), round(d['dist_ms'],3))"
 done
+BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-fp-text --no-c4 --no-c5 --no-cli --no-split --no-full-grid --no-parity" \
+  timeout -k 10 600 bash tools/ab_bench.sh fp-mash_amd/lib/libfpmash.so fp-mash_amd/lib/libfpmash_prexcd.so 2 \
+  > $O/c3_xcd_ab.txt 2>&1 || { tail -20 $O/c3_xcd_ab.txt; exit 1; }
+cat $O/c3_xcd_ab.txt
 OUT=$O/cli_ab REPS=3 timeout -k 10 400 bash tools/cli_dist_ab.sh FPMASH_DIST_WRITE=pwrite > $O/cli_ab.txt 2>&1 \
   || { tail -30 $O/cli_ab.txt; exit 1; }
 cat $O/cli_ab.txt
