@@ -1474,21 +1474,27 @@ __global__ __launch_bounds__(1024) void compare_grid_img_kernel(
     uint16_t *img = reinterpret_cast<uint16_t *>(lds32);
     constexpr int kPer = (kImgTile * kImgMaxW + 1023) / 1024;   // ref values per thread (<= 32)
     const uint32_t Wp = img_row_u16(W, BLK);
-    // XCD-aware tiles: workgroup b runs on XCD b % 8, and each XCD owns a fixed range of ~nrb / 8
-    // ref blocks, which it sweeps for one query block after another: its ref rows (~2.5 MB at
-    // C3's 5,000 x 1,000 u32) stay in the XCD's 4 MB L2 for every query block, and a query
-    // block's union and images are fetched once per XCD (row-major tiles re-read every ref block
-    // from the fabric once per query block: 7.6 GB per C3 launch)
+    // XCD-aware tiles: workgroup b runs on XCD b % 8, and XCD x owns ref blocks [x per,
+    // (x + 1) per), per = nrb / 8, which it sweeps for one query block after another: its ref
+    // rows (~2.4 MB at C3's 5,000 x 1,000 u32) stay in the XCD's 4 MB L2 for every query
+    // block, and a query block's union and images are fetched once per XCD (row-major tiles
+    // re-read every ref block from the fabric once per query block).  The nrb % 8 ref blocks
+    // left over are dealt tile by tile round the XCDs, so every XCD gets the same number of
+    // tiles (whole leftover blocks per XCD left 3 XCDs idle at the end: +1.7 %).
     uint32_t rb, qb;
     {
+        const uint32_t nqb = (n_qry + kImgTile - 1) / kImgTile;
         const uint32_t x = blockIdx.x % kXcds, k = blockIdx.x / kXcds;
-        const uint32_t per = (nrb + kXcds - 1) / kXcds;          // ref blocks per XCD (max)
-        const uint32_t lo = x * per, hi = min(nrb, lo + per);
-        if (lo >= hi) return;
-        const uint32_t mine = hi - lo;
-        qb = k / per;
-        rb = lo + (k - qb * per);
-        if (k - qb * per >= mine || qb >= (n_qry + kImgTile - 1) / kImgTile) return;
+        const uint32_t per = nrb / kXcds, rem = nrb - per * kXcds;
+        if (k < per * nqb) {
+            qb = k / per;
+            rb = x * per + (k - qb * per);
+        } else {
+            const uint32_t e = x + kXcds * (k - per * nqb);
+            if (!rem || e >= rem * nqb) return;
+            qb = e / rem;
+            rb = per * kXcds + (e - qb * rem);
+        }
     }
     const uint32_t t = threadIdx.x, r0 = rb * kImgTile, q0 = qb * kImgTile;
     const uint32_t us = usize[2 * qb], maxb = usize[2 * qb + 1];
@@ -1693,9 +1699,11 @@ static hipError_t compare_grid_img_c(const uint32_t *ref, const uint32_t *ref_le
         return e;
     hipLaunchKernelGGL(qblock_union_kernel, dim3(nqb), dim3(1024), lds_u, st, qry, qry_len,
                        qry_stride, n_qry, W, Wimg, ublk, usize, bimg);
-    // a 1-D grid of kXcds x (ref blocks per XCD x query blocks) tiles (the kernel's tile map)
-    const uint32_t per = (nrb + kXcds - 1) / kXcds;
-    hipLaunchKernelGGL((compare_grid_img_kernel<kBlk, C>), dim3(kXcds * per * nqb, 1), dim3(1024),
+    // a 1-D grid: kXcds x (the XCD's own ref blocks x query blocks + its share of the leftover
+    // tiles) (the kernel's tile map)
+    const uint32_t per = nrb / kXcds, rem = nrb - per * kXcds;
+    const uint32_t grid = kXcds * (per * nqb + (rem * nqb + kXcds - 1) / kXcds);
+    hipLaunchKernelGGL((compare_grid_img_kernel<kBlk, C>), dim3(grid, 1), dim3(1024),
                        lds_t, st, ref, ref_len, ref_stride, n_ref, qry_len, n_qry,
                        (const uint32_t *)ublk, (const uint32_t *)usize, (const uint16_t *)bimg,
                        Wimg, S, W, nrb, numer, denom);

@@ -24,7 +24,8 @@
 #include <thread>
 
 #include <fcntl.h>
-#include <sys/mman.h>
+#include <climits>
+#include <sys/uio.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -109,116 +110,37 @@ inline char *uTo(char *p, uint64_t x)
     return p + n;
 }
 
-// Output into a shared mapping of the stdout file: windows of 1 GiB mapped on first use.  The
-// file's pages are allocated ahead of the copies by a thread of its own (fallocate in 64 MB
-// steps, up to kAhead past the last block handed out; the excess is cut at the end): pages
-// first touched through the mapping cost a fault each, and faults on one tmpfs file
-// serialise (4 GB into /dev/shm on the MI355X box: 3.5 GB/s faulting, 8-9 GB/s into
-// fallocated pages, 5.6-6.1 GB/s by one pwrite stream: tools/micro/write_rate.cpp).  Page
-// faults of a mapping run in parallel, where write() / pwrite() to one file serialise on its
-// inode lock.
-class MappedOut {
-  public:
-    bool open(int ofd)
-    {
-        char path[64];
-        snprintf(path, sizeof path, "/proc/self/fd/%d", ofd);
-        fd_ = ::open(path, O_RDWR);   // the same file, opened for reading too (mmap needs it)
-        if (fd_ < 0) return false;
-        struct stat st {};
-        if (fstat(fd_, &st) == 0) size_ = want_ = st.st_size;
-        alloc_ = std::thread([this] { allocate(); });
-        return true;
-    }
-    // the file allocated up to `upto` (waits for the allocator thread), and asked ahead
-    bool extend(off_t upto)
-    {
-        std::unique_lock<std::mutex> lk(amu_);
-        want_ = std::max(want_, upto + kAhead);
-        acv_.notify_all();
-        acv_.wait(lk, [&] { return size_ >= upto || failed_; });
-        return !failed_;
-    }
-    void put(off_t at, const char *src, size_t n)
-    {
-        while (n) {
-            const size_t w = (size_t)at / kWin, off = (size_t)at % kWin;
-            const size_t c = std::min(n, kWin - off);
-            char *base = window(w);
-            // map the range's (allocated) pages writable in one call (MADV_POPULATE_WRITE,
-            // Linux >= 5.14; where the kernel lacks it the copy takes the faults)
-            const uintptr_t a0 = (uintptr_t)(base + off) & ~(uintptr_t)4095;
-            const uintptr_t a1 = (uintptr_t)(base + off + c);
-            (void)madvise((void *)a0, a1 - a0, 23);
-            memcpy(base + off, src, c);
-            at += (off_t)c;
-            src += c;
-            n -= c;
-        }
-    }
-    // unmap, and cut the file to the bytes written (drops the pages allocated ahead)
-    bool close(off_t final_size)
-    {
-        {
-            std::lock_guard<std::mutex> lk(amu_);
-            stop_ = true;
-        }
-        acv_.notify_all();
-        if (alloc_.joinable()) alloc_.join();
-        for (char *p : wins_)
-            if (p) munmap(p, kWin);
-        wins_.clear();
-        const bool ok = !failed_ && ftruncate(fd_, final_size) == 0;
-        ::close(fd_);
-        fd_ = -1;
-        return ok;
-    }
-
-  private:
-    static constexpr size_t kWin = size_t(1) << 30;
-    static constexpr off_t kStep = off_t(64) << 20, kAhead = off_t(512) << 20;
-    void allocate()
-    {
-        std::unique_lock<std::mutex> lk(amu_);
-        for (;;) {
-            acv_.wait(lk, [&] { return stop_ || want_ > size_; });
-            if (stop_) return;
-            const off_t at = size_, n = std::min(kStep, want_ - size_);
-            lk.unlock();
-            const bool ok = fallocate(fd_, 0, at, n) == 0 || ftruncate(fd_, at + n) == 0;
-            lk.lock();
-            if (!ok) {
-                failed_ = true;
-                acv_.notify_all();
-                return;
+// writes the pieces at `at` in one pwritev() per IOV_MAX pieces (short writes resumed); false on
+// an error.  One call per block: the formatter threads keep formatting instead of queueing on
+// the file's inode lock, which serialises writes to one file anyway (tmpfs on the MI355X box:
+// one stream 5.6-6.1 GB/s; a shared mapping of the file faulted in at 3.5 GB/s and, with the
+// pages allocated ahead, still lost to this path in the CLI: tools/micro/write_rate.cpp, DESIGN
+// §5).
+bool writePieces(int fd, off_t at, const std::vector<std::string> &pieces)
+{
+    std::vector<struct iovec> iov;
+    iov.reserve(pieces.size());
+    for (const auto &t : pieces)
+        if (!t.empty()) iov.push_back({(void *)t.data(), t.size()});
+    size_t i = 0;
+    while (i < iov.size()) {
+        const int n = (int)std::min<size_t>(iov.size() - i, IOV_MAX);
+        const ssize_t w = pwritev(fd, &iov[i], n, at);
+        if (w <= 0) return false;
+        at += (off_t)w;
+        for (size_t left = (size_t)w; left;) {
+            if (left >= iov[i].iov_len) {
+                left -= iov[i].iov_len;
+                i++;
+            } else {
+                iov[i].iov_base = (char *)iov[i].iov_base + left;
+                iov[i].iov_len -= left;
+                left = 0;
             }
-            size_ = at + n;
-            acv_.notify_all();
         }
     }
-    char *window(size_t w)
-    {
-        std::lock_guard<std::mutex> g(mu_);
-        if (wins_.size() <= w) wins_.resize(w + 1, nullptr);
-        if (!wins_[w]) {
-            void *p = mmap(nullptr, kWin, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, (off_t)(w * kWin));
-            if (p == MAP_FAILED) {
-                std::cerr << "ERROR: mapping the distance output failed." << std::endl;
-                fatalExit();
-            }
-            wins_[w] = (char *)p;
-        }
-        return wins_[w];
-    }
-    int fd_ = -1;
-    std::mutex mu_;
-    std::vector<char *> wins_;
-    std::thread alloc_;
-    std::mutex amu_;
-    std::condition_variable acv_;
-    off_t size_ = 0, want_ = 0;   // allocated, asked for
-    bool stop_ = false, failed_ = false;
-};
+    return true;
+}
 
 }  // namespace
 
@@ -606,10 +528,8 @@ int CommandDistance::run() const
                 cv.notify_all();
             }
         });
-    // stdout a regular file (not O_APPEND): the pieces of a block are copied into a shared
-    // mapping of the file at their offsets by the formatter threads (write() / pwrite() to one
-    // file hold its inode lock: 4.1 GB of C2 text went out one writer at a time); the file is
-    // extended block by block.  Otherwise (pipes, terminals) this thread writes the pieces.
+    // stdout a regular file (not O_APPEND): each block goes out by pwritev() at its offset;
+    // otherwise (pipes, terminals) by fwrite.
     out.flush();
     fflush(stdout);
     const int ofd = fileno(stdout);
@@ -618,10 +538,7 @@ int CommandDistance::run() const
     off_t opos = -1;
     const bool direct = nBlocks && fstat(ofd, &ost) == 0 && S_ISREG(ost.st_mode) && ofl >= 0 &&
                         !(ofl & O_APPEND) && (opos = lseek(ofd, 0, SEEK_CUR)) >= 0;
-    MappedOut mapped;
-    const char *wm = getenv("FPMASH_DIST_WRITE");   // A/B: "pwrite" keeps the pwrite path
-    const bool useMap = direct && !(wm && strcmp(wm, "pwrite") == 0) && mapped.open(ofd);
-    std::atomic<bool> writeFailed{false};
+    bool writeFailed = false;
     double waitMs = 0, writeMs = 0;
     for (uint64_t b = 0; b < nBlocks; b++) {
         Slot &sl = slots[b % nSlots];
@@ -634,35 +551,8 @@ int CommandDistance::run() const
         }
         auto t1 = std::chrono::steady_clock::now();
         if (direct) {
-            int left = (int)pieces.size();
-            off_t end = opos;
-            for (auto &t : pieces) end += (off_t)t.size();
-            if (useMap && !mapped.extend(end)) writeFailed = true;
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                for (auto &t : pieces) {
-                    const off_t at = opos;
-                    opos += (off_t)t.size();
-                    tasks.emplace_front([&, at, piece = &t] {
-                        if (useMap) {
-                            if (!writeFailed) mapped.put(at, piece->data(), piece->size());
-                        } else {
-                            for (size_t q = 0; q < piece->size();) {
-                                const ssize_t w = pwrite(ofd, piece->data() + q, piece->size() - q,
-                                                         at + (off_t)q);
-                                if (w <= 0) { writeFailed = true; break; }
-                                q += (size_t)w;
-                            }
-                        }
-                        std::lock_guard<std::mutex> lk2(mu);
-                        --left;
-                        cv.notify_all();
-                    });
-                }
-            }
-            cv.notify_all();
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return left == 0; });
+            if (!writeFailed && !writePieces(ofd, opos, pieces)) writeFailed = true;
+            for (auto &t : pieces) opos += (off_t)t.size();
         } else {
             for (auto &t : pieces) fwrite(t.data(), 1, t.size(), stdout);
         }
@@ -678,7 +568,6 @@ int CommandDistance::run() const
         }
         cv.notify_all();
     }
-    if (useMap && !mapped.close(opos)) writeFailed = true;
     if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
     if (writeFailed) {
         std::cerr << "ERROR: writing the distance output failed." << std::endl;
@@ -687,7 +576,7 @@ int CommandDistance::run() const
     if (timingOn())
         fprintf(stderr, "[fpmash] writer waiting for blocks: %.1f ms\n[fpmash] writer copying "
                         "pieces out (%s): %.1f ms\n", waitMs,
-                useMap ? "mapped file" : direct ? "pwrite" : "stdout", writeMs);
+                direct ? "pwritev" : "stdout", writeMs);
     if (timingOn())
         fprintf(stderr, "[fpmash] device blocks (compare + fetch + row order, summed): %.1f ms\n",
                 devUs.load() / 1e3);

@@ -482,15 +482,14 @@ def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
 @pytest.mark.gpu
 @pytest.mark.parametrize("block_pairs,to_file,devices",
                          [(None, False, None), ("50000", False, None), (None, True, None),
-                          ("50000", True, None), ("50000", False, "0,0"), ("50000", True, "0,0,0"),
-                          ("50000", "pwrite", None)])
+                          ("50000", True, None), ("50000", False, "0,0"), ("50000", True, "0,0,0")])
 def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file, devices):
     """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
     blocks of 50,000 pairs (FPMASH_DIST_BLOCK_PAIRS) written by the formatter threads in
     order: every line equals the oracle's, in the reference's query-major order.  With
     FPMASH_DEVICE_LIST the blocks go round the contexts (2-3 on the one GPU standing in for
-    a node's devices).  A regular file as stdout takes the mapped-file writer (its pages
-    allocated ahead, the excess cut at the end), or pwrite() with FPMASH_DIST_WRITE=pwrite."""
+    a node's devices).  A regular file as stdout takes one pwritev() per block at its
+    offset."""
     from fpmash import datagen
     seqs = datagen.family_dna(12, 100, 2000, sub_rate=(0.01, 0.10), seed=23)
     ids = datagen.lyn2vec_ids(len(seqs), seed=23)
@@ -501,11 +500,9 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file,
         env["FPMASH_DIST_BLOCK_PAIRS"] = block_pairs
     if devices:
         env["FPMASH_DEVICE_LIST"] = devices
-    if to_file == "pwrite":
-        env["FPMASH_DIST_WRITE"] = "pwrite"
     if to_file:
-        # stdout a regular file: the pieces are pwrite()n at their offsets by the formatter
-        # threads; the file starts with bytes already written (the offsets start after them)
+        # stdout a regular file: each block is pwritev()n at its offset; the file starts with
+        # bytes already written (the offsets start after them)
         with open(tmp_path / "out.tsv", "wb") as f:
             f.write(b"head\n")
             f.flush()

@@ -21,7 +21,7 @@ for i in $(seq 1 "$REPS"); do
   for s in base "$@"; do
     envs=(); [ "$s" != base ] && IFS=',' read -ra envs <<< "$s"
     ( cd "$T" && a=$(date +%s%N) && env "${envs[@]}" FPMASH_TIMING=1 timeout -k 10 120 "$EXE" dist -p 16 c2.msh c2.msh > out.tsv \
-        2> "$OLDPWD/$OUT/ph.txt" && b=$(date +%s%N) && echo "$s wall_ms $(( (b - a) / 1000000 )) $(grep -o 'blocks computed[^:]*: [0-9.]*' $OLDPWD/$OUT/ph.txt)" ) || exit 1
+        2> "$OLDPWD/$OUT/ph.txt" && b=$(date +%s%N) && echo "$s wall_ms $(( (b - a) / 1000000 )) $(grep -oE '(blocks computed|writer [a-z]+|device blocks|reference sketch|rows packed)[^:]*: [0-9.]*' $OLDPWD/$OUT/ph.txt | tr '\n' ' ')" ) || exit 1
     rm -f "$T/out.tsv"
   done
 done

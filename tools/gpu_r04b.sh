@@ -23,6 +23,6 @@ BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-fp-text --no-c4 --no-c5 
   timeout -k 10 600 bash tools/ab_bench.sh fp-mash_amd/lib/libfpmash.so fp-mash_amd/lib/libfpmash_prexcd.so 2 \
   > $O/c3_xcd_ab.txt 2>&1 || { tail -20 $O/c3_xcd_ab.txt; exit 1; }
 cat $O/c3_xcd_ab.txt
-OUT=$O/cli_ab REPS=3 timeout -k 10 400 bash tools/cli_dist_ab.sh FPMASH_DIST_WRITE=pwrite > $O/cli_ab.txt 2>&1 \
+OUT=$O/cli_ab REPS=3 timeout -k 10 400 bash tools/cli_dist_ab.sh FPMASH_DIST_BLOCK_PAIRS=2000000 > $O/cli_ab.txt 2>&1 \
   || { tail -30 $O/cli_ab.txt; exit 1; }
 cat $O/cli_ab.txt
