@@ -216,21 +216,72 @@ __global__ __launch_bounds__(256) void compare_grid_lds_kernel(
     denom[o] = (C)d;
 }
 
+// The literal walk restricted to its tie stretches (unsorted lists; the record filter in
+// dist_index.hip).  Every equal step happens where both running maxima equal one shared record
+// value v; the walk enters that stretch exactly at (pA(v), pB(v)), the records' positions:
+// every earlier entry of either list has a running maximum below v, so it is taken before
+// the other list's v (KA(i) < KB(j) implies A[i] < B[j] at a reached state), and the walk
+// cannot pass v in one list while the other is short of it.  Entering takes
+// pA + pB - (equal steps so far) steps.  The stretch ends when either list reaches its next
+// record (a value above v: no equal step until the next shared record).  So the shared
+// records are merged in increasing order and only their stretches are walked literally;
+// denom = min(S, la + lb - common), the reference's steps + remainders (:402-415).
+template <typename H>
+__device__ __forceinline__ void walk_pair_rec(const H *__restrict__ A, uint32_t la,
+                                              const H *__restrict__ B, uint32_t lb, uint32_t S,
+                                              const H *__restrict__ RA, const uint32_t *__restrict__ PA,
+                                              uint32_t na, const H *__restrict__ RB,
+                                              const uint32_t *__restrict__ PB, uint32_t nb,
+                                              uint32_t &numer, uint32_t &denom)
+{
+    uint32_t common = 0, x = 0, y = 0;
+    H ra = na ? RA[0] : H(0), rb = nb ? RB[0] : H(0);
+    while (x < na && y < nb) {
+        if (ra < rb) { if (++x < na) ra = RA[x]; continue; }
+        if (rb < ra) { if (++y < nb) rb = RB[y]; continue; }
+        uint32_t i = PA[x], j = PB[y];
+        uint32_t n = i + j - common;
+        if (n >= S) break;
+        const uint32_t ea = x + 1 < na ? PA[x + 1] : la, eb = y + 1 < nb ? PB[y + 1] : lb;
+        H a = A[i], b = B[j];
+        while (i < ea && j < eb && n < S) {
+            const bool lt = a < b, gt = b < a;
+            if (!gt) { i++; if (i < ea) a = A[i]; }
+            if (!lt) { j++; if (j < eb) b = B[j]; }
+            common += (!lt && !gt) ? 1u : 0u;
+            n++;
+        }
+        if (++x < na) ra = RA[x];
+        if (++y < nb) rb = RB[y];
+    }
+    numer = common;
+    const uint64_t dd = (uint64_t)la + lb - common;
+    denom = dd > S ? S : (uint32_t)dd;
+}
+
 // Walk only the candidate pairs found by the inverted index (dist_index.hip).
 template <typename H, typename C>
 __global__ __launch_bounds__(256) void walk_cand_kernel(
     const uint64_t *__restrict__ cand, const unsigned long long *__restrict__ n_cand,
     const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
     uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, C *__restrict__ numer, C *__restrict__ denom)
+    uint64_t qry_stride, uint32_t S, RecRows rr, RecRows rq, C *__restrict__ numer,
+    C *__restrict__ denom)
 {
     const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= *n_cand) return;
     const uint64_t o = cand[idx];
     const uint32_t q = (uint32_t)(o / n_ref), r = (uint32_t)(o % n_ref);
     uint32_t c, d;
-    walk_pair(ref + (uint64_t)r * ref_stride, ref_len[r], qry + (uint64_t)q * qry_stride,
-              qry_len[q], S, c, d);
+    if (rr.val)
+        walk_pair_rec(ref + (uint64_t)r * ref_stride, ref_len[r], qry + (uint64_t)q * qry_stride,
+                      qry_len[q], S, (const H *)rr.val + (uint64_t)r * rr.stride,
+                      rr.pos + (uint64_t)r * rr.stride, rr.len[r],
+                      (const H *)rq.val + (uint64_t)q * rq.stride, rq.pos + (uint64_t)q * rq.stride,
+                      rq.len[q], c, d);
+    else
+        walk_pair(ref + (uint64_t)r * ref_stride, ref_len[r], qry + (uint64_t)q * qry_stride,
+                  qry_len[q], S, c, d);
     numer[o] = (C)c;
     denom[o] = (C)d;
 }
@@ -257,6 +308,9 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //  * when max(|A|, |B|) >= S, denom is S whatever #shared is, and no A element after the
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
+#ifndef FPM_RANK_SPLIT
+#define FPM_RANK_SPLIT 1
+#endif
 constexpr int kRankWaves = 4;        // waves per query row (2 and 8 measured slower)
 constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest unrolled probe
 constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one more)
@@ -435,10 +489,18 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
+#if FPM_RANK_SPLIT
+            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
+            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
+                                                                 0, 0);
+            dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
+            dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
+#else
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(R.rsrc, (t * kChunk + 2 * lane) * 8u,
                                                                  0, 0);
             dst[u].e0 = ((uint64_t)v[1] << 32) | v[0];
             dst[u].e1 = ((uint64_t)v[3] << 32) | v[2];
+#endif
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -461,8 +523,13 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
             const int rem = (int)la - (int)i0;
+#if FPM_RANK_SPLIT
+            // values past la (row padding) count nothing: lane l holds i0 + l, i0 + 64 + l
+            const int r0 = min(rem, 64), r1 = rem - 64;     // lanes whose e0 / e1 are valid
+#else
             // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
             const int r0 = (rem + 1) >> 1, r1 = rem >> 1;   // lanes whose e0 / e1 are valid
+#endif
             const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
             const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
@@ -470,16 +537,26 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
+#if FPM_RANK_SPLIT
+            const uint32_t k0 = shared_below + b0;
+            const uint32_t k1 = shared_below + (uint32_t)__popcll(a0) + b1;
+            const uint32_t u0 = i0 + lane + j0[g] - k0, u1 = i0 + 64 + lane + j1[g] - k1;
+#else
             const uint32_t k0 = shared_below + b0 + b1;
             const uint32_t k1 = k0 + (uint32_t)((a0 >> lane) & 1);
             const uint32_t i = i0 + 2 * lane;
             const uint32_t u0 = i + j0[g] - k0, u1 = i + 1 + j1[g] - k1;   // union ranks
+#endif
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
             shared_below += __popcll(a0) + __popcll(a1);
             if (g == kGroup - 1) {
                 const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
+#if FPM_RANK_SPLIT
+                u_last = (uint32_t)__builtin_amdgcn_readlane((int)(e >= 64 ? u1 : u0), (int)(e & 63));
+#else
                 u_last = (uint32_t)__builtin_amdgcn_readlane((int)((e & 1) ? u1 : u0), (int)(e >> 1));
+#endif
             }
         }
         return u_last;
@@ -1732,18 +1809,20 @@ static hipError_t walk_candidates_c(const uint64_t *d_cand, const unsigned long 
                                     uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
                                     uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                                     const uint32_t *d_qry_len, uint64_t qry_stride,
-                                    uint32_t hash_bytes, uint32_t S, C *d_numer, C *d_denom,
-                                    hipStream_t st)
+                                    uint32_t hash_bytes, uint32_t S, RecRows rr, RecRows rq,
+                                    C *d_numer, C *d_denom, hipStream_t st)
 {
     dim3 grid((uint32_t)((cap + 255) / 256));
     if (hash_bytes == 8)
         hipLaunchKernelGGL((walk_cand_kernel<uint64_t, C>), grid, dim3(256), 0, st, d_cand, d_n_cand,
                            (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
-                           (const uint64_t *)d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
+                           (const uint64_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
+                           d_denom);
     else
         hipLaunchKernelGGL((walk_cand_kernel<uint32_t, C>), grid, dim3(256), 0, st, d_cand, d_n_cand,
                            (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
-                           (const uint32_t *)d_qry, d_qry_len, qry_stride, S, d_numer, d_denom);
+                           (const uint32_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
+                           d_denom);
     return hipGetLastError();
 }
 
@@ -1751,16 +1830,18 @@ hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long lo
                                   uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                                   const uint32_t *d_qry_len, uint64_t qry_stride,
-                                  uint32_t hash_bytes, uint32_t S, Counts cnt, hipStream_t st)
+                                  uint32_t hash_bytes, uint32_t S, Counts cnt, RecRows rec_ref,
+                                  RecRows rec_qry, hipStream_t st)
 {
     if (!cap) return hipSuccess;
+    if (!rec_ref.val || !rec_qry.val) rec_ref = rec_qry = RecRows{};   // both sides or neither
     if (cnt.c16)
         return walk_candidates_c(d_cand, d_n_cand, cap, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
-                                 d_qry_len, qry_stride, hash_bytes, S, (uint16_t *)cnt.numer,
-                                 (uint16_t *)cnt.denom, st);
+                                 d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
+                                 (uint16_t *)cnt.numer, (uint16_t *)cnt.denom, st);
     return walk_candidates_c(d_cand, d_n_cand, cap, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
-                             d_qry_len, qry_stride, hash_bytes, S, (uint32_t *)cnt.numer,
-                             (uint32_t *)cnt.denom, st);
+                             d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
+                             (uint32_t *)cnt.numer, (uint32_t *)cnt.denom, st);
 }
 
 hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const uint64_t *d_qry_length,

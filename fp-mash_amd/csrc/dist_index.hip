@@ -668,7 +668,7 @@ void probe_rows_kernel(
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) rowbits[w] = 0;
     __syncthreads();
     // lq: the row's list length (the defaults); lit: the hashes probed, which differ from lq
-    // when the probed rows are the deduplicated copies of unsorted lists (dedup_rows_kernel)
+    // when the probed rows are the record rows of unsorted lists (record_rows_kernel)
     const uint32_t lq = qry_len[q];
     const uint32_t lit = qry_it_len ? qry_it_len[q] : lq;
     // one set against itself: row q's own entry sits in the bucket of each of its hashes,
@@ -827,91 +827,78 @@ void probe_rows_kernel(
     }
 }
 
-// ---- unsorted (-fp) lists: the posting events of the raw lists are sum_v n_v^2 over
-// occurrences, and CFL k-finger lists repeat a few values hundreds of times per list (the
-// line "100" is ~1 % of all lines: C3 gives 2.9e10 events, more than walking every pair).
-// Whether a pair shares a value does not depend on order or multiplicity, and the literal
-// walk (CommandDistance.cpp:376-400) only ever reads A[i] with i < min(la, S) (i <= steps <
-// S), so the index and the probe run on each row's first min(len, S) entries sorted and
-// deduplicated; the candidates they find are then walked on the original lists.
-// One workgroup per row: bitonic sort of NP (pow2 >= the row cap) keys in LDS, pads = ~0
-// (a real ~0 sorts among the pads, but only positions < m are read), then a block scan
-// of the first-of-run flags compacts the distinct values into out[row * out_stride ...].
-template <typename H, int NP>
-__global__ __launch_bounds__(256) void dedup_rows_kernel(
-    const H *__restrict__ in, const uint32_t *__restrict__ in_len, uint64_t in_stride,
-    uint32_t S, H *__restrict__ out, uint32_t *__restrict__ out_len, uint64_t out_stride)
+// ---- unsorted (-fp) lists: which pairs can the literal walk (CommandDistance.cpp:376-400)
+// count anything for?  Let KA(i) = max(A[0..i]) and KB(j) = max(B[0..j]).  At a state (i, j)
+// the walk reaches, A[i] < B[j] implies KA(i) <= KB(j): the previous maximum of A was taken
+// at a state (i', j') with j' <= j, so it was <= B[j'] <= KB(j).  Likewise B[j] < A[i]
+// implies KB(j) <= KA(i), and an equal step A[i] == B[j] implies KA(i) == KB(j) = v: v is
+// the running maximum of both prefixes, i.e. a RECORD value (a strict increase of the running
+// maximum) of both lists, among their first min(len, S) entries (the walk only reads A[i]
+// with i <= steps < S).  So a pair whose lists share no record value has common = 0 and
+// denom = min(S, la + lb), the values the probe writes for every pair.  The index and probe
+// therefore run on each row's records (strictly increasing: sorted and distinct), and the
+// pairs sharing one are walked literally on the original lists.  Random-order lists hold
+// ~ln(S) + 0.58 records (C3's CFL lists: 7.5 of their first 1,000 entries), and the pairs
+// sharing a record are nearly exactly those the walk counts something for (C3: 5.4 % vs
+// 5.3 %), where the sorted distinct copies of every entry gave 2.9e10 posting events on C3
+// (its frequent k-fingers are in nearly every list) and left the dense walk cheaper.
+// One wave per row: chunks of 64 entries, the running maximum by a wave max-scan, the
+// records compacted by ballot into out[row * out_stride ...] (and, with pos_out, their
+// positions in the row beside them: the candidate walk starts at the shared ones).
+constexpr int kRecWaves = 4;
+template <typename H>
+__global__ __launch_bounds__(64 * kRecWaves) void record_rows_kernel(
+    const H *__restrict__ in, const uint32_t *__restrict__ in_len, uint64_t in_stride, uint32_t n,
+    uint32_t S, H *__restrict__ out, uint32_t *__restrict__ pos_out, uint32_t *__restrict__ out_len,
+    uint64_t out_stride)
 {
-    __shared__ H key[NP];
-    __shared__ uint32_t wsum[4];
-    constexpr int PT = NP / 256;          // elements per thread in the compaction
-    const uint32_t row = blockIdx.x, t = threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t row = blockIdx.x * kRecWaves + (threadIdx.x >> 6);
+    if (row >= n) return;
     const uint32_t m = min(min(in_len[row], S), (uint32_t)out_stride);
     const H *src = in + (uint64_t)row * in_stride;
-    for (uint32_t i = t; i < NP; i += 256) key[i] = i < m ? src[i] : (H)~(H)0;
-    __syncthreads();
-    for (uint32_t k = 2; k <= NP; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = t; i < NP; i += 256) {
-                const uint32_t x = i ^ j;
-                if (x > i) {
-                    const H a = key[i], b = key[x];
-                    if ((a > b) == ((i & k) == 0)) { key[i] = b; key[x] = a; }
-                }
-            }
-            __syncthreads();
-        }
-    H v[PT];
-    uint32_t f = 0, cnt = 0;
-#pragma unroll
-    for (int u = 0; u < PT; u++) {
-        const uint32_t i = t * PT + u;
-        v[u] = key[i];
-        const bool first = i < m && (i == 0 || key[i - 1] != v[u]);
-        f |= (first ? 1u : 0u) << u;
-        cnt += first ? 1u : 0u;
-    }
-    const uint32_t lane = t & 63, wave = t >> 6;
-    uint32_t x = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) { const uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
-    if (lane == 63) wsum[wave] = x;
-    __syncthreads();
-    uint32_t pos = x - cnt, tot = 0;
-    for (uint32_t w = 0; w < 4; w++) { if (w < wave) pos += wsum[w]; tot += wsum[w]; }
     H *dst = out + (uint64_t)row * out_stride;
+    uint32_t *pdst = pos_out ? pos_out + (uint64_t)row * out_stride : nullptr;
+    H run = 0;              // the running maximum before the chunk (entry 0 always counts)
+    uint32_t cnt = 0;
+    for (uint32_t c0 = 0; c0 < m; c0 += 64) {
+        const uint32_t i = c0 + lane;
+        const H v = i < m ? src[i] : H(0);
+        H pm = v;           // inclusive max-scan over the chunk
 #pragma unroll
-    for (int u = 0; u < PT; u++)
-        if (f >> u & 1u) dst[pos++] = v[u];
-    if (t == 0) out_len[row] = tot;
+        for (int d = 1; d < 64; d <<= 1) {
+            const H y = (H)__shfl_up((unsigned long long)pm, d, 64);
+            if ((int)lane >= d) pm = pm > y ? pm : y;
+        }
+        H before = (H)__shfl_up((unsigned long long)pm, 1, 64);
+        before = lane == 0 ? run : (before > run ? before : run);
+        const bool rec = i < m && (i == 0 || v > before);
+        const uint64_t bm = __ballot(rec);
+        const uint32_t at = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        if (rec) dst[at] = v;
+        if (rec && pdst) pdst[at] = i;
+        cnt += (uint32_t)__popcll(bm);
+        const H top = (H)__shfl((unsigned long long)pm, 63, 64);
+        run = top > run ? top : run;
+    }
+    if (lane == 0) out_len[row] = cnt;
 }
 
-template <typename H>
-static hipError_t dedup_rows_h(const void *in, const uint32_t *in_len, uint64_t in_stride,
-                               uint32_t n, uint32_t S, void *out, uint32_t *out_len,
-                               uint64_t out_stride, hipStream_t st)
-{
-#define FPM_DEDUP(NP)                                                                         \
-    hipLaunchKernelGGL((dedup_rows_kernel<H, NP>), dim3(n), dim3(256), 0, st, (const H *)in,  \
-                       in_len, in_stride, S, (H *)out, out_len, out_stride)
-    if (out_stride <= 256) FPM_DEDUP(256);
-    else if (out_stride <= 512) FPM_DEDUP(512);
-    else if (out_stride <= 1024) FPM_DEDUP(1024);
-    else if (out_stride <= 2048) FPM_DEDUP(2048);
-    else FPM_DEDUP(4096);
-#undef FPM_DEDUP
-    return hipGetLastError();
-}
-
-hipError_t launch_dedup_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
-                             uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
-                             uint32_t *out_len, uint64_t out_stride, hipStream_t st)
+hipError_t launch_record_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
+                              uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
+                              uint32_t *pos_out, uint32_t *out_len, uint64_t out_stride,
+                              hipStream_t st)
 {
     if (!n) return hipSuccess;
-    if (out_stride > kDedupMax) return hipErrorInvalidValue;
-    return hash_bytes == 8
-               ? dedup_rows_h<uint64_t>(in, in_len, in_stride, n, S, out, out_len, out_stride, st)
-               : dedup_rows_h<uint32_t>(in, in_len, in_stride, n, S, out, out_len, out_stride, st);
+    const dim3 g((n + kRecWaves - 1) / kRecWaves), b(64 * kRecWaves);
+    if (hash_bytes == 8)
+        hipLaunchKernelGGL(record_rows_kernel<uint64_t>, g, b, 0, st, (const uint64_t *)in, in_len,
+                           in_stride, n, S, (uint64_t *)out, pos_out, out_len, out_stride);
+    else
+        hipLaunchKernelGGL(record_rows_kernel<uint32_t>, g, b, 0, st, (const uint32_t *)in, in_len,
+                           in_stride, n, S, (uint32_t *)out, pos_out, out_len, out_stride);
+    return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kPubWords) void publish_kernel(const unsigned long long *__restrict__ src,

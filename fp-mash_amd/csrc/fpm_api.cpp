@@ -75,7 +75,7 @@ struct fpm_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
     // grow-only device scratch, one buffer per named slot (no allocation in steady state)
     struct Slot { void *p = nullptr; size_t bytes = 0; };
-    Slot scratch[20];
+    Slot scratch[22];
     unsigned long long *host_counters = nullptr;   // pinned + mapped, for the events read-back
     unsigned long long *dev_counters = nullptr;    // its device-side address
     unsigned long long pub_seq = 0;                // last sequence number published into it
@@ -1907,7 +1907,7 @@ struct fpm_refset {
     IdxGeom geom{};
     bool sparse_ok = false;       // the index exists (the sparse path is possible)
     bool ref_unsorted = false;    // some reference row is unsorted / carries duplicates
-    bool deduped = false;         // the index holds launch_dedup_rows copies (slots 10, 11)
+    bool recorded = false;        // the index holds launch_record_rows copies (slots 10, 11)
     uint64_t mr = 0;              // their row stride
     uint64_t self_events = 0;     // sum_b |b|^2: the posting events of the set against itself
     // per-query-block host buffers (fpm_refset_dist): pinned staging + device copies
@@ -1933,8 +1933,8 @@ static hipError_t slot_buf(fpm_ctx::Slot &s, size_t bytes, void **out)
 }
 
 // Build the reference index of a resident set (once): over the raw rows, or, when a row is
-// unsorted / carries duplicates (-fp lists) and min(stride, S) <= kDedupMax, over their
-// sorted distinct copies (the probe then sees each value once per list).
+// unsorted / carries duplicates (-fp lists), over their records (launch_record_rows: only
+// pairs sharing a record value can count anything in the literal walk).
 static int refset_build_index(fpm_refset *rs, hipStream_t st)
 {
     fpm_ctx *ctx = rs->ctx;
@@ -1961,16 +1961,17 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
     rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
     rs->self_events = ctx->host_counters[0];
     rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
-    rs->deduped = rs->ref_unsorted && rs->mr <= kDedupMax;
-    if (rs->deduped) {
-        void *dref, *dref_len;
+    rs->recorded = rs->ref_unsorted;
+    if (rs->recorded) {
+        void *dref, *dref_len, *dref_pos;
         HIP_TRY(slot_buf(rs->slot[10], (size_t)rs->n_ref * rs->mr * rs->hash_bytes, &dref));
         HIP_TRY(slot_buf(rs->slot[11], (size_t)rs->n_ref * 4, &dref_len));
+        HIP_TRY(slot_buf(rs->slot[12], (size_t)rs->n_ref * rs->mr * 4, &dref_pos));
         {
             TimedLaunch tl(ctx, FPM_K_INDEX, st);
-            HIP_TRY(launch_dedup_rows(rs->ref, rs->ref_len, rs->ref_stride, rs->n_ref,
-                                      rs->hash_bytes, rs->sketch_size, dref,
-                                      (uint32_t *)dref_len, rs->mr, st));
+            HIP_TRY(launch_record_rows(rs->ref, rs->ref_len, rs->ref_stride, rs->n_ref,
+                                       rs->hash_bytes, rs->sketch_size, dref, (uint32_t *)dref_pos,
+                                       (uint32_t *)dref_len, rs->mr, st));
             tl.done();
         }
         geom = make_geom(rs->n_ref, (uint64_t)rs->n_ref * rs->mr);
@@ -2073,6 +2074,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const uint32_t *dir = nullptr, *entries = nullptr;
         uint64_t ev = 0;
         bool all_sorted = true;
+        RecRows rec_r{}, rec_q{};                   // record rows (unsorted lists) for the walk
         // A resident sorted set against another block of sorted rows (the C4 block pairs, the
         // CLI's query blocks): no probe count.  The count pass reads every query hash's
         // bucket bounds at random (~0.27 ms for 2.2e7 hashes at N = 8, as long as the index
@@ -2083,12 +2085,12 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         // density (its self events per row) says the block is far from the dense regime.
         const long double ev_est =
             rs ? (long double)rs->self_events * n_qry / std::max<uint32_t>(1, rs->n_ref) : 0.0L;
-        const bool skip_count = rs && !self_set && !rs->deduped && !rs->ref_unsorted &&
+        const bool skip_count = rs && !self_set && !rs->recorded && !rs->ref_unsorted &&
                                 hash_bytes == 8 &&
                                 (ctx->dist_mode == FPM_DIST_SPARSE ||
                                  (ctx->dist_mode == FPM_DIST_AUTO &&
                                   ev_est * 16.0L <= (long double)n_pairs * sketch_size));
-        if (rs && self_set && !rs->deduped) {
+        if (rs && self_set && !rs->recorded) {
             // the resident set against itself: its posting events and sortedness are the
             // index build's (sum_b |b|^2, the reference flag), no probe count
             geom = rs->geom;
@@ -2111,13 +2113,18 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             entries = (const uint32_t *)rs->slot[5].p;
             TimedLaunch tl(ctx, FPM_K_INDEX, st);
             HIP_TRY(hipMemsetAsync(ctr, 0, 67 * 8, st));
-            if (rs->deduped) {
+            if (rs->recorded) {
                 const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
-                void *dqry, *dqry_len;
+                void *dqry, *dqry_len, *dqry_pos;
                 HIP_TRY(scratch(ctx, 12, (size_t)n_qry * mq * hash_bytes, &dqry));
                 HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
-                HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                          sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
+                HIP_TRY(scratch(ctx, 20, (size_t)n_qry * mq * 4, &dqry_pos));
+                HIP_TRY(launch_record_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                           sketch_size, dqry, (uint32_t *)dqry_pos,
+                                           (uint32_t *)dqry_len, mq, st));
+                rec_r = RecRows{rs->slot[10].p, (const uint32_t *)rs->slot[12].p,
+                                (const uint32_t *)rs->slot[11].p, rs->mr};
+                rec_q = RecRows{dqry, (const uint32_t *)dqry_pos, (const uint32_t *)dqry_len, mq};
                 p_qry = dqry;
                 p_qry_it = (const uint32_t *)dqry_len;
                 p_qry_stride = mq;
@@ -2128,9 +2135,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
             ev = ctx->host_counters[0];
             const bool q_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
-            // deduplicated probe rows are sorted by construction: the query's own order is
-            // what the walk needs, so test the originals when the index is deduplicated
-            all_sorted = !rs->ref_unsorted && (rs->deduped ? false : !q_unsorted);
+            // record rows are sorted by construction: the query's own order is what the walk
+            // needs, so the walk is literal whenever the index holds records
+            all_sorted = !rs->ref_unsorted && (rs->recorded ? false : !q_unsorted);
         } else {
             void *dir_, *entries_;
             HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir_));
@@ -2154,30 +2161,40 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             entries = (const uint32_t *)entries_;
             ev = ctx->host_counters[0];
             all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
-            // Unsorted lists (-fp): re-index each row's first min(len, S) entries sorted and
-            // deduplicated (launch_dedup_rows); repeated values no longer square the posting
-            // events.  The candidates are walked on the original lists.
+            // Unsorted lists (-fp): re-index each row's records among its first min(len, S)
+            // entries (launch_record_rows): ~ln(S) values per row instead of every distinct
+            // one, and only pairs sharing a record can count anything.  The candidates are
+            // walked on the original lists.
             const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
             const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
-            if (!all_sorted && mr <= kDedupMax && mq <= kDedupMax && ev > 0) {
-                void *dref, *dref_len, *dqry = nullptr, *dqry_len = nullptr;
+            if (!all_sorted && ev > 0) {
+                void *dref, *dref_len, *dref_pos, *dqry = nullptr, *dqry_len = nullptr,
+                     *dqry_pos = nullptr;
                 HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
                 HIP_TRY(scratch(ctx, 11, (size_t)n_ref * 4, &dref_len));
+                HIP_TRY(scratch(ctx, 19, (size_t)n_ref * mr * 4, &dref_pos));
                 if (!self_set) {
                     HIP_TRY(scratch(ctx, 12, (size_t)n_qry * mq * hash_bytes, &dqry));
                     HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
+                    HIP_TRY(scratch(ctx, 20, (size_t)n_qry * mq * 4, &dqry_pos));
                 }
                 geom = make_geom(n_ref, (uint64_t)n_ref * mr);
                 geom.kmax = events + 68;
                 {
                     TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                    HIP_TRY(launch_dedup_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
-                                              sketch_size, dref, (uint32_t *)dref_len, mr, st));
+                    HIP_TRY(launch_record_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
+                                               sketch_size, dref, (uint32_t *)dref_pos,
+                                               (uint32_t *)dref_len, mr, st));
                     if (!self_set)
-                        HIP_TRY(launch_dedup_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                                  sketch_size, dqry, (uint32_t *)dqry_len, mq, st));
+                        HIP_TRY(launch_record_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                                   sketch_size, dqry, (uint32_t *)dqry_pos,
+                                                   (uint32_t *)dqry_len, mq, st));
                     tl.done();
                 }
+                rec_r = RecRows{dref, (const uint32_t *)dref_pos, (const uint32_t *)dref_len, mr};
+                rec_q = self_set ? rec_r
+                                 : RecRows{dqry, (const uint32_t *)dqry_pos,
+                                           (const uint32_t *)dqry_len, mq};
                 p_qry = self_set ? dref : dqry;
                 p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
                 p_qry_stride = self_set ? mr : mq;
@@ -2271,7 +2288,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                                                    qry_stride, hash_bytes, sketch_size, cnt,
-                                                   st));
+                                                   rec_r, rec_q, st));
                 tl.done();
             }
             if (defer_fill)

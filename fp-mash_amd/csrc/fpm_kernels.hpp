@@ -99,11 +99,21 @@ hipError_t launch_compare_grid_img(const void *d_ref, const uint32_t *d_ref_len,
                                    const uint32_t *d_qry_len, uint64_t qry_stride, uint32_t n_qry,
                                    uint32_t sketch_size, void *ublk, void *bimg, Counts cnt,
                                    hipStream_t st);
+// the record rows of one side of a candidate walk (launch_record_rows): values, positions,
+// counts, row stride; val == nullptr: none (the walk starts at (0, 0))
+struct RecRows {
+    const void *val = nullptr;
+    const uint32_t *pos = nullptr, *len = nullptr;
+    uint64_t stride = 0;
+};
+// the literal walk of each candidate pair; with record rows of both sides (unsorted lists),
+// only the stretches where both running maxima equal a shared record are walked
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
                                   uint64_t cap, const void *d_ref, const uint32_t *d_ref_len,
                                   uint64_t ref_stride, uint32_t n_ref, const void *d_qry,
                                   const uint32_t *d_qry_len, uint64_t qry_stride,
-                                  uint32_t hash_bytes, uint32_t S, Counts cnt, hipStream_t st);
+                                  uint32_t hash_bytes, uint32_t S, Counts cnt, RecRows rec_ref,
+                                  RecRows rec_qry, hipStream_t st);
 
 // bucket index over ref hashes (dist_index.hip)
 constexpr uint32_t kIdxL1 = 10;        // level-1 partition bits
@@ -141,12 +151,14 @@ uint64_t scan_scratch_words(uint64_t n);
 constexpr uint32_t kPubWords = 128;
 hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned long long *h_dst,
                           unsigned long long seq, hipStream_t st);
-// each row's first min(len, S, out_stride) entries sorted and deduplicated (dist_index.hip),
-// the index / probe input for unsorted lists; out_stride <= kDedupMax
-constexpr uint32_t kDedupMax = 4096;
-hipError_t launch_dedup_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
-                             uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
-                             uint32_t *out_len, uint64_t out_stride, hipStream_t st);
+// each row's records among its first min(len, S, out_stride) entries (the strict increases of
+// its running maximum: sorted and distinct; dist_index.hip), the index / probe input for
+// unsorted lists: only pairs sharing a record value can count anything in the literal walk
+// (pos_out, may be null: each record's position in its row, at the same offsets)
+hipError_t launch_record_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
+                              uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
+                              uint32_t *pos_out, uint32_t *out_len, uint64_t out_stride,
+                              hipStream_t st);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
@@ -179,7 +191,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
                              unsigned long long *events, hipStream_t st, uint32_t q_lo = 0);
 // (q_lo, n_qry: the query rows [q_lo, q_lo + n_qry) of the grid)
-// (d_qry_it_len non-null: the probed query rows are launch_dedup_rows copies of length
+// (d_qry_it_len non-null: the probed query rows are launch_record_rows copies of length
 // d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)
 // (self_set: the query set is the indexed ref set, same buffers: buckets of one entry are
 // the row's own hash and are not read)

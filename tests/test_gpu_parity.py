@@ -190,10 +190,11 @@ def _skewed_fp_lists(rng, base, n, heavy=4, max_len=2100):
 
 
 @pytest.mark.parametrize("mode", ["auto", "sparse"])
-def test_dist_unsorted_dedup_index(ctx, oracle, mode):
+def test_dist_unsorted_record_index(ctx, oracle, mode):
     """Unsorted lists with heavily repeated values: the index is rebuilt over each row's
-    sorted, deduplicated first min(len, S) entries and the candidates are walked on the
-    original lists.  Self set and a separate query set, against the literal-walk oracle."""
+    records (the strict increases of its running maximum among its first min(len, S)
+    entries) and the pairs sharing a record are walked on the original lists.  Self set and
+    a separate query set, against the literal-walk oracle."""
     import fpmash
     rng = np.random.default_rng(77)
     base = rng.integers(0, 2 ** 32, size=20000, dtype=np.uint64).astype(np.uint32)
@@ -216,6 +217,47 @@ def test_dist_unsorted_dedup_index(ctx, oracle, mode):
                 if mode == "sparse":
                     assert st["sparse"] == 1, st          # index + literal walk
                     assert st["candidates"] < len(a) * len(b)
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
+def _record_edge_lists(rng):
+    """-fp lists at the edges of the record filter: ascending (every entry a record),
+    descending (one record), a leading 0, small alphabets (repeated maxima), the shared value
+    first in one list and last in the other, long lists whose shared records lie past S
+    steps, and empty lists."""
+    L = [np.arange(0, 300, dtype=np.uint32), np.arange(0, 300, 2, dtype=np.uint32),
+         np.arange(300, 0, -1, dtype=np.uint32), np.array([0, 0, 5, 0, 5, 7], np.uint32),
+         np.array([0], np.uint32), np.zeros(0, np.uint32), np.array([9, 1, 2, 3], np.uint32),
+         np.array([1, 2, 3, 9], np.uint32),
+         np.concatenate([rng.integers(0, 1000, 1500), [4000000000]]).astype(np.uint32),
+         np.concatenate([[4000000000], rng.integers(0, 1000, 1500)]).astype(np.uint32)]
+    for _ in range(30):
+        L.append(rng.integers(0, int(rng.choice([3, 8, 50, 2 ** 32])), int(rng.integers(0, 400)),
+                              dtype=np.uint64).astype(np.uint32))
+    return L
+
+
+@pytest.mark.parametrize("mode", ["auto", "sparse"])
+def test_dist_unsorted_record_edges(ctx, oracle, mode):
+    """The record filter's edge cases (_record_edge_lists) for S = 1, 5, 64, 1000, self set
+    and a separate query set, against the literal-walk oracle."""
+    import fpmash
+    rng = np.random.default_rng(5)
+    refs = _record_edge_lists(rng)
+    qrys = _record_edge_lists(rng)[::-1]
+    rl = [max(1, len(x)) for x in refs]
+    ql = [max(1, len(x)) for x in qrys]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE if mode == "sparse" else fpmash.DIST_AUTO)
+    try:
+        for S in (1, 5, 64, 1000):
+            for (a, al), (b, bl) in (((refs, rl), (refs, rl)), ((refs, rl), (qrys, ql))):
+                got = ctx.dist(a, b, S, use64=False, k=1, kmer_space=10.0, ref_lengths=al,
+                               qry_lengths=bl)
+                nu, de, di, pv = oracle.dist_grid(a, al, b, bl, S, 1, 10.0, use64=False)
+                assert np.array_equal(got["numer"], nu), S
+                assert np.array_equal(got["denom"], de), S
+                np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
     finally:
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 

@@ -1,13 +1,17 @@
 #!/bin/bash
-# tools/gpu_r04c.sh — the balanced XCD tile map for the C3 walk (A) against the pre-XCD build
-# (B), and the CLI dist with one pwritev() per block (default blocks vs 4 M-pair blocks).
+# tools/gpu_r04c.sh — C3 through the record index (A) against the build before it and the XCD
+# tile map (B, the dense image walk), the rank kernel on interleaved lanes (A) against adjacent pairs per lane (B), and the CLI dist with one pwritev() per block (default blocks vs 4 M-pair blocks).
 set -o pipefail
 cd "$(dirname "$0")/.."
 O=gpurun_out/r04c; mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
-  -k "resident_blocks or fp" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
+  -k "resident_blocks or fp or dist or refset or c4 or record or unsorted" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
+BENCH_ARGS="--steps 20 --warmup 3 --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-split --no-full-grid --no-parity" \
+  timeout -k 10 600 bash tools/ab_bench.sh fp-mash_amd/lib/libfpmash.so fp-mash_amd/lib/libfpmash_pair.so 3 \
+  > $O/rank_ab.txt 2>&1 || { tail -20 $O/rank_ab.txt; exit 1; }
+cat $O/rank_ab.txt
 BENCH_ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-fp-text --no-c4 --no-c5 --no-cli --no-split --no-full-grid --no-parity" \
   timeout -k 10 600 bash tools/ab_bench.sh fp-mash_amd/lib/libfpmash.so fp-mash_amd/lib/libfpmash_prexcd.so 3 \
   > $O/c3_xcd_ab.txt 2>&1 || { tail -20 $O/c3_xcd_ab.txt; exit 1; }
