@@ -513,10 +513,15 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
     denom = outs[1].to_array(np.uint16, np_)
     # full-size parity of the index path: the same grid by the dense literal walk of every pair
     same_as_dense = None
+    dense_ms = None
     if st["sparse"]:
         ctx.set_dist_mode(fpmash.DIST_DENSE)
         run()
         ctx.synchronize()
+        t0 = time.perf_counter()
+        run()           # timed once beside the index path: the dense image walk of every pair
+        ctx.synchronize()
+        dense_ms = (time.perf_counter() - t0) * 1e3
         ctx.set_dist_mode(fpmash.DIST_AUTO)
         same_as_dense = bool(np.array_equal(numer, outs[0].to_array(np.uint16, np_)) and
                              np.array_equal(denom, outs[1].to_array(np.uint16, np_)))
@@ -559,7 +564,8 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
             "dist_path": fpmash.DIST_PATHS[int(st["sparse"])],
             "posting_events": st["events"], "candidate_pairs": st["candidates"],
             "pairs_sharing_a_hash": int((numer > 0).sum()),
-            "counts_equal_dense_walk": same_as_dense, "parity": par}
+            "counts_equal_dense_walk": same_as_dense, "dense_walk_ms": dense_ms,
+            "parity": par}
 
 
 def compact_out(ctx, cells):
@@ -1273,7 +1279,8 @@ def compact_line(d, detail_path=None):
         "dist_path": g(d, "dist", "path"),
         "c2_full_grid_ms": _r(g(d, "config", "full_grid_ms_per_step")),
         "fp_text_lines_per_s": _r(g(d, "fp_text", "lines_per_s_device")),
-        "c3_dist_ms": _r(g(c3, "dist_ms")), "c3_parse_device_ms": _r(g(c3, "parse_device_ms")),
+        "c3_dist_ms": _r(g(c3, "dist_ms")), "c3_dense_walk_ms": _r(g(c3, "dense_walk_ms")),
+        "c3_parse_device_ms": _r(g(c3, "parse_device_ms")),
         "c4_ms_per_step": _r(g(c4, "ms_per_step")), "c4_mpairs_per_s": _r(g(c4, "mpairs_per_s")),
         "c4_output": g(c4, "output"),
         "c5_ms_per_step": _r(g(c5, "ms_per_step")), "c5_bases_per_s": _r(g(c5, "bases_per_s")),
