@@ -242,7 +242,9 @@ __device__ __forceinline__ void walk_pair_rec(const H *__restrict__ A, uint32_t 
         uint32_t i = PA[x], j = PB[y];
         uint32_t n = i + j - common;
         if (n >= S) break;
-        const uint32_t ea = x + 1 < na ? PA[x + 1] : la, eb = y + 1 < nb ? PB[y + 1] : lb;
+        // (the last stretch ends at min(len, S): no step reads past entry S - 1)
+        const uint32_t ea = x + 1 < na ? PA[x + 1] : min(la, S);
+        const uint32_t eb = y + 1 < nb ? PB[y + 1] : min(lb, S);
         H a = A[i], b = B[j];
         while (i < ea && j < eb && n < S) {
             const bool lt = a < b, gt = b < a;
@@ -284,6 +286,57 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
                   qry_len[q], S, c, d);
     numer[o] = (C)c;
     denom[o] = (C)d;
+}
+
+// The same stretch walk with one workgroup per query row (the probe's row segments): the
+// query row's first min(lb, S) entries and its records staged in LDS, so every step of the
+// walk reads one list from LDS instead of both from L2; each lane takes one candidate ref
+// row.  Rows past the LDS capacity walk both lists from global memory.
+constexpr uint32_t kWalkRowCap = 4096;   // staged query entries
+constexpr uint32_t kWalkRecCap = 1024;   // staged query records
+template <typename H, typename C>
+__global__ __launch_bounds__(256) void walk_rows_rec_kernel(
+    const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
+    const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
+    uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
+    uint64_t qry_stride, uint32_t S, RecRows rr, RecRows rq, C *__restrict__ numer,
+    C *__restrict__ denom)
+{
+    __shared__ H Bs[kWalkRowCap];
+    __shared__ H Rb[kWalkRecCap];
+    __shared__ uint32_t Pb[kWalkRecCap];
+    const uint32_t q = xcd_row(blockIdx.x, n_qry);
+    if (q >= n_qry) return;
+    const uint64_t seg = row_seg[q];
+    const uint32_t n = (uint32_t)(seg & 0xFFFFFF);
+    if (n == 0) return;
+    const uint64_t base = seg >> 24;
+    const uint32_t lb = qry_len[q], mb = min(lb, S), nb = rq.len[q];
+    const H *B = qry + (uint64_t)q * qry_stride;
+    const H *RB = (const H *)rq.val + (uint64_t)q * rq.stride;
+    const uint32_t *PB = rq.pos + (uint64_t)q * rq.stride;
+    const bool staged = mb <= kWalkRowCap && nb <= kWalkRecCap;   // block-uniform
+    if (staged) {
+        for (uint32_t t = threadIdx.x; t < mb; t += 256) Bs[t] = B[t];
+        for (uint32_t t = threadIdx.x; t < nb; t += 256) { Rb[t] = RB[t]; Pb[t] = PB[t]; }
+        __syncthreads();
+    }
+    const uint64_t pair_row = (uint64_t)q * n_ref;
+    for (uint32_t c = threadIdx.x; c < n; c += 256) {
+        const uint64_t o = cand[base + c];
+        const uint32_t r = (uint32_t)(o - pair_row);
+        const H *A = ref + (uint64_t)r * ref_stride;
+        const H *RA = (const H *)rr.val + (uint64_t)r * rr.stride;
+        const uint32_t *PA = rr.pos + (uint64_t)r * rr.stride;
+        uint32_t cm, dn;
+        if (staged)
+            walk_pair_rec(A, ref_len[r], (const H *)Bs, lb, S, RA, PA, rr.len[r], (const H *)Rb,
+                          (const uint32_t *)Pb, nb, cm, dn);
+        else
+            walk_pair_rec(A, ref_len[r], B, lb, S, RA, PA, rr.len[r], RB, PB, nb, cm, dn);
+        numer[o] = (C)cm;
+        denom[o] = (C)dn;
+    }
 }
 
 // Sorted, distinct lists (every sketch the k-mer path produces): the walk of
@@ -1824,6 +1877,44 @@ static hipError_t walk_candidates_c(const uint64_t *d_cand, const unsigned long 
                            (const uint32_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
                            d_denom);
     return hipGetLastError();
+}
+
+template <typename C>
+static hipError_t walk_rows_rec_c(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
+                                  const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                                  uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
+                                  uint64_t qry_stride, uint32_t hash_bytes, uint32_t S, RecRows rr,
+                                  RecRows rq, C *d_numer, C *d_denom, hipStream_t st)
+{
+    const dim3 g(xcd_grid(n_qry)), b(256);
+    if (hash_bytes == 8)
+        hipLaunchKernelGGL((walk_rows_rec_kernel<uint64_t, C>), g, b, 0, st, d_cand, row_seg, n_qry,
+                           (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                           (const uint64_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
+                           d_denom);
+    else
+        hipLaunchKernelGGL((walk_rows_rec_kernel<uint32_t, C>), g, b, 0, st, d_cand, row_seg, n_qry,
+                           (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
+                           (const uint32_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
+                           d_denom);
+    return hipGetLastError();
+}
+
+hipError_t launch_walk_rows_rec(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
+                                const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
+                                uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
+                                uint64_t qry_stride, uint32_t hash_bytes, uint32_t S, Counts cnt,
+                                RecRows rec_ref, RecRows rec_qry, hipStream_t st)
+{
+    if (!n_qry) return hipSuccess;
+    if (!rec_ref.val || !rec_qry.val) return hipErrorInvalidValue;
+    if (cnt.c16)
+        return walk_rows_rec_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                               d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
+                               (uint16_t *)cnt.numer, (uint16_t *)cnt.denom, st);
+    return walk_rows_rec_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
+                           d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
+                           (uint32_t *)cnt.numer, (uint32_t *)cnt.denom, st);
 }
 
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,
