@@ -288,57 +288,6 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
     denom[o] = (C)d;
 }
 
-// The same stretch walk with one workgroup per query row (the probe's row segments): the
-// query row's first min(lb, S) entries and its records staged in LDS, so every step of the
-// walk reads one list from LDS instead of both from L2; each lane takes one candidate ref
-// row.  Rows past the LDS capacity walk both lists from global memory.
-constexpr uint32_t kWalkRowCap = 4096;   // staged query entries
-constexpr uint32_t kWalkRecCap = 1024;   // staged query records
-template <typename H, typename C>
-__global__ __launch_bounds__(256) void walk_rows_rec_kernel(
-    const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
-    const H *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t ref_stride,
-    uint32_t n_ref, const H *__restrict__ qry, const uint32_t *__restrict__ qry_len,
-    uint64_t qry_stride, uint32_t S, RecRows rr, RecRows rq, C *__restrict__ numer,
-    C *__restrict__ denom)
-{
-    __shared__ H Bs[kWalkRowCap];
-    __shared__ H Rb[kWalkRecCap];
-    __shared__ uint32_t Pb[kWalkRecCap];
-    const uint32_t q = xcd_row(blockIdx.x, n_qry);
-    if (q >= n_qry) return;
-    const uint64_t seg = row_seg[q];
-    const uint32_t n = (uint32_t)(seg & 0xFFFFFF);
-    if (n == 0) return;
-    const uint64_t base = seg >> 24;
-    const uint32_t lb = qry_len[q], mb = min(lb, S), nb = rq.len[q];
-    const H *B = qry + (uint64_t)q * qry_stride;
-    const H *RB = (const H *)rq.val + (uint64_t)q * rq.stride;
-    const uint32_t *PB = rq.pos + (uint64_t)q * rq.stride;
-    const bool staged = mb <= kWalkRowCap && nb <= kWalkRecCap;   // block-uniform
-    if (staged) {
-        for (uint32_t t = threadIdx.x; t < mb; t += 256) Bs[t] = B[t];
-        for (uint32_t t = threadIdx.x; t < nb; t += 256) { Rb[t] = RB[t]; Pb[t] = PB[t]; }
-        __syncthreads();
-    }
-    const uint64_t pair_row = (uint64_t)q * n_ref;
-    for (uint32_t c = threadIdx.x; c < n; c += 256) {
-        const uint64_t o = cand[base + c];
-        const uint32_t r = (uint32_t)(o - pair_row);
-        const H *A = ref + (uint64_t)r * ref_stride;
-        const H *RA = (const H *)rr.val + (uint64_t)r * rr.stride;
-        const uint32_t *PA = rr.pos + (uint64_t)r * rr.stride;
-        uint32_t cm, dn;
-        if (staged)
-            walk_pair_rec(A, ref_len[r], (const H *)Bs, lb, S, RA, PA, rr.len[r], (const H *)Rb,
-                          (const uint32_t *)Pb, nb, cm, dn);
-        else
-            walk_pair_rec(A, ref_len[r], B, lb, S, RA, PA, rr.len[r], RB, PB, nb, cm, dn);
-        numer[o] = (C)cm;
-        denom[o] = (C)dn;
-    }
-}
-
 // Sorted, distinct lists (every sketch the k-mer path produces): the walk of
 // compareSketches (CommandDistance.cpp:365-398) is a merge of two sets and visits the
 // union elements in ascending order, so with U(c) = the union rank of value c
@@ -361,9 +310,6 @@ __global__ __launch_bounds__(256) void walk_rows_rec_kernel(
 //  * when max(|A|, |B|) >= S, denom is S whatever #shared is, and no A element after the
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
-#ifndef FPM_RANK_SPLIT
-#define FPM_RANK_SPLIT 1
-#endif
 constexpr int kRankWaves = 4;        // waves per query row (2 and 8 measured slower)
 constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest unrolled probe
 constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one more)
@@ -515,9 +461,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
-    // A rows are read in chunks of 128 values, 16 B per lane (lane l holds A[i0 + 2l] and
-    // A[i0 + 2l + 1]: 16-B loads run at about twice the rate of 8-B ones), in groups of
-    // kGroup chunks through a bounds-checked buffer descriptor (reads past ld return 0).
+    // A rows are read in chunks of 128 values, two 8-B loads per lane (lane l holds A[i0 + l]
+    // and A[i0 + 64 + l]: neighbouring lanes then probe neighbouring directory words and keys
+    // of B, about half the LDS bank conflicts of one 16-B load of A[i0 + 2l], A[i0 + 2l + 1]
+    // per lane: rank kernel 0.415 -> 0.405 ms, C2 step 1.051 -> 1.042 ms, same box, r04c), in
+    // groups of kGroup chunks through a bounds-checked buffer descriptor (reads past ld
+    // return 0).
     // Three register groups: `cur` (being ranked), `nxt` (this candidate's next group,
     // issued before `cur` is ranked) and `pf` (the next candidate's first group, issued when
     // a candidate starts); the groups after an early exit are never loaded.
@@ -542,18 +491,11 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
-#if FPM_RANK_SPLIT
             const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
             const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
                                                                  0, 0);
             dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
             dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
-#else
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(R.rsrc, (t * kChunk + 2 * lane) * 8u,
-                                                                 0, 0);
-            dst[u].e0 = ((uint64_t)v[1] << 32) | v[0];
-            dst[u].e1 = ((uint64_t)v[3] << 32) | v[2];
-#endif
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -576,13 +518,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
             const int rem = (int)la - (int)i0;
-#if FPM_RANK_SPLIT
             // values past la (row padding) count nothing: lane l holds i0 + l, i0 + 64 + l
             const int r0 = min(rem, 64), r1 = rem - 64;     // lanes whose e0 / e1 are valid
-#else
-            // values past la (row padding) count nothing: lane l holds i0 + 2l, i0 + 2l + 1
-            const int r0 = (rem + 1) >> 1, r1 = rem >> 1;   // lanes whose e0 / e1 are valid
-#endif
             const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
             const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
@@ -590,26 +527,15 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
-#if FPM_RANK_SPLIT
             const uint32_t k0 = shared_below + b0;
             const uint32_t k1 = shared_below + (uint32_t)__popcll(a0) + b1;
             const uint32_t u0 = i0 + lane + j0[g] - k0, u1 = i0 + 64 + lane + j1[g] - k1;
-#else
-            const uint32_t k0 = shared_below + b0 + b1;
-            const uint32_t k1 = k0 + (uint32_t)((a0 >> lane) & 1);
-            const uint32_t i = i0 + 2 * lane;
-            const uint32_t u0 = i + j0[g] - k0, u1 = i + 1 + j1[g] - k1;   // union ranks
-#endif
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
             shared_below += __popcll(a0) + __popcll(a1);
             if (g == kGroup - 1) {
                 const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
-#if FPM_RANK_SPLIT
                 u_last = (uint32_t)__builtin_amdgcn_readlane((int)(e >= 64 ? u1 : u0), (int)(e & 63));
-#else
-                u_last = (uint32_t)__builtin_amdgcn_readlane((int)((e & 1) ? u1 : u0), (int)(e >> 1));
-#endif
             }
         }
         return u_last;
@@ -1877,44 +1803,6 @@ static hipError_t walk_candidates_c(const uint64_t *d_cand, const unsigned long 
                            (const uint32_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
                            d_denom);
     return hipGetLastError();
-}
-
-template <typename C>
-static hipError_t walk_rows_rec_c(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                                  const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                                  uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
-                                  uint64_t qry_stride, uint32_t hash_bytes, uint32_t S, RecRows rr,
-                                  RecRows rq, C *d_numer, C *d_denom, hipStream_t st)
-{
-    const dim3 g(xcd_grid(n_qry)), b(256);
-    if (hash_bytes == 8)
-        hipLaunchKernelGGL((walk_rows_rec_kernel<uint64_t, C>), g, b, 0, st, d_cand, row_seg, n_qry,
-                           (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
-                           (const uint64_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
-                           d_denom);
-    else
-        hipLaunchKernelGGL((walk_rows_rec_kernel<uint32_t, C>), g, b, 0, st, d_cand, row_seg, n_qry,
-                           (const uint32_t *)d_ref, d_ref_len, ref_stride, n_ref,
-                           (const uint32_t *)d_qry, d_qry_len, qry_stride, S, rr, rq, d_numer,
-                           d_denom);
-    return hipGetLastError();
-}
-
-hipError_t launch_walk_rows_rec(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                                const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                                uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
-                                uint64_t qry_stride, uint32_t hash_bytes, uint32_t S, Counts cnt,
-                                RecRows rec_ref, RecRows rec_qry, hipStream_t st)
-{
-    if (!n_qry) return hipSuccess;
-    if (!rec_ref.val || !rec_qry.val) return hipErrorInvalidValue;
-    if (cnt.c16)
-        return walk_rows_rec_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
-                               d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
-                               (uint16_t *)cnt.numer, (uint16_t *)cnt.denom, st);
-    return walk_rows_rec_c(d_cand, row_seg, n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
-                           d_qry_len, qry_stride, hash_bytes, S, rec_ref, rec_qry,
-                           (uint32_t *)cnt.numer, (uint32_t *)cnt.denom, st);
 }
 
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,

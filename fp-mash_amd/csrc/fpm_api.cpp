@@ -68,10 +68,6 @@ static const int g_merge_small_env = [] {
     return v ? atoi(v) : 1;
 }();
 
-#ifndef FPM_WALK_ROWS
-#define FPM_WALK_ROWS 1   // A/B: 0 walks the record stretches one candidate per lane
-#endif
-
 struct fpm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2288,11 +2284,6 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,
                                               sketch_size, sym, cnt, cnum, cden, st));
-                else if (rec_r.val && FPM_WALK_ROWS)
-                    HIP_TRY(launch_walk_rows_rec((const uint64_t *)cand, (const uint64_t *)row_seg,
-                                                 n_qry, d_ref, d_ref_len, ref_stride, n_ref, d_qry,
-                                                 d_qry_len, qry_stride, hash_bytes, sketch_size,
-                                                 cnt, rec_r, rec_q, st));
                 else
                     HIP_TRY(launch_walk_candidates((const uint64_t *)cand, n_cand, cap, d_ref,
                                                    d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,

@@ -106,13 +106,6 @@ struct RecRows {
     const uint32_t *pos = nullptr, *len = nullptr;
     uint64_t stride = 0;
 };
-// the stretch walk (record rows of both sides) with one workgroup per query row of the probe's
-// row segments, the query row and its records staged in LDS
-hipError_t launch_walk_rows_rec(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                                const void *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                                uint32_t n_ref, const void *d_qry, const uint32_t *d_qry_len,
-                                uint64_t qry_stride, uint32_t hash_bytes, uint32_t S, Counts cnt,
-                                RecRows rec_ref, RecRows rec_qry, hipStream_t st);
 // the literal walk of each candidate pair; with record rows of both sides (unsorted lists),
 // only the stretches where both running maxima equal a shared record are walked
 hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long long *d_n_cand,

@@ -19,3 +19,6 @@ cat $O/c3_xcd_ab.txt
 OUT=$O/cli_ab REPS=3 timeout -k 10 400 bash tools/cli_dist_ab.sh FPMASH_DIST_BLOCK_PAIRS=4000000 > $O/cli_ab.txt 2>&1 \
   || { tail -30 $O/cli_ab.txt; exit 1; }
 cat $O/cli_ab.txt
+AB_LEG=c4 timeout -k 10 600 bash tools/env_ab.sh FPM_FILL_COUNTS=0 > $O/c4_fillcnt_ab.txt 2>&1 \
+  || { tail -20 $O/c4_fillcnt_ab.txt; exit 1; }
+cat $O/c4_fillcnt_ab.txt
