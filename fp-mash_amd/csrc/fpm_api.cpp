@@ -1855,10 +1855,13 @@ static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
 // the query side's probe count).  The one-pass build first; if a level-1 partition overflowed
 // its slot, the exact two-pass build (g.cap = 0) replaces it.
 template <typename Then>
+// raw_of_unsorted: the caller re-indexes unsorted rows over their records, so when the rows
+// turn out unsorted an overflowed one-pass build is left as it is (its flags and counters
+// are all the caller reads) instead of being rebuilt exactly.
 static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint64_t stride,
                        uint32_t n_ref, uint32_t hash_bytes, IdxGeom &g, uint32_t *dir,
                        uint32_t *entries, unsigned long long *ctr, bool self_events,
-                       hipStream_t st, Then then)
+                       hipStream_t st, Then then, bool raw_of_unsorted = false)
 {
     for (;;) {
         const uint64_t E = (uint64_t)n_ref * stride;
@@ -1882,6 +1885,8 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
         }
         if (int rc = read_counters(ctx, ctr, 68, st)) return rc;
         if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
+            if (raw_of_unsorted && ((const uint32_t *)(ctx->host_counters + 66))[0] != 0)
+                return FPM_OK;
             g.cap = 0;
             ctx->idx_rebuilds++;
             continue;
@@ -1945,7 +1950,8 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
     void *ctr;
     HIP_TRY(scratch(ctx, 7, kCtrWords * 8, &ctr));
     if (!rs->kmax) HIP_TRY(hipMalloc((void **)&rs->kmax, 8));
-    auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom &g) -> int {
+    auto build = [&](const void *rows, const uint32_t *len, uint64_t stride, IdxGeom &g,
+                     bool raw) -> int {
         const uint64_t En = (uint64_t)rs->n_ref * stride;
         void *dir, *entries;
         HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
@@ -1954,10 +1960,10 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
         // then needs no probe count)
         return build_index(ctx, rows, len, stride, rs->n_ref, rs->hash_bytes, g, (uint32_t *)dir,
                            (uint32_t *)entries, (unsigned long long *)ctr, true, st,
-                           [] { return FPM_OK; });
+                           [] { return FPM_OK; }, raw);
     };
     geom.kmax = rs->kmax;
-    if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom)) return rc;
+    if (int rc = build(rs->ref, rs->ref_len, rs->ref_stride, geom, true)) return rc;
     rs->ref_unsorted = ((const uint32_t *)(ctx->host_counters + 66))[0] != 0;
     rs->self_events = ctx->host_counters[0];
     rs->mr = std::min<uint64_t>(rs->ref_stride, rs->sketch_size);
@@ -1976,7 +1982,7 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
         }
         geom = make_geom(rs->n_ref, (uint64_t)rs->n_ref * rs->mr);
         geom.kmax = rs->kmax;
-        if (int rc = build(dref, (const uint32_t *)dref_len, rs->mr, geom)) return rc;
+        if (int rc = build(dref, (const uint32_t *)dref_len, rs->mr, geom, false)) return rc;
     }
     rs->geom = geom;
     return FPM_OK;
@@ -2155,7 +2161,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                                         (const uint32_t *)dir_,
                                                                         events, unsorted, st));
                                          return FPM_OK;
-                                     }))
+                                     }, true))
                 return rc;
             dir = (const uint32_t *)dir_;
             entries = (const uint32_t *)entries_;
@@ -2167,7 +2173,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // walked on the original lists.
             const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
             const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
-            if (!all_sorted && ev > 0) {
+            if (!all_sorted) {
                 void *dref, *dref_len, *dref_pos, *dqry = nullptr, *dqry_len = nullptr,
                      *dqry_pos = nullptr;
                 HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
