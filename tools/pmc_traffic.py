@@ -42,6 +42,7 @@ GROUPS = [
     ("dist_fill_kernel", "dist_fill_kernel"),
     ("dist_fill_flat_kernel", "dist_fill_kernel"),
     ("idx_", "dist index build"),
+    ("record_rows_kernel", "dist index build"),
     ("scan_", "dist index build"),
     ("probe_count_kernel", "dist index build"),
     ("sum64_kernel", "dist index build"),
