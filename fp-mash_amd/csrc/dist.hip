@@ -528,11 +528,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
             const int rem = (int)la - (int)i0;
-            // values past la (row padding) count nothing: lane l holds i0 + l, i0 + 64 + l
-            const int r0 = min(rem, 64), r1 = rem - 64;     // lanes whose e0 / e1 are valid
-            const uint64_t v0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
-            const uint64_t v1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
-            const uint64_t a0 = m0[g] & v0, a1 = m1[g] & v1;
+            uint64_t a0 = m0[g], a1 = m1[g];
+            if (rem < (int)kChunk) {
+                // the row's last chunk (wave-uniform branch: full chunks skip the masks): values
+                // past la (row padding) count nothing; lane l holds i0 + l, i0 + 64 + l
+                const int r0 = min(rem, 64), r1 = rem - 64;     // lanes whose e0 / e1 are valid
+                a0 &= r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
+                a1 &= r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
+            }
             const uint32_t b0 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
@@ -543,10 +546,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
             shared_below += __popcll(a0) + __popcll(a1);
-            if (g == kGroup - 1) {
-                const uint32_t e = min(la - 1 - i0, kChunk - 1);   // last valid value
-                u_last = (uint32_t)__builtin_amdgcn_readlane((int)(e >= 64 ? u1 : u0), (int)(e & 63));
-            }
+            // the union rank of the chunk's last value (lane 63's e1), read for the early exit
+            // after full chunks only: after the row's last chunk the walk ends anyway
+            if (g == kGroup - 1) u_last = (uint32_t)__builtin_amdgcn_readlane((int)u1, 63);
         }
         return u_last;
     };
