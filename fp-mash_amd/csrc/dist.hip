@@ -337,17 +337,28 @@ constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one
 // sentinels): j = lb.
 // NP = 0 (any row): 64-bit reads over the row's largest bucket (maxn), every position
 // clamped to the sentinel and tested against lb.
-template <int NP>
+// HI (rows whose largest value has bit 63 set, i.e. kshift = 32: full-range 64-bit hashes):
+// the key is a's high dword and the bucket a 32-bit shift of it, instead of two 64-bit shifts
+// and a 64-bit compare per value.
+template <int NP, bool HI = false>
 __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_t *K32,
                                                const uint16_t *Bkt, uint32_t shift,
                                                uint32_t kshift, uint32_t top, uint32_t lb,
                                                uint32_t maxn, uint64_t a, uint32_t &j)
 {
-    const uint64_t t = a >> shift;
-    const bool over = t > (uint64_t)top;
-    const uint32_t lo = Bkt[over ? top + 1 : (uint32_t)t];
+    bool over;
+    uint32_t lo;
+    if constexpr (HI) {
+        const uint32_t t = (uint32_t)(a >> 32) >> (shift - 32);
+        over = t > top;
+        lo = Bkt[over ? top + 1 : t];
+    } else {
+        const uint64_t t = a >> shift;
+        over = t > (uint64_t)top;
+        lo = Bkt[over ? top + 1 : (uint32_t)t];
+    }
     if constexpr (NP > 0) {
-        const uint32_t ka = (uint32_t)(a >> kshift);
+        const uint32_t ka = HI ? (uint32_t)(a >> 32) : (uint32_t)(a >> kshift);
         uint32_t p = lo;
 #pragma unroll
         for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
@@ -514,8 +525,11 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // one group of kGroup chunks: shared-hash count below the union rank S (cnt), shared
     // values so far (shared_below); returns the union rank of the last valid element of the
     // group's last chunk
-    auto rank_group = [&](auto probe, uint32_t g0, uint32_t la, const Pair (&cur)[kGroup],
-                          uint32_t &shared_below, uint32_t &cnt) -> uint32_t {
+    // vm0 / vm1: the lanes whose e0 / e1 are values of the row (all of them but in a row's
+    // last chunk, whose masks the candidate loop computes once)
+    auto rank_group = [&](auto probe, uint32_t g0, uint64_t vm0, uint64_t vm1,
+                          const Pair (&cur)[kGroup], uint32_t &shared_below,
+                          uint32_t &cnt) -> uint32_t {
         uint32_t j0[kGroup], j1[kGroup];
         uint64_t m0[kGroup], m1[kGroup];
 #pragma unroll
@@ -527,15 +541,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int g = 0; g < kGroup; g++) {
             const uint32_t i0 = (g0 + g) * kChunk;
-            const int rem = (int)la - (int)i0;
-            uint64_t a0 = m0[g], a1 = m1[g];
-            if (rem < (int)kChunk) {
-                // the row's last chunk (wave-uniform branch: full chunks skip the masks): values
-                // past la (row padding) count nothing; lane l holds i0 + l, i0 + 64 + l
-                const int r0 = min(rem, 64), r1 = rem - 64;     // lanes whose e0 / e1 are valid
-                a0 &= r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
-                a1 &= r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
-            }
+            const uint64_t a0 = m0[g] & vm0, a1 = m1[g] & vm1;
             const uint32_t b0 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
@@ -566,11 +572,22 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             const bool need_all = la < S && lb < S;       // denom depends on #shared
             const uint32_t nch = (la + kChunk - 1) / kChunk;
             const uint32_t ngr = (nch + kGroup - 1) / kGroup;
+            static_assert(kGroup == 1, "the last-chunk masks assume one chunk per group");
+            // values past la (row padding) count nothing: in the last chunk (lane l holds
+            // A[i0 + l], A[i0 + 64 + l]) the lanes below r0 / r1 hold row values.  Computed once
+            // per candidate, selected per chunk (computed in the chunk loop they cost ~20 scalar
+            // instructions per chunk: the compiler turns a branch around them into selects)
+            const int rl = (int)la - (int)(nch - 1) * (int)kChunk;          // 1 .. 128
+            const int r0 = min(rl, 64), r1 = rl - 64;
+            const uint64_t vl0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
+            const uint64_t vl1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             uint32_t shared_below = 0, cnt = 0;
             for (uint32_t gi = 0; gi < ngr; gi++) {
                 if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
                 const uint32_t g0 = gi * kGroup;
-                const uint32_t u_last = rank_group(probe, g0, la, cur, shared_below, cnt);
+                const bool last = gi + 1 == ngr;
+                const uint32_t u_last = rank_group(probe, g0, last ? vl0 : ~0ULL, last ? vl1 : ~0ULL,
+                                                   cur, shared_below, cnt);
                 // union rank of the group's last element (the group is full when g0 + kGroup
                 // <= nch); later A elements rank higher
                 if (!need_all && g0 + kGroup <= nch && u_last >= S) break;
@@ -599,15 +616,16 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint16_t *bk_ = Bkt;
     const uint64_t *bs_ = Bs;
     const uint32_t *k_ = K32;
-#define FPM_RANK_NP(NP_) \
+#define FPM_RANK_NP(NP_, HI_) \
     run([&](uint64_t a, uint32_t &j) { \
-        return rank_chunk<NP_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+        return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+    const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
     switch (np) {
-    case 2: FPM_RANK_NP(2); break;
-    case 3: FPM_RANK_NP(3); break;
-    case 4: FPM_RANK_NP(4); break;
-    case kRankProbeMax: FPM_RANK_NP(kRankProbeMax); break;
-    default: FPM_RANK_NP(0); break;
+    case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;
+    case 3: if (hi) FPM_RANK_NP(3, true); else FPM_RANK_NP(3, false); break;
+    case 4: if (hi) FPM_RANK_NP(4, true); else FPM_RANK_NP(4, false); break;
+    case kRankProbeMax: FPM_RANK_NP(kRankProbeMax, false); break;
+    default: FPM_RANK_NP(0, false); break;
     }
 #undef FPM_RANK_NP
 }
