@@ -582,18 +582,22 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             const uint64_t vl0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
             const uint64_t vl1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
             uint32_t shared_below = 0, cnt = 0;
-            for (uint32_t gi = 0; gi < ngr; gi++) {
-                if (gi + 1 < ngr) load_group(R, gi + 1, nxt);
-                const uint32_t g0 = gi * kGroup;
-                const bool last = gi + 1 == ngr;
-                const uint32_t u_last = rank_group(probe, g0, last ? vl0 : ~0ULL, last ? vl1 : ~0ULL,
-                                                   cur, shared_below, cnt);
-                // union rank of the group's last element (the group is full when g0 + kGroup
-                // <= nch); later A elements rank higher
-                if (!need_all && g0 + kGroup <= nch && u_last >= S) break;
+            // the early exit: after a chunk whose last value's union rank reaches S no later
+            // value can count (need_all: the denom needs every shared value, no exit)
+            const uint32_t s_exit = need_all ? 0xFFFFFFFFu : S;
+            // the full chunks, then the row's last chunk with its masks (peeled: the loop
+            // carries no per-chunk mask selects)
+            bool exited = false;
+            uint32_t gi = 0;
+            for (; gi + 1 < ngr; gi++) {
+                load_group(R, gi + 1, nxt);
+                const uint32_t u_last = rank_group(probe, gi * kGroup, ~0ULL, ~0ULL, cur,
+                                                   shared_below, cnt);
+                if (u_last >= s_exit) { exited = true; break; }
 #pragma unroll
                 for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
             }
+            if (!exited && ngr) rank_group(probe, gi * kGroup, vl0, vl1, cur, shared_below, cnt);
             if (lane == 0) {
                 const uint64_t un = (uint64_t)la + lb - shared_below;
                 const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
