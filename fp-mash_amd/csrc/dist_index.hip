@@ -741,17 +741,27 @@ void probe_rows_kernel(
                     const uint32_t e = e0 + 64 * u;
                     en[u] = e < wn ? entries[(uint32_t)tab[u] + wb + e] : 0u;
                 }
+                // a read first: lanes of a shared bucket hit the same few words (family
+                // members have adjacent ids), where an atomic per lane serialises; the bits
+                // are almost always set already.  Branch-free per event (the read is done for
+                // every lane, at word 0 when the event is not this row's), the rare atomics
+                // after the kU events: a branch per event cost 11 scalar instructions of exec
+                // mask handling each
+                uint32_t wi[kU], need = 0;
 #pragma unroll
                 for (int u = 0; u < kU; u++) {
                     const uint32_t e = e0 + 64 * u;
-                    if (e < wn && (en[u] >> g.rbits) == (uint32_t)(tab[u] >> 32)) {
-                        const uint32_t r = en[u] & rmask;
-                        // a read first: lanes of a shared bucket hit the same few words
-                        // (family members have adjacent ids), where an atomic per lane
-                        // serialises; the bits are almost always set already
-                        const uint32_t wi = (r - r0) >> 5, bit = 1u << ((r - r0) & 31);
-                        if (r >= r0 && r < r1c && !(rowbits[wi] & bit)) atomicOr(&rowbits[wi], bit);
-                    }
+                    const uint32_t r = en[u] & rmask;
+                    const bool hit = e < wn && (en[u] >> g.rbits) == (uint32_t)(tab[u] >> 32) &&
+                                     r >= r0 && r < r1c;
+                    wi[u] = hit ? r - r0 : 0u;
+                    const uint32_t word = rowbits[wi[u] >> 5];
+                    need |= (hit && !(word & (1u << (wi[u] & 31)))) ? (1u << u) : 0u;
+                }
+                if (__any(need != 0)) {
+#pragma unroll
+                    for (int u = 0; u < kU; u++)
+                        if (need >> u & 1u) atomicOr(&rowbits[wi[u] >> 5], 1u << (wi[u] & 31));
                 }
             }
             __builtin_amdgcn_wave_barrier();   // before the next window's owner map
