@@ -262,6 +262,40 @@ def test_dist_unsorted_record_edges(ctx, oracle, mode):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 
 
+@pytest.mark.parametrize("mode", ["auto", "sparse"])
+def test_rank_crowded_buckets(ctx, oracle, mode):
+    """Sorted u64 lists with a crowded rank bucket: 40-120 values 2^33 apart (distinct 32-bit
+    keys, one directory bucket of the rank kernel) beside uniform ones.  The rank kernel reads
+    two keys per value and continues one key at a time inside such a bucket; every grid cell
+    against the oracle, self set and a separate query set."""
+    import fpmash
+    rng = np.random.default_rng(31)
+    base = np.uint64(0x9000000000000000)
+    pool_c = base + np.arange(400, dtype=np.uint64) * np.uint64(1 << 33)
+    pool_u = rng.integers(1, 2 ** 63, size=20000, dtype=np.uint64) * np.uint64(2)
+    def lists(n):
+        out = []
+        for _ in range(n):
+            c = rng.choice(pool_c, size=int(rng.integers(40, 120)), replace=False)
+            u = rng.choice(pool_u, size=int(rng.integers(200, 900)), replace=False)
+            out.append(np.unique(np.concatenate([c, u])))
+        return out
+    refs, qrys = lists(60), lists(45)
+    rl = [len(x) * 5 for x in refs]
+    ql = [len(x) * 5 for x in qrys]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE if mode == "sparse" else fpmash.DIST_AUTO)
+    try:
+        for S in (1000, 300):
+            for (a, al), (b, bl) in (((refs, rl), (refs, rl)), ((refs, rl), (qrys, ql))):
+                got = ctx.dist(a, b, S, ref_lengths=al, qry_lengths=bl)
+                nu, de, di, pv = oracle.dist_grid(a, al, b, bl, S, 21, 4.0 ** 21)
+                assert np.array_equal(got["numer"], nu), S
+                assert np.array_equal(got["denom"], de), S
+                assert (nu > 0).any()
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
 def test_dist_filters(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
     # 16 lists (a multiple of 4: the fill kernel's vector path) with an empty one (an empty
