@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void walk_cand_kernel(
 //    first one whose union rank reaches S can count: the wave stops there (about half of A
 //    for unrelated pairs).
 constexpr int kRankWaves = 4;        // waves per query row (2 and 8 measured slower)
-constexpr int kRankProbeMax = 8;     // sentinels past the end of B
+constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest unrolled probe
 constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one more)
 
 // One chunk of 64 A elements against B (one per lane): j = #{B < a} and the lanes whose a
@@ -329,11 +329,10 @@ constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one
 // NP > 0 (the fast path): B's values have distinct 32-bit keys K32 = the top 32 bits of the
 // row's value window (v >> max(bits - 32, 0)), which order them exactly, and the bucket of
 // a value is the top kLogB bits of its key.  The NP reads K32[lo .. lo + NP) at lo =
-// Bkt[bucket(a)], continued one key at a time while the keys are still below a (a bucket of
-// more than NP values; rare); later positions hold larger keys (next buckets, or the
-// 0xFFFFFFFF sentinels past the end), so p = lo + #{keys < key(a)} is the first position
-// whose value is not below a on the key, and one 64-bit read of Bs[p] settles the rest:
-// j = p + (Bs[p] < a), eq = (Bs[p] == a).
+// Bkt[bucket(a)] cover a's whole bucket (NP >= the row's largest bucket); later positions
+// hold larger keys (next buckets, or the 0xFFFFFFFF sentinels past the end), so
+// p = lo + #{keys < key(a)} is the first position whose value is not below a on the key,
+// and one 64-bit read of Bs[p] settles the rest: j = p + (Bs[p] < a), eq = (Bs[p] == a).
 // A value past the last B value's bucket `top` clamps to bucket top + 1 (lo = lb, the
 // sentinels): j = lb.
 // NP = 0 (any row): 64-bit reads over the row's largest bucket (maxn), every position
@@ -363,13 +362,6 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
         uint32_t p = lo;
 #pragma unroll
         for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
-        // past the NP keys read, later keys may still be below a (a bucket of more than NP
-        // values): continue one key at a time, rarely (every key after a's bucket is larger,
-        // and the 0xFFFFFFFF sentinels stop it)
-        const bool more = K32[lo + NP - 1] < ka;
-        if (__any(more))
-            if (more)
-                while (K32[p] < ka) p++;
         const uint64_t v = Bs[p];
         j = p + (v < a ? 1u : 0u);
         return __builtin_amdgcn_ballot_w64(v == a) & ~__builtin_amdgcn_ballot_w64(over);
@@ -482,11 +474,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     if (lane == 0 && mx) atomicMax(&s_maxn, mx);
     __syncthreads();
     const uint32_t maxn = s_maxn;
-    // probe width (row-uniform): two keys read per value, the rare values past the second
-    // key of a longer bucket continue one key at a time (rank_chunk; reading every row's
-    // largest bucket, 3-4 keys for most C2 rows, cost a second ds_read2 per value);
-    // 0 = the clamped loop (keys that do not order the row)
-    const uint32_t np = s_keydup ? 0u : 2u;
+    // probe width (row-uniform): unrolled reads for buckets of up to 2 / 3 / 4 / 8 values;
+    // 0 = the clamped loop (a crowded bucket, or keys that do not order the row)
+    // (two keys per value with a rare one-key-at-a-time continuation past them measured
+    // slower: 0.346 -> 0.372 ms, the wave-wide test of the continuation costs more than the
+    // second ds_read2 it saves)
+    const uint32_t np = s_keydup ? 0u
+                      : maxn <= 2 ? 2u : maxn <= 3 ? 3u : maxn <= 4 ? 4u
+                      : maxn <= (uint32_t)kRankProbeMax ? (uint32_t)kRankProbeMax : 0u;
 
     const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
     const uint64_t pair_row = (uint64_t)q * n_ref;
@@ -632,9 +627,13 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     run([&](uint64_t a, uint32_t &j) { \
         return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
     const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
-    if (np == 0) FPM_RANK_NP(0, false);
-    else if (hi) FPM_RANK_NP(2, true);
-    else FPM_RANK_NP(2, false);
+    switch (np) {
+    case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;
+    case 3: if (hi) FPM_RANK_NP(3, true); else FPM_RANK_NP(3, false); break;
+    case 4: if (hi) FPM_RANK_NP(4, true); else FPM_RANK_NP(4, false); break;
+    case kRankProbeMax: FPM_RANK_NP(kRankProbeMax, false); break;
+    default: FPM_RANK_NP(0, false); break;
+    }
 #undef FPM_RANK_NP
 }
 

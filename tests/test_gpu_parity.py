@@ -265,9 +265,9 @@ def test_dist_unsorted_record_edges(ctx, oracle, mode):
 @pytest.mark.parametrize("mode", ["auto", "sparse"])
 def test_rank_crowded_buckets(ctx, oracle, mode):
     """Sorted u64 lists with a crowded rank bucket: 40-120 values 2^33 apart (distinct 32-bit
-    keys, one directory bucket of the rank kernel) beside uniform ones.  The rank kernel reads
-    two keys per value and continues one key at a time inside such a bucket; every grid cell
-    against the oracle, self set and a separate query set."""
+    keys, one directory bucket of the rank kernel) beside uniform ones: the rows past the
+    unrolled probe widths take the clamped 64-bit loop (NP = 0).  Every grid cell against the
+    oracle, self set and a separate query set."""
     import fpmash
     rng = np.random.default_rng(31)
     base = np.uint64(0x9000000000000000)
