@@ -590,18 +590,15 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             const uint32_t s_exit = need_all ? 0xFFFFFFFFu : S;
             // the full chunks, then the row's last chunk with its masks (peeled: the loop
             // carries no per-chunk mask selects)
-            // A chunks are loaded two ahead (chunk gi + 2 issued before chunk gi is ranked)
             bool exited = false;
             uint32_t gi = 0;
-            Pair nxt2[kGroup];
-            if (ngr > 1) load_group(R, 1, nxt);
             for (; gi + 1 < ngr; gi++) {
-                if (gi + 2 < ngr) load_group(R, gi + 2, nxt2);
+                load_group(R, gi + 1, nxt);
                 const uint32_t u_last = rank_group(probe, gi * kGroup, ~0ULL, ~0ULL, cur,
                                                    shared_below, cnt);
                 if (u_last >= s_exit) { exited = true; break; }
 #pragma unroll
-                for (int u = 0; u < kGroup; u++) { cur[u] = nxt[u]; nxt[u] = nxt2[u]; }
+                for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
             }
             if (!exited && ngr) rank_group(probe, gi * kGroup, vl0, vl1, cur, shared_below, cnt);
             if (lane == 0) {
