@@ -589,7 +589,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             // value can count (need_all: the denom needs every shared value, no exit)
             const uint32_t s_exit = need_all ? 0xFFFFFFFFu : S;
             // the full chunks, then the row's last chunk with its masks (peeled: the loop
-            // carries no per-chunk mask selects)
+            // carries no per-chunk mask selects).  (Chunks loaded two ahead instead of one:
+            // 0.345 -> 0.375 ms.)
             bool exited = false;
             uint32_t gi = 0;
             for (; gi + 1 < ngr; gi++) {
