@@ -654,7 +654,7 @@ void probe_rows_kernel(
     // window (which of the 64 hashes each event belongs to)
     constexpr uint32_t kWin = 1024;
     __shared__ uint64_t w_tab[4][64];
-    __shared__ __attribute__((aligned(16))) uint8_t w_own[4][kWin];
+    __shared__ uint8_t w_own[4][kWin];
     // XCD-contiguous rows (shared buckets in L2) of rows [q_lo, q_lo + n_qry)
     const uint32_t qr = xcd_row(blockIdx.x, n_qry);
     if (qr >= n_qry) return;
@@ -721,17 +721,9 @@ void probe_rows_kernel(
         const uint32_t pre = inc - cnt;
         w_tab[wave][lane] = ((uint64_t)tgt << 32) | (uint32_t)(st - pre);
         for (uint32_t wb = 0; wb < total; wb += kWin) {
-            // owner map of events [wb, wb + kWin): each lane marks its own hash's events,
-            // 4 per dword store inside its range and single bytes at its ends (a family-shared
-            // hash owns ~100 events: one byte per store made this loop the longest of the
-            // batch; wb is a multiple of kWin, so x and x - wb align alike)
+            // owner map of events [wb, wb + kWin): each lane marks its own hash's events
             const uint32_t a0 = max(pre, wb), a1 = min(pre + cnt, wb + kWin);
-            uint8_t *own = w_own[wave];
-            uint32_t x = a0;
-            for (; x < a1 && (x & 3u); x++) own[x - wb] = (uint8_t)lane;
-            const uint32_t w4 = lane * 0x01010101u;
-            for (; x + 4 <= a1; x += 4) *reinterpret_cast<uint32_t *>(own + (x - wb)) = w4;
-            for (; x < a1; x++) own[x - wb] = (uint8_t)lane;
+            for (uint32_t e = a0; e < a1; e++) w_own[wave][e - wb] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
             const uint32_t wn = min(kWin, total - wb);
             // kU events per lane in flight: owner byte -> (base, fingerprint) -> entry
