@@ -722,6 +722,8 @@ void probe_rows_kernel(
         w_tab[wave][lane] = ((uint64_t)tgt << 32) | (uint32_t)(st - pre);
         for (uint32_t wb = 0; wb < total; wb += kWin) {
             // owner map of events [wb, wb + kWin): each lane marks its own hash's events
+            // (4 per dword store inside a lane's range: 3 spilled VGPRs under the 8-wave cap,
+            // 0.29 -> 0.306 ms)
             const uint32_t a0 = max(pre, wb), a1 = min(pre + cnt, wb + kWin);
             for (uint32_t e = a0; e < a1; e++) w_own[wave][e - wb] = (uint8_t)lane;
             __builtin_amdgcn_wave_barrier();
