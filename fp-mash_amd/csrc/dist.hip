@@ -1125,6 +1125,47 @@ __device__ __forceinline__ void cell_values(uint32_t c, uint32_t d, uint64_t len
     }
 }
 
+// Distance and p-value of n independent cells from their counts and genome lengths (the
+// optional batch call of SURVEY §8(b): the values the compact output leaves out, for the cells
+// a caller asks for), no filters.
+template <typename C>
+__global__ __launch_bounds__(256) void pvalue_batch_kernel(const C *__restrict__ numer,
+                                                           const C *__restrict__ denom,
+                                                           const uint64_t *__restrict__ len_ref,
+                                                           const uint64_t *__restrict__ len_qry,
+                                                           uint64_t n, uint32_t kmer_size,
+                                                           double kmer_space,
+                                                           double *__restrict__ dist,
+                                                           double *__restrict__ pvalue)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    double dv, pv;
+    bool ok;
+    cell_values(numer[i], denom[i], len_ref[i], len_qry[i], kmer_size, kmer_space, -1.0, -1.0,
+                dv, pv, ok);
+    if (dist) dist[i] = dv;
+    if (pvalue) pvalue[i] = pv;
+}
+
+hipError_t launch_pvalue_batch(const void *numer, const void *denom, uint32_t count_bytes,
+                               const uint64_t *len_ref, const uint64_t *len_qry, uint64_t n,
+                               uint32_t kmer_size, double kmer_space, double *dist,
+                               double *pvalue, hipStream_t st)
+{
+    if (!n) return hipSuccess;
+    const dim3 g((uint32_t)((n + 255) / 256));
+    if (count_bytes == 2)
+        hipLaunchKernelGGL(pvalue_batch_kernel<uint16_t>, g, dim3(256), 0, st,
+                           (const uint16_t *)numer, (const uint16_t *)denom, len_ref, len_qry, n,
+                           kmer_size, kmer_space, dist, pvalue);
+    else
+        hipLaunchKernelGGL(pvalue_batch_kernel<uint32_t>, g, dim3(256), 0, st,
+                           (const uint32_t *)numer, (const uint32_t *)denom, len_ref, len_qry, n,
+                           kmer_size, kmer_space, dist, pvalue);
+    return hipGetLastError();
+}
+
 // Block-wide slot reservation: thread t needs k_t entries; returns its first slot.  One
 // global atomic per workgroup (a per-wave atomic on the one counter serialised: the C2
 // candidate list took 0.21 ms for 1e6 cells).  Every thread of the block calls it.

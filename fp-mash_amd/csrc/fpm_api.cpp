@@ -2520,6 +2520,23 @@ int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t 
     return FPM_OK;
 }
 
+int fpm_pvalue_batch_dev(fpm_ctx *ctx, const void *d_numer, const void *d_denom,
+                         uint32_t count_bytes, const uint64_t *d_len_ref,
+                         const uint64_t *d_len_qry, uint64_t n, uint32_t kmer_size,
+                         double kmer_space, double *d_dist, double *d_pvalue, void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (count_bytes != 2 && count_bytes != 4) return fail(FPM_EINVAL, "count_bytes must be 2 or 4");
+    if (n && (!d_numer || !d_denom || !d_len_ref || !d_len_qry))
+        return fail(FPM_EINVAL, "null input");
+    hipStream_t st = pick_stream(ctx, stream);
+    TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
+    HIP_TRY(launch_pvalue_batch(d_numer, d_denom, count_bytes, d_len_ref, d_len_qry, n, kmer_size,
+                                kmer_space, d_dist, d_pvalue, st));
+    tl.done();
+    return FPM_OK;
+}
+
 namespace {
 struct DevBuf {
     void *p = nullptr;

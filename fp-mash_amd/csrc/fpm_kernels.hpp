@@ -272,6 +272,11 @@ hipError_t launch_dist_cand_finalize(const uint64_t *d_cand, const unsigned long
                                      uint32_t kmer_size, double kmer_space, double max_dist,
                                      double max_pvalue, double *d_dist, double *d_pvalue,
                                      uint8_t *d_pass, const MirrorOut &mir, hipStream_t st);
+// distance and p-value of n cells from their u16 / u32 counts and per-cell genome lengths
+hipError_t launch_pvalue_batch(const void *numer, const void *denom, uint32_t count_bytes,
+                               const uint64_t *len_ref, const uint64_t *len_qry, uint64_t n,
+                               uint32_t kmer_size, double kmer_space, double *dist,
+                               double *pvalue, hipStream_t st);
 hipError_t launch_dist_finalize(Counts cnt, const uint64_t *d_ref_length, const uint64_t *d_qry_length,
                                 uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
                                 double kmer_space, double max_dist, double max_pvalue,

@@ -87,6 +87,8 @@ SYMBOLS = [
                                        C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp]),
     ("fpm_dist_finalize_dev", C.c_int, [vp, vp, vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32,
                                         C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
+    ("fpm_pvalue_batch_dev", C.c_int, [vp, vp, vp, C.c_uint32, vp, vp, C.c_uint64, C.c_uint32,
+                                       C.c_double, vp, vp, vp]),
     ("fpm_dist_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp, C.c_uint64,
                                C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_double,
                                C.c_double, C.c_double, vp, vp, vp, vp, vp, vp]),
@@ -643,6 +645,30 @@ class Context:
         if not expand:
             return nu, de, listed
         return expand_compact(nu, de, listed, nr, max_dist, max_pvalue)
+
+    def pvalue_batch(self, numer, denom, len_ref, len_qry, k=21, kmer_space=None):
+        """fpm_pvalue_batch_dev on host arrays: (distance, p-value) of each cell from its
+        counts (u16 or u32) and genome lengths."""
+        numer = np.ascontiguousarray(numer)
+        denom = np.ascontiguousarray(denom, dtype=numer.dtype)
+        if numer.dtype not in (np.uint16, np.uint32):
+            raise ValueError("counts must be uint16 or uint32")
+        n = len(numer)
+        if kmer_space is None:
+            kmer_space = 4.0 ** k
+        bufs = [DeviceBuffer.from_array(self, a) for a in
+                (numer, denom, np.ascontiguousarray(len_ref, dtype=np.uint64),
+                 np.ascontiguousarray(len_qry, dtype=np.uint64))]
+        outs = [DeviceBuffer(self, max(n, 1) * 8) for _ in range(2)]
+        try:
+            _check(lib().fpm_pvalue_batch_dev(self.h, bufs[0].ptr, bufs[1].ptr,
+                                              numer.dtype.itemsize, bufs[2].ptr, bufs[3].ptr, n,
+                                              k, kmer_space, outs[0].ptr, outs[1].ptr, None))
+            self.synchronize()
+            return outs[0].to_array(np.float64, n), outs[1].to_array(np.float64, n)
+        finally:
+            for b in bufs + outs:
+                b.free()
 
     def refset(self, ref_lists, sketch_size, use64=True, ref_lengths=None, width=None):
         """A resident reference set (fpm_refset_create): rows uploaded and indexed once."""

@@ -241,6 +241,15 @@ int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t 
                           uint32_t n_ref, uint32_t n_qry, uint32_t kmer_size,
                           double kmer_space, double max_dist, double max_pvalue,
                           double *d_dist, double *d_pvalue, uint8_t *d_pass, void *stream);
+/* Distance and p-value of n independent cells from their counts (u16 when count_bytes = 2,
+ * u32 when 4) and per-cell genome lengths, device pointers, stream-ordered, no -d / -v
+ * filters: the values the compact output (fpm_dist_list_dev) leaves out, for the cells a
+ * caller wants.  Replaces the per-pair distance + pValue of CommandDistance.cpp:404-419,
+ * 433-450 (SURVEY §8(b)'s optional fpm_pvalue_batch).  d_dist / d_pvalue may each be NULL. */
+int fpm_pvalue_batch_dev(fpm_ctx *ctx, const void *d_numer, const void *d_denom,
+                         uint32_t count_bytes, const uint64_t *d_len_ref,
+                         const uint64_t *d_len_qry, uint64_t n, uint32_t kmer_size,
+                         double kmer_space, double *d_dist, double *d_pvalue, void *stream);
 /* compare + finalize in one call on device buffers (= fpm_compare_grid_dev followed by
  * fpm_dist_finalize_dev on the same stream). */
 int fpm_dist_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len,

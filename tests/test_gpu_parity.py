@@ -296,6 +296,29 @@ def test_rank_crowded_buckets(ctx, oracle, mode):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 
 
+def test_pvalue_batch(ctx, oracle):
+    """fpm_pvalue_batch_dev: distance and p-value of arbitrary cells (u16 and u32 counts)
+    against the oracle's distance / pValue, including x = 0 (p = 1), numer = denom
+    (distance 0), tiny and huge genome lengths and the -fp k-mer space."""
+    rng = np.random.default_rng(12)
+    n = 3000
+    denom = rng.integers(1, 2000, size=n).astype(np.uint32)
+    numer = np.minimum(rng.integers(0, 2000, size=n), denom).astype(np.uint32)
+    numer[:50] = 0
+    numer[50:100] = denom[50:100]
+    lr = rng.integers(1, 10 ** 9, size=n, dtype=np.uint64)
+    lq = rng.integers(1, 10 ** 9, size=n, dtype=np.uint64)
+    lr[100:150] = 21
+    for dt, k, space in ((np.uint32, 21, 4.0 ** 21), (np.uint16, 21, 4.0 ** 21),
+                         (np.uint16, 1, 10.0)):
+        d, p = ctx.pvalue_batch(numer.astype(dt), denom.astype(dt), lr, lq, k=k, kmer_space=space)
+        for i in range(n):
+            assert d[i] == pytest.approx(oracle.distance(int(numer[i]), int(denom[i]), k),
+                                         rel=RTOL, abs=0), i
+            assert p[i] == pytest.approx(oracle.pvalue(int(numer[i]), int(lr[i]), int(lq[i]),
+                                                       space, int(denom[i])), rel=RTOL, abs=0), i
+
+
 def test_dist_filters(ctx, oracle, dist_mode):
     seqs, sk = _family_sketches(oracle, n_fam=3, members=5)
     # 16 lists (a multiple of 4: the fill kernel's vector path) with an empty one (an empty
