@@ -68,10 +68,6 @@ static const int g_merge_small_env = [] {
     return v ? atoi(v) : 1;
 }();
 
-#ifndef FPM_FILL_EARLY
-#define FPM_FILL_EARLY 1   // A/B: 0 submits the side fill after the probe
-#endif
-
 struct fpm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -2245,10 +2241,6 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // symmetric in the two sets, so only candidates r <= q are ranked and each result
             // is written to both cells (q, r) and (r, q)
             const bool sym = rows_merge && self_set;
-            const bool defer_fill = need_fill && skip_count && rows_merge;
-            const bool fill_early = FPM_FILL_EARLY && need_fill && !defer_fill;
-            if (fill_early)
-                if (int rc = launch_fill(true)) return rc;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
@@ -2283,10 +2275,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // first would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
             // ends (ev_in recorded here) but is submitted after the candidate compare.
+            const bool defer_fill = need_fill && skip_count && rows_merge;
             if (defer_fill) {
                 HIP_TRY(ensure_aux(ctx));
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
-            } else if (need_fill && !fill_early) {
+            } else if (need_fill) {
                 if (int rc = launch_fill(true)) return rc;
             }
             if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
