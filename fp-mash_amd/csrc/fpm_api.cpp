@@ -2271,6 +2271,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 cnum = (uint32_t *)cres;
                 cden = cnum + cap;
             }
+            // (Submitted before the probe instead, the fill slows the probe more than it gains:
+            // C4 one GPU 6.66 -> 6.80-6.86 ms, same box, r04.)
             // After the host read of the probe's counters the GPU is idle: a fill submitted
             // first would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
