@@ -245,17 +245,13 @@ __device__ __forceinline__ void walk_pair_rec(const H *__restrict__ A, uint32_t 
         // (the last stretch ends at min(len, S): no step reads past entry S - 1)
         const uint32_t ea = x + 1 < na ? PA[x + 1] : min(la, S);
         const uint32_t eb = y + 1 < nb ? PB[y + 1] : min(lb, S);
-        // branch-free steps: both heads reloaded every step (the index that did not move
-        // reloads the same entry), no per-step exec-mask handling of two conditional loads
         H a = A[i], b = B[j];
         while (i < ea && j < eb && n < S) {
             const bool lt = a < b, gt = b < a;
-            i += gt ? 0u : 1u;
-            j += lt ? 0u : 1u;
+            if (!gt) { i++; if (i < ea) a = A[i]; }
+            if (!lt) { j++; if (j < eb) b = B[j]; }
             common += (!lt && !gt) ? 1u : 0u;
             n++;
-            a = A[min(i, ea - 1)];
-            b = B[min(j, eb - 1)];
         }
         if (++x < na) ra = RA[x];
         if (++y < nb) rb = RB[y];
