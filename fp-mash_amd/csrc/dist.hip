@@ -245,6 +245,7 @@ __device__ __forceinline__ void walk_pair_rec(const H *__restrict__ A, uint32_t 
         // (the last stretch ends at min(len, S): no step reads past entry S - 1)
         const uint32_t ea = x + 1 < na ? PA[x + 1] : min(la, S);
         const uint32_t eb = y + 1 < nb ? PB[y + 1] : min(lb, S);
+        // (branch-free steps reloading both heads every step: 1.47 -> 1.59 ms on C3)
         H a = A[i], b = B[j];
         while (i < ea && j < eb && n < S) {
             const bool lt = a < b, gt = b < a;
