@@ -1348,32 +1348,31 @@ def main():
     # on a second stream beside the dist of batch i: the VALU-bound tile kernel fills the CUs
     # the latency-bound index / probe / rank kernels leave idle.  Events order each buffer's
     # sketch after the dist that last read it, and each dist after its sketch.
+    # (the library's own streams and events: fpm_stream_create / fpm_event_*; torch's bundled
+    # HIP runtime is a different one)
     pipe = None
     if not args.no_pipeline:
-        import torch
-        dev = torch.device("cuda", local)
         job2 = ctx.sketch_job(P, seqs)
         rows2, cnt2, _, stride2 = job2.device_output()
         assert stride2 == stride
         pipe = {"jobs": [job, job2], "rows": [(d_rows, d_cnt), (rows2, cnt2)],
-                "sA": torch.cuda.ExternalStream(st, device=dev),
-                "sB": torch.cuda.Stream(device=dev),
-                "ev_sk": [torch.cuda.Event(), torch.cuda.Event()],
-                "ev_dd": [torch.cuda.Event(), torch.cuda.Event()]}
+                "sB": ctx.new_stream(),
+                "ev_sk": [ctx.new_event(), ctx.new_event()],
+                "ev_dd": [ctx.new_event(), ctx.new_event()]}
 
     def sketch_into(b):
-        pipe["sB"].wait_event(pipe["ev_dd"][b])      # the dist that last read buffer b
-        pipe["jobs"][b].run(pipe["sB"].cuda_stream)
-        pipe["ev_sk"][b].record(pipe["sB"])
+        ctx.wait(pipe["sB"], pipe["ev_dd"][b])       # the dist that last read buffer b
+        pipe["jobs"][b].run(pipe["sB"])
+        ctx.record(pipe["ev_sk"][b], pipe["sB"])
 
     def dist_from(b):
-        pipe["sA"].wait_event(pipe["ev_sk"][b])
+        ctx.wait(st, pipe["ev_sk"][b])
         rows, cnt = pipe["rows"][b]
         fpmash._check(L.fpm_dist_list_dev(ctx.h, rows, cnt, d_len.ptr, stride, n, rows, cnt,
                                           d_len.ptr, stride, n, 8, args.s, args.k,
                                           4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
                                           cells.ref, st))
-        pipe["ev_dd"][b].record(pipe["sA"])
+        ctx.record(pipe["ev_dd"][b], st)
 
     def run_pipelined(k):
         b = 0

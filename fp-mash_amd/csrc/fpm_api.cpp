@@ -455,6 +455,56 @@ int fpm_ctx_warm(fpm_ctx *ctx)
 
 void *fpm_ctx_stream(fpm_ctx *ctx) { return ctx ? (void *)ctx->stream : nullptr; }
 
+int fpm_stream_create(fpm_ctx *ctx, void **stream)
+{
+    if (!stream) return fail(FPM_EINVAL, "null stream");
+    if (int rc = set_device(ctx)) return rc;
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return FPM_OK;
+}
+
+int fpm_stream_destroy(fpm_ctx *ctx, void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (stream) HIP_TRY(hipStreamDestroy((hipStream_t)stream));
+    return FPM_OK;
+}
+
+int fpm_event_create(fpm_ctx *ctx, void **event)
+{
+    if (!event) return fail(FPM_EINVAL, "null event");
+    if (int rc = set_device(ctx)) return rc;
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *event = e;
+    return FPM_OK;
+}
+
+int fpm_event_destroy(fpm_ctx *ctx, void *event)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (event) HIP_TRY(hipEventDestroy((hipEvent_t)event));
+    return FPM_OK;
+}
+
+int fpm_event_record(fpm_ctx *ctx, void *event, void *stream)
+{
+    if (!event) return fail(FPM_EINVAL, "null event");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipEventRecord((hipEvent_t)event, pick_stream(ctx, stream)));
+    return FPM_OK;
+}
+
+int fpm_stream_wait_event(fpm_ctx *ctx, void *stream, void *event)
+{
+    if (!event) return fail(FPM_EINVAL, "null event");
+    if (int rc = set_device(ctx)) return rc;
+    HIP_TRY(hipStreamWaitEvent(pick_stream(ctx, stream), (hipEvent_t)event, 0));
+    return FPM_OK;
+}
+
 int fpm_ctx_synchronize(fpm_ctx *ctx)
 {
     if (int rc = set_device(ctx)) return rc;

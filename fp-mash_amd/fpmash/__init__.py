@@ -50,6 +50,12 @@ SYMBOLS = [
     ("fpm_ctx_create", C.c_int, [C.c_int, C.POINTER(vp)]),
     ("fpm_ctx_destroy", None, [vp]),
     ("fpm_ctx_stream", vp, [vp]),
+    ("fpm_stream_create", C.c_int, [vp, C.POINTER(vp)]),
+    ("fpm_stream_destroy", C.c_int, [vp, vp]),
+    ("fpm_event_create", C.c_int, [vp, C.POINTER(vp)]),
+    ("fpm_event_destroy", C.c_int, [vp, vp]),
+    ("fpm_event_record", C.c_int, [vp, vp, vp]),
+    ("fpm_stream_wait_event", C.c_int, [vp, vp, vp]),
     ("fpm_ctx_synchronize", C.c_int, [vp]),
     ("fpm_ctx_warm", C.c_int, [vp]),
     ("fpm_malloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
@@ -409,6 +415,30 @@ class Context:
 
     def synchronize(self):
         _check(lib().fpm_ctx_synchronize(self.h))
+
+    def new_stream(self):
+        """fpm_stream_create: a non-blocking stream of the library's runtime (free with
+        free_stream)."""
+        s = vp()
+        _check(lib().fpm_stream_create(self.h, C.byref(s)))
+        return s.value
+
+    def free_stream(self, s):
+        _check(lib().fpm_stream_destroy(self.h, s))
+
+    def new_event(self):
+        e = vp()
+        _check(lib().fpm_event_create(self.h, C.byref(e)))
+        return e.value
+
+    def free_event(self, e):
+        _check(lib().fpm_event_destroy(self.h, e))
+
+    def record(self, event, stream):
+        _check(lib().fpm_event_record(self.h, event, stream))
+
+    def wait(self, stream, event):
+        _check(lib().fpm_stream_wait_event(self.h, stream, event))
 
     def set_timing(self, on=True):
         _check(lib().fpm_ctx_set_timing(self.h, int(on)))

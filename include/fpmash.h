@@ -64,6 +64,16 @@ int fpm_ctx_create(int device, fpm_ctx **out);
 void fpm_ctx_destroy(fpm_ctx *ctx);
 void *fpm_ctx_stream(fpm_ctx *ctx);          /* the context's hipStream_t */
 int fpm_ctx_synchronize(fpm_ctx *ctx);
+/* Extra streams and events on the context's device, for callers that overlap independent
+ * batches (e.g. the sketch of batch i+1 beside the dist of batch i): every call above takes
+ * a stream argument.  Handles are the library's own hipStream_t / hipEvent_t (the HIP runtime
+ * libfpmash links, which need not be the one another framework in the process bundles). */
+int fpm_stream_create(fpm_ctx *ctx, void **stream);
+int fpm_stream_destroy(fpm_ctx *ctx, void *stream);
+int fpm_event_create(fpm_ctx *ctx, void **event);
+int fpm_event_destroy(fpm_ctx *ctx, void *event);
+int fpm_event_record(fpm_ctx *ctx, void *event, void *stream);
+int fpm_stream_wait_event(fpm_ctx *ctx, void *stream, void *event);
 /* first-use costs of a process up front: the pinned staging ring and one small DMA each way
  * (~15-25 ms in a fresh process, paid by the first staged upload otherwise).  Optional; for a caller that can run it beside other start-up work (the CLI's
  * device warm-up thread). */

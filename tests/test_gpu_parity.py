@@ -296,6 +296,52 @@ def test_rank_crowded_buckets(ctx, oracle, mode):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 
 
+def test_streams_events_pipeline(ctx, oracle):
+    """fpm_stream_create / fpm_event_*: two sketch jobs of different batches on a second
+    stream, each dist on the context stream after its sketch's event (the bench's pipelined
+    steps): every grid equals the serial one and the oracle's."""
+    import fpmash
+    import fpmash.datagen as D
+    L = fpmash.lib()
+    P = fpmash.make_params(k=21, s=1000)
+    batches = [D.family_dna(4, 6, 2000, sub_rate=(0.0, 0.08), seed=sd) for sd in (3, 4, 5)]
+    jobs = [ctx.sketch_job(P, b) for b in batches]
+    n = len(batches[0])
+    lens = fpmash.DeviceBuffer.from_array(ctx, np.full(n, 2000, np.uint64))
+    sB = ctx.new_stream()
+    ev = [ctx.new_event() for _ in jobs]
+    outs = [(fpmash.DeviceBuffer(ctx, n * n * 2), fpmash.DeviceBuffer(ctx, n * n * 2),
+             fpmash.CellList(ctx, n * n)) for _ in jobs]
+    try:
+        for j, e in zip(jobs, ev):          # all sketches on stream B, events after each
+            j.run(sB)
+            ctx.record(e, sB)
+        for j, e, (nu, de, cl) in zip(jobs, ev, outs):
+            ctx.wait(ctx.stream, e)
+            rows, cnt, _, stride = j.device_output()
+            fpmash._check(L.fpm_dist_list_dev(ctx.h, rows, cnt, lens.ptr, stride, n, rows, cnt,
+                                              lens.ptr, stride, n, 8, 1000, 21, 4.0 ** 21, 1.0,
+                                              1.0, nu.ptr, de.ptr, cl.ref, ctx.stream))
+        ctx.synchronize()
+        for b, (nu, de, cl) in zip(batches, outs):
+            sk = oracle.sketch_batch(oracle.params(k=21, s=1000), b)
+            L2 = [2000] * n
+            gnu, gde, _, _ = oracle.dist_grid(sk, L2, sk, L2, 1000, 21, 4.0 ** 21)
+            assert np.array_equal(nu.to_array(np.uint16, n * n), gnu)
+            assert np.array_equal(de.to_array(np.uint16, n * n), gde)
+    finally:
+        for nu, de, cl in outs:
+            nu.free()
+            de.free()
+            cl.free()
+        lens.free()
+        for e in ev:
+            ctx.free_event(e)
+        ctx.free_stream(sB)
+        for j in jobs:
+            j.free()
+
+
 def test_pvalue_batch(ctx, oracle):
     """fpm_pvalue_batch_dev: distance and p-value of arbitrary cells (u16 and u32 counts)
     against the oracle's distance / pValue, including x = 0 (p = 1), numer = denom
