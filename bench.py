@@ -109,9 +109,6 @@ def parse():
     ap.add_argument("--no-split", action="store_true",
                     help="skip the one-genome-over-all-GPUs sketch leg (RCCL min-merge)")
     ap.add_argument("--split-bases", type=int, default=1_000_000_000)
-    ap.add_argument("--no-pipeline", action="store_true",
-                    help="time the C2 steps one after the other on one stream (default: the "
-                         "sketch of batch i+1 runs on a second stream beside the dist of batch i)")
     ap.add_argument("--no-full-grid", action="store_true",
                     help="skip the comparison run of the C2 step with the full five-array dist "
                          "output (fpm_dist_dev16)")
@@ -1280,7 +1277,6 @@ def compact_line(d, detail_path=None):
         "dist_mpairs_per_s": _r(g(d, "dist", "mpairs_per_s")),
         "dist_device_ms": _r(g(d, "dist", "device_ms_per_step")),
         "dist_path": g(d, "dist", "path"),
-        "c2_serial_ms": _r(g(d, "config", "serial_ms_per_step")),
         "c2_full_grid_ms": _r(g(d, "config", "full_grid_ms_per_step")),
         "fp_text_lines_per_s": _r(g(d, "fp_text", "lines_per_s_device")),
         "c3_dist_ms": _r(g(c3, "dist_ms")), "c3_dense_walk_ms": _r(g(c3, "dense_walk_ms")),
@@ -1339,72 +1335,26 @@ def main():
                                           4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
                                           cells.ref, st))
 
-    def run_serial(k):
+    def run_steps(k):
         for _ in range(k):
             step()
 
-    # Pipelined steps (the default): every batch is sketched and compared in full, but the
-    # sketch of batch i+1 (a second job over the same staged input, its own output rows) runs
-    # on a second stream beside the dist of batch i: the VALU-bound tile kernel fills the CUs
-    # the latency-bound index / probe / rank kernels leave idle.  Events order each buffer's
-    # sketch after the dist that last read it, and each dist after its sketch.
-    # (the library's own streams and events: fpm_stream_create / fpm_event_*; torch's bundled
-    # HIP runtime is a different one)
-    pipe = None
-    if not args.no_pipeline:
-        job2 = ctx.sketch_job(P, seqs)
-        rows2, cnt2, _, stride2 = job2.device_output()
-        assert stride2 == stride
-        pipe = {"jobs": [job, job2], "rows": [(d_rows, d_cnt), (rows2, cnt2)],
-                "sB": ctx.new_stream(),
-                "ev_sk": [ctx.new_event(), ctx.new_event()],
-                "ev_dd": [ctx.new_event(), ctx.new_event()]}
-
-    def sketch_into(b):
-        ctx.wait(pipe["sB"], pipe["ev_dd"][b])       # the dist that last read buffer b
-        pipe["jobs"][b].run(pipe["sB"])
-        ctx.record(pipe["ev_sk"][b], pipe["sB"])
-
-    def dist_from(b):
-        ctx.wait(st, pipe["ev_sk"][b])
-        rows, cnt = pipe["rows"][b]
-        fpmash._check(L.fpm_dist_list_dev(ctx.h, rows, cnt, d_len.ptr, stride, n, rows, cnt,
-                                          d_len.ptr, stride, n, 8, args.s, args.k,
-                                          4.0 ** args.k, 1.0, 1.0, d_numer.ptr, d_denom.ptr,
-                                          cells.ref, st))
-        ctx.record(pipe["ev_dd"][b], st)
-
-    def run_pipelined(k):
-        b = 0
-        if k:
-            sketch_into(b)
-        for i in range(k):
-            if i + 1 < k:
-                sketch_into(1 - b)                   # the next batch, beside this dist
-            dist_from(b)
-            b = 1 - b
-
-    run_steps = run_serial if pipe is None else run_pipelined
-
-    def timed(run, k):
-        run(args.warmup)
-        ctx.synchronize()
-        grp.barrier()
-        ctx.synchronize()
-        t0 = time.perf_counter()
-        run(k)
-        ctx.synchronize()
-        t1 = time.perf_counter()
-        grp.barrier()
-        return grp.max(t1 - t0)
-
-    elapsed = timed(run_steps, args.steps)
+    # (Pipelined steps — the sketch of batch i+1 on a second stream, fpm_stream_create /
+    # fpm_event_*, beside the dist of batch i — measured 1.023 vs 0.962 ms per step serial,
+    # same box: the tile kernel's workgroups take LDS and CUs from the rank kernel.)
+    run_steps(args.warmup)
+    ctx.synchronize()
+    grp.barrier()
+    ctx.synchronize()
+    t0 = time.perf_counter()
+    run_steps(args.steps)
+    ctx.synchronize()
+    t1 = time.perf_counter()
+    grp.barrier()
+    elapsed = grp.max(t1 - t0)
     n_listed = cells.count()
     if n_listed > cells.cap:
         raise RuntimeError(f"C2 cell list overflow: {n_listed} cells > {cells.cap}")
-    # the same steps one after the other on one stream (reported beside, not `value`)
-    serial_ms = elapsed / args.steps * 1e3 if pipe is None else \
-        timed(run_serial, args.steps) / args.steps * 1e3
 
     # the same step with the full five-array output (fpm_dist_dev16: distance / p-value / pass
     # written for every cell, 21 B per pair), for comparison with rounds 1-3: not `value`
@@ -1590,10 +1540,6 @@ def main():
                 "n_seqs_per_gpu": n, "seq_len": args.seq_len, "k": args.k, "s": args.s,
                 "pairs_per_gpu": n_pairs, "parallelism": f"independent batch per GPU x{ws}",
                 "listed_pairs_per_gpu": n_listed,
-                "steps": ("pipelined: the sketch of batch i+1 on a second stream beside the dist "
-                          "of batch i (every batch sketched and compared in full)"
-                          if pipe is not None else "serial, one stream"),
-                "serial_ms_per_step": serial_ms,    # the same steps one after the other
                 "full_grid_ms_per_step": full_ms,   # distance/p-value/pass written for every pair
             },
             "kernel_timing_steps": n_timed,
