@@ -1304,6 +1304,10 @@ def compact_line(d, detail_path=None):
 def main():
     args = parse()
     ws, rank, local = dist_env()
+    # torch (RCCL groups) before the library's context: torch bundles its own HIP runtime,
+    # which finds no GPU when it starts after libfpmash's (system ROCm) runtime has; started
+    # first, both see the device and device pointers pass between them (fpm_memcpy_d2d of a
+    # torch tensor checked on the MI355X box, r04)
     grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split))
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
