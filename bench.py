@@ -149,6 +149,10 @@ def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("FPMASH_BENCH_ONE_DEVICE"):
+        # rehearsal of the N-rank flow on a one-GPU box (tools/rehearse_ranks.sh): every rank
+        # on device 0, gathers over gloo (RCCL refuses two ranks on one GPU)
+        local = 0
     return ws, rank, local
 
 
@@ -1308,7 +1312,8 @@ def main():
     # which finds no GPU when it starts after libfpmash's (system ROCm) runtime has; started
     # first, both see the device and device pointers pass between them (fpm_memcpy_d2d of a
     # torch tensor checked on the MI355X box, r04)
-    grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split))
+    grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split) and
+                not os.environ.get("FPMASH_BENCH_ONE_DEVICE"))
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
     n = len(seqs)
