@@ -862,11 +862,26 @@ template <typename H>
 __global__ __launch_bounds__(64 * kRecWaves) void record_rows_kernel(
     const H *__restrict__ in, const uint32_t *__restrict__ in_len, uint64_t in_stride, uint32_t n,
     uint32_t S, H *__restrict__ out, uint32_t *__restrict__ pos_out, uint32_t *__restrict__ out_len,
-    uint64_t out_stride)
+    uint64_t out_stride, uint32_t *__restrict__ unsorted)
 {
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t row = blockIdx.x * kRecWaves + (threadIdx.x >> 6);
     if (row >= n) return;
+    if (unsorted) {
+        // the index build's sortedness test (every entry of the row below the next one), so
+        // a caller can take the record index without building the raw one first
+        const uint32_t len = in_len[row];
+        const H *r = in + (uint64_t)row * in_stride;
+        bool uns = false;
+        for (uint32_t c0 = 0; c0 < len; c0 += 64) {
+            const uint32_t i = c0 + lane;
+            const H v = i < len ? r[i] : H(0);
+            H nx = (H)__shfl_down((unsigned long long)v, 1, 64);
+            if (lane == 63 && i + 1 < len) nx = r[i + 1];
+            uns |= i + 1 < len && !(v < nx);
+        }
+        if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
+    }
     const uint32_t m = min(min(in_len[row], S), (uint32_t)out_stride);
     const H *src = in + (uint64_t)row * in_stride;
     H *dst = out + (uint64_t)row * out_stride;
@@ -900,16 +915,18 @@ __global__ __launch_bounds__(64 * kRecWaves) void record_rows_kernel(
 hipError_t launch_record_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
                               uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
                               uint32_t *pos_out, uint32_t *out_len, uint64_t out_stride,
-                              hipStream_t st)
+                              hipStream_t st, uint32_t *unsorted)
 {
     if (!n) return hipSuccess;
     const dim3 g((n + kRecWaves - 1) / kRecWaves), b(64 * kRecWaves);
     if (hash_bytes == 8)
         hipLaunchKernelGGL(record_rows_kernel<uint64_t>, g, b, 0, st, (const uint64_t *)in, in_len,
-                           in_stride, n, S, (uint64_t *)out, pos_out, out_len, out_stride);
+                           in_stride, n, S, (uint64_t *)out, pos_out, out_len, out_stride,
+                           unsorted);
     else
         hipLaunchKernelGGL(record_rows_kernel<uint32_t>, g, b, 0, st, (const uint32_t *)in, in_len,
-                           in_stride, n, S, (uint32_t *)out, pos_out, out_len, out_stride);
+                           in_stride, n, S, (uint32_t *)out, pos_out, out_len, out_stride,
+                           unsorted);
     return hipGetLastError();
 }
 

@@ -2198,34 +2198,18 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             void *dir_, *entries_;
             HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir_));
             HIP_TRY(scratch(ctx, 5, E * 4, &entries_));
-            geom.kmax = events + 68;
-            // one set against itself: the query side is the ref side, so its sortedness is
-            // the ref flag and its posting events are sum_b |b|^2 from the bucket pass.
-            // The counters are zeroed by the first index kernel.
-            if (int rc = build_index(ctx, d_ref, d_ref_len, ref_stride, n_ref, hash_bytes, geom,
-                                     (uint32_t *)dir_, (uint32_t *)entries_, events, self_set, st,
-                                     [&]() -> int {
-                                         if (!self_set)
-                                             HIP_TRY(launch_probe_count(d_qry, d_qry_len, qry_stride,
-                                                                        n_qry, hash_bytes, geom,
-                                                                        (const uint32_t *)dir_,
-                                                                        events, unsorted, st));
-                                         return FPM_OK;
-                                     }, true))
-                return rc;
             dir = (const uint32_t *)dir_;
             entries = (const uint32_t *)entries_;
-            ev = ctx->host_counters[0];
-            all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
-            // Unsorted lists (-fp): re-index each row's records among its first min(len, S)
-            // entries (launch_record_rows): ~ln(S) values per row instead of every distinct
-            // one, and only pairs sharing a record can count anything.  The candidates are
-            // walked on the original lists.
+            // Unsorted lists (-fp): the index runs over each row's records among its first
+            // min(len, S) entries (launch_record_rows): ~ln(S) values per row instead of every
+            // distinct one, and only pairs sharing a record can count anything.  The
+            // candidates are walked on the original lists.
             const uint64_t mr = std::min<uint64_t>(ref_stride, sketch_size);
             const uint64_t mq = std::min<uint64_t>(qry_stride, sketch_size);
-            if (!all_sorted) {
-                void *dref, *dref_len, *dref_pos, *dqry = nullptr, *dqry_len = nullptr,
-                     *dqry_pos = nullptr;
+            void *dref = nullptr, *dref_len = nullptr, *dref_pos = nullptr, *dqry = nullptr,
+                 *dqry_len = nullptr, *dqry_pos = nullptr;
+            // the record rows of both sides; flag: also test every row's order into `unsorted`
+            auto records = [&](uint32_t *flag) -> int {
                 HIP_TRY(scratch(ctx, 10, (size_t)n_ref * mr * hash_bytes, &dref));
                 HIP_TRY(scratch(ctx, 11, (size_t)n_ref * 4, &dref_len));
                 HIP_TRY(scratch(ctx, 19, (size_t)n_ref * mr * 4, &dref_pos));
@@ -2234,19 +2218,19 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                     HIP_TRY(scratch(ctx, 13, (size_t)n_qry * 4, &dqry_len));
                     HIP_TRY(scratch(ctx, 20, (size_t)n_qry * mq * 4, &dqry_pos));
                 }
-                geom = make_geom(n_ref, (uint64_t)n_ref * mr);
-                geom.kmax = events + 68;
-                {
-                    TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                    HIP_TRY(launch_record_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
-                                               sketch_size, dref, (uint32_t *)dref_pos,
-                                               (uint32_t *)dref_len, mr, st));
-                    if (!self_set)
-                        HIP_TRY(launch_record_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
-                                                   sketch_size, dqry, (uint32_t *)dqry_pos,
-                                                   (uint32_t *)dqry_len, mq, st));
-                    tl.done();
-                }
+                TimedLaunch tl(ctx, FPM_K_INDEX, st);
+                HIP_TRY(launch_record_rows(d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
+                                           sketch_size, dref, (uint32_t *)dref_pos,
+                                           (uint32_t *)dref_len, mr, st, flag));
+                if (!self_set)
+                    HIP_TRY(launch_record_rows(d_qry, d_qry_len, qry_stride, n_qry, hash_bytes,
+                                               sketch_size, dqry, (uint32_t *)dqry_pos,
+                                               (uint32_t *)dqry_len, mq, st, flag));
+                tl.done();
+                return FPM_OK;
+            };
+            // the index over the record rows (after records())
+            auto record_index = [&]() -> int {
                 rec_r = RecRows{dref, (const uint32_t *)dref_pos, (const uint32_t *)dref_len, mr};
                 rec_q = self_set ? rec_r
                                  : RecRows{dqry, (const uint32_t *)dqry_pos,
@@ -2254,6 +2238,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 p_qry = self_set ? dref : dqry;
                 p_qry_it = (const uint32_t *)(self_set ? dref_len : dqry_len);
                 p_qry_stride = self_set ? mr : mq;
+                geom = make_geom(n_ref, (uint64_t)n_ref * mr);
+                geom.kmax = events + 68;
                 if (int rc = build_index(ctx, dref, (const uint32_t *)dref_len, mr, n_ref, hash_bytes,
                                          geom, (uint32_t *)dir_, (uint32_t *)entries_, events,
                                          self_set, st, [&]() -> int {
@@ -2265,7 +2251,47 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                              return FPM_OK;
                                          }))
                     return rc;
+                all_sorted = false;
                 ev = ctx->host_counters[0];
+                return FPM_OK;
+            };
+            bool indexed = false;
+            if (hash_bytes == 4) {
+                // u32 rows (the -fp lists; k <= 16 sketches): their order is tested with the
+                // records, and unsorted rows go straight to the record index (C3: the raw
+                // index built only to learn the order cost ~0.2 ms of 1.45)
+                HIP_TRY(hipMemsetAsync(unsorted, 0, sizeof(uint32_t), st));
+                if (int rc = records(unsorted)) return rc;
+                if (int rc = read_counters(ctx, (const unsigned long long *)events, 67, st)) return rc;
+                if (((const uint32_t *)(ctx->host_counters + 66))[0] != 0) {
+                    if (int rc = record_index()) return rc;
+                    indexed = true;
+                }
+            }
+            if (!indexed) {
+                geom.kmax = events + 68;
+                // one set against itself: the query side is the ref side, so its sortedness
+                // is the ref flag and its posting events are sum_b |b|^2 from the bucket pass.
+                // The counters are zeroed by the first index kernel.
+                if (int rc = build_index(ctx, d_ref, d_ref_len, ref_stride, n_ref, hash_bytes,
+                                         geom, (uint32_t *)dir_, (uint32_t *)entries_, events,
+                                         self_set, st,
+                                         [&]() -> int {
+                                             if (!self_set)
+                                                 HIP_TRY(launch_probe_count(
+                                                     d_qry, d_qry_len, qry_stride, n_qry,
+                                                     hash_bytes, geom, (const uint32_t *)dir_,
+                                                     events, unsorted, st));
+                                             return FPM_OK;
+                                         }, true))
+                    return rc;
+                ev = ctx->host_counters[0];
+                all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
+                if (!all_sorted) {
+                    if (hash_bytes != 4)
+                        if (int rc = records(nullptr)) return rc;
+                    if (int rc = record_index()) return rc;
+                }
             }
         }
         ctx->last_events = ev;

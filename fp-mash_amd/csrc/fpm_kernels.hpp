@@ -154,11 +154,12 @@ hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned 
 // each row's records among its first min(len, S, out_stride) entries (the strict increases of
 // its running maximum: sorted and distinct; dist_index.hip), the index / probe input for
 // unsorted lists: only pairs sharing a record value can count anything in the literal walk
-// (pos_out, may be null: each record's position in its row, at the same offsets)
+// (pos_out, may be null: each record's position in its row, at the same offsets; unsorted,
+// may be null: set to 1 when some row is not strictly increasing, the index build's test)
 hipError_t launch_record_rows(const void *in, const uint32_t *in_len, uint64_t in_stride,
                               uint32_t n, uint32_t hash_bytes, uint32_t S, void *out,
                               uint32_t *pos_out, uint32_t *out_len, uint64_t out_stride,
-                              hipStream_t st);
+                              hipStream_t st, uint32_t *unsorted = nullptr);
 hipError_t launch_exscan(const uint32_t *in, uint32_t *out, uint32_t *out2, uint64_t n,
                          uint32_t *scratch, uint32_t *total, hipStream_t st);
 hipError_t launch_probe_count(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,
