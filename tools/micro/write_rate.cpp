@@ -1,7 +1,8 @@
 // tools/micro/write_rate.cpp — how fast can `fpmash dist` put its text into a regular file?
 // Writes SIZE bytes of a pre-made buffer to PATH by: (1) one pwrite stream, (2) T threads
 // pwriting disjoint pieces, (3) T threads copying into a MAP_SHARED mapping after one
-// ftruncate, (4) the same with MADV_POPULATE_WRITE per piece, (5) fallocate + T pwrite threads.
+// ftruncate, (4) the same with MADV_POPULATE_WRITE per piece, (5) fallocate + T pwrite threads,
+// (6) fallocate alone and (7) one pwrite stream into the allocated pages.
 // Build: g++ -O2 -pthread tools/micro/write_rate.cpp -o /tmp/write_rate
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -75,5 +76,22 @@ int main(int argc, char **argv)
         if (fallocate(fd, 0, 0, size)) perror("fallocate");
         par([&](size_t at, size_t n) { if (pwrite(fd, src.data(), n, at) < 0) abort(); });
     });
+    // (6) / (7): the two halves of (5) timed apart — the pages allocated ahead (what the CLI
+    // could do while the HIP runtime starts), then one pwrite stream into them
+    {
+        unlink(path);
+        int fd = open(path, O_RDWR | O_CREAT | O_TRUNC, 0644);
+        double t0 = now();
+        if (fallocate(fd, 0, 0, size)) perror("fallocate");
+        double t1 = now();
+        printf("%-28s %7.1f ms  %6.2f GB/s\n", "fallocate alone", (t1 - t0) * 1e3, size / (t1 - t0) / 1e9);
+        t0 = now();
+        for (size_t p = 0; p < np; p++)
+            if (pwrite(fd, src.data(), std::min(piece, size - p * piece), p * piece) < 0) abort();
+        t1 = now();
+        printf("%-28s %7.1f ms  %6.2f GB/s\n", "pwrite 1 thr, pages allocated", (t1 - t0) * 1e3, size / (t1 - t0) / 1e9);
+        close(fd);
+        unlink(path);
+    }
     return 0;
 }
