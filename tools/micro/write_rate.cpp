@@ -2,7 +2,8 @@
 // Writes SIZE bytes of a pre-made buffer to PATH by: (1) one pwrite stream, (2) T threads
 // pwriting disjoint pieces, (3) T threads copying into a MAP_SHARED mapping after one
 // ftruncate, (4) the same with MADV_POPULATE_WRITE per piece, (5) fallocate + T pwrite threads,
-// (6) fallocate alone and (7) one pwrite stream into the allocated pages.
+// (6) fallocate alone, (7) one pwrite stream into the allocated pages and (8)/(9) T threads
+// writing through a shared mapping of allocated pages.
 // Build: g++ -O2 -pthread tools/micro/write_rate.cpp -o /tmp/write_rate
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -90,6 +91,24 @@ int main(int argc, char **argv)
             if (pwrite(fd, src.data(), std::min(piece, size - p * piece), p * piece) < 0) abort();
         t1 = now();
         printf("%-28s %7.1f ms  %6.2f GB/s\n", "pwrite 1 thr, pages allocated", (t1 - t0) * 1e3, size / (t1 - t0) / 1e9);
+        close(fd);
+        unlink(path);
+    }
+    // (8) / (9): pages allocated ahead (untimed), then T threads writing into a shared mapping
+    // of them (with / without MADV_POPULATE_WRITE per piece), munmap included
+    for (int pop = 0; pop < 2; pop++) {
+        unlink(path);
+        int fd = open(path, O_RDWR | O_CREAT | O_TRUNC, 0644);
+        if (fallocate(fd, 0, 0, size)) perror("fallocate");
+        double t0 = now();
+        char *m = (char *)mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        if (m == MAP_FAILED) abort();
+        par([&](size_t at, size_t n) { if (pop) madvise(m + at, n, 23); memcpy(m + at, src.data(), n); });
+        double t1 = now();
+        munmap(m, size);
+        double t2 = now();
+        printf("%-28s %7.1f ms  %6.2f GB/s  (munmap %.1f ms)\n", pop ? "alloc'd, mmap+populate T thr" : "alloc'd, mmap T thr",
+               (t2 - t0) * 1e3, size / (t2 - t0) / 1e9, (t2 - t1) * 1e3);
         close(fd);
         unlink(path);
     }
