@@ -25,6 +25,7 @@
 
 #include <fcntl.h>
 #include <climits>
+#include <sys/mman.h>
 #include <sys/uio.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -101,8 +102,30 @@ inline char *numTo(char *p, double x)
     if (x == 0.0 && !std::signbit(x)) { *p++ = '0'; return p; }
     return p + snprintf(p, 32, "%g", x);
 }
+// counts of up to 4 digits (a sketch size of 1000 and below: every count of the C2 text) by
+// two-digit table lookups, the rest digit by digit (14.6 against 17.6 ns per list line)
+constexpr char kDigits2[] =
+    "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+    "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+    "8081828384858687888990919293949596979899";
 inline char *uTo(char *p, uint64_t x)
 {
+    if (x < 100) {
+        if (x < 10) { *p = (char)('0' + x); return p + 1; }
+        memcpy(p, kDigits2 + 2 * x, 2);
+        return p + 2;
+    }
+    if (x < 10000) {
+        const uint32_t a = (uint32_t)x / 100, b = (uint32_t)x % 100;
+        if (a < 10) {
+            *p = (char)('0' + a);
+            memcpy(p + 1, kDigits2 + 2 * b, 2);
+            return p + 3;
+        }
+        memcpy(p, kDigits2 + 2 * a, 2);
+        memcpy(p + 2, kDigits2 + 2 * b, 2);
+        return p + 4;
+    }
     char t[20];
     int n = 0;
     do { t[19 - n++] = (char)('0' + x % 10); x /= 10; } while (x);
@@ -110,25 +133,29 @@ inline char *uTo(char *p, uint64_t x)
     return p + n;
 }
 
-// Allocates the output file's pages ahead of the writer: fallocate in 64 MB steps from the
-// output position up to an estimate of the text's size, on a thread of its own that starts
-// while the HIP runtime comes up and the rows are packed (idle cores).  pwrite into allocated
-// tmpfs pages copies at ~9.7 GB/s against ~6.0 GB/s when every page is allocated on the way,
-// and fallocate alone runs at ~18 GB/s (4 GB into /dev/shm on the MI355X box,
-// tools/micro/write_rate.cpp).  The pages past the final size are cut by trim().
+// Allocates the output file's pages ahead of the writer: the file's size set to an estimate of
+// the text's end, then fallocate (sizes kept) in 64 MB steps from the output position, on a
+// thread of its own that starts while the HIP runtime comes up and the rows are packed (idle
+// cores).  pwrite into allocated tmpfs pages copies at ~9.7 GB/s against ~6.0 GB/s when every
+// page is allocated on the way, and fallocate alone runs at ~18 GB/s (4 GB into /dev/shm on the
+// MI355X box, tools/micro/write_rate.cpp).  The file's size stays the caller's to change; the
+// pages past the final size are cut by trim().
 class Prealloc {
   public:
     void start(int fd, off_t from, off_t upto)
     {
+        struct stat st {};
+        if (fstat(fd, &st) != 0 || (st.st_size < upto && ftruncate(fd, upto) != 0)) return;
         fd_ = fd;
         pos_ = from;
         upto_ = upto;
         th_ = std::thread([this] {
-            // only until the writer starts: allocating beside its writes made them queue on the
-            // file's inode lock (CLI A/B on the box: 1.0-1.7 s against 1.05-1.28 s)
+            // pwrite mode: only until the writer starts (allocating beside its writes made them
+            // queue on the file's inode lock, CLI A/B on the box: 1.0-1.7 s against 1.05-1.28 s);
+            // writes through a mapping take no inode lock and run beside it
             while (!stop_.load(std::memory_order_relaxed) && !started_.load(std::memory_order_relaxed)) {
                 const off_t n = std::min<off_t>(kStep, upto_ - pos_);
-                if (n <= 0 || fallocate(fd_, 0, pos_, n) != 0) break;
+                if (n <= 0 || fallocate(fd_, FALLOC_FL_KEEP_SIZE, pos_, n) != 0) break;
                 pos_ += n;
             }
         });
@@ -156,6 +183,57 @@ class Prealloc {
     std::atomic<bool> stop_{false}, started_{false};
     std::thread th_;
 };
+
+// A shared writable mapping of the output file (stdout reopened read-write through /proc, since
+// a shell's `>` opens it write-only), reserved up to a bound on the text's size: the formatter
+// threads write every piece straight into its pages at its offset, with no copy and no inode
+// lock between them (a mapping's page faults take none; pwrite serialises on it).
+struct MapOut {
+    int fd = -1;
+    char *base = nullptr;
+    off_t origin = 0;                   // file offset of base (page aligned)
+    size_t len = 0;
+    bool open(int out_fd, off_t at, uint64_t max_bytes)
+    {
+        const long pg = sysconf(_SC_PAGESIZE);
+        if (pg <= 0 || max_bytes > (1ULL << 44)) return false;
+        char path[64];
+        snprintf(path, sizeof path, "/proc/self/fd/%d", out_fd);
+        fd = ::open(path, O_RDWR | O_CLOEXEC);
+        struct stat a {}, b {};
+        if (fd < 0 || fstat(out_fd, &a) != 0 || fstat(fd, &b) != 0 || a.st_ino != b.st_ino ||
+            a.st_dev != b.st_dev) {
+            close();
+            return false;
+        }
+        origin = at / pg * pg;
+        len = (size_t)((at - origin) + max_bytes + pg) / pg * pg;
+        void *m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_NORESERVE, fd, origin);
+        if (m == MAP_FAILED) {
+            close();
+            return false;
+        }
+        base = (char *)m;
+        return true;
+    }
+    char *at(off_t off) const { return base + (off - origin); }
+    void close()
+    {
+        if (fd >= 0) ::close(fd);
+        fd = -1;
+    }
+};
+
+// number of decimal digits of x (no loop: a line's counts are measured per cell)
+inline int decDigits(uint64_t x)
+{
+    return 1 + (x >= 10) + (x >= 100) + (x >= 1000) + (x >= 10000) + (x >= 100000) +
+           (x >= 1000000) + (x >= 10000000) + (x >= 100000000) + (x >= 1000000000) +
+           (x >= 10000000000ULL) + (x >= 100000000000ULL) + (x >= 1000000000000ULL) +
+           (x >= 10000000000000ULL) + (x >= 100000000000000ULL) + (x >= 1000000000000000ULL) +
+           (x >= 10000000000000000ULL) + (x >= 100000000000000000ULL) +
+           (x >= 1000000000000000000ULL) + (x >= 10000000000000000000ULL);
+}
 
 // writes the pieces at `at` in one pwritev() per IOV_MAX pieces (short writes resumed); false on
 // an error.  One call per block: the formatter threads keep formatting instead of queueing on
@@ -293,22 +371,32 @@ int CommandDistance::run() const
                                                    sketchRef.getMinHashesPerWindow());
     const bool use64 = sketchRef.getUse64();
     const uint32_t hb = use64 ? 8 : 4;
-    // The output file's pages allocated ahead (Prealloc) while the devices come up: stdout a
-    // regular file (not O_APPEND), the list format and no -d / -v filter, so the text size is
-    // about known: every line names its pair and most carry "1\t1\t0/<denom>" (pairs sharing
-    // hashes write a few bytes more, past the estimate, into pages allocated on the way)
-    Prealloc prealloc;
-    const char *pa_env = getenv("FPMASH_DIST_PREALLOC");   // A/B: 0 = pages allocated by pwrite
-    if (nR && nQ && !table && !options.at("distance").active && !options.at("pvalue").active &&
-        !(pa_env && strcmp(pa_env, "0") == 0)) {
-        std::cout.flush();
-        fflush(stdout);
-        const int fd = fileno(stdout);
+    // stdout a regular file (not O_APPEND): the text goes in at its offsets, through a mapping
+    // of the file (MapOut, list format) or one pwritev() per block; otherwise (pipes,
+    // terminals) by fwrite.
+    out.flush();
+    std::cout.flush();
+    fflush(stdout);
+    const int ofd = fileno(stdout);
+    off_t opos = -1;
+    {
         struct stat st {};
-        const int fl = fcntl(fd, F_GETFL);
-        const off_t at = fl >= 0 && !(fl & O_APPEND) && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)
-                             ? lseek(fd, 0, SEEK_CUR) : (off_t)-1;
-        if (at >= 0) {
+        const int fl = fcntl(ofd, F_GETFL);
+        if (nR && nQ && fl >= 0 && !(fl & O_APPEND) && fstat(ofd, &st) == 0 && S_ISREG(st.st_mode))
+            opos = lseek(ofd, 0, SEEK_CUR);
+    }
+    const bool direct = opos >= 0;
+    // The output file's pages allocated ahead (Prealloc) while the devices come up: the list
+    // format and no -d / -v filter, so the text size is about known: every line names its pair
+    // and most carry "1\t1\t0/<denom>" (pairs sharing hashes write a few bytes more, past the
+    // estimate, into pages allocated on the way)
+    Prealloc prealloc;
+    MapOut mo;
+    const char *pa_env = getenv("FPMASH_DIST_PREALLOC");   // A/B: 0 = pages allocated on the way
+    const char *map_env = getenv("FPMASH_DIST_MAP");        // 1 = in place through MapOut
+    if (direct && !table) {
+        const off_t at = opos;
+        {
             uint64_t rn = 0, qn = 0;
             for (uint64_t j = 0; j < nR; j++) {
                 const Reference &r = sketchRef.getReference(j);
@@ -321,9 +409,21 @@ int CommandDistance::run() const
             const uint64_t digits = std::to_string(sketchSize).size();
             const long double est = (long double)nQ * rn + (long double)nR * qn +
                                     (long double)nR * nQ * (7 + digits);
-            prealloc.start(fd, at, at + (off_t)std::min<long double>(est, (long double)(1ULL << 46)));
+            // every line is at most its two names + kLineNums
+            const long double most = (long double)nQ * rn + (long double)nR * qn +
+                                     (long double)nR * nQ * kLineNums;
+            // (off by default: with 16 formatter threads writing through the mapping the C2
+            // command measured 0.93-1.34 s against 0.93-1.03 s by pwritev, same box)
+            if (map_env && strcmp(map_env, "1") == 0 && most < (long double)(1ULL << 44))
+                mo.open(ofd, at, (uint64_t)most);
+            if (!options.at("distance").active && !options.at("pvalue").active &&
+                !(pa_env && strcmp(pa_env, "0") == 0))
+                prealloc.start(ofd, at, at + (off_t)std::min<long double>(est, (long double)(1ULL << 46)));
         }
     }
+    const bool mapped = mo.base != nullptr;
+    const char *pop_env = getenv("FPMASH_DIST_POPULATE");   // A/B
+    const bool mapPopulate = !(pop_env && strcmp(pop_env, "0") == 0);
     // dense device layout: one row per sketch
     // (zero pages, populated in one call: a value-initialised vector paid a memset and ~20k
     // page faults on one thread for C2's 80 MB)
@@ -364,7 +464,9 @@ int CommandDistance::run() const
     if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
     const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
     const uint64_t nBlocks = nR ? (nQ + block - 1) / block : 0;
-    const int nSlots = std::max(2, 2 * nDev + 1);
+    // (mapped: a block's slot is free once its pieces are formatted in place; more blocks in
+    // flight keep the formatter threads busy)
+    const int nSlots = mapped ? std::max(4, 2 * nDev + 3) : std::max(2, 2 * nDev + 1);
     const int nFmt = std::max(1, std::min(parameters.parallelism > 1 ? parameters.parallelism
                                           : (int)std::thread::hardware_concurrency(), 64));
     // A block's results in the compact form (fpm_refset_dist_list): u16 numer / denom of
@@ -385,13 +487,18 @@ int CommandDistance::run() const
         int dev = 0;
         uint64_t b = ~0ULL;                 // block held
         std::vector<std::string> text;      // formatted pieces
-        int pending = 0;                    // pieces still being formatted
-        bool ready = false;
+        std::vector<uint64_t> psz;          // mapped: each piece's bytes, rows per piece
+        uint64_t per = 1;
+        int pending = 0;                    // pieces still being formatted (mapped: measured,
+        bool ready = false;                 // then written)
+        bool sized = false;
+        uint64_t nextB = 0;                 // the next block this slot may take
     };
     std::vector<Slot> slots(nSlots);
+    for (int i = 0; i < nSlots; i++) slots[i].nextB = (uint64_t)i;
+    uint64_t blocksDone = 0;                // mapped: blocks formatted into the file
     std::mutex mu;
     std::condition_variable cv;
-    uint64_t written = 0;                   // blocks already written out
     std::deque<std::function<void()>> tasks;
     bool stop = false;
     auto allocList = [&](Slot &sl, uint64_t cap) {
@@ -521,6 +628,80 @@ int CommandDistance::run() const
         }
         dst.swap(o.buf);
     };
+    // mapped: a piece's list lines measured (listSize), then written in place at the piece's
+    // offset (listTo) — the same bytes format() makes
+    auto qtailOf = [&](uint64_t q, std::string &qt) {
+        const Reference &qr = sketchQuery.getReference(q);
+        qt.assign(1, '\t');
+        qt += qr.name;
+        if (comment) { qt.push_back(':'); qt += qr.comment; }
+        qt.push_back('\t');
+    };
+    auto listSize = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb) {
+        uint64_t bytes = 0;
+        std::string qt;
+        char t[kLineNums];
+        for (uint64_t qi = qa; qi < qb; qi++) {
+            qtailOf(q0 + qi, qt);
+            const uint64_t fix = qt.size() + 7;   // "\t<query>\t" + "1\t1\t0/" + '\n'
+            uint32_t cur = sl.rowStart[qi];
+            for (uint64_t j = 0; j < nR; j++) {
+                const uint64_t k = qi * nR + j;
+                const uint32_t nm = cb == 2 ? ((const uint16_t *)sl.nu)[k] : ((const uint32_t *)sl.nu)[k];
+                const uint32_t dn = cb == 2 ? ((const uint16_t *)sl.de)[k] : ((const uint32_t *)sl.de)[k];
+                if (nm == 0) {
+                    if (dn == 0 ? passEmpty : passNone) bytes += refTag[j].size() + fix + decDigits(dn);
+                } else {
+                    const uint32_t e = sl.byRow[cur++];
+                    if (!sl.la[e]) continue;
+                    char *p = numTo(t, sl.ld[e]);
+                    *p++ = '\t';
+                    p = numTo(p, sl.lp[e]);
+                    bytes += refTag[j].size() + qt.size() + (uint64_t)(p - t) + 3 + decDigits(nm) + decDigits(dn);
+                }
+            }
+        }
+        return bytes;
+    };
+    auto listTo = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, char *p) {
+        std::string qt;
+        for (uint64_t qi = qa; qi < qb; qi++) {
+            qtailOf(q0 + qi, qt);
+            uint32_t cur = sl.rowStart[qi];
+            for (uint64_t j = 0; j < nR; j++) {
+                const uint64_t k = qi * nR + j;
+                const uint32_t nm = cb == 2 ? ((const uint16_t *)sl.nu)[k] : ((const uint32_t *)sl.nu)[k];
+                const uint32_t dn = cb == 2 ? ((const uint16_t *)sl.de)[k] : ((const uint32_t *)sl.de)[k];
+                const std::string &tag = refTag[j];
+                if (nm == 0) {
+                    if (!(dn == 0 ? passEmpty : passNone)) continue;
+                    memcpy(p, tag.data(), tag.size());
+                    p += tag.size();
+                    memcpy(p, qt.data(), qt.size());
+                    p += qt.size();
+                    memcpy(p, dn == 0 ? "0\t1\t0/" : "1\t1\t0/", 6);
+                    p = uTo(p + 6, dn);
+                    *p++ = '\n';
+                } else {
+                    const uint32_t e = sl.byRow[cur++];
+                    if (!sl.la[e]) continue;
+                    memcpy(p, tag.data(), tag.size());
+                    p += tag.size();
+                    memcpy(p, qt.data(), qt.size());
+                    p += qt.size();
+                    p = numTo(p, sl.ld[e]);   // (snprintf's NUL lands where the tab goes)
+                    *p++ = '\t';
+                    p = numTo(p, sl.lp[e]);
+                    *p++ = '\t';
+                    p = uTo(p, nm);
+                    *p++ = '/';
+                    p = uTo(p, dn);
+                    *p++ = '\n';
+                }
+            }
+        }
+        return p;
+    };
     std::vector<std::thread> fmt;
     for (int t = 0; t < nFmt; t++)
         fmt.emplace_back([&] {
@@ -548,7 +729,7 @@ int CommandDistance::run() const
                 {
                     // the slot's previous block must be written out first
                     std::unique_lock<std::mutex> lk(mu);
-                    cv.wait(lk, [&] { return written + nSlots > b; });
+                    cv.wait(lk, [&] { return sl.nextB == b; });
                 }
                 const uint64_t q0 = b * block, nq = std::min(block, nQ - q0);
                 const auto tb0 = std::chrono::steady_clock::now();
@@ -579,15 +760,30 @@ int CommandDistance::run() const
                               [&](uint32_t x, uint32_t y) { return sl.lr[x] < sl.lr[y]; });
                 devUs += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                              std::chrono::steady_clock::now() - tb0).count();
-                // pieces of ~1 M pairs (at least one query row) for the formatter threads
-                const uint64_t per = std::max<uint64_t>(1, (1ULL << 20) / nR);
+                // pieces of ~1 M pairs (mapped: 256 K; at least one query row) for the
+                // formatter threads
+                const uint64_t per = std::max<uint64_t>(1, (mapped ? 1ULL << 18 : 1ULL << 20) / nR);
                 const uint64_t parts = (nq + per - 1) / per;
                 std::lock_guard<std::mutex> lk(mu);
                 sl.b = b;
                 sl.dev = d;
-                sl.text.resize(parts);
                 sl.pending = (int)parts;
                 sl.ready = false;
+                if (mapped) {
+                    sl.psz.assign(parts, 0);
+                    sl.per = per;
+                    sl.sized = false;
+                    for (uint64_t p = 0; p < parts; p++)
+                        tasks.emplace_back([&, q0, nq, per, p, bslot = &sl] {
+                            bslot->psz[p] = listSize(*bslot, q0, p * per, std::min(nq, p * per + per));
+                            std::lock_guard<std::mutex> lk2(mu);
+                            if (--bslot->pending == 0) bslot->sized = true;
+                            cv.notify_all();
+                        });
+                    cv.notify_all();
+                    continue;
+                }
+                sl.text.resize(parts);
                 for (uint64_t p = 0; p < parts; p++) {
                     const uint64_t qa = p * per, qb = std::min(nq, qa + per);
                     tasks.emplace_back([&, q0, qa, qb, p, bslot = &sl] {
@@ -606,19 +802,67 @@ int CommandDistance::run() const
                 cv.notify_all();
             }
         });
-    // stdout a regular file (not O_APPEND): each block goes out by pwritev() at its offset;
-    // otherwise (pipes, terminals) by fwrite.
-    out.flush();
-    fflush(stdout);
-    const int ofd = fileno(stdout);
-    struct stat ost {};
-    const int ofl = fcntl(ofd, F_GETFL);
-    off_t opos = -1;
-    const bool direct = nBlocks && fstat(ofd, &ost) == 0 && S_ISREG(ost.st_mode) && ofl >= 0 &&
-                        !(ofl & O_APPEND) && (opos = lseek(ofd, 0, SEEK_CUR)) >= 0;
     bool writeFailed = false;
+    std::atomic<bool> mapBad{false};
     double waitMs = 0, writeMs = 0;
-    for (uint64_t b = 0; b < nBlocks; b++) {
+    if (mapped) {
+        // blocks in order: once a block's pieces are measured, their offsets follow the text
+        // before them; the file grows (ftruncate: this thread alone sets its size) before the
+        // pieces are written in place by the formatter threads
+        struct stat st {};
+        off_t fsz = fstat(mo.fd, &st) == 0 ? st.st_size : 0;
+        for (uint64_t b = 0; b < nBlocks && !writeFailed; b++) {
+            Slot &sl = slots[b % nSlots];
+            auto t0 = std::chrono::steady_clock::now();
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return sl.b == b && sl.sized; });
+            waitMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            const uint64_t nq = std::min(block, nQ - b * block);
+            const uint64_t parts = sl.psz.size(), per = sl.per;
+            off_t end = opos;
+            for (uint64_t x : sl.psz) end += (off_t)x;
+            if (end > fsz) {
+                const off_t grow = std::max<off_t>(end, fsz + (off_t(256) << 20));
+                if (ftruncate(mo.fd, grow) != 0) { writeFailed = true; break; }
+                fsz = grow;
+            }
+            sl.pending = (int)parts;
+            off_t at = opos;
+            for (uint64_t p = 0; p < parts; p++) {
+                tasks.emplace_back([&, b, nq, per, p, at, bslot = &sl] {
+                    char *dst = mo.at(at);
+                    if (mapPopulate) {
+                        // the piece's page-table entries made writable in one call instead of
+                        // one fault per 4 KiB page as the lines land (MADV_POPULATE_WRITE)
+                        const uintptr_t pg = 4096, a = (uintptr_t)dst & ~(pg - 1);
+                        const uintptr_t z = ((uintptr_t)dst + bslot->psz[p] + pg - 1) & ~(pg - 1);
+                        if (z > a) madvise((void *)a, z - a, 23);
+                    }
+                    char *e = listTo(*bslot, b * block, p * per, std::min(nq, p * per + per), dst);
+                    std::lock_guard<std::mutex> lk2(mu);
+                    if ((uint64_t)(e - dst) != bslot->psz[p]) mapBad = true;   // (a bug)
+                    if (--bslot->pending == 0) {
+                        bslot->nextB += nSlots;
+                        blocksDone++;
+                    }
+                    cv.notify_all();
+                });
+                at += (off_t)sl.psz[p];
+            }
+            opos = end;
+            cv.notify_all();
+        }
+        auto t1 = std::chrono::steady_clock::now();
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return writeFailed || mapBad || blocksDone == nBlocks; });
+        }
+        writeMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        // the allocator stopped before the file is cut to the text's size
+        if (mapBad || (!writeFailed && (!prealloc.trim(opos) || ftruncate(mo.fd, opos) != 0)))
+            writeFailed = true;
+    }
+    for (uint64_t b = 0; b < nBlocks && !mapped; b++) {
         Slot &sl = slots[b % nSlots];
         std::vector<std::string> pieces;
         auto t0 = std::chrono::steady_clock::now();
@@ -643,7 +887,7 @@ int CommandDistance::run() const
             // unmapping ~40 MB strings per piece cost ~0.4 s of page faults and munmap
             std::lock_guard<std::mutex> lk(mu);
             pieces.swap(sl.text);
-            written = b + 1;
+            sl.nextB = b + nSlots;
         }
         cv.notify_all();
     }
@@ -656,7 +900,7 @@ int CommandDistance::run() const
     if (timingOn())
         fprintf(stderr, "[fpmash] writer waiting for blocks: %.1f ms\n[fpmash] writer copying "
                         "pieces out (%s): %.1f ms\n", waitMs,
-                direct ? "pwritev" : "stdout", writeMs);
+                mapped ? "in place, last pieces" : direct ? "pwritev" : "stdout", writeMs);
     if (timingOn())
         fprintf(stderr, "[fpmash] device blocks (compare + fetch + row order, summed): %.1f ms\n",
                 devUs.load() / 1e3);
@@ -676,7 +920,9 @@ int CommandDistance::run() const
                               (void *)sl.ld, (void *)sl.lp, (void *)sl.la})
                 if (ptr) fpm_host_free(device(0), ptr);
         for (auto *rs : sets) fpm_refset_free(rs);
+        if (mapped) munmap(mo.base, mo.len);
     }
+    mo.close();
     out.flush();
     fflush(stdout);
     if (warningCount > 0 && !parameters.reads)

@@ -480,46 +480,64 @@ def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("block_pairs,to_file,devices",
-                         [(None, False, None), ("50000", False, None), (None, True, None),
-                          ("50000", True, None), ("50000", False, "0,0"), ("50000", True, "0,0,0")])
-def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file, devices):
+@pytest.mark.parametrize("block_pairs,to_file,devices,knobs,extra",
+                         [(None, False, None, {}, []), ("50000", False, None, {}, []),
+                          (None, True, None, {}, []), ("50000", True, None, {}, []),
+                          ("50000", False, "0,0", {}, []), ("50000", True, "0,0,0", {}, []),
+                          (None, True, None, {"FPMASH_DIST_MAP": "1"}, []),
+                          ("50000", True, "0,0,0", {"FPMASH_DIST_MAP": "1"}, []),
+                          ("50000", True, None, {"FPMASH_DIST_MAP": "1",
+                                                 "FPMASH_DIST_PREALLOC": "0"}, []),
+                          ("50000", True, None, {"FPMASH_DIST_MAP": "1",
+                                                 "FPMASH_DIST_POPULATE": "0"}, []),
+                          ("50000", True, None, {}, ["-d", "0.2"]),
+                          ("50000", True, None, {"FPMASH_DIST_MAP": "1"}, ["-d", "0.2"])])
+def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file, devices, knobs,
+                                         extra):
     """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
     blocks of 50,000 pairs (FPMASH_DIST_BLOCK_PAIRS) written by the formatter threads in
     order: every line equals the oracle's, in the reference's query-major order.  With
     FPMASH_DEVICE_LIST the blocks go round the contexts (2-3 on the one GPU standing in for
-    a node's devices).  A regular file as stdout takes one pwritev() per block at its
-    offset."""
+    a node's devices).  A regular file as stdout takes one pwritev() per block at its offset,
+    or (FPMASH_DIST_MAP=1) is written in place through a mapping of the file (pieces
+    measured, then formatted at their offsets), with and without its pages allocated ahead
+    or populated per piece, and with a -d filter (no estimate: the file grows as the blocks
+    come)."""
     from fpmash import datagen
     seqs = datagen.family_dna(12, 100, 2000, sub_rate=(0.01, 0.10), seed=23)
     ids = datagen.lyn2vec_ids(len(seqs), seed=23)
     (tmp_path / "all.fa").write_bytes(datagen.fasta_bytes(seqs, ids))
     run(["sketch", "-i", "-o", "all", "all.fa"], cwd=tmp_path)
     env = dict(os.environ)
+    env.update(knobs)
     if block_pairs:
         env["FPMASH_DIST_BLOCK_PAIRS"] = block_pairs
     if devices:
         env["FPMASH_DEVICE_LIST"] = devices
+    cmd = [FPMASH, "dist", "-p", "4"] + extra + ["all.msh", "all.msh"]
     if to_file:
-        # stdout a regular file: each block is pwritev()n at its offset; the file starts with
-        # bytes already written (the offsets start after them)
+        # stdout a regular file; it starts with bytes already written (the offsets start after
+        # them, off a page boundary)
         with open(tmp_path / "out.tsv", "wb") as f:
             f.write(b"head\n")
             f.flush()
-            p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
-                               stdout=f, stderr=subprocess.PIPE, env=env)
+            p = subprocess.run(cmd, cwd=tmp_path, stdout=f, stderr=subprocess.PIPE, env=env)
         text = (tmp_path / "out.tsv").read_bytes()
         assert text.startswith(b"head\n") and text.endswith(b"\n")
         text = text[5:]
     else:
-        p = subprocess.run([FPMASH, "dist", "-p", "4", "all.msh", "all.msh"], cwd=tmp_path,
-                           capture_output=True, env=env)
+        p = subprocess.run(cmd, cwd=tmp_path, capture_output=True, env=env)
         text = p.stdout
     assert p.returncode == 0, p.stderr.decode()
     refs = mshfmt.read_msh(str(tmp_path / "all.msh"))["references"]
     exp = _oracle_dist_lines(oracle, refs, refs, 1000, 21, 4.0 ** 21)
+    assert len(exp) == len(refs) ** 2
+    if extra:
+        # compareSketches (CommandDistance.cpp:421-429): a pair past -d is not written
+        exp = [x for x in exp if float(x.split("\t")[2]) <= 0.2]
+        assert 0 < len(exp) < len(refs) ** 2
     got = text.decode().splitlines()
-    assert len(got) == len(exp) == len(refs) ** 2
+    assert len(got) == len(exp)
     assert got == exp
 
 

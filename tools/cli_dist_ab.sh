@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/cli_dist_ab.sh "VAR=VAL[,VAR=VAL]" ... — same-box A/B of environment settings on the
 # CLI `fpmash dist c2.msh c2.msh > out` (1e8 lines) of bench C2's sketches; REPS interleaved
-# runs per setting; one line per run: wall and the dist phases.
+# runs per setting; one line per run: wall, the dist phases and the output's md5.
 set -o pipefail
 cd "$(dirname "$0")/.."
 OUT=${OUT:-gpurun_out/cli_dist_ab}
@@ -21,7 +21,7 @@ for i in $(seq 1 "$REPS"); do
   for s in base "$@"; do
     envs=(); [ "$s" != base ] && IFS=',' read -ra envs <<< "$s"
     ( cd "$T" && a=$(date +%s%N) && env "${envs[@]}" FPMASH_TIMING=1 timeout -k 10 120 "$EXE" dist -p 16 c2.msh c2.msh > out.tsv \
-        2> "$OLDPWD/$OUT/ph.txt" && b=$(date +%s%N) && echo "$s wall_ms $(( (b - a) / 1000000 )) $(grep -oE '(blocks computed|writer [a-z]+|device blocks|reference sketch|rows packed)[^:]*: [0-9.]*' $OLDPWD/$OUT/ph.txt | tr '\n' ' ')" ) || exit 1
+        2> "$OLDPWD/$OUT/ph.txt" && b=$(date +%s%N) && echo "$s wall_ms $(( (b - a) / 1000000 )) $(grep -oE '(blocks computed|writer [a-z]+|device blocks|reference sketch|rows packed)[^:]*: [0-9.]*' $OLDPWD/$OUT/ph.txt | tr '\n' ' ') md5 $(md5sum < out.tsv | cut -c1-10)" ) || exit 1
     rm -f "$T/out.tsv"
   done
 done
