@@ -913,6 +913,9 @@ __global__ __launch_bounds__(256) void dist_fill_kernel(
 // workgroups put every wave store off the 64-B line grid whenever n_ref is not a multiple of
 // 1024, and left a partial workgroup per row: 4.8 -> 6.5 TB/s at n_ref = 10,000, 4.1 -> 5.8 at
 // 21,876, 5.6 -> 6.6 at 50,000 (tools/micro/fill_real.hip, one MI355X).
+// (A counts-only form with 8 cells and one 16-B store per array per lane, half the lanes: the
+// fill took as long and the rank kernel beside it 2.95 -> 3.4 ms, C4 6.67 -> 6.89 ms, same
+// box, r04.)
 template <typename C>
 __global__ __launch_bounds__(256) void dist_fill_flat_kernel(
     const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
