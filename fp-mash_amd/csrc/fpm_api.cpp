@@ -2348,7 +2348,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 cden = cnum + cap;
             }
             // (Submitted before the probe instead, the fill slows the probe more than it gains:
-            // C4 one GPU 6.66 -> 6.80-6.86 ms, same box, r04.)
+            // C4 one GPU 6.66 -> 6.80-6.86 ms, same box, r04.  Written by the rank kernel's own
+            // row workgroups after their candidates instead of beside them: rank 2.7 -> 3.3 ms
+            // with the fill inside, C4 6.48-6.55 -> 6.69-6.72 ms, same box, r04.)
             // After the host read of the probe's counters the GPU is idle: a fill submitted
             // first would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
