@@ -26,6 +26,9 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k)
     return k;
 }
 
+// (h * 5 as a shift-add on 32-bit halves instead of the two v_mad_u64_u32 it lowers to: 4 fewer
+// quarter-rate multiplies per window, yet C5 31.3 -> 31.6 ms and the C2 sketch unchanged, same
+// box, r04: the tile kernel is not bound by its multiplies.)
 __device__ __forceinline__ void mur_block(uint64_t &h1, uint64_t &h2, uint64_t k1, uint64_t k2)
 {
     k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
