@@ -760,9 +760,11 @@ int CommandDistance::run() const
                               [&](uint32_t x, uint32_t y) { return sl.lr[x] < sl.lr[y]; });
                 devUs += (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
                              std::chrono::steady_clock::now() - tb0).count();
-                // pieces of ~1 M pairs (mapped: 256 K; at least one query row) for the
-                // formatter threads
-                const uint64_t per = std::max<uint64_t>(1, (mapped ? 1ULL << 18 : 1ULL << 20) / nR);
+                // pieces of ~256 K pairs (at least one query row) for the formatter threads:
+                // four per block keep the writer fed (C2 command, same box: writer waiting
+                // 81-107 -> 24-29 ms, wall 0.93-1.07 -> 0.87-0.92 s against pieces of 1 M; 128 K
+                // pieces 0.97-1.06 s)
+                const uint64_t per = std::max<uint64_t>(1, (1ULL << 18) / nR);
                 const uint64_t parts = (nq + per - 1) / per;
                 std::lock_guard<std::mutex> lk(mu);
                 sl.b = b;
