@@ -491,7 +491,9 @@ def _oracle_dist_lines(oracle, refs, qrys, S, k, space, comment=False):
                           ("50000", True, None, {"FPMASH_DIST_MAP": "1",
                                                  "FPMASH_DIST_POPULATE": "0"}, []),
                           ("50000", True, None, {}, ["-d", "0.2"]),
-                          ("50000", True, None, {"FPMASH_DIST_MAP": "1"}, ["-d", "0.2"])])
+                          ("50000", True, None, {"FPMASH_DIST_MAP": "1"}, ["-d", "0.2"]),
+                          ("50000", True, None, {}, ["-C"]),
+                          ("50000", True, None, {"FPMASH_DIST_MAP": "1"}, ["-C"])])
 def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file, devices, knobs,
                                          extra):
     """`dist all.msh all.msh` through the resident reference set: one block, and 30+ query
@@ -501,8 +503,8 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file,
     a node's devices).  A regular file as stdout takes one pwritev() per block at its offset,
     or (FPMASH_DIST_MAP=1) is written in place through a mapping of the file (pieces
     measured, then formatted at their offsets), with and without its pages allocated ahead
-    or populated per piece, and with a -d filter (no estimate: the file grows as the blocks
-    come)."""
+    or populated per piece, with a -d filter (no estimate: the file grows as the blocks
+    come) and with -C (name:comment on both sides of every line)."""
     from fpmash import datagen
     seqs = datagen.family_dna(12, 100, 2000, sub_rate=(0.01, 0.10), seed=23)
     ids = datagen.lyn2vec_ids(len(seqs), seed=23)
@@ -530,9 +532,9 @@ def test_dist_resident_blocks_text_exact(tmp_path, oracle, block_pairs, to_file,
         text = p.stdout
     assert p.returncode == 0, p.stderr.decode()
     refs = mshfmt.read_msh(str(tmp_path / "all.msh"))["references"]
-    exp = _oracle_dist_lines(oracle, refs, refs, 1000, 21, 4.0 ** 21)
+    exp = _oracle_dist_lines(oracle, refs, refs, 1000, 21, 4.0 ** 21, comment="-C" in extra)
     assert len(exp) == len(refs) ** 2
-    if extra:
+    if "-d" in extra:
         # compareSketches (CommandDistance.cpp:421-429): a pair past -d is not written
         exp = [x for x in exp if float(x.split("\t")[2]) <= 0.2]
         assert 0 < len(exp) < len(refs) ** 2
