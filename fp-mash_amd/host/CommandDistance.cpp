@@ -145,7 +145,11 @@ class Prealloc {
     void start(int fd, off_t from, off_t upto)
     {
         struct stat st {};
-        if (fstat(fd, &st) != 0 || (st.st_size < upto && ftruncate(fd, upto) != 0)) return;
+        if (fstat(fd, &st) != 0) return;
+        if (st.st_size < upto) {
+            fatalCutsOutput(fd, st.st_size);    // an error exit leaves the file as it was
+            if (ftruncate(fd, upto) != 0) return;
+        }
         fd_ = fd;
         pos_ = from;
         upto_ = upto;
@@ -894,6 +898,7 @@ int CommandDistance::run() const
         cv.notify_all();
     }
     if (direct && !prealloc.trim(opos)) writeFailed = true;   // pages allocated past the text
+    if (!writeFailed) fatalCutsOutput(-1, 0);                // the text is complete
     if (direct) lseek(ofd, opos, SEEK_SET);   // later output (if any) follows the grid
     if (writeFailed) {
         std::cerr << "ERROR: writing the distance output failed." << std::endl;

@@ -1,6 +1,7 @@
 #include "Device.h"
 #include "Timing.h"
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <iostream>
@@ -89,8 +90,19 @@ void init_ids()
 // meets them: GPU, pinner and formatter threads may still be running, so the process leaves
 // with _exit after flushing, without the atexit teardown that would destroy the contexts
 // those threads are using.
+static std::atomic<int> g_cut_fd{-1};
+static std::atomic<long long> g_cut_at{0};
+void fatalCutsOutput(int fd, off_t at)
+{
+    g_cut_at = (long long)at;
+    g_cut_fd = fd;
+}
+
 void fatalExit()
 {
+    // an output file sized ahead of its text (the dist writer) goes back to what was there
+    const int cfd = g_cut_fd.exchange(-1);
+    if (cfd >= 0 && ftruncate(cfd, (off_t)g_cut_at.load()) != 0) {}
     std::cout.flush();
     std::cerr.flush();
     fflush(stdout);

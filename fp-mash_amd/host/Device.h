@@ -7,6 +7,7 @@
 // commands spread query blocks / sketch groups over device(0..deviceCount()-1), the way
 // the reference spreads them over its -p threads (CommandDistance.cpp:191, Sketch.cpp:253).
 #pragma once
+#include <sys/types.h>
 
 #include "fpmash.h"
 
@@ -20,5 +21,7 @@ void check(int rc, const char *what);
 // exit status 1 after flushing stdout / stderr, without the atexit context teardown (safe from
 // any thread: other threads may still be using the contexts)
 [[noreturn]] void fatalExit();
+// fatalExit first cuts file `fd` back to `at` bytes (an output sized ahead of its text)
+void fatalCutsOutput(int fd, off_t at);
 
 }  // namespace fpmhost

@@ -94,6 +94,23 @@ def test_cli_fails_loudly_without_device():
     assert p.returncode != 0 and b"no CPU fallback" in p.stderr
 
 
+def test_dist_failure_leaves_output_file_as_it_was(tmp_path):
+    """`dist ... > file` sizes the file ahead of its text (pages allocated while the devices
+    come up); an error exit cuts it back to what it held before the command."""
+    import fpmash
+    if fpmash.device_count() > 0:
+        pytest.skip("device present")
+    out = tmp_path / "out.tsv"
+    out.write_bytes(b"head\n")
+    with open(out, "r+b") as f:
+        f.seek(0, 2)
+        p = subprocess.run([FPMASH, "dist", os.path.join(GOLDEN, "genome1.fna.msh"),
+                            os.path.join(GOLDEN, "genome2.fna.msh")], stdout=f,
+                           stderr=subprocess.PIPE)
+    assert p.returncode == 1 and b"no CPU fallback" in p.stderr
+    assert out.read_bytes() == b"head\n"
+
+
 def test_option_errors():
     p = run(["sketch", "-k", "40", "x.fa"], check=False)
     assert p.returncode != 0 and b"must be an integer between 1 and 32" in p.stderr
