@@ -678,6 +678,11 @@ struct fpm_sketch_job {
     MergeDesc *d_sfmerge = nullptr;
     std::vector<uint32_t> sfround_begin;
     std::vector<uint8_t> sfround_small;
+    // class-4 tiles all bounded (C5's genomes): the survivors-only tile kernel, whose
+    // overflowing tiles (d_redo, count d_redo_n) run again through the plain one
+    bool thr4 = false;
+    TileDesc *d_redo = nullptr;
+    uint32_t *d_redo_n = nullptr, *h_redo_n = nullptr;
     // -M pass (allocated on first use)
     uint32_t *d_mult = nullptr;
     unsigned long long *d_first = nullptr;
@@ -692,6 +697,8 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_merge);
     (void)hipFree(j->d_stiles); (void)hipFree(j->d_smerge); (void)hipFree(j->d_srow);
     (void)hipFree(j->d_thr);
+    (void)hipFree(j->d_redo); (void)hipFree(j->d_redo_n);
+    if (j->h_redo_n) (void)hipHostFree(j->h_redo_n);
     (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
@@ -1081,6 +1088,19 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     alloc((void **)&job->d_sel_failed, (sel.size() + 2) * sizeof(uint32_t));
     if (e == hipSuccess && !sel.empty())
         e = hipHostMalloc((void **)&job->h_sel_failed, 2 * sizeof(uint32_t), hipHostMallocDefault);
+    {
+        const uint32_t b4 = class_begin[4], n4 = class_begin[5] - b4;
+        // (C5 one GPU: 31.2 -> 25.8 ms, same box, r04)
+        bool all = n4 > 0;
+        for (uint32_t i = 0; all && i < n4; i++) all = by_class[b4 + i].thr_slot != 0;
+        job->thr4 = all;
+        if (all) {
+            alloc((void **)&job->d_redo, (size_t)n4 * sizeof(TileDesc));
+            alloc((void **)&job->d_redo_n, sizeof(uint32_t));
+            if (e == hipSuccess)
+                e = hipHostMalloc((void **)&job->h_redo_n, sizeof(uint32_t), hipHostMallocDefault);
+        }
+    }
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -1159,13 +1179,28 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     fpm_ctx *ctx = job->ctx;
     if (int rc = set_device(ctx)) return rc;
     hipStream_t st = pick_stream(ctx, stream);
-    auto tiles_pass = [&](const TileDesc *d_t, const uint32_t *begin) -> int {
+    auto tiles_pass = [&](const TileDesc *d_t, const uint32_t *begin, bool main) -> int {
         for (int c = 0; c < kTileClasses; c++) {
             uint32_t b = begin[c], n = begin[c + 1] - b;
             if (!n) continue;
             TimedLaunch tl(ctx, FPM_K_SKETCH, st);
-            HIP_TRY(launch_sketch_tiles(c, job->d_seq, d_t + b, n, job->kp, job->d_thr,
-                                        job->d_rows, job->d_count, st));
+            if (main && c == 4 && job->thr4) {
+                HIP_TRY(hipMemsetAsync(job->d_redo_n, 0, sizeof(uint32_t), st));
+                HIP_TRY(launch_sketch_tiles_thr(job->d_seq, d_t + b, n, job->kp, job->d_thr,
+                                                job->d_rows, job->d_count, job->d_redo,
+                                                job->d_redo_n, st));
+                HIP_TRY(hipMemcpyAsync(job->h_redo_n, job->d_redo_n, sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                const uint32_t nr = *job->h_redo_n;
+                if (nr > n) return fail(FPM_EHIP, "sketch: redo list overflow");
+                if (nr)
+                    HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_redo, nr, job->kp,
+                                                job->d_thr, job->d_rows, job->d_count, st));
+            } else {
+                HIP_TRY(launch_sketch_tiles(c, job->d_seq, d_t + b, n, job->kp, job->d_thr,
+                                            job->d_rows, job->d_count, st));
+            }
             tl.done();
         }
         return FPM_OK;
@@ -1188,7 +1223,7 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         HIP_TRY(hipMemsetAsync(job->d_sel_failed, 0, (job->n_ssel + job->n_sel + 2) * sizeof(uint32_t),
                                st));
     if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
-        if (int rc = tiles_pass(job->d_stiles, job->sclass_begin)) return rc;
+        if (int rc = tiles_pass(job->d_stiles, job->sclass_begin, false)) return rc;
         if (job->n_ssel) {
             for (size_t l = 0; l + 1 < job->ssel_begin.size(); l++) {
                 const uint32_t b = job->ssel_begin[l], n = job->ssel_begin[l + 1] - b;
@@ -1214,7 +1249,7 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     }
     // (the selections of each batch of genomes on a side stream beside the next batch's
     // tiles measured a wash on C5: the 120 KB-LDS selection workgroups take the tiles' CUs)
-    if (int rc = tiles_pass(job->d_tiles, job->class_begin)) return rc;
+    if (int rc = tiles_pass(job->d_tiles, job->class_begin, true)) return rc;
     if (job->n_sel) {
         for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
             const uint32_t b = job->sel_begin[l], n = job->sel_begin[l + 1] - b;

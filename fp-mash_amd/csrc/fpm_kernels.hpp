@@ -50,6 +50,13 @@ struct Counts {
 constexpr int kTileClasses = 6;
 constexpr uint32_t kTileCap[kTileClasses] = {256, 512, 1024, 2048, 4096, 8192};
 
+// class-4 (4096-window) tiles that all carry a bound (thr_slot != 0): survivors only; tiles
+// with more than the kernel holds are appended to d_redo (count *d_redo_n, zeroed by the
+// caller) for launch_sketch_tiles
+hipError_t launch_sketch_tiles_thr(const uint8_t *d_seq, const TileDesc *d_tiles, uint32_t n_tiles,
+                                   const SketchKParams &p, const uint64_t *d_thr, uint64_t *d_out,
+                                   uint32_t *d_count, TileDesc *d_redo, uint32_t *d_redo_n,
+                                   hipStream_t st);
 hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
                                uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_thr,
                                uint64_t *d_out, uint32_t *d_count, hipStream_t st);

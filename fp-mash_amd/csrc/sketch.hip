@@ -247,10 +247,11 @@ __device__ __forceinline__ void tile_stage(const uint8_t *__restrict__ seq, cons
 // bytes are one run of F (and of R, backwards), loaded as ~E/4 + 9 dwords once and cut per
 // window by v_alignbyte with compile-time shifts.  Returns bit e set when kr[e] is the hash
 // of a valid k-mer (kr[e] = ~0 otherwise).
-template <int P, int K>
+// Each valid window's key goes to sink(e, key) (the caller's register array, or the
+// thresholded kernel's survivor slots).
+template <int P, int K, typename Sink>
 __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKParams &p,
-                                              const uint32_t *img, int tid,
-                                              uint64_t (&kr)[TileImg<P>::E])
+                                              const uint32_t *img, int tid, Sink &&sink)
 {
     using I = TileImg<P>;
     constexpr int E = I::E;
@@ -268,10 +269,8 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
     const uint32_t kmask = (k == 32) ? 0xffffffffu : ((1u << k) - 1u);
     constexpr int KW = K ? (K + 3) / 4 : 8;                // dwords per window (max)
     constexpr int W = (E + 3) / 4 + KW + 1;                // dwords covering the E windows
-    uint32_t vbits = 0;                                    // bit e: kr[e] is a valid k-mer hash
+    uint32_t vbits = 0;                                    // bit e: window e is a valid k-mer
     const uint32_t i0 = (uint32_t)tid * E;
-#pragma unroll
-    for (int e = 0; e < E; e++) kr[e] = ~0ULL;
     if (i0 < nk) {
         // validity of the E windows from one 64-bit read of the bit image
         const uint32_t yb = a0 + i0;
@@ -355,7 +354,7 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
 #pragma unroll
                 for (int j = 0; j < 4; j++) wd[j] = (uint64_t)d[2 * j] | ((uint64_t)d[2 * j + 1] << 32);
                 const uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
-                kr[e] = p.use64 ? h : (h & 0xffffffffULL);   // getHash hash.cpp:30-37
+                sink(e, p.use64 ? h : (h & 0xffffffffULL));   // getHash hash.cpp:30-37
             }
             vbits = okbits;
         }
@@ -363,23 +362,39 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
     return vbits;
 }
 
-template <int P, int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+// THR (tiles of long groups, every one with a bound: C5's genomes): the windows' keys above the
+// group's bound are dropped as they are hashed, the others go to kSurv LDS slots of their
+// thread and, past those, to a block-shared overflow area (an LDS atomic), so no thread holds
+// E keys in registers (VGPRs 128 -> 68: 7 waves per SIMD instead of 4) and the sort runs on at
+// most kBlock * kSurv + kSurvShared = 1024 keys (a bound keeps ~3 % of a tile's 4,096: ~0.5
+// per thread).  A tile whose survivors do not fit appends itself to `redo` and writes
+// nothing; the caller runs those tiles again through the plain kernel.  (4 slots per thread
+// and no shared area sent 2.7 % of C5's tiles to the redo pass.)
+constexpr int kSurv = 2;
+constexpr int kSurvShared = 512;
+template <int P, int K, bool THR = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 || THR ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
-    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count,
+    TileDesc *__restrict__ redo, uint32_t *__restrict__ redo_n)
 {
     using I = TileImg<P>;
     constexpr int E = I::E;
+    constexpr int PS = THR ? kBlock * kSurv + kSurvShared : P;   // keys the sort holds at most
+    constexpr int ES = PS / kBlock;                         // their slots per thread
     // the staging images live inside keys[] (dead before the first key is scattered): 20 KB
     // of LDS per P = 2048 tile instead of 25.7 KB, 7 tiles per CU instead of 6
-    __shared__ __attribute__((aligned(16))) uint64_t keys[P];
-    static_assert(I::kBytes <= 8 * P, "staging fits in keys");
+    constexpr int KW = THR ? (PS > (I::kBytes + 7) / 8 ? PS : (I::kBytes + 7) / 8) : P;
+    __shared__ __attribute__((aligned(16))) uint64_t keys[KW];
+    static_assert(I::kBytes <= 8 * KW, "staging fits in keys");
+    __shared__ uint64_t surv[THR ? kBlock * kSurv + kSurvShared : 1];   // shared area last
+    __shared__ uint32_t s_over, s_shared;
     uint32_t *const img = reinterpret_cast<uint32_t *>(keys);
     uint8_t *const alpha = reinterpret_cast<uint8_t *>(img + (I::kFBytes + I::kRBytes) / 4 +
                                                        I::kMaskWords);
     uint8_t *const compl_tab = alpha + 256;
     __shared__ uint32_t scan_tmp[kWaves + 1];
-    __shared__ uint32_t wcnt[E * kWaves + 1];
+    __shared__ uint32_t wcnt[ES * kWaves + 1];
     __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
     __shared__ uint32_t big_bucket, s_cut;
 
@@ -390,6 +405,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
 
     alpha[tid] = p.alphabet[tid];
     compl_tab[tid] = p.complement[tid];
+    if (THR && tid == 0) { s_over = 0; s_shared = 0; }
     __syncthreads();
 
     // ---- stage the tile: uppercase, validity bits, reverse complement
@@ -397,14 +413,55 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
     __syncthreads();
     FPM_PHASE(1);
 
+    uint64_t kr[ES];                                       // key of window tE + e (THR: of
+    uint32_t vbits;                                        // sort slot e * kBlock + tid)
+    uint64_t hmax = p.use64 ? ~0ULL : 0xffffffffULL;
+    if constexpr (THR) {
+        // ---- hash, keeping the keys <= the group's bound in this thread's survivor slots
+        hmax = min(hmax, thr[td.thr_slot - 1]);
+        uint32_t ns = 0;
+        tile_hash<P, K>(td, p, img, tid, [&](int, uint64_t h) {
+            if (h <= hmax) {
+                if (ns < (uint32_t)kSurv) {
+                    surv[tid * kSurv + ns] = h;
+                    ns++;
+                } else {
+                    const uint32_t j = atomicAdd(&s_shared, 1u);
+                    if (j < (uint32_t)kSurvShared) surv[kBlock * kSurv + j] = h;
+                    else s_over = 1;
+                }
+            }
+        });
+        uint32_t total;
+        uint32_t at = block_exscan(ns, scan_tmp, &total);      // (barriers: s_over settled)
+        if (s_over) {                                          // block-uniform
+            if (tid == 0) redo[atomicAdd(redo_n, 1u)] = td;
+            return;
+        }
+        // keys[] aliases the staging images: every window read is done (the scan's barriers);
+        // the shared area's keys follow the threads' own
+        for (uint32_t i = 0; i < ns; i++) keys[at + i] = surv[tid * kSurv + i];
+        const uint32_t nsh = s_shared;
+        for (uint32_t i = tid; i < nsh; i += kBlock) keys[total + i] = surv[kBlock * kSurv + i];
+        total += nsh;
+        __syncthreads();
+        vbits = 0;
+#pragma unroll
+        for (int e = 0; e < ES; e++) {
+            const uint32_t j = (uint32_t)tid + (uint32_t)e * kBlock;
+            kr[e] = ~0ULL;
+            if (j < total) { kr[e] = keys[j]; vbits |= 1u << e; }
+        }
+        __syncthreads();
+    } else {
+#pragma unroll
+    for (int e = 0; e < E; e++) kr[e] = ~0ULL;
     // ---- hash this thread's E consecutive windows
-    uint64_t kr[E];                                        // key of window tE + e
-    uint32_t vbits = tile_hash<P, K>(td, p, img, tid, kr);
+    vbits = tile_hash<P, K>(td, p, img, tid, [&](int e, uint64_t h) { kr[e] = h; });
 
     // ---- long groups: keep only hashes <= the group's bound (the s-th smallest hash of a
     // sample of the group's tiles, an upper bound of the group's own s-th smallest)
     FPM_PHASE(2);
-    uint64_t hmax = p.use64 ? ~0ULL : 0xffffffffULL;
     if (td.thr_slot) {
         hmax = min(hmax, thr[td.thr_slot - 1]);
 #pragma unroll
@@ -434,6 +491,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
             }
         }
     }
+    }
 
     // ---- sort: counting sort by the top log2(P/2) bits of the (uniform) hash values in
     // [0, hmax], then insertion sort inside each bucket (~2 keys per bucket).  A bucket
@@ -451,7 +509,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
     if (tid == 0) { big_bucket = 0; s_cut = NB; }
     __syncthreads();
 #pragma unroll
-    for (int e = 0; e < E; e++)
+    for (int e = 0; e < ES; e++)
         if (vbits >> e & 1) atomicAdd(&bins[(uint32_t)(kr[e] >> bshift)], 1u);
     __syncthreads();
     FPM_PHASE(3);
@@ -496,13 +554,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
         // start = bins[b - 1]; each key keeps its slot for the in-bucket rank below
         uint32_t act = 0;
 #pragma unroll
-        for (int e = 0; e < E; e++) {
+        for (int e = 0; e < ES; e++) {
             const uint32_t bk = (uint32_t)(kr[e] >> bsh);
             act |= ((vbits >> e & 1) && bk >= lo_b && bk < hi_b) ? (1u << e) : 0u;
         }
-        uint32_t slot[E];
+        uint32_t slot[ES];
 #pragma unroll
-        for (int e = 0; e < E; e++)
+        for (int e = 0; e < ES; e++)
             if (act >> e & 1) {
                 slot[e] = atomicAdd(&bins[(uint32_t)(kr[e] >> bsh)], 1u);
                 keys[slot[e]] = kr[e];
@@ -515,7 +573,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
             // insertion sort per bucket was a chain of dependent LDS round trips: 26 % of the
             // tile's time, tools/micro/sketch_phases.hip)
 #pragma unroll
-            for (int e = 0; e < E; e++)
+            for (int e = 0; e < ES; e++)
                 if (act >> e & 1) {
                     const uint32_t b = (uint32_t)(kr[e] >> bsh);
                     const uint32_t s0 = b ? bins[b - 1] : 0u, s1 = bins[b];
@@ -526,7 +584,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
 #pragma unroll
                     for (uint32_t u = 0; u < 8; u++) {
                         const uint32_t t = s0 + u;
-                        const uint64_t y = keys[t < (uint32_t)P ? t : (uint32_t)P - 1];
+                        const uint64_t y = keys[t < (uint32_t)PS ? t : (uint32_t)PS - 1];
                         r += (u < mb) & ((y < kr[e]) | ((y == kr[e]) & (t < slot[e])));
                     }
                     for (uint32_t t = s0 + 8; t < s1; t++) {
@@ -537,14 +595,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
                 }
             __syncthreads();
 #pragma unroll
-            for (int e = 0; e < E; e++)
+            for (int e = 0; e < ES; e++)
                 if (act >> e & 1) keys[slot[e]] = kr[e];
             __syncthreads();
         } else {
-            for (int i = tid; i < P; i += kBlock)
+            for (int i = tid; i < PS; i += kBlock)
                 if ((uint32_t)i >= nvalid) keys[i] = ~0ULL;
             __syncthreads();
-            bitonic_sort<P>(keys);
+            bitonic_sort<PS>(keys);
         }
         FPM_PHASE(6);
 
@@ -553,7 +611,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
         // written by consecutive lanes at consecutive ranks (coalesced); a slot's rank is
         // the distinct count of the (round, wave) pairs before it + its lane prefix.
         uint32_t total;
-        write_distinct<P>(keys, nv, out + (uint64_t)td.out_row * p.s, p.s, wcnt, &total, tid);
+        write_distinct<PS>(keys, nv, out + (uint64_t)td.out_row * p.s, p.s, wcnt, &total, tid);
         // block-uniform: done unless duplicates left fewer than s distinct in the kept buckets
         if (total >= p.s || hi_b >= (uint32_t)NB) {
             if (tid == 0) out_count[td.out_row] = total < p.s ? total : p.s;
@@ -640,10 +698,25 @@ static hipError_t launch_p(const uint8_t *d_seq, const TileDesc *d_tiles, uint32
     if (n_tiles == 0) return hipSuccess;
     if (p.k == 21)      // Mash's default k (sketchParameterSetup, C2/C4/C5)
         hipLaunchKernelGGL((sketch_tiles_kernel<P, 21>), dim3(n_tiles), dim3(kBlock), 0, st,
-                           d_seq, d_tiles, p, d_thr, d_out, d_count);
+                           d_seq, d_tiles, p, d_thr, d_out, d_count, nullptr, nullptr);
     else
         hipLaunchKernelGGL((sketch_tiles_kernel<P, 0>), dim3(n_tiles), dim3(kBlock), 0, st,
-                           d_seq, d_tiles, p, d_thr, d_out, d_count);
+                           d_seq, d_tiles, p, d_thr, d_out, d_count, nullptr, nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_sketch_tiles_thr(const uint8_t *d_seq, const TileDesc *d_tiles, uint32_t n_tiles,
+                                   const SketchKParams &p, const uint64_t *d_thr, uint64_t *d_out,
+                                   uint32_t *d_count, TileDesc *d_redo, uint32_t *d_redo_n,
+                                   hipStream_t st)
+{
+    if (n_tiles == 0) return hipSuccess;
+    if (p.k == 21)
+        hipLaunchKernelGGL((sketch_tiles_kernel<4096, 21, true>), dim3(n_tiles), dim3(kBlock), 0,
+                           st, d_seq, d_tiles, p, d_thr, d_out, d_count, d_redo, d_redo_n);
+    else
+        hipLaunchKernelGGL((sketch_tiles_kernel<4096, 0, true>), dim3(n_tiles), dim3(kBlock), 0,
+                           st, d_seq, d_tiles, p, d_thr, d_out, d_count, d_redo, d_redo_n);
     return hipGetLastError();
 }
 
@@ -712,7 +785,9 @@ __global__ __launch_bounds__(kBlock) void sketch_mult_kernel(
     tile_stage<P>(seq, td, p, img, tid);
     __syncthreads();
     uint64_t kr[E];
-    const uint32_t vbits = tile_hash<P, 0>(td, p, img, tid, kr);
+#pragma unroll
+    for (int e = 0; e < E; e++) kr[e] = ~0ULL;
+    const uint32_t vbits = tile_hash<P, 0>(td, p, img, tid, [&](int e, uint64_t h) { kr[e] = h; });
     const uint64_t *row = rows + (uint64_t)g * p.s;
     const uint64_t hmax = row[ng - 1];
     uint32_t *mrow = mult + (uint64_t)g * p.s;
