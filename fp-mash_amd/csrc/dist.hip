@@ -326,7 +326,9 @@ constexpr int kRankProbeMax = 8;     // sentinels past the end of B = the widest
 constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one more)
                                      // (11: 4 KB less LDS, 8 workgroups per CU instead of 7,
                                      // but larger buckets: 0.346 -> 0.383 ms; 13: 0.345 ->
-                                     // 0.365 ms, same box, r04)
+                                     // 0.365 ms, same box, r04.  A CAP = 1000 instance,
+                                     // 20.3 KB of LDS: 8 workgroups per CU at 12 bits, rank
+                                     // 0.347 either way, same box, r04)
 
 // One chunk of 64 A elements against B (one per lane): j = #{B < a} and the lanes whose a
 // is in B (a wave mask).
