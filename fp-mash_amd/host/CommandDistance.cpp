@@ -188,57 +188,6 @@ class Prealloc {
     std::thread th_;
 };
 
-// A shared writable mapping of the output file (stdout reopened read-write through /proc, since
-// a shell's `>` opens it write-only), reserved up to a bound on the text's size: the formatter
-// threads write every piece straight into its pages at its offset, with no copy and no inode
-// lock between them (a mapping's page faults take none; pwrite serialises on it).
-struct MapOut {
-    int fd = -1;
-    char *base = nullptr;
-    off_t origin = 0;                   // file offset of base (page aligned)
-    size_t len = 0;
-    bool open(int out_fd, off_t at, uint64_t max_bytes)
-    {
-        const long pg = sysconf(_SC_PAGESIZE);
-        if (pg <= 0 || max_bytes > (1ULL << 44)) return false;
-        char path[64];
-        snprintf(path, sizeof path, "/proc/self/fd/%d", out_fd);
-        fd = ::open(path, O_RDWR | O_CLOEXEC);
-        struct stat a {}, b {};
-        if (fd < 0 || fstat(out_fd, &a) != 0 || fstat(fd, &b) != 0 || a.st_ino != b.st_ino ||
-            a.st_dev != b.st_dev) {
-            close();
-            return false;
-        }
-        origin = at / pg * pg;
-        len = (size_t)((at - origin) + max_bytes + pg) / pg * pg;
-        void *m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_NORESERVE, fd, origin);
-        if (m == MAP_FAILED) {
-            close();
-            return false;
-        }
-        base = (char *)m;
-        return true;
-    }
-    char *at(off_t off) const { return base + (off - origin); }
-    void close()
-    {
-        if (fd >= 0) ::close(fd);
-        fd = -1;
-    }
-};
-
-// number of decimal digits of x (no loop: a line's counts are measured per cell)
-inline int decDigits(uint64_t x)
-{
-    return 1 + (x >= 10) + (x >= 100) + (x >= 1000) + (x >= 10000) + (x >= 100000) +
-           (x >= 1000000) + (x >= 10000000) + (x >= 100000000) + (x >= 1000000000) +
-           (x >= 10000000000ULL) + (x >= 100000000000ULL) + (x >= 1000000000000ULL) +
-           (x >= 10000000000000ULL) + (x >= 100000000000000ULL) + (x >= 1000000000000000ULL) +
-           (x >= 10000000000000000ULL) + (x >= 100000000000000000ULL) +
-           (x >= 1000000000000000000ULL) + (x >= 10000000000000000000ULL);
-}
-
 // writes the pieces at `at` in one pwritev() per IOV_MAX pieces (short writes resumed); false on
 // an error.  One call per block: the formatter threads keep formatting instead of queueing on
 // the file's inode lock, which serialises writes to one file anyway (tmpfs on the MI355X box:
@@ -375,9 +324,8 @@ int CommandDistance::run() const
                                                    sketchRef.getMinHashesPerWindow());
     const bool use64 = sketchRef.getUse64();
     const uint32_t hb = use64 ? 8 : 4;
-    // stdout a regular file (not O_APPEND): the text goes in at its offsets, through a mapping
-    // of the file (MapOut, list format) or one pwritev() per block; otherwise (pipes,
-    // terminals) by fwrite.
+    // stdout a regular file (not O_APPEND): the text goes in at its offsets, one pwritev() per
+    // block; otherwise (pipes, terminals) by fwrite.
     out.flush();
     std::cout.flush();
     fflush(stdout);
@@ -395,9 +343,7 @@ int CommandDistance::run() const
     // and most carry "1\t1\t0/<denom>" (pairs sharing hashes write a few bytes more, past the
     // estimate, into pages allocated on the way)
     Prealloc prealloc;
-    MapOut mo;
     const char *pa_env = getenv("FPMASH_DIST_PREALLOC");   // A/B: 0 = pages allocated on the way
-    const char *map_env = getenv("FPMASH_DIST_MAP");        // 1 = in place through MapOut
     if (direct && !table) {
         const off_t at = opos;
         {
@@ -413,21 +359,11 @@ int CommandDistance::run() const
             const uint64_t digits = std::to_string(sketchSize).size();
             const long double est = (long double)nQ * rn + (long double)nR * qn +
                                     (long double)nR * nQ * (7 + digits);
-            // every line is at most its two names + kLineNums
-            const long double most = (long double)nQ * rn + (long double)nR * qn +
-                                     (long double)nR * nQ * kLineNums;
-            // (off by default: with 16 formatter threads writing through the mapping the C2
-            // command measured 0.93-1.34 s against 0.93-1.03 s by pwritev, same box)
-            if (map_env && strcmp(map_env, "1") == 0 && most < (long double)(1ULL << 44))
-                mo.open(ofd, at, (uint64_t)most);
             if (!options.at("distance").active && !options.at("pvalue").active &&
                 !(pa_env && strcmp(pa_env, "0") == 0))
                 prealloc.start(ofd, at, at + (off_t)std::min<long double>(est, (long double)(1ULL << 46)));
         }
     }
-    const bool mapped = mo.base != nullptr;
-    const char *pop_env = getenv("FPMASH_DIST_POPULATE");   // A/B
-    const bool mapPopulate = !(pop_env && strcmp(pop_env, "0") == 0);
     // dense device layout: one row per sketch
     // (zero pages, populated in one call: a value-initialised vector paid a memset and ~20k
     // page faults on one thread for C2's 80 MB)
@@ -468,9 +404,7 @@ int CommandDistance::run() const
     if (const char *bp = getenv("FPMASH_DIST_BLOCK_PAIRS")) blockPairs = std::max(1ULL, strtoull(bp, nullptr, 10));
     const uint64_t block = nR ? std::max<uint64_t>(1, blockPairs / nR) : 1;
     const uint64_t nBlocks = nR ? (nQ + block - 1) / block : 0;
-    // (mapped: a block's slot is free once its pieces are formatted in place; more blocks in
-    // flight keep the formatter threads busy)
-    const int nSlots = mapped ? std::max(4, 2 * nDev + 3) : std::max(2, 2 * nDev + 1);
+    const int nSlots = std::max(2, 2 * nDev + 1);
     const int nFmt = std::max(1, std::min(parameters.parallelism > 1 ? parameters.parallelism
                                           : (int)std::thread::hardware_concurrency(), 64));
     // A block's results in the compact form (fpm_refset_dist_list): u16 numer / denom of
@@ -491,16 +425,12 @@ int CommandDistance::run() const
         int dev = 0;
         uint64_t b = ~0ULL;                 // block held
         std::vector<std::string> text;      // formatted pieces
-        std::vector<uint64_t> psz;          // mapped: each piece's bytes, rows per piece
-        uint64_t per = 1;
-        int pending = 0;                    // pieces still being formatted (mapped: measured,
-        bool ready = false;                 // then written)
-        bool sized = false;
+        int pending = 0;                    // pieces still being formatted
+        bool ready = false;
         uint64_t nextB = 0;                 // the next block this slot may take
     };
     std::vector<Slot> slots(nSlots);
     for (int i = 0; i < nSlots; i++) slots[i].nextB = (uint64_t)i;
-    uint64_t blocksDone = 0;                // mapped: blocks formatted into the file
     std::mutex mu;
     std::condition_variable cv;
     std::deque<std::function<void()>> tasks;
@@ -632,80 +562,6 @@ int CommandDistance::run() const
         }
         dst.swap(o.buf);
     };
-    // mapped: a piece's list lines measured (listSize), then written in place at the piece's
-    // offset (listTo) — the same bytes format() makes
-    auto qtailOf = [&](uint64_t q, std::string &qt) {
-        const Reference &qr = sketchQuery.getReference(q);
-        qt.assign(1, '\t');
-        qt += qr.name;
-        if (comment) { qt.push_back(':'); qt += qr.comment; }
-        qt.push_back('\t');
-    };
-    auto listSize = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb) {
-        uint64_t bytes = 0;
-        std::string qt;
-        char t[kLineNums];
-        for (uint64_t qi = qa; qi < qb; qi++) {
-            qtailOf(q0 + qi, qt);
-            const uint64_t fix = qt.size() + 7;   // "\t<query>\t" + "1\t1\t0/" + '\n'
-            uint32_t cur = sl.rowStart[qi];
-            for (uint64_t j = 0; j < nR; j++) {
-                const uint64_t k = qi * nR + j;
-                const uint32_t nm = cb == 2 ? ((const uint16_t *)sl.nu)[k] : ((const uint32_t *)sl.nu)[k];
-                const uint32_t dn = cb == 2 ? ((const uint16_t *)sl.de)[k] : ((const uint32_t *)sl.de)[k];
-                if (nm == 0) {
-                    if (dn == 0 ? passEmpty : passNone) bytes += refTag[j].size() + fix + decDigits(dn);
-                } else {
-                    const uint32_t e = sl.byRow[cur++];
-                    if (!sl.la[e]) continue;
-                    char *p = numTo(t, sl.ld[e]);
-                    *p++ = '\t';
-                    p = numTo(p, sl.lp[e]);
-                    bytes += refTag[j].size() + qt.size() + (uint64_t)(p - t) + 3 + decDigits(nm) + decDigits(dn);
-                }
-            }
-        }
-        return bytes;
-    };
-    auto listTo = [&](const Slot &sl, uint64_t q0, uint64_t qa, uint64_t qb, char *p) {
-        std::string qt;
-        for (uint64_t qi = qa; qi < qb; qi++) {
-            qtailOf(q0 + qi, qt);
-            uint32_t cur = sl.rowStart[qi];
-            for (uint64_t j = 0; j < nR; j++) {
-                const uint64_t k = qi * nR + j;
-                const uint32_t nm = cb == 2 ? ((const uint16_t *)sl.nu)[k] : ((const uint32_t *)sl.nu)[k];
-                const uint32_t dn = cb == 2 ? ((const uint16_t *)sl.de)[k] : ((const uint32_t *)sl.de)[k];
-                const std::string &tag = refTag[j];
-                if (nm == 0) {
-                    if (!(dn == 0 ? passEmpty : passNone)) continue;
-                    memcpy(p, tag.data(), tag.size());
-                    p += tag.size();
-                    memcpy(p, qt.data(), qt.size());
-                    p += qt.size();
-                    memcpy(p, dn == 0 ? "0\t1\t0/" : "1\t1\t0/", 6);
-                    p = uTo(p + 6, dn);
-                    *p++ = '\n';
-                } else {
-                    const uint32_t e = sl.byRow[cur++];
-                    if (!sl.la[e]) continue;
-                    memcpy(p, tag.data(), tag.size());
-                    p += tag.size();
-                    memcpy(p, qt.data(), qt.size());
-                    p += qt.size();
-                    p = numTo(p, sl.ld[e]);   // (snprintf's NUL lands where the tab goes)
-                    *p++ = '\t';
-                    p = numTo(p, sl.lp[e]);
-                    *p++ = '\t';
-                    p = uTo(p, nm);
-                    *p++ = '/';
-                    p = uTo(p, dn);
-                    *p++ = '\n';
-                }
-            }
-        }
-        return p;
-    };
     std::vector<std::thread> fmt;
     for (int t = 0; t < nFmt; t++)
         fmt.emplace_back([&] {
@@ -775,20 +631,6 @@ int CommandDistance::run() const
                 sl.dev = d;
                 sl.pending = (int)parts;
                 sl.ready = false;
-                if (mapped) {
-                    sl.psz.assign(parts, 0);
-                    sl.per = per;
-                    sl.sized = false;
-                    for (uint64_t p = 0; p < parts; p++)
-                        tasks.emplace_back([&, q0, nq, per, p, bslot = &sl] {
-                            bslot->psz[p] = listSize(*bslot, q0, p * per, std::min(nq, p * per + per));
-                            std::lock_guard<std::mutex> lk2(mu);
-                            if (--bslot->pending == 0) bslot->sized = true;
-                            cv.notify_all();
-                        });
-                    cv.notify_all();
-                    continue;
-                }
                 sl.text.resize(parts);
                 for (uint64_t p = 0; p < parts; p++) {
                     const uint64_t qa = p * per, qb = std::min(nq, qa + per);
@@ -809,66 +651,8 @@ int CommandDistance::run() const
             }
         });
     bool writeFailed = false;
-    std::atomic<bool> mapBad{false};
     double waitMs = 0, writeMs = 0;
-    if (mapped) {
-        // blocks in order: once a block's pieces are measured, their offsets follow the text
-        // before them; the file grows (ftruncate: this thread alone sets its size) before the
-        // pieces are written in place by the formatter threads
-        struct stat st {};
-        off_t fsz = fstat(mo.fd, &st) == 0 ? st.st_size : 0;
-        for (uint64_t b = 0; b < nBlocks && !writeFailed; b++) {
-            Slot &sl = slots[b % nSlots];
-            auto t0 = std::chrono::steady_clock::now();
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return sl.b == b && sl.sized; });
-            waitMs += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-            const uint64_t nq = std::min(block, nQ - b * block);
-            const uint64_t parts = sl.psz.size(), per = sl.per;
-            off_t end = opos;
-            for (uint64_t x : sl.psz) end += (off_t)x;
-            if (end > fsz) {
-                const off_t grow = std::max<off_t>(end, fsz + (off_t(256) << 20));
-                if (ftruncate(mo.fd, grow) != 0) { writeFailed = true; break; }
-                fsz = grow;
-            }
-            sl.pending = (int)parts;
-            off_t at = opos;
-            for (uint64_t p = 0; p < parts; p++) {
-                tasks.emplace_back([&, b, nq, per, p, at, bslot = &sl] {
-                    char *dst = mo.at(at);
-                    if (mapPopulate) {
-                        // the piece's page-table entries made writable in one call instead of
-                        // one fault per 4 KiB page as the lines land (MADV_POPULATE_WRITE)
-                        const uintptr_t pg = 4096, a = (uintptr_t)dst & ~(pg - 1);
-                        const uintptr_t z = ((uintptr_t)dst + bslot->psz[p] + pg - 1) & ~(pg - 1);
-                        if (z > a) madvise((void *)a, z - a, 23);
-                    }
-                    char *e = listTo(*bslot, b * block, p * per, std::min(nq, p * per + per), dst);
-                    std::lock_guard<std::mutex> lk2(mu);
-                    if ((uint64_t)(e - dst) != bslot->psz[p]) mapBad = true;   // (a bug)
-                    if (--bslot->pending == 0) {
-                        bslot->nextB += nSlots;
-                        blocksDone++;
-                    }
-                    cv.notify_all();
-                });
-                at += (off_t)sl.psz[p];
-            }
-            opos = end;
-            cv.notify_all();
-        }
-        auto t1 = std::chrono::steady_clock::now();
-        {
-            std::unique_lock<std::mutex> lk(mu);
-            cv.wait(lk, [&] { return writeFailed || mapBad || blocksDone == nBlocks; });
-        }
-        writeMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
-        // the allocator stopped before the file is cut to the text's size
-        if (mapBad || (!writeFailed && (!prealloc.trim(opos) || ftruncate(mo.fd, opos) != 0)))
-            writeFailed = true;
-    }
-    for (uint64_t b = 0; b < nBlocks && !mapped; b++) {
+    for (uint64_t b = 0; b < nBlocks; b++) {
         Slot &sl = slots[b % nSlots];
         std::vector<std::string> pieces;
         auto t0 = std::chrono::steady_clock::now();
@@ -907,7 +691,7 @@ int CommandDistance::run() const
     if (timingOn())
         fprintf(stderr, "[fpmash] writer waiting for blocks: %.1f ms\n[fpmash] writer copying "
                         "pieces out (%s): %.1f ms\n", waitMs,
-                mapped ? "in place, last pieces" : direct ? "pwritev" : "stdout", writeMs);
+                direct ? "pwritev" : "stdout", writeMs);
     if (timingOn())
         fprintf(stderr, "[fpmash] device blocks (compare + fetch + row order, summed): %.1f ms\n",
                 devUs.load() / 1e3);
@@ -927,9 +711,7 @@ int CommandDistance::run() const
                               (void *)sl.ld, (void *)sl.lp, (void *)sl.la})
                 if (ptr) fpm_host_free(device(0), ptr);
         for (auto *rs : sets) fpm_refset_free(rs);
-        if (mapped) munmap(mo.base, mo.len);
     }
-    mo.close();
     out.flush();
     fflush(stdout);
     if (warningCount > 0 && !parameters.reads)

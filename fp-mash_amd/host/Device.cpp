@@ -145,8 +145,7 @@ void warmDevices()
         });
         const auto t2 = clk::now();
         // the staging ring and the first DMA, before the first upload needs them
-        static const bool noWarm = getenv("FPM_NO_WARM") != nullptr;   // A/B
-        if (g_ctx[0] && !noWarm) (void)fpm_ctx_warm(g_ctx[0]);
+        if (g_ctx[0]) (void)fpm_ctx_warm(g_ctx[0]);
         const auto t3 = clk::now();
         auto ms = [](clk::time_point a, clk::time_point b) {
             return std::chrono::duration<double, std::milli>(b - a).count();

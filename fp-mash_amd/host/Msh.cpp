@@ -115,8 +115,7 @@ public:
     // fallocate, the file mapped, and the blocks copied in by up to 16 threads over disjoint
     // byte ranges (page faults of a shared mapping run in parallel; pwrite calls on one file
     // serialise on its inode lock: 80 MB of a C2 .msh took ~40 ms that way on /dev/shm).
-    // Small messages, file systems without fallocate, and FPMASH_MSH_WRITE=pwrite (A/B) take
-    // the pwrite path; a failed reservation never leaves a mapping that could fault past the
+    // Small messages and file systems without fallocate take the pwrite path; a failed reservation never leaves a mapping that could fault past the
     // end of the device.
     bool write(const std::string &path) const
     {
@@ -129,10 +128,6 @@ public:
         if (fd < 0) return false;
         const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
         const unsigned nt = total < (8u << 20) ? 1u : std::min(16u, hw);
-        static const bool usePwrite = [] {
-            const char *v = getenv("FPMASH_MSH_WRITE");
-            return v && strcmp(v, "pwrite") == 0;
-        }();
         // blocks overlapping [a, e): fn(block index, first byte, end byte)
         auto forRange = [&](uint64_t a, uint64_t e, auto fn) {
             size_t i = std::upper_bound(at.begin(), at.end(), a) - at.begin() - 1;
@@ -153,7 +148,7 @@ public:
             return good.load();
         };
         bool ok = false, done = false;
-        if (nt > 1 && !usePwrite && fallocate(fd, 0, 0, (off_t)total) == 0) {
+        if (nt > 1 && fallocate(fd, 0, 0, (off_t)total) == 0) {
             void *m = mmap(nullptr, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
             if (m != MAP_FAILED) {
                 char *dst = static_cast<char *>(m);

@@ -16,6 +16,7 @@
 #include <cctype>
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <thread>
 #include <unistd.h>
 #include <vector>
@@ -71,7 +72,11 @@ std::vector<std::pair<size_t, size_t>> bgzfMembers(const unsigned char *p, size_
             }
             x += 4 + slen;
         }
-        if (!bsize || at + bsize > n) break;
+        // a member is at least its 18-byte header + an empty deflate block + the 8-byte trailer,
+        // and inflates to at most 64 KiB (SAM spec 4.1): anything else is no BGZF member
+        if (bsize < 28 || at + bsize > n) break;
+        const unsigned char *t = p + at + bsize - 4;
+        if ((t[0] | (size_t)t[1] << 8 | (size_t)t[2] << 16 | (size_t)t[3] << 24) > 65536) break;
         m.push_back({at, bsize});
         at += bsize;
     }
@@ -110,6 +115,7 @@ bool gunzipImage(const unsigned char *p, size_t n, std::string &image)
 {
     const Deflate &D = deflate();
     const auto mem = bgzfMembers(p, n);
+    try {
     if (mem.size() >= 8) {
         // every BGZF member inflates to at most 64 KiB: slots of ISIZE (its last 4 bytes)
         std::vector<size_t> off(mem.size() + 1, 0);
@@ -149,11 +155,19 @@ bool gunzipImage(const unsigned char *p, size_t n, std::string &image)
         size_t hint = 0;
         if (at == 0 && n >= 4)
             hint = p[n - 4] | (size_t)p[n - 3] << 8 | (size_t)p[n - 2] << 16 | (size_t)p[n - 1] << 24;
+        // (a corrupt ISIZE must not size the output: deflate expands at most ~1032:1)
+        hint = std::min(hint, n * 1032);
         if (!gunzipMember(dec, p + at, n - at, image, hint + 1, &used)) { ok = false; break; }
         at += used;
     }
     D.free_(dec);
     return ok;
+    } catch (const std::bad_alloc &) {
+        // (the caller falls back to zlib's gzread, which grows the image as it inflates)
+        image.clear();
+        image.shrink_to_fit();
+        return false;
+    }
 }
 
 }  // namespace

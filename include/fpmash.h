@@ -353,8 +353,6 @@ int fpm_refset_dist_mirror_dev(fpm_refset *rs, const void *d_qry, const uint32_t
                                void *d_numer, void *d_denom, double *d_dist, double *d_pvalue,
                                uint8_t *d_pass, void *m_numer, void *m_denom, double *m_dist,
                                double *m_pvalue, uint8_t *m_pass, void *stream);
-/* Rebuild the set's bucket index from its (device, borrowed) rows in place, e.g. after the
- * rows were rewritten by a new sketch run; no reallocation when the geometry is unchanged. */
 /* The compact output (fpm_dist_list_dev) against a resident set, and with its transposed grid
  * (m_numer / m_denom cell (r, q) at r * n_qry + q, m_list its own list of cells). */
 int fpm_refset_dist_list_dev(fpm_refset *rs, const void *d_qry, const uint32_t *d_qry_len,
@@ -369,6 +367,8 @@ int fpm_refset_dist_mirror_list_dev(fpm_refset *rs, const void *d_qry, const uin
                                     uint16_t *d_numer, uint16_t *d_denom,
                                     const fpm_cell_list *list, uint16_t *m_numer,
                                     uint16_t *m_denom, const fpm_cell_list *m_list, void *stream);
+/* Rebuild the set's bucket index from its (device, borrowed) rows in place, e.g. after the
+ * rows were rewritten by a new sketch run; no reallocation when the geometry is unchanged. */
 int fpm_refset_reindex(fpm_refset *rs, void *stream);
 int fpm_refset_dist(fpm_refset *rs, const void *qry, const uint32_t *qry_len,
                     const uint64_t *qry_length, uint64_t qry_stride, uint32_t n_qry,
