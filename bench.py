@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
+    ap.add_argument("--no-gather-check", action="store_true",
+                    help="at N = 1: skip the C4 gathered-path check (one-rank RCCL group)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 RefSeq-scale sketch leg")
     ap.add_argument("--no-cli", action="store_true",
                     help="skip the end-to-end CLI leg (fpmash sketch + dist, 1e8 text lines)")
@@ -160,13 +162,23 @@ class Group:
     """Barrier + max over ranks.  gloo (host-side) keeps the timing collective off
     the device; the data path itself has no collective (independent batches)."""
 
-    def __init__(self, ws, local=0, nccl=False):
+    def __init__(self, ws, local=0, nccl=False, single_rank_nccl=False):
+        """single_rank_nccl: at ws = 1, a one-rank process group with its RCCL group anyway
+        (the C4 leg's gathered data path run once on one GPU, c4_gather_check)"""
         self.ws = ws
         self.nccl = None
-        if ws > 1:
+        if ws > 1 or (nccl and single_rank_nccl):
             import datetime
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if ws == 1 and "MASTER_PORT" not in os.environ:
+                import socket
+                so = socket.socket()
+                so.bind(("127.0.0.1", 0))
+                os.environ["MASTER_PORT"] = str(so.getsockname()[1])
+                so.close()
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", str(ws))
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
             self.dist = dist
             if nccl:
@@ -419,10 +431,11 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4, c5=None, cli=None, split=None):
+def parity_summary(c2, c3, c4, c5=None, cli=None, split=None, c4_gather=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
              "c4": c4.get("parity") if c4 else None,
+             "c4_gather": c4_gather.get("parity") if c4_gather else None,
              "c5": c5.get("parity") if c5 else None,
              "split": split.get("parity") if split else None,
              "cli": cli.get("parity") if cli else None}
@@ -582,7 +595,7 @@ def compact_out(ctx, cells):
 
 
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
-           steps=3, warmup=1, parity=True):
+           steps=3, warmup=1, parity=True, vblocks=1):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
     the ranks (strong scaling).  A timed step is the whole job on every rank:
       1. sketch its contiguous block of families (each family generated from its own seed,
@@ -598,7 +611,11 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
          every cell + distance / FP64 p-value / pass of the cells with numer > 0 (the indexes
          are rebuilt inside the step).
     With one rank there is no gather and the whole grid is the library's symmetric self
-    path (fpm_dist_list_dev with the queries = the references)."""
+    path (fpm_dist_list_dev with the queries = the references).
+    vblocks > 1 (one rank, the check of the gathered data path on one GPU): the rank's rows go
+    through the all-gather anyway (RCCL with a one-rank nccl group), the set is cut into
+    vblocks blocks, and the rank runs every virtual rank's block-pair jobs (pair_block_jobs) on
+    the gathered rows: refsets and the self / mirror list calls on torch-allocated pointers."""
     import ctypes as C
     from fpmash.shard import all_gather_rows, pair_block_jobs, shard_range
     fams = n // members
@@ -615,8 +632,15 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     L = fpmash.lib()
     st = ctx.stream
     g = {}
-    jobs = pair_block_jobs(bounds, rank)
-    if ws > 1:
+    gathered = ws > 1 or vblocks > 1
+    if vblocks > 1:
+        if ws != 1:
+            raise ValueError("vblocks > 1 stands in for more ranks on one rank only")
+        vb = [tuple(x * members for x in shard_range(fams, vblocks, r)) for r in range(vblocks)]
+        jobs = [j for vr in range(vblocks) for j in pair_block_jobs(vb, vr)]
+    else:
+        jobs = pair_block_jobs(bounds, rank)
+    if gathered:
         import torch
         # RCCL gathers device tensors over xGMI; without an nccl group (the 2-rank GPU test
         # on one card) the same rows go through gloo on host tensors and back to the device.
@@ -652,7 +676,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     # multi-rank phases: the sketch, the all-gather window (this rank's own block against
     # itself runs beside it: that job reads only local rows), the jobs after the gather
     phase = ({"sketch": 0.0, "gather_beside_self_job": 0.0, "dist_after_gather": 0.0}
-             if ws > 1 else {"sketch": 0.0, "gather": 0.0, "dist": 0.0})
+             if gathered else {"sketch": 0.0, "gather": 0.0, "dist": 0.0})
 
     def gather_start():
         """The rank's rows and counts into the collective's buffers, then the all-gathers
@@ -685,9 +709,14 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
 
     own = (lo, hi)
 
+    def local_job(j):
+        """the own block against itself: its rows as the sketch left them (no gathered copy
+        needed, so it runs beside the gather)"""
+        return j["kind"] == "self" and j["ref"] == own
+
     def job_query(j):
         (ql, qh) = j["qry"]
-        if j["kind"] == "self":
+        if local_job(j):
             # the own block's rows as the sketch left them (the refset's own pointers: the
             # library's symmetric self path)
             return (d_rows, d_cnt, Ln + ql * 8, stride, qh - ql)
@@ -700,7 +729,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             if which == "all" or (which == "self") == (key == own):
                 fpmash._check(L.fpm_refset_reindex(rs, st))
         for j, o in zip(jobs, outs):
-            if which != "all" and (which == "self") != (j["kind"] == "self"):
+            if which != "all" and (which == "self") != local_job(j):
                 continue
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
             rs = refsets[(rl, rh)]
@@ -721,14 +750,14 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         if timed:
             ctx.synchronize()
         t1 = time.perf_counter()
-        if ws > 1:
+        if gathered:
             finish = gather_start()
             dist_share("self")          # beside the gather: local rows only
             finish()
             if timed:
                 ctx.synchronize()
         t2 = time.perf_counter()
-        if ws > 1:
+        if gathered:
             dist_share("rest")
         else:
             p_ = outs[0]["p"]
@@ -742,7 +771,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             phase[ks[0]] += t1 - t0
             phase[ks[1]] += t2 - t1
             phase[ks[2]] += t3 - t2
-    if ws > 1:
+    if gathered:
         # the indexes live as long as the leg (rebuilt in every step by fpm_refset_reindex)
         job.run(st)
         ctx.synchronize()
@@ -800,7 +829,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         # transposes) x all their references
         from oracle import oracle as O
         t_c = time.perf_counter()
-        if ws > 1:
+        if gathered:
             rows_h = g["rows"].cpu().numpy().view(np.uint64)
             cnt_h = g["cnt"].cpu().numpy()[:, 0]
         else:
@@ -829,7 +858,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         for bl in o.values():
             for b in bl:
                 b.free()
-    if ws == 1:
+    if not gathered:
         d_len.free()
     for key in ("d_rows", "d_cnt", "d_len"):
         if key in g:
@@ -847,7 +876,9 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
             "kernels_rank0": kt,
-            "collective": "all_gather (nccl = RCCL)" if ws > 1 else None,
+            "collective": (None if not gathered else "all_gather (nccl = RCCL)" if on_dev
+                           else "all_gather (gloo, host tensors)"),
+            "virtual_blocks": vblocks,
             "jobs_rank0": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                            for j in jobs], "cells_rank0": cells,
             "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
@@ -1270,7 +1301,8 @@ def compact_line(d, detail_path=None):
         "value": cpu.get("value"), "unit": cpu.get("unit"), "cores": cpu.get("cores"),
         "kind": cpu.get("kind"), "sample": cpu.get("sample"), "cpu_model": cpu.get("cpu_model")}
     line["parity"] = {"c2": _ok(par.get("c2")), "c3_fp": _ok(par.get("c3_fp")),
-                      "c4": _ok(par.get("c4")), "c5": _ok(par.get("c5")),
+                      "c4": _ok(par.get("c4")), "c4_gather": _ok(par.get("c4_gather")),
+                      "c5": _ok(par.get("c5")),
                       "split": _ok(par.get("split")), "cli": _ok(par.get("cli")),
                       "all_ok": par.get("all_ok")}
     c3, c4, c5 = d.get("c3_fp"), d.get("c4_dist"), d.get("c5_sketch")
@@ -1313,7 +1345,8 @@ def main():
     # first, both see the device and device pointers pass between them (fpm_memcpy_d2d of a
     # torch tensor checked on the MI355X box, r04)
     grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split) and
-                not os.environ.get("FPMASH_BENCH_ONE_DEVICE"))
+                not os.environ.get("FPMASH_BENCH_ONE_DEVICE"),
+                single_rank_nccl=not (args.no_c4 or args.no_gather_check))
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
     n = len(seqs)
@@ -1503,6 +1536,13 @@ def main():
         cells.free()
         c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
                     parity=not args.no_parity)
+    c4g = None
+    if ws == 1 and grp.nccl is not None:
+        # the multi-GPU data path once on this GPU, outside every timed number: rows
+        # all-gathered by a one-rank RCCL group into torch tensors, three virtual blocks'
+        # self / mirror jobs on those pointers, every grid sampled against the oracle
+        c4g = c4_leg(ctx, grp, ws, rank, local, n=6000, s=args.s, k=args.k, steps=1, warmup=1,
+                     parity="all" if not args.no_parity else False, vblocks=3)
 
     c5 = None
     if not args.no_c5:
@@ -1564,6 +1604,7 @@ def main():
             "fp_text": fp_leg,
             "c3_fp": c3,
             "c4_dist": c4,
+            "c4_gather_check": c4g,
             "c5_sketch": c5,
             "split_sketch": split,
             "cli": cli,
@@ -1571,7 +1612,7 @@ def main():
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4, c5, cli, split),
+            "parity": parity_summary(c2par, c3, c4, c5, cli, split, c4g),
         }
         path = write_detail(detail, args.detail)
         print(json.dumps(compact_line(detail, path)))

@@ -682,7 +682,8 @@ struct fpm_sketch_job {
     // overflowing tiles (d_redo, count d_redo_n) run again through the plain one
     bool thr4 = false;
     TileDesc *d_redo = nullptr;
-    uint32_t *d_redo_n = nullptr, *h_redo_n = nullptr;
+    uint32_t *d_redo_n = nullptr;
+    uint32_t n4 = 0;                 // class-4 tiles (the redo list's capacity)
     // -M pass (allocated on first use)
     uint32_t *d_mult = nullptr;
     unsigned long long *d_first = nullptr;
@@ -698,7 +699,6 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_stiles); (void)hipFree(j->d_smerge); (void)hipFree(j->d_srow);
     (void)hipFree(j->d_thr);
     (void)hipFree(j->d_redo); (void)hipFree(j->d_redo_n);
-    if (j->h_redo_n) (void)hipHostFree(j->h_redo_n);
     (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
@@ -1089,16 +1089,27 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     if (e == hipSuccess && !sel.empty())
         e = hipHostMalloc((void **)&job->h_sel_failed, 2 * sizeof(uint32_t), hipHostMallocDefault);
     {
+        // the survivors-only tile kernel for the class-4 tiles when every one carries its
+        // group's bound and that bound leaves few survivors per tile: a group's main pass keeps
+        // about kSampleEvery * s of its hashes (the sample's s-th smallest bounds them), so a
+        // tile keeps ~kSampleEvery * s / (the group's tiles); est (2x margin + 64, above) must
+        // stay within half of what one tile holds, or most tiles would be hashed twice (their
+        // survivors overflow and the plain kernel redoes them).  (C5 one GPU: 31.2 -> 25.8 ms,
+        // same box, r04; C5 tiles: est 326 of 1,024)
         const uint32_t b4 = class_begin[4], n4 = class_begin[5] - b4;
-        // (C5 one GPU: 31.2 -> 25.8 ms, same box, r04)
+        std::vector<uint64_t> slot_est(srow.size() + 1, ~0ULL);
+        for (uint32_t g = 0; g < n_groups; g++)
+            if (slot_of[g]) slot_est[slot_of[g]] = 2ULL * kSampleEvery * s / ntile_of[g] + 64;
         bool all = n4 > 0;
-        for (uint32_t i = 0; all && i < n4; i++) all = by_class[b4 + i].thr_slot != 0;
+        for (uint32_t i = 0; all && i < n4; i++) {
+            const uint32_t sl = by_class[b4 + i].thr_slot;
+            all = sl != 0 && slot_est[sl] <= kThrTileKeys / 2;
+        }
         job->thr4 = all;
+        job->n4 = n4;
         if (all) {
             alloc((void **)&job->d_redo, (size_t)n4 * sizeof(TileDesc));
             alloc((void **)&job->d_redo_n, sizeof(uint32_t));
-            if (e == hipSuccess)
-                e = hipHostMalloc((void **)&job->h_redo_n, sizeof(uint32_t), hipHostMallocDefault);
         }
     }
     if (e != hipSuccess) {
@@ -1189,14 +1200,10 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
                 HIP_TRY(launch_sketch_tiles_thr(job->d_seq, d_t + b, n, job->kp, job->d_thr,
                                                 job->d_rows, job->d_count, job->d_redo,
                                                 job->d_redo_n, st));
-                HIP_TRY(hipMemcpyAsync(job->h_redo_n, job->d_redo_n, sizeof(uint32_t),
-                                       hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
-                const uint32_t nr = *job->h_redo_n;
-                if (nr > n) return fail(FPM_EHIP, "sketch: redo list overflow");
-                if (nr)
-                    HIP_TRY(launch_sketch_tiles(c, job->d_seq, job->d_redo, nr, job->kp,
-                                                job->d_thr, job->d_rows, job->d_count, st));
+                // the tiles whose survivors did not fit, again through the plain kernel; the
+                // count stays on the device (the list holds at most n: one entry per tile)
+                HIP_TRY(launch_sketch_redo(job->d_seq, job->d_redo, job->d_redo_n, n, job->kp,
+                                           job->d_thr, job->d_rows, job->d_count, st));
             } else {
                 HIP_TRY(launch_sketch_tiles(c, job->d_seq, d_t + b, n, job->kp, job->d_thr,
                                             job->d_rows, job->d_count, st));
@@ -1352,6 +1359,19 @@ int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_ti
     if (seq_bytes) *seq_bytes = job->seq_bytes;
     if (n_tiles) *n_tiles = job->n_tiles;
     if (n_kmers) *n_kmers = job->n_kmers;
+    return FPM_OK;
+}
+
+int fpm_sketch_job_redo_tiles(fpm_sketch_job *job, int32_t *n_redo)
+{
+    if (!job || !n_redo) return fail(FPM_EINVAL, "null argument");
+    *n_redo = -1;
+    if (!job->thr4 || !job->d_redo_n) return FPM_OK;
+    if (int rc = set_device(job->ctx)) return rc;
+    uint32_t v = 0;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&v, job->d_redo_n, sizeof v, hipMemcpyDeviceToHost));
+    *n_redo = (int32_t)v;
     return FPM_OK;
 }
 

@@ -57,6 +57,13 @@ hipError_t launch_sketch_tiles_thr(const uint8_t *d_seq, const TileDesc *d_tiles
                                    const SketchKParams &p, const uint64_t *d_thr, uint64_t *d_out,
                                    uint32_t *d_count, TileDesc *d_redo, uint32_t *d_redo_n,
                                    hipStream_t st);
+// the tiles a launch_sketch_tiles_thr pass listed (d_redo[0 .. *d_redo_n), at most max_tiles),
+// through the plain P = 4096 kernel, the count read on the device
+hipError_t launch_sketch_redo(const uint8_t *d_seq, const TileDesc *d_redo, const uint32_t *d_redo_n,
+                              uint32_t max_tiles, const SketchKParams &p, const uint64_t *d_thr,
+                              uint64_t *d_out, uint32_t *d_count, hipStream_t st);
+// survivors one THR tile holds (kBlock * kSurv + kSurvShared, sketch.hip)
+constexpr uint32_t kThrTileKeys = 1024;
 hipError_t launch_sketch_tiles(int cls, const uint8_t *d_seq, const TileDesc *d_tiles,
                                uint32_t n_tiles, const SketchKParams &p, const uint64_t *d_thr,
                                uint64_t *d_out, uint32_t *d_count, hipStream_t st);

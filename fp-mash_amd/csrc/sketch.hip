@@ -372,9 +372,12 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
 // and no shared area sent 2.7 % of C5's tiles to the redo pass.)
 constexpr int kSurv = 2;
 constexpr int kSurvShared = 512;
-template <int P, int K, bool THR = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 || THR ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
-    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
+static_assert(kBlock * kSurv + kSurvShared == (int)kThrTileKeys, "fpm_api.cpp sizes thr4 by it");
+// One tile: the body of sketch_tiles_kernel (one workgroup per tile) and of
+// sketch_redo_kernel (the tiles a THR pass listed, taken in turn by a fixed grid).
+template <int P, int K, bool THR>
+__device__ __forceinline__ void sketch_tile(
+    const uint8_t *__restrict__ seq, const TileDesc td, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count,
     TileDesc *__restrict__ redo, uint32_t *__restrict__ redo_n)
 {
@@ -400,7 +403,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
 
     FPM_PHASE_DECL;
     FPM_PHASE(0);
-    const TileDesc td = tiles[blockIdx.x];
     const int tid = threadIdx.x;
 
     alpha[tid] = p.alphabet[tid];
@@ -625,6 +627,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 204
     FPM_PHASE_FLUSH;
 }
 
+template <int P, int K, bool THR = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 || THR ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
+    const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count,
+    TileDesc *__restrict__ redo, uint32_t *__restrict__ redo_n)
+{
+    sketch_tile<P, K, THR>(seq, tiles[blockIdx.x], p, thr, out, out_count, redo, redo_n);
+}
+
+// The tiles a THR pass could not keep (redo[0 .. *redo_n)), through the plain kernel's body:
+// a fixed grid takes them in turn, so the count stays on the device (no host read between
+// the two launches: fpm_sketch_run stays asynchronous on its stream).
+template <int K>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void sketch_redo_kernel(
+    const uint8_t *__restrict__ seq, const TileDesc *__restrict__ redo,
+    const uint32_t *__restrict__ redo_n, SketchKParams p, const uint64_t *__restrict__ thr,
+    uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)
+{
+    const uint32_t n = *redo_n;
+    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+        sketch_tile<4096, K, false>(seq, redo[t], p, thr, out, out_count, nullptr, nullptr);
+        __syncthreads();                       // the next tile reuses the LDS
+    }
+}
+
 // Merge of two ascending distinct lists, keeping the first s distinct of the union.
 // A[i] lands at i + lower_bound(B, A[i]) - #dups among A[0..i); B[j] that equals an
 // A element is dropped, the others land at j + upper_bound(A, B[j]) - #dups among B[0..j).
@@ -717,6 +744,24 @@ hipError_t launch_sketch_tiles_thr(const uint8_t *d_seq, const TileDesc *d_tiles
     else
         hipLaunchKernelGGL((sketch_tiles_kernel<4096, 0, true>), dim3(n_tiles), dim3(kBlock), 0,
                            st, d_seq, d_tiles, p, d_thr, d_out, d_count, d_redo, d_redo_n);
+    return hipGetLastError();
+}
+
+hipError_t launch_sketch_redo(const uint8_t *d_seq, const TileDesc *d_redo, const uint32_t *d_redo_n,
+                              uint32_t max_tiles, const SketchKParams &p, const uint64_t *d_thr,
+                              uint64_t *d_out, uint32_t *d_count, hipStream_t st)
+{
+    if (max_tiles == 0) return hipSuccess;
+    // about one resident workgroup per slot of the chip (4 per CU at 128 VGPRs): most exit at
+    // once (C5: no tile overflows), and a low-complexity input's many redo tiles are taken in
+    // turn
+    const uint32_t grid = std::min<uint32_t>(max_tiles, 1024);
+    if (p.k == 21)
+        hipLaunchKernelGGL((sketch_redo_kernel<21>), dim3(grid), dim3(kBlock), 0, st, d_seq, d_redo,
+                           d_redo_n, p, d_thr, d_out, d_count);
+    else
+        hipLaunchKernelGGL((sketch_redo_kernel<0>), dim3(grid), dim3(kBlock), 0, st, d_seq, d_redo,
+                           d_redo_n, p, d_thr, d_out, d_count);
     return hipGetLastError();
 }
 

@@ -79,6 +79,7 @@ SYMBOLS = [
     ("fpm_sketch_mult", C.c_int, [vp, vp, u32p]),
     ("fpm_merge_small_spills", C.c_int, [vp, u64p]),
     ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
+    ("fpm_sketch_job_redo_tiles", C.c_int, [vp, C.POINTER(C.c_int32)]),
     ("fpm_sketch_job_free", None, [vp]),
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
     ("fpm_fp_hash_lines_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32, vp,
@@ -355,6 +356,13 @@ class SketchJob:
         a, b, c = C.c_uint64(), C.c_uint64(), C.c_uint64()
         _check(lib().fpm_sketch_job_info(self.h, C.byref(a), C.byref(b), C.byref(c)))
         return {"seq_bytes": a.value, "n_tiles": b.value, "n_kmers": c.value}
+
+    def redo_tiles(self):
+        """tiles of the last run() the survivors-only kernel handed to the plain one (-1: the
+        job does not use that kernel); waits for the device"""
+        n = C.c_int32()
+        _check(lib().fpm_sketch_job_redo_tiles(self.h, C.byref(n)))
+        return n.value
 
     def device_output(self):
         dh, dc = vp(), vp()

@@ -163,6 +163,11 @@ int fpm_sketch_mult(fpm_sketch_job *job, void *stream, uint32_t *out_mult);
 /* bytes the run() kernels read + write by algorithm (for roofline accounting) */
 int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_tiles,
                         uint64_t *n_kmers);
+/* Tiles of the last run() that the survivors-only tile kernel could not keep and the plain
+ * kernel redid (a test hook beside the MinHashHeap restatement, MinHashHeap.cpp:68-146, the
+ * result does not depend on it): -1 when the job does not use that kernel (no long groups, or
+ * s too large for their bound to leave few survivors per tile).  Waits for the device. */
+int fpm_sketch_job_redo_tiles(fpm_sketch_job *job, int32_t *n_redo);
 void fpm_sketch_job_free(fpm_sketch_job *job);
 
 /* Bottom-s of the union of n_lists sketches (device rows of stride s, ascending and

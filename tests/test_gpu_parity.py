@@ -591,6 +591,50 @@ def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
     check_sketches(got, exp)
 
 
+@pytest.mark.parametrize("kind", ["random", "repeat"])
+def test_sketch_survivors_kernel_redo(ctx, oracle, kind):
+    """The survivors-only tile kernel (sketch_tiles_kernel<4096, K, true>: C5's genomes) and
+    its redo pass.  A long random group keeps ~130 of a tile's 4,096 windows below its sampled
+    bound: no tile overflows (redo_tiles() == 0).  A 2 Mb group of one repeated 3 kb unit has
+    ~3,000 distinct k-mers, a third of them below the bound, so every tile's ~1,300 survivors
+    (repeats included) overflow its 1,024 slots: each is listed and redone by the plain kernel
+    through the device-side count (redo_tiles() > 0).  Both sketches equal the reference
+    heap's (MinHashHeap.cpp:68-146)."""
+    import fpmash
+    rng = np.random.default_rng(11 if kind == "random" else 12)
+    seq = rand_seq(rng, 2_000_000) if kind == "random" else rand_seq(rng, 3000) * 667
+    P = fpmash.make_params(k=21, s=1000)
+    job = ctx.sketch_job(P, [seq], groups=[0], n_groups=1)
+    try:
+        for _ in range(2):                      # the count is reset by every run
+            job.run(ctx.stream)
+            n_redo = job.redo_tiles()
+            if kind == "random":
+                assert n_redo == 0
+            else:
+                assert n_redo > 400             # 488 tiles, nearly all of them
+        rows, cnt = job.fetch()
+    finally:
+        job.free()
+    exp = oracle.sketch_batch(oracle.params(k=21, s=1000), [seq])
+    check_sketches([rows[0, : cnt[0]]], exp)
+
+
+def test_sketch_survivors_kernel_off_for_large_s(ctx):
+    """s so large that a long group's bound keeps about half a tile's slots (2 x 16 s / tiles
+    + 64 > 512): the plain kernel takes the class-4 tiles (redo_tiles() == -1) instead of
+    hashing most of them twice."""
+    import fpmash
+    rng = np.random.default_rng(13)
+    job = ctx.sketch_job(fpmash.make_params(k=21, s=20_000), [rand_seq(rng, 2_000_000)],
+                         groups=[0], n_groups=1)
+    try:
+        job.run(ctx.stream)
+        assert job.redo_tiles() == -1
+    finally:
+        job.free()
+
+
 def test_merge_small_kernel_forced():
     """Every merge round on merge_small_kernel (FPM_MERGE_SMALL=2, in a child process: the
     switch is read when the library loads), including lists longer than its LDS cap that

@@ -66,6 +66,30 @@ def test_c4_leg_ranks_one_gpu(ws):
 
 
 @pytest.mark.gpu
+def test_c4_gathered_path_nccl_one_gpu():
+    """The on-device multi-GPU data path, run on the one GPU with a one-rank RCCL group
+    (tests/_c4_nccl_worker.py): the C4 leg's all-gather into torch tensors over RCCL, block
+    indexes and self / mirror compares on those torch-allocated pointers (2 and 3 virtual
+    blocks: the even split's half blocks too), every grid and transpose row sampled against
+    the oracle and the cells adding up to the whole grid; and shard.min_merge with device=."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
+           os.path.join(ROOT, "tests", "_c4_nccl_worker.py")]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines()
+           if l.startswith("C4NCCL ")]
+    assert len(res) == 1
+    r = res[0]
+    for vb, c in r["c4"].items():
+        assert c["collective"] == "all_gather (nccl = RCCL)", c
+        assert c["cells"] == c["pairs"], (vb, c)
+        assert c["parity"]["ok"] and c["parity"]["pairs_sharing"] > 0, (vb, c)
+        assert any(j["kind"] == "mirror" for j in c["jobs"])
+    assert r["min_merge_ok"]
+
+
+@pytest.mark.gpu
 def test_c5_leg_two_ranks_one_gpu():
     """bench.c5_leg at world size 2 (both ranks on the one visible GPU, sketch rows gathered
     over gloo): uneven file shards (7 genomes over 2 ranks), and every genome of the ordered
