@@ -102,6 +102,8 @@ def parse():
     ap.add_argument("--no-c3", action="store_true", help="skip the -fp C3 leg")
     ap.add_argument("--no-c4", action="store_true", help="skip the sharded C4 dist leg")
     ap.add_argument("--c4-n", type=int, default=50_000)
+    ap.add_argument("--no-cli-fp", action="store_true",
+                    help="skip the -fp CLI leg (sketch -fp x10, paste -fp, dist -fp)")
     ap.add_argument("--no-gather-check", action="store_true",
                     help="at N = 1: skip the C4 gathered-path check (one-rank RCCL group)")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 RefSeq-scale sketch leg")
@@ -280,6 +282,9 @@ def cpu_baseline(args, seqs):
         "value": n * args.seq_len / step_s,
         "unit": "bases/s",
         "cores": threads,
+        "cores_note": (f"threads used = the CPUs available to this process ({threads}: "
+                       f"OMP_NUM_THREADS / sched_getaffinity) of the machine's "
+                       f"{os.cpu_count()}"),
         "kind": "port",
         **extra,
         "sample": (f"oracle CPU port on {threads} threads: sketch of {n_s} x {args.seq_len} bp "
@@ -342,23 +347,6 @@ def fp_text_leg(ctx, reps=5):
             "lines_per_s_wall_pcie": n / wall, "wall_ms": wall * 1e3,
             "note": f"{lines} lines in the file, the first 1,000,000 parsed (the -fp line cap); "
                     f"mean of {reps} calls"}
-
-
-def _group_fp_lines(r, text):
-    """initFromFingerprints' grouping (Sketch.cpp:104-134) of one parsed file: a new
-    reference wherever the line's ID differs from the previous one; length = the first
-    line's value count counted twice + the rest (:117, :134)."""
-    n = len(r["hash"])
-    new = r["new_id"].astype(bool)
-    if n:
-        new[0] = True
-    starts = np.flatnonzero(new)
-    ends = np.append(starts[1:], n)
-    nv = r["n_vals"].astype(np.uint64)
-    csum = np.concatenate([[0], np.cumsum(nv)])
-    lengths = nv[starts] + (csum[ends] - csum[starts])
-    return starts, ends, lengths
-
 
 
 # ---- parity (the CPU leg's checker: oracle/ restatement, outside every timed region) ----
@@ -431,14 +419,15 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4, c5=None, cli=None, split=None, c4_gather=None):
+def parity_summary(c2, c3, c4, c5=None, cli=None, split=None, c4_gather=None, cli_fp=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
              "c4": c4.get("parity") if c4 else None,
              "c4_gather": c4_gather.get("parity") if c4_gather else None,
              "c5": c5.get("parity") if c5 else None,
              "split": split.get("parity") if split else None,
-             "cli": cli.get("parity") if cli else None}
+             "cli": cli.get("parity") if cli else None,
+             "cli_fp": cli_fp.get("parity") if cli_fp else None}
     done = [v["ok"] for v in parts.values() if v]
     parts["all_ok"] = all(done) if done else None
     parts["checker"] = ("oracle/ CPU restatement (pinned to the reference's fixtures), "
@@ -485,14 +474,17 @@ def c3_leg(ctx, n_seqs=5000, per_file=500, s=1000, reps=3, parity=True):
     t0 = time.perf_counter()
     n_lines = 0
     for f in files:
-        r = ctx.fp_text(f, max_lines=1_000_000)
-        n_lines += len(r["hash"])
-        st, en, ln = _group_fp_lines(r, f)
+        # parsed, hashed and grouped into References on the device (fpm_fp_text_refs): the
+        # host fetches the line hashes and ~500 reference descriptors per file
+        r = ctx.fp_refs(f, max_lines=1_000_000)
+        n_lines += r["n_lines"]
         h = r["hash"]
+        st = r["first"].astype(np.int64)
+        en = np.append(st[1:], r["n_lines"])
         for a, b in zip(st, en):
             rows.append(h[a:b])
         lens.append(en - st)
-        lengths.append(ln)
+        lengths.append(r["length"])
     t_parse_wall = time.perf_counter() - t0
     ctx.set_timing(False)
     parse_ms, _ = ctx.kernel_time(fpmash.K_FPTEXT)
@@ -908,8 +900,9 @@ def cli_leg(args, seqs, cpu=None, check=True):
       fpmash dist c2.msh c2.msh > out                 (1e8 lines: resident reference set,
                                                        pipelined blocks, ordered text)
     Outside the timed commands: the .msh is byte-compared with the .msh the oracle's
-    sketches encode to (tests/mshfmt.write_msh), and the first and last 20 query rows of the
-    text with the oracle's lines."""
+    sketches encode to (tests/mshfmt.write_msh), and the first and last 50 query rows of the
+    text (1 M lines, 1 % of the grid) with the oracle's lines; the reference's text step is
+    timed on those 1 M lines."""
     import shutil
     import subprocess
     import tempfile
@@ -983,7 +976,7 @@ def cli_leg(args, seqs, cpu=None, check=True):
                        noncanonical=False, preserveCase=False, error=0.0, seed=42,
                        alphabet=b"ACGT")
             msh_ok = open(os.path.join(tmp, "c2.msh"), "rb").read() == mshfmt.write_msh(hdr, refs)
-            rows = list(range(20)) + list(range(n - 20, n))
+            rows = list(range(50)) + list(range(n - 50, n))
             nu, de, di, pv = O.dist_grid(exp, [len(q) for q in seqs], [exp[r] for r in rows],
                                          [len(seqs[r]) for r in rows], args.s, args.k,
                                          4.0 ** args.k, threads=_threads())
@@ -994,13 +987,14 @@ def cli_leg(args, seqs, cpu=None, check=True):
                     c = x * n + r
                     want.append(b"%s\t%s\t%s\t%s\t%d/%d" % (
                         names[r], names[qr], (b"%g" % di[c]), (b"%g" % pv[c]), nu[c], de[c]))
+            h = len(rows) // 2
             with open(out_path, "rb") as f:
-                head = [f.readline().rstrip(b"\n") for _ in range(20 * n)]
-                f.seek(max(0, out_bytes - 20 * n * 200))
-                tail = f.read().split(b"\n")[:-1][-20 * n:]
-            text_ok = head == want[:20 * n] and tail == want[20 * n:]
+                head = [f.readline().rstrip(b"\n") for _ in range(h * n)]
+                f.seek(max(0, out_bytes - h * n * 200))
+                tail = f.read().split(b"\n")[:-1][-h * n:]
+            text_ok = head == want[:h * n] and tail == want[h * n:]
             if cpu and "cpu_same_work" in res:
-                # the reference's text step on the 40 checked rows (400k lines, endl per line)
+                # the reference's text step on the 100 checked rows (1 M lines, endl per line)
                 tpath = os.path.join(tmp, "ref_text.tsv")
                 t0 = time.perf_counter()
                 O.write_dist_text(tpath, names, rows, nu, de, di, pv, flush_each=True)
@@ -1010,12 +1004,163 @@ def cli_leg(args, seqs, cpu=None, check=True):
                 cw["dist_s"] = load + max(res["cpu_port_dist_s"], t_txt)
                 cw["dist_parts_s"] = {"msh load (shared host code)": load,
                                       "compare + p-values": res["cpu_port_dist_s"],
-                                      "text, endl per line (extrapolated from 40 rows)": t_txt,
+                                      "text, endl per line (timed on 1 M lines = 100 rows, "
+                                      "scaled)": t_txt,
                                       "combined as": "load + max(compare, text)"}
                 res["speedup_dist"] = cw["dist_s"] / t_dist
                 # the north-star figure: sketch + dist of C2, CPU same work / GPU wall
                 res["speedup_sketch_plus_dist"] = (cw["sketch_s"] + cw["dist_s"]) / (t_sketch + t_dist)
             res["parity"] = {"msh_byte_identical": bool(msh_ok),
+                             "dist_text_rows_checked": len(rows), "dist_text_exact": bool(text_ok),
+                             "ok": bool(msh_ok and text_ok), "check_s": time.perf_counter() - t_c}
+        return res
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def cli_fp_leg(args, cpu=None, check=True, n_seqs=5000, per_file=500):
+    """The -fp drop-in end to end (north_star: `mash sketch -fp`, `mash dist -fp`), on C3's
+    5,000 lyn2vec-shaped 2 kb sequences as CFL k-finger text in 10 files of 1 M lines
+    (`sketch -fp` reads at most 1,000,000 lines per call, Sketch.cpp:37, :82):
+      fpmash sketch -fp c3_<i>.txt -o c3_<i>     x 10  (parse + hash + group on the device)
+      fpmash paste -fp c3_0.txt ... c3_9.txt -o c3      (host: the .msh inputs joined)
+      fpmash dist -fp c3.msh c3.msh > out               (25 M lines: unsorted u32 lists,
+                                                          the literal walk, ordered text)
+    CPU same work (the reference's per-call structure, timed here):
+      sketch = initFromFingerprints' istringstream parse around the reference's compiled
+               getHashFingerPrint + HashList::add on one thread (oracle/_ref
+               ref_fp_sketch_file; the reference runs it on its main thread) on 2 of the 10
+               files, scaled x5, + the .msh write (shared host code, the GPU command's phase);
+      paste  = the same host code: its GPU-side wall counts on both sides;
+      dist   = the .msh loads (shared host code, measured) + max(compare: the oracle's literal
+               walk on all cores over 100 query rows x 5,000, scaled to the grid; text: the
+               reference's `endl`-per-line writer on 50 rows x 5,000 = 1 % of the lines,
+               scaled), as the reference's workers compute while its main thread writes.
+    Outside the timed commands: c3.msh's 5,000 references (names, lengths, hash lists) against
+    the oracle's initFromFingerprints, and the first and last 20 query rows of the text
+    against the oracle's lines."""
+    import shutil
+    import subprocess
+    import tempfile
+    exe = os.path.join(ROOT, "fp-mash_amd", "bin", "fpmash")
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    tmp = tempfile.mkdtemp(prefix="fpm_clifp_", dir=base)
+    try:
+        seqs = datagen.random_dna(n_seqs, 2000, seed=33)
+        ids = datagen.lyn2vec_ids(n_seqs, seed=33)
+        names = [f"c3_{i}" for i in range(0, n_seqs // per_file)]
+        sizes = []
+        for j, nm in enumerate(names):
+            t = datagen.cfl_text_fast(seqs[j * per_file:(j + 1) * per_file],
+                                      ids[j * per_file:(j + 1) * per_file])
+            with open(os.path.join(tmp, nm + ".txt"), "wb") as f:
+                f.write(t)
+            sizes.append(len(t))
+        del seqs
+        env = dict(os.environ, FPMASH_TIMING="1")
+        sk_walls, ph_sk = [], []
+        for nm in names:
+            t0 = time.perf_counter()
+            pr = subprocess.run([exe, "sketch", "-fp", nm + ".txt", "-o", nm], cwd=tmp, check=True,
+                                capture_output=True, env=env)
+            sk_walls.append(time.perf_counter() - t0)
+            ph_sk.append(cli_phases(pr.stderr))
+        t0 = time.perf_counter()
+        subprocess.run([exe, "paste", "-fp"] + [nm + ".txt" for nm in names] + ["-o", "c3"],
+                       cwd=tmp, check=True, capture_output=True, env=env)
+        t_paste = time.perf_counter() - t0
+        out_path = os.path.join(tmp, "out.tsv")
+        t0 = time.perf_counter()
+        with open(out_path, "wb") as f:
+            pd = subprocess.run([exe, "dist", "-fp", "-p", str(_threads()), "c3.msh", "c3.msh"],
+                                cwd=tmp, check=True, stdout=f, stderr=subprocess.PIPE, env=env)
+        t_dist = time.perf_counter() - t0
+        ph_d = cli_phases(pd.stderr)
+        t_sk = sum(sk_walls)
+        res = {"command_sketch": "fpmash sketch -fp c3_<i>.txt -o c3_<i> (x10, 1 M lines each)",
+               "command_paste": "fpmash paste -fp c3_0.txt ... c3_9.txt -o c3",
+               "command_dist": "fpmash dist -fp c3.msh c3.msh > out",
+               "text_bytes": sum(sizes), "cli_sketch_fp_wall_s": t_sk,
+               "cli_sketch_fp_wall_s_per_call": sk_walls, "cli_paste_fp_wall_s": t_paste,
+               "cli_dist_fp_wall_s": t_dist, "dist_lines": n_seqs * n_seqs,
+               "dist_text_bytes": os.path.getsize(out_path),
+               "phases_ms_sketch_first_call": ph_sk[0], "phases_ms_dist": ph_d}
+        from oracle import oracle as O
+        th = _threads()
+        refs = []
+        if check or cpu:
+            for nm in names:
+                r, _u, _l = O.fp_references(open(os.path.join(tmp, nm + ".txt"), "rb").read())
+                refs += r
+        if cpu:
+            t0 = time.perf_counter()
+            scan = [O.ref_fp_sketch_files([os.path.join(tmp, nm + ".txt")]) for nm in names[:2]]
+            t_scan = time.perf_counter() - t0
+            if all(x is not None for x in scan):
+                msh_w = sum(p_.get("msh write", 0.0) for p_ in ph_sk) * 1e-3
+                cpu_sk = t_scan * len(names) / 2 + msh_w
+                # compare: the oracle's literal walk (unsorted u32 lists, S = 1000, k = 1)
+                lists = [h for _n, _l, h in refs]
+                lens = [l_ for _n, l_, _h in refs]
+                n = len(lists)
+                qrows = sample_rows(n, 100, salt=5)
+                t0 = time.perf_counter()
+                nu, de, di, pv = O.dist_grid(lists, lens, [lists[int(q)] for q in qrows],
+                                             [lens[int(q)] for q in qrows], 1000, 1, 10.0,
+                                             use64=False, threads=th)
+                t_cmp = (time.perf_counter() - t0) * n / len(qrows)
+                # text: the reference's writer (endl per line) on 50 rows = 1 % of the lines
+                nms = [x for x, _l, _h in refs]
+                tpath = os.path.join(tmp, "ref_text.tsv")
+                t0 = time.perf_counter()
+                O.write_dist_text(tpath, nms, qrows[:50], nu[:50 * n], de[:50 * n], di[:50 * n],
+                                  pv[:50 * n], flush_each=True)
+                t_txt = (time.perf_counter() - t0) * n / 50
+                load = (ph_d.get("reference sketch loaded", 0.0) +
+                        ph_d.get("query sketch loaded", 0.0)) * 1e-3
+                cpu_d = load + max(t_cmp, t_txt)
+                res["cpu_same_work"] = {
+                    "sketch_fp_s": cpu_sk, "paste_s": t_paste, "dist_fp_s": cpu_d,
+                    "sketch_parts_s": {"istringstream parse + getHashFingerPrint (reference, "
+                                       "compiled), 1 thread, 2 files x5": t_scan * len(names) / 2,
+                                       ".msh writes (shared host code)": msh_w},
+                    "dist_parts_s": {".msh loads (shared host code)": load,
+                                     f"literal walk + p-values ({th} threads, 100 rows scaled)": t_cmp,
+                                     "text, endl per line (50 rows = 1 % of the lines, scaled)":
+                                         t_txt, "combined as": "load + max(compare, text)"},
+                    "cores": th}
+                res["speedup_sketch_fp"] = cpu_sk / t_sk
+                res["speedup_dist_fp"] = cpu_d / t_dist
+                res["speedup_dist_fp_compute_only"] = t_cmp / t_dist
+                res["speedup_fp_sketch_paste_dist"] = (cpu_sk + t_paste + cpu_d) / \
+                    (t_sk + t_paste + t_dist)
+        if check:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import mshfmt
+            t_c = time.perf_counter()
+            got = mshfmt.read_msh(os.path.join(tmp, "c3.msh"))["references"]
+            msh_ok = len(got) == len(refs) and all(
+                g["name"] == e[0] and int(g["length"]) == int(e[1]) and
+                np.array_equal(np.asarray(g["hashes32"], np.uint32), e[2])
+                for g, e in zip(got, refs))
+            lists = [h for _n, _l, h in refs]
+            lens = [l_ for _n, l_, _h in refs]
+            n = len(lists)
+            rows = list(range(20)) + list(range(n - 20, n))
+            nu, de, di, pv = O.dist_grid(lists, lens, [lists[r] for r in rows],
+                                         [lens[r] for r in rows], 1000, 1, 10.0, use64=False,
+                                         threads=th)
+            nms = [x for x, _l, _h in refs]
+            want = [b"%s\t%s\t%s\t%s\t%d/%d" % (nms[r], nms[qr], b"%g" % di[x * n + r],
+                                                b"%g" % pv[x * n + r], nu[x * n + r], de[x * n + r])
+                    for x, qr in enumerate(rows) for r in range(n)]
+            size = os.path.getsize(out_path)
+            with open(out_path, "rb") as f:
+                head = [f.readline().rstrip(b"\n") for _ in range(20 * n)]
+                f.seek(max(0, size - 20 * n * 200))
+                tail = f.read().split(b"\n")[:-1][-20 * n:]
+            text_ok = head == want[:20 * n] and tail == want[20 * n:]
+            res["parity"] = {"msh_references_exact": bool(msh_ok), "references": len(refs),
                              "dist_text_rows_checked": len(rows), "dist_text_exact": bool(text_ok),
                              "ok": bool(msh_ok and text_ok), "check_s": time.perf_counter() - t_c}
         return res
@@ -1299,14 +1444,16 @@ def compact_line(d, detail_path=None):
                                                roof["wave_state_frac"].items()}
     line["cpu_baseline"] = None if not cpu else {
         "value": cpu.get("value"), "unit": cpu.get("unit"), "cores": cpu.get("cores"),
+        "cores_note": cpu.get("cores_note"),
         "kind": cpu.get("kind"), "sample": cpu.get("sample"), "cpu_model": cpu.get("cpu_model")}
     line["parity"] = {"c2": _ok(par.get("c2")), "c3_fp": _ok(par.get("c3_fp")),
                       "c4": _ok(par.get("c4")), "c4_gather": _ok(par.get("c4_gather")),
                       "c5": _ok(par.get("c5")),
                       "split": _ok(par.get("split")), "cli": _ok(par.get("cli")),
+                      "cli_fp": _ok(par.get("cli_fp")),
                       "all_ok": par.get("all_ok")}
     c3, c4, c5 = d.get("c3_fp"), d.get("c4_dist"), d.get("c5_sketch")
-    sp, cli = d.get("split_sketch"), d.get("cli")
+    sp, cli, clf = d.get("split_sketch"), d.get("cli"), d.get("cli_fp")
     legs = {
         "sketch_bases_per_s": _r(g(d, "sketch", "bases_per_s")),
         "sketch_device_ms": _r(g(d, "sketch", "device_ms_per_step")),
@@ -1325,7 +1472,16 @@ def compact_line(d, detail_path=None):
         "cli_dist_wall_s": _r(g(cli, "cli_dist_wall_s")),
         "cli_speedup_sketch": _r(g(cli, "speedup_sketch"), 3),
         "cli_speedup_dist": _r(g(cli, "speedup_dist"), 3),
+        "cli_speedup_dist_compute_only": _r(g(cli, "speedup_dist_compute_only"), 3),
         "cli_speedup_sketch_plus_dist": _r(g(cli, "speedup_sketch_plus_dist"), 3),
+        "cli_fp_sketch_wall_s": _r(g(clf, "cli_sketch_fp_wall_s")),
+        "cli_fp_paste_wall_s": _r(g(clf, "cli_paste_fp_wall_s")),
+        "cli_fp_dist_wall_s": _r(g(clf, "cli_dist_fp_wall_s")),
+        "cli_fp_speedup_sketch": _r(g(clf, "speedup_sketch_fp"), 3),
+        "cli_fp_speedup_dist": _r(g(clf, "speedup_dist_fp"), 3),
+        "cli_fp_speedup_dist_compute_only": _r(g(clf, "speedup_dist_fp_compute_only"), 3),
+        "cli_fp_speedup_all": _r(g(clf, "speedup_fp_sketch_paste_dist"), 3),
+        "c3_parse_wall_ms_pcie": _r(g(c3, "parse_wall_ms_pcie")),
     }
     line["legs"] = {k: v for k, v in legs.items() if v is not None}
     line["detail"] = detail_path
@@ -1564,6 +1720,9 @@ def main():
     cli = None
     if rank == 0 and ws == 1 and not args.no_cli:
         cli = cli_leg(args, seqs, cpu, check=not args.no_parity)
+    cli_fp = None
+    if rank == 0 and ws == 1 and not args.no_cli_fp:
+        cli_fp = cli_fp_leg(args, cpu, check=not args.no_parity)
 
     if rank == 0:
         detail = {
@@ -1608,11 +1767,12 @@ def main():
             "c5_sketch": c5,
             "split_sketch": split,
             "cli": cli,
+            "cli_fp": cli_fp,
             "kernels": ktimes,
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4, c5, cli, split, c4g),
+            "parity": parity_summary(c2par, c3, c4, c5, cli, split, c4g, cli_fp),
         }
         path = write_detail(detail, args.detail)
         print(json.dumps(compact_line(detail, path)))

@@ -271,4 +271,103 @@ hipError_t launch_fp_lines(const uint8_t *d_text, uint64_t len, const uint64_t *
     return hipGetLastError();
 }
 
+// ---- the References of one parsed file (Sketch::initFromFingerprints' grouping, Sketch.cpp:
+// 104-145): a new Reference starts at line 0 (checked against the previous file's last ID by
+// the host) and wherever the ID differs from the previous line's (new_id == 1); its length is
+// the first line's value count (set at creation, :117) plus every line's count (:134, the first
+// line's again).  Heads are compacted in line order (per-block counts, an exclusive scan, an
+// ordered scatter), then one wave per Reference sums its lines' counts.  The host then fetches
+// ~ a few KB per file instead of every line's ID bounds and counts (21 B per line).
+constexpr uint32_t kHeadLines = 1024;   // lines per workgroup (256 threads x 4)
+
+__device__ __forceinline__ uint32_t fp_is_head(const uint8_t *__restrict__ new_id, uint64_t li,
+                                               uint64_t n)
+{
+    return li < n && (li == 0 || new_id[li] == 1) ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void fp_head_count_kernel(const uint8_t *__restrict__ new_id,
+                                                           uint64_t n, uint32_t *__restrict__ cnt)
+{
+    __shared__ uint32_t wsum[4];
+    const uint64_t l0 = (uint64_t)blockIdx.x * kHeadLines + threadIdx.x * 4;
+    uint32_t c = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) c += fp_is_head(new_id, l0 + u, n);
+    for (int d = 32; d > 0; d >>= 1) c += __shfl_down(c, d, 64);
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+    __syncthreads();
+    if (threadIdx.x == 0) cnt[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+__global__ __launch_bounds__(256) void fp_head_scatter_kernel(const uint8_t *__restrict__ new_id,
+                                                             uint64_t n,
+                                                             const uint32_t *__restrict__ blk_off,
+                                                             uint64_t *__restrict__ first)
+{
+    __shared__ uint32_t wsum[4];
+    const uint64_t l0 = (uint64_t)blockIdx.x * kHeadLines + threadIdx.x * 4;
+    uint32_t h[4], c = 0;
+#pragma unroll
+    for (int u = 0; u < 4; u++) { h[u] = fp_is_head(new_id, l0 + u, n); c += h[u]; }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t x = c;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint64_t k = blk_off[blockIdx.x] + x - c;
+    for (int w = 0; w < wave; w++) k += wsum[w];
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (h[u]) first[k++] = l0 + u;
+}
+
+// one wave per Reference r: lines [first[r], first[r + 1]) (the last one to n)
+__global__ __launch_bounds__(256) void fp_ref_len_kernel(
+    const uint64_t *__restrict__ first, uint64_t n_refs, uint64_t n,
+    const uint32_t *__restrict__ n_vals, const uint64_t *__restrict__ id_off,
+    const uint32_t *__restrict__ id_len, uint64_t *__restrict__ length,
+    uint64_t *__restrict__ ref_id_off, uint32_t *__restrict__ ref_id_len)
+{
+    const uint64_t r = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    if (r >= n_refs) return;
+    const uint64_t a = first[r], b = r + 1 < n_refs ? first[r + 1] : n;
+    uint64_t sum = 0;
+    for (uint64_t l = a + lane; l < b; l += 64) sum += n_vals[l];
+    for (int d = 32; d > 0; d >>= 1) sum += __shfl_down(sum, d, 64);
+    if (lane == 0) {
+        length[r] = sum + n_vals[a];
+        ref_id_off[r] = id_off[a];
+        ref_id_len[r] = id_len[a];
+    }
+}
+
+uint32_t fp_head_blocks(uint64_t n_lines) { return (uint32_t)((n_lines + kHeadLines - 1) / kHeadLines); }
+
+hipError_t launch_fp_heads(const uint8_t *d_new_id, uint64_t n_lines, uint32_t *blk_cnt,
+                           uint32_t *blk_off, uint32_t *scan_s, hipStream_t st)
+{
+    const uint32_t nb = fp_head_blocks(n_lines);
+    if (!nb) return hipSuccess;
+    hipLaunchKernelGGL(fp_head_count_kernel, dim3(nb), dim3(256), 0, st, d_new_id, n_lines, blk_cnt);
+    return launch_exscan(blk_cnt, blk_off, nullptr, nb, scan_s, blk_off + nb, st);
+}
+
+hipError_t launch_fp_refs(const uint8_t *d_new_id, uint64_t n_lines, const uint32_t *blk_off,
+                          uint64_t n_refs, const uint32_t *d_n_vals, const uint64_t *d_id_off,
+                          const uint32_t *d_id_len, uint64_t *d_first, uint64_t *d_length,
+                          uint64_t *d_ref_id_off, uint32_t *d_ref_id_len, hipStream_t st)
+{
+    const uint32_t nb = fp_head_blocks(n_lines);
+    if (!nb || !n_refs) return hipSuccess;
+    hipLaunchKernelGGL(fp_head_scatter_kernel, dim3(nb), dim3(256), 0, st, d_new_id, n_lines,
+                       blk_off, d_first);
+    hipLaunchKernelGGL(fp_ref_len_kernel, dim3((uint32_t)((n_refs + 3) / 4)), dim3(256), 0, st,
+                       d_first, n_refs, n_lines, d_n_vals, d_id_off, d_id_len, d_length,
+                       d_ref_id_off, d_ref_id_len);
+    return hipGetLastError();
+}
+
 }  // namespace fpm

@@ -18,6 +18,7 @@
 #include <thread>
 #include <cstdio>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -68,6 +69,73 @@ static const int g_merge_small_env = [] {
     return v ? atoi(v) : 1;
 }();
 
+// Host memcpy split over a few persistent threads: the pinned ring's copies of pageable caller
+// memory ran at one thread's ~8 GB/s, below the DMA behind them (C3's 301 MB of -fp text:
+// ~40 ms of the parse wall).  Parts of >= 1 MB; the caller copies the first part itself.
+class CopyPool {
+  public:
+    ~CopyPool()
+    {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    void copy(void *dst, const void *src, size_t n)
+    {
+        constexpr size_t kPart = size_t(1) << 20;
+        const unsigned want = (unsigned)std::min<size_t>(kMaxThreads + 1, n / kPart);
+        if (want <= 1) { memcpy(dst, src, n); return; }
+        std::unique_lock<std::mutex> lk(mu_);
+        while (th_.size() + 1 < want && th_.size() < threads())
+            th_.emplace_back([this] { work(); });
+        const unsigned parts = (unsigned)std::min<size_t>(want, th_.size() + 1);
+        const size_t per = (n + parts - 1) / parts;
+        char *d = static_cast<char *>(dst);
+        const char *sp = static_cast<const char *>(src);
+        for (unsigned i = 1; i < parts; i++) {
+            const size_t a = i * per, b = std::min(n, a + per);
+            if (a < b) { q_.push_back({d + a, sp + a, b - a}); pending_++; }
+        }
+        lk.unlock();
+        cv_.notify_all();
+        memcpy(d, sp, std::min(n, per));
+        lk.lock();
+        done_.wait(lk, [this] { return pending_ == 0; });
+    }
+
+  private:
+    static constexpr unsigned kMaxThreads = 7;
+    static unsigned threads()
+    {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        return std::min(kMaxThreads, std::max(1u, hw / 2));
+    }
+    struct Task { char *d; const char *s; size_t n; };
+    void work()
+    {
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+            cv_.wait(lk, [this] { return stop_ || !q_.empty(); });
+            if (q_.empty()) return;
+            const Task t = q_.back();
+            q_.pop_back();
+            lk.unlock();
+            memcpy(t.d, t.s, t.n);
+            lk.lock();
+            if (--pending_ == 0) done_.notify_all();
+        }
+    }
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::vector<std::thread> th_;
+    std::vector<Task> q_;
+    size_t pending_ = 0;
+    bool stop_ = false;
+};
+
 struct fpm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -95,6 +163,7 @@ struct fpm_ctx {
     static constexpr size_t kRingBytes = 8u << 20;
     void *ring[kRing] = {};
     hipEvent_t ring_ev[kRing] = {};
+    CopyPool copier;                       // the ring's host-side copies
     // device buffers of released -fp text jobs, reused by the next jobs: a fresh hipMalloc of
     // tens of MB is cleared by the driver before first use, and a kernel writing it could wait
     // ~27 ms for that (tools/micro/fp_text_time.py under rocprofv3: fp_line_kernel 0.06 ms,
@@ -193,7 +262,7 @@ static hipError_t h2d_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
         const int slot = (int)(i % fpm_ctx::kRing);
         const size_t n = std::min(fpm_ctx::kRingBytes, bytes - off);
         if (used[slot] && (e = hipEventSynchronize(ctx->ring_ev[slot])) != hipSuccess) return e;
-        memcpy(ctx->ring[slot], s + off, n);
+        ctx->copier.copy(ctx->ring[slot], s + off, n);
         if ((e = hipMemcpyAsync(d + off, ctx->ring[slot], n, hipMemcpyHostToDevice, ctx->stream)) !=
             hipSuccess)
             return e;
@@ -230,7 +299,7 @@ static hipError_t d2h_staged(fpm_ctx *ctx, void *dst, const void *src, size_t by
         const int slot = (int)(i % fpm_ctx::kRing);
         const size_t off = i * R, n = std::min(R, bytes - off);
         if ((e = hipEventSynchronize(ctx->ring_ev[slot])) != hipSuccess) return e;
-        memcpy(d + off, ctx->ring[slot], n);
+        ctx->copier.copy(d + off, ctx->ring[slot], n);
         if (i + fpm_ctx::kRing < n_pieces && (e = issue(i + fpm_ctx::kRing)) != hipSuccess) return e;
     }
     return hipSuccess;
@@ -1508,6 +1577,11 @@ struct fpm_fptext {
     uint32_t *d_id_len = nullptr, *d_n_vals = nullptr;
     void *d_hash = nullptr;
     uint8_t *d_new_id = nullptr;
+    // the file's References (fpm_fp_text_refs), computed on the first call
+    bool refs_done = false;
+    uint64_t n_refs = 0;
+    uint64_t *d_first = nullptr, *d_length = nullptr, *d_ref_id_off = nullptr;
+    uint32_t *d_ref_id_len = nullptr;
     std::vector<std::pair<void *, size_t>> bufs;   // every buffer above, with its size
     template <typename T> hipError_t alloc(T **p, size_t bytes)
     {
@@ -1602,6 +1676,50 @@ int fpm_fp_text_fetch(fpm_fptext *j, uint64_t *id_off, uint32_t *id_len, uint32_
         if (hash) HIP_TRY(copy_out(ctx, hash, j->d_hash, n * (j->use64 ? 8 : 4)));
         if (new_id) HIP_TRY(copy_out(ctx, new_id, j->d_new_id, n));
     }
+    return FPM_OK;
+}
+
+int fpm_fp_text_refs(fpm_fptext *j, uint64_t cap, uint64_t *n_refs, uint64_t *first_line,
+                     uint64_t *id_off, uint32_t *id_len, uint64_t *length)
+{
+    if (!j || !n_refs) return fail(FPM_EINVAL, "fp_text_refs: null argument");
+    if (int rc = set_device(j->ctx)) return rc;
+    fpm_ctx *ctx = j->ctx;
+    hipStream_t st = ctx->stream;
+    const uint64_t n = j->n_lines;
+    if (!j->refs_done && n) {
+        const uint32_t nb = fp_head_blocks(n);
+        uint32_t *blk;
+        HIP_TRY(j->alloc(&blk, ((size_t)2 * nb + 2 + scan_scratch_words(nb)) * 4));
+        uint32_t *blk_cnt = blk, *blk_off = blk + nb, *scan_s = blk + 2 * nb + 2;
+        {
+            TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
+            HIP_TRY(launch_fp_heads(j->d_new_id, n, blk_cnt, blk_off, scan_s, st));
+            tl.done();
+        }
+        uint32_t tot = 0;
+        HIP_TRY(hipMemcpyAsync(&tot, blk_off + nb, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        j->n_refs = tot;
+        HIP_TRY(j->alloc(&j->d_first, (size_t)tot * 8 + 8));
+        HIP_TRY(j->alloc(&j->d_length, (size_t)tot * 8 + 8));
+        HIP_TRY(j->alloc(&j->d_ref_id_off, (size_t)tot * 8 + 8));
+        HIP_TRY(j->alloc(&j->d_ref_id_len, (size_t)tot * 4 + 4));
+        TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
+        HIP_TRY(launch_fp_refs(j->d_new_id, n, blk_off, tot, j->d_n_vals, j->d_id_off,
+                               j->d_id_len, j->d_first, j->d_length, j->d_ref_id_off,
+                               j->d_ref_id_len, st));
+        tl.done();
+    }
+    j->refs_done = true;
+    *n_refs = j->n_refs;
+    if (cap < j->n_refs || !j->n_refs) return FPM_OK;     // sized by this call
+    const uint64_t m = j->n_refs;
+    HIP_TRY(hipStreamSynchronize(st));
+    if (first_line) HIP_TRY(copy_out(ctx, first_line, j->d_first, m * 8));
+    if (id_off) HIP_TRY(copy_out(ctx, id_off, j->d_ref_id_off, m * 8));
+    if (id_len) HIP_TRY(copy_out(ctx, id_len, j->d_ref_id_len, m * 4));
+    if (length) HIP_TRY(copy_out(ctx, length, j->d_length, m * 8));
     return FPM_OK;
 }
 

@@ -225,6 +225,16 @@ hipError_t launch_fp_nl_count(const uint8_t *d_text, uint64_t len, uint32_t *blk
                               uint32_t *blk_off, uint32_t *scan_s, hipStream_t st);
 hipError_t launch_fp_nl_scatter(const uint8_t *d_text, uint64_t len, const uint32_t *blk_off,
                                 uint64_t *d_line_start, hipStream_t st);
+// the References of a parsed -fp file (heads: line 0 and new_id == 1): per-block head counts +
+// their exclusive scan (blk_off[nb] = the total), then the ordered heads, each Reference's
+// length (the first line's count twice, Sketch.cpp:117, 134) and its ID bounds
+uint32_t fp_head_blocks(uint64_t n_lines);
+hipError_t launch_fp_heads(const uint8_t *d_new_id, uint64_t n_lines, uint32_t *blk_cnt,
+                           uint32_t *blk_off, uint32_t *scan_s, hipStream_t st);
+hipError_t launch_fp_refs(const uint8_t *d_new_id, uint64_t n_lines, const uint32_t *blk_off,
+                          uint64_t n_refs, const uint32_t *d_n_vals, const uint64_t *d_id_off,
+                          const uint32_t *d_id_len, uint64_t *d_first, uint64_t *d_length,
+                          uint64_t *d_ref_id_off, uint32_t *d_ref_id_len, hipStream_t st);
 hipError_t launch_fp_lines(const uint8_t *d_text, uint64_t len, const uint64_t *d_line_start,
                            uint64_t n_nl, uint64_t n_lines, uint32_t seed, uint32_t use64,
                            uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals, void *hash,

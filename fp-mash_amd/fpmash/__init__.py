@@ -87,6 +87,7 @@ SYMBOLS = [
     ("fpm_fp_text_stage", C.c_int, [vp, C.c_char_p, C.c_uint64, C.c_uint64, C.c_uint32,
                                     C.c_uint32, C.POINTER(vp), u64p]),
     ("fpm_fp_text_fetch", C.c_int, [vp, u64p, u32p, u32p, vp, u8p]),
+    ("fpm_fp_text_refs", C.c_int, [vp, C.c_uint64, u64p, u64p, u64p, u32p, u64p]),
     ("fpm_fp_text_free", None, [vp]),
     ("fpm_compare_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p, C.c_uint64,
                                    C.c_uint32, C.c_uint32, C.c_uint32, u32p, u32p]),
@@ -730,6 +731,32 @@ class Context:
             lib().fpm_fp_text_free(job)
         return {"id_off": io[:n], "id_len": il[:n], "n_vals": nv[:n], "hash": h[:n],
                 "new_id": ni[:n]}
+
+    def fp_refs(self, text, max_lines=1_000_000, seed=42, use64=False):
+        """-fp file image -> its References as initFromFingerprints groups them (Sketch.cpp:
+        104-145), grouped on the device (fpm_fp_text_refs): first line, ID (offset, length in
+        the text), length, and the line hashes (the only per-line fetch)."""
+        job, n = vp(), C.c_uint64()
+        _check(lib().fpm_fp_text_stage(self.h, text, len(text), max_lines, seed, int(use64),
+                                       C.byref(job), C.byref(n)))
+        n = n.value
+        try:
+            nr = C.c_uint64()
+            _check(lib().fpm_fp_text_refs(job, 0, C.byref(nr), None, None, None, None))
+            m = nr.value
+            first = np.zeros(max(m, 1), np.uint64)
+            io = np.zeros(max(m, 1), np.uint64)
+            il = np.zeros(max(m, 1), np.uint32)
+            ln = np.zeros(max(m, 1), np.uint64)
+            if m:
+                _check(lib().fpm_fp_text_refs(job, m, C.byref(nr), _p(first, u64p), _p(io, u64p),
+                                              _p(il, u32p), _p(ln, u64p)))
+            h = np.zeros(max(n, 1), np.uint64 if use64 else np.uint32)
+            _check(lib().fpm_fp_text_fetch(job, None, None, None, h.ctypes.data, None))
+        finally:
+            lib().fpm_fp_text_free(job)
+        return {"first": first[:m], "id_off": io[:m], "id_len": il[:m], "length": ln[:m],
+                "hash": h[:n], "n_lines": n}
 
     def positional(self, ref_lists, qry_lists, use64=False, max_dist=1.0, max_pvalue=1.0):
         """triangle -fp's positional compare over the grid (query-major)."""

@@ -586,6 +586,7 @@ void Sketch::initFromFingerprints(const std::vector<std::string> &files, const P
                       << std::endl;
             fatalExit();
         }
+        phaseMark("fingerprint file read");
         // parse + hash on the device (getline / `iss >> id` / `while (iss >> v)` /
         // getHashFingerPrint per line, Sketch.cpp:82-101, 131), at most the lines left
         // of the global cap
@@ -595,41 +596,51 @@ void Sketch::initFromFingerprints(const std::vector<std::string> &files, const P
         check(fpm_fp_text_stage(device(), text.data(), text.size(), remaining, parameters.seed,
                                 parameters.use64, &job, &n),
               "fingerprint parse");
-        std::vector<uint64_t> idOff(n), h64(parameters.use64 ? n : 0);
-        std::vector<uint32_t> idLen(n), nVals(n), h32(parameters.use64 ? 0 : n);
-        std::vector<uint8_t> newId(n);
-        const int rc = fpm_fp_text_fetch(job, idOff.data(), idLen.data(), nVals.data(),
-                                         parameters.use64 ? (void *)h64.data() : (void *)h32.data(),
-                                         newId.data());
+        // the lines' References grouped on the device (:104-145): their first lines, IDs and
+        // lengths; the host fetches those and the line hashes only
+        uint64_t nr = 0;
+        std::vector<uint64_t> first, idOff, len;
+        std::vector<uint32_t> idLen;
+        int rc = fpm_fp_text_refs(job, 0, &nr, nullptr, nullptr, nullptr, nullptr);
+        if (rc == FPM_OK && nr) {
+            first.resize(nr);
+            idOff.resize(nr);
+            idLen.resize(nr);
+            len.resize(nr);
+            rc = fpm_fp_text_refs(job, nr, &nr, first.data(), idOff.data(), idLen.data(),
+                                  len.data());
+        }
+        std::vector<uint64_t> h64(parameters.use64 ? n : 0);
+        std::vector<uint32_t> h32(parameters.use64 ? 0 : n);
+        if (rc == FPM_OK)
+            rc = fpm_fp_text_fetch(job, nullptr, nullptr, nullptr,
+                                   parameters.use64 ? (void *)h64.data() : (void *)h32.data(),
+                                   nullptr);
         fpm_fp_text_free(job);
         check(rc, "fingerprint parse");
         counterLine += n;
-        // group lines into References: a new one wherever the ID changes (:104-129)
-        Reference *cur = nullptr;
-        std::vector<Reference> fileRefs;
-        for (uint64_t i = 0; i < n; i++) {
-            const uint64_t nv = nVals[i];
-            const bool isNew = i == 0 ? std::string(text.data() + idOff[0], idLen[0]) != lastID
-                                      : newId[i] != 0;
-            if (isNew) {
-                const std::string id(text.data() + idOff[i], idLen[i]);
-                fileRefs.emplace_back();
-                cur = &fileRefs.back();
-                cur->id = id;
-                cur->length = nv;
-                cur->name = id;
-                cur->comment = "FingerPrint : " + id;
-            }
-            if (!cur) {
-                // the reference dereferences a null Reference here (Sketch.cpp:131-134)
-                std::cerr << "ERROR: fingerprint line " << i + 1 << " of " << file
-                          << " continues ID \"" << lastID << "\" from a previous file." << std::endl;
-                fatalExit();
-            }
-            cur->hashes.push_back(parameters.use64 ? h64[i] : (uint64_t)h32[i]);
-            cur->length += nv;
+        if (nr && std::string(text.data() + idOff[0], idLen[0]) == lastID) {
+            // line 0 continues the previous file's last ID: the reference dereferences a null
+            // Reference here (Sketch.cpp:131-134, the Reference pointer is reset per file)
+            std::cerr << "ERROR: fingerprint line 1 of " << file << " continues ID \"" << lastID
+                      << "\" from a previous file." << std::endl;
+            fatalExit();
         }
-        if (n) lastID.assign(text.data() + idOff[n - 1], idLen[n - 1]);
+        std::vector<Reference> fileRefs(nr);
+        for (uint64_t r = 0; r < nr; r++) {
+            Reference &ref = fileRefs[r];
+            const std::string id(text.data() + idOff[r], idLen[r]);
+            ref.id = id;
+            ref.length = len[r];
+            ref.name = id;
+            ref.comment = "FingerPrint : " + id;
+            const uint64_t a = first[r], b = r + 1 < nr ? first[r + 1] : n;
+            ref.hashes.resize(b - a);
+            for (uint64_t i = a; i < b; i++)
+                ref.hashes[i - a] = parameters.use64 ? h64[i] : (uint64_t)h32[i];
+        }
+        if (nr) lastID.assign(text.data() + idOff[nr - 1], idLen[nr - 1]);
+        phaseMark("fingerprint parse + references (device)");
         for (auto &r : fileRefs) references.push_back(std::move(r));
     }
     createIndex();

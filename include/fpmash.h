@@ -229,6 +229,16 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
                       uint32_t seed, uint32_t use64, fpm_fptext **job, uint64_t *n_lines);
 int fpm_fp_text_fetch(fpm_fptext *job, uint64_t *id_off, uint32_t *id_len, uint32_t *n_vals,
                       void *hash, uint8_t *new_id);
+/* The References the staged file's lines make (Sketch.cpp:104-145, the grouping of
+ * initFromFingerprints): one at line 0 (the caller checks its ID against the previous file's
+ * last ID: equal IDs across files crash the reference, :131) and one wherever the ID changes.
+ * Per Reference: its first line, its ID (byte offset, length in the text) and its length (the
+ * first line's value count, :117, plus every line's, :134).  Computed on the device on the
+ * first call; *n_refs is always set, the arrays are filled when cap >= *n_refs (a first call
+ * with cap 0 sizes them).  With it a caller fetches only the hashes (fpm_fp_text_fetch with
+ * the other outputs NULL): 4 B per line instead of 21. */
+int fpm_fp_text_refs(fpm_fptext *job, uint64_t cap, uint64_t *n_refs, uint64_t *first_line,
+                     uint64_t *id_off, uint32_t *id_len, uint64_t *length);
 void fpm_fp_text_free(fpm_fptext *job);
 
 /* ---- dist ---------------------------------------------------------------------

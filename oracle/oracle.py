@@ -105,6 +105,8 @@ def ref():
         R.ref_kseq_records.argtypes = [C.c_char_p, u64p, C.POINTER(C.c_int), u64p]
         R.ref_kseq_scan.restype = C.c_int
         R.ref_kseq_scan.argtypes = [C.c_char_p, u64p, u64p]
+        R.ref_fp_sketch_file.restype = C.c_longlong
+        R.ref_fp_sketch_file.argtypes = [C.c_char_p, C.c_ulonglong, u64p, C.c_uint, C.c_int, u64p]
         R.ref_free.argtypes = [C.c_void_p]
         _REF = R
     return _REF
@@ -159,6 +161,24 @@ def ref_kseq_records(path):
             at += 8 + ln
         recs.append(tuple(f))
     return recs, st.value
+
+
+def ref_fp_sketch_files(paths, limit=1_000_000, seed=42, use64=False):
+    """initFromFingerprints' per-file loop (istringstream parse, the reference's compiled
+    getHashFingerPrint, HashList::add) over `paths` on one thread, the line budget shared as
+    in one call: (references, lines, hash checksum), or None when oracle/_ref is not built.
+    A timing source for the CPU same-work leg of `sketch -fp`, not a parity source."""
+    R = ref()
+    if R is None:
+        return None
+    used, hsum, refs = C.c_uint64(0), C.c_uint64(0), 0
+    for path in paths:
+        n = R.ref_fp_sketch_file(os.fsencode(path), limit, C.byref(used), seed, int(use64),
+                                 C.byref(hsum))
+        if n < 0:
+            raise OSError(f"cannot open {path}")
+        refs += n
+    return refs, used.value, hsum.value
 
 
 def ref_kseq_scan(path):

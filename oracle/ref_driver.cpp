@@ -13,10 +13,14 @@
 #include "hash.h"
 #include "MinHashHeap.h"
 
+#include "HashList.h"
+
 #include <zlib.h>
 #include <atomic>
 #include <cstdlib>
 #include <cstring>
+#include <fstream>
+#include <sstream>
 #include <string>
 #include <thread>
 #include <vector>
@@ -215,6 +219,55 @@ int ref_kseq_scan(const char *path, unsigned long long *n_rec, unsigned long lon
     *n_rec = c;
     *n_bases = b;
     return l;
+}
+
+// The per-file work of Sketch::initFromFingerprints (Sketch.cpp:67-145), restated around the
+// reference's own getHashFingerPrint (hash.cpp:45-73) and HashList::add (HashList.h:27-33), on
+// one thread as the reference runs it: std::getline per line (at most `limit` lines counted
+// across the call's files, :37, :82), `istringstream >> id`, `>> number` until it fails (a
+// space after a number skipped), a new Reference wherever the ID differs from the previous
+// line's, its length the first line's count plus every line's.  For the bench's CPU
+// same-work leg of `sketch -fp` (timed, not a parity source: the oracle's C restatement
+// pins the parse).  Returns the References made, or -1 when the file cannot be opened;
+// *lines_used accumulates, *hash_sum is a checksum over every hash.
+long long ref_fp_sketch_file(const char *path, unsigned long long limit,
+                             unsigned long long *lines_used, unsigned seed, int use64,
+                             unsigned long long *hash_sum)
+{
+    std::ifstream in(path);
+    if (!in) return -1;
+    struct Ref { std::string id; unsigned long long length = 0; HashList hashes; };
+    std::vector<Ref> refs;
+    std::string line, last;
+    bool open_ref = false;
+    unsigned long long sum = 0;
+    while (*lines_used < limit && std::getline(in, line)) {
+        ++*lines_used;
+        std::istringstream ss(line);
+        std::string id;
+        ss >> id;
+        std::vector<uint64_t> values;
+        uint64_t v;
+        while (ss >> v) {
+            values.push_back(v);
+            if (ss.peek() == ' ') ss.ignore();
+        }
+        if (!open_ref || id != last) {
+            refs.emplace_back();
+            refs.back().id = id;
+            refs.back().length = values.size();
+            refs.back().hashes.setUse64(use64 != 0);
+            last = id;
+            open_ref = true;
+        }
+        const hash_u h = getHashFingerPrint(values, (int)(values.size() * sizeof(uint64_t)), seed,
+                                            use64 != 0);
+        refs.back().hashes.add(h);
+        refs.back().length += values.size();
+        sum += use64 ? h.hash64 : h.hash32;
+    }
+    *hash_sum += sum;
+    return (long long)refs.size();
 }
 
 void ref_free(void *p) { free(p); }

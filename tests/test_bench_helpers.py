@@ -26,25 +26,6 @@ def test_cflgen_matches_python_generator():
     assert datagen.cfl_text_fast(seqs, ids, window=17) == datagen.cfl_text(seqs, ids, window=17)
 
 
-def test_c3_grouping_matches_fixture_lengths(oracle):
-    """bench._group_fp_lines == initFromFingerprints' grouping (Sketch.cpp:104-134): the
-    references, their hash lists and the double-counted first-line length of
-    DNA{1,2,3}-sketch.msh."""
-    import bench
-    for i in (1, 2, 3):
-        text = open(os.path.join(GOLDEN, f"DNA{i}-CFL.txt"), "rb").read()
-        refs, _used, _ = oracle.fp_references(text)
-        ids, vals, _ = oracle.fp_parse(text)
-        r = {"hash": np.array([oracle.get_hash_fp(v, 42, False) for v in vals], np.uint32),
-             "new_id": np.array([1] + [int(a != b) for a, b in zip(ids[1:], ids[:-1])], np.uint8),
-             "n_vals": np.array([len(v) for v in vals], np.uint32)}
-        st, en, ln = bench._group_fp_lines(r, text)
-        assert len(st) == len(refs)
-        for a, b, length, (name, e_len, e_hash) in zip(st, en, ln, refs):
-            assert ids[a] == name and int(length) == e_len
-            assert np.array_equal(r["hash"][a:b], e_hash)
-
-
 def test_c4_row_shards_cover_grid():
     """The C4 leg's query-row blocks partition [0, n) for every GPU count."""
     from fpmash.shard import shard_range

@@ -566,6 +566,30 @@ def test_fp_text_parse_matches_oracle(ctx, oracle, use64):
                 prev = idv
 
 
+@pytest.mark.parametrize("use64", [False, True])
+def test_fp_refs_match_oracle(ctx, oracle, use64):
+    """fpm_fp_text_refs (the References grouped on the device) == initFromFingerprints'
+    grouping of the istream-semantics parse (Sketch.cpp:104-145): a Reference at line 0 and at
+    every ID change, its ID, its length (the first line's value count twice, :117 + :134) and
+    its line hashes, over the edge-case texts, the three CFL fixtures whole, and line caps."""
+    texts = _fp_texts() + [open(os.path.join(GOLDEN, f"DNA{i}-CFL.txt"), "rb").read()
+                           for i in (1, 2, 3)]
+    for t in texts:
+        for cap in (1_000_000, 7, 1, 0):
+            got = ctx.fp_refs(t, max_lines=cap, seed=42, use64=use64)
+            ids, vals, used = oracle.fp_parse(t, limit=cap)
+            assert got["n_lines"] == used
+            heads = [i for i in range(used) if i == 0 or ids[i] != ids[i - 1]]
+            assert list(got["first"]) == heads
+            for r, a in enumerate(heads):
+                b = heads[r + 1] if r + 1 < len(heads) else used
+                o, n = int(got["id_off"][r]), int(got["id_len"][r])
+                assert t[o:o + n] == ids[a]
+                assert int(got["length"][r]) == len(vals[a]) + sum(len(v) for v in vals[a:b])
+                exp_h = [oracle.get_hash_fp(v, 42, use64) for v in vals[a:b]]
+                assert [int(x) for x in got["hash"][a:b]] == exp_h
+
+
 @pytest.mark.parametrize("k,s", [(21, 1000), (21, 5000), (12, 2000), (21, 10000), (21, 16384),
                                  (21, 16385), (21, 50000)])
 def test_sketch_long_groups_sample_bound(ctx, oracle, k, s):
