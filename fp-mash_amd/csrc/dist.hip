@@ -387,15 +387,48 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     }
 }
 
-template <int CAP, typename C>
+// IDS (rows of u32 dense value ids, dist_ids.hip): the ids order and identify the values
+// exactly, so K32 holds B's ids themselves, the NP reads of a's bucket give both j and the
+// equality, and there is no 64-bit confirm read (nor B's values in LDS)
+template <int NP>
+__device__ __forceinline__ uint64_t rank_chunk_ids(const uint32_t *K32, const uint16_t *Bkt,
+                                                   uint32_t shift, uint32_t top, uint32_t lb,
+                                                   uint32_t maxn, uint32_t a, uint32_t &j)
+{
+    const uint32_t t = a >> shift;
+    const uint32_t lo = Bkt[t > top ? top + 1 : t];
+    uint32_t p = lo;
+    bool eq = false;
+    if constexpr (NP > 0) {
+#pragma unroll
+        for (int q = 0; q < NP; q++) {
+            const uint32_t k = K32[lo + q];
+            p += k < a ? 1u : 0u;
+            eq |= k == a;
+        }
+    } else {
+        for (uint32_t q = 0; q < maxn; q++) {
+            const uint32_t k = K32[min(lo + q, lb)];
+            p += (k < a && lo + q < lb) ? 1u : 0u;
+            eq |= k == a && lo + q < lb;
+        }
+    }
+    j = p;
+    return __builtin_amdgcn_ballot_w64(eq);
+}
+
+template <int CAP, typename C, bool IDS = false>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
-    uint32_t q_lo, const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len,
-    uint64_t ref_stride, uint32_t n_ref, const uint64_t *__restrict__ qry,
+    uint32_t q_lo, const void *__restrict__ ref_v, const uint32_t *__restrict__ ref_len,
+    uint64_t ref_stride, uint32_t n_ref, const void *__restrict__ qry_v,
     const uint32_t *__restrict__ qry_len, uint64_t qry_stride, uint32_t S, uint32_t sym,
     C *__restrict__ numer, C *__restrict__ denom, uint32_t *__restrict__ cnum,
     uint32_t *__restrict__ cden)
 {
+    using V = std::conditional_t<IDS, uint32_t, uint64_t>;
+    const V *__restrict__ ref = static_cast<const V *>(ref_v);
+    const V *__restrict__ qry = static_cast<const V *>(qry_v);
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? kRankLogB : kRankLogB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
     // fixed-size LDS arrays: their compile-time offsets fold into the ds_read instructions.
@@ -407,7 +440,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // 16 KB: one address add per key read)
     __shared__ struct {
         uint32_t k[CAP + kRankProbeMax];
-        uint64_t v[CAP + kRankProbeMax];
+        uint64_t v[IDS ? 1 : CAP + kRankProbeMax];
     } sKB;
     uint32_t *const K32 = sKB.k;
     uint64_t *const Bs = sKB.v;
@@ -423,14 +456,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t base = seg >> 24;
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
-    const uint64_t *B = qry + (uint64_t)q * qry_stride;
+    const V *B = qry + (uint64_t)q * qry_stride;
     if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; }
     {
         // stage B: every load of the row issued before the first LDS store (4 in flight per
         // thread: CAP / 256 with CAP 1024; a serial load-store loop paid the global latency
         // once per value)
         constexpr int kStage = (CAP + 64 * kRankWaves - 1) / (64 * kRankWaves);
-        uint64_t v[kStage];
+        V v[kStage];
 #pragma unroll
         for (int u = 0; u < kStage; u++) {
             const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
@@ -439,16 +472,19 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kStage; u++) {
             const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            if (t < lb) Bs[t] = v[u];
+            if (t < lb) {
+                if constexpr (IDS) K32[t] = v[u];
+                else Bs[t] = v[u];
+            }
         }
     }
-    // sentinels past the end: no A value is below them
+    // sentinels past the end: no A value is below them (ids are < 2^31)
     if (threadIdx.x < kRankProbeMax) {
-        Bs[lb + threadIdx.x] = ~0ULL;
+        if constexpr (!IDS) Bs[lb + threadIdx.x] = ~0ULL;
         K32[lb + threadIdx.x] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    const uint64_t bmax = lb ? Bs[lb - 1] : 0;
+    const uint64_t bmax = lb ? (IDS ? (uint64_t)K32[lb - 1] : Bs[lb - 1]) : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
     const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
     const uint32_t kshift = bits > 32 ? bits - 32 : 0;
@@ -461,8 +497,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // bucket up to its own, so each thread fills one gap.
     uint32_t dup = 0;
     for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
-        const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
-        if (j < lb) {
+        const uint64_t v = j < lb ? (IDS ? (uint64_t)K32[j] : Bs[j]) : 0;
+        const uint64_t vp = j > 0 ? (IDS ? (uint64_t)K32[j - 1] : Bs[j - 1]) : 0;
+        if (!IDS && j < lb) {
             const uint32_t k = (uint32_t)(v >> kshift);
             K32[j] = k;
             dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
@@ -476,7 +513,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // the largest bucket: element j is the (j - Bkt[bucket(j)] + 1)-th of its bucket
     uint32_t mx = 0;
     for (uint32_t j = threadIdx.x; j < lb; j += blockDim.x)
-        mx = max(mx, j + 1 - (uint32_t)Bkt[(uint32_t)(Bs[j] >> shift)]);
+        mx = max(mx, j + 1 - (uint32_t)Bkt[(uint32_t)((IDS ? (uint64_t)K32[j] : Bs[j]) >> shift)]);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
     if (lane == 0 && mx) atomicMax(&s_maxn, mx);
@@ -512,22 +549,28 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(Ar >> 32));
         Row R;
         R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)phi << 32) | plo), 0,
-                                                   (int)__builtin_amdgcn_readfirstlane(ld * 8u),
+                                                   (int)__builtin_amdgcn_readfirstlane(ld * (uint32_t)sizeof(V)),
                                                    0x00020000);
         R.la = ref_len[rr];
         R.o = o;
         return R;
     };
-    struct Pair { uint64_t e0, e1; };
+    struct Pair { V e0, e1; };
     auto load_group = [&](const Row &R, uint32_t gi, Pair (&dst)[kGroup]) {
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
-            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
-            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
+            if constexpr (IDS) {
+                dst[u].e0 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + lane) * 4u, 0, 0);
+                dst[u].e1 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + 64 + lane) * 4u,
                                                                  0, 0);
-            dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
-            dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
+            } else {
+                const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
+                const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
+                                                                     0, 0);
+                dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
+                dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
+            }
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -635,6 +678,19 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #define FPM_RANK_NP(NP_, HI_) \
     run([&](uint64_t a, uint32_t &j) { \
         return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+#define FPM_RANK_ID(NP_) \
+    run([&](uint32_t a, uint32_t &j) { \
+        return rank_chunk_ids<NP_>(k_, bk_, shift, top, lb, maxn, a, j); })
+    if constexpr (IDS) {
+        (void)bs_;
+        switch (np) {
+        case 2: FPM_RANK_ID(2); break;
+        case 3: FPM_RANK_ID(3); break;
+        case 4: FPM_RANK_ID(4); break;
+        case kRankProbeMax: FPM_RANK_ID(kRankProbeMax); break;
+        default: FPM_RANK_ID(0); break;
+        }
+    } else {
     const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
     switch (np) {
     case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;
@@ -643,201 +699,9 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     case kRankProbeMax: FPM_RANK_NP(kRankProbeMax, false); break;
     default: FPM_RANK_NP(0, false); break;
     }
+    }
 #undef FPM_RANK_NP
-}
-
-// The same rank walk on rows of u32 IDS instead of u64 hashes: id = the value's rank among the
-// set's distinct values (fpm dense ids, an order- and equality-preserving map), so B's ids in
-// LDS order and identify its values exactly: j = #{B < a} and a's membership come from the NP
-// id reads of a's directory bucket with no 64-bit confirm read, and A streams 4 B per value.
-// B's directory spans its id range [B[0], B[lb - 1]] in 4096 buckets.
-template <int CAP, typename C>
-__global__ __launch_bounds__(64 * kRankWaves) void rank_ids_kernel(
-    const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
-    uint32_t q_lo, const uint32_t *__restrict__ ref, const uint32_t *__restrict__ ref_len,
-    uint64_t ref_stride, uint32_t n_ref, const uint32_t *__restrict__ qry,
-    const uint32_t *__restrict__ qry_len, uint64_t qry_stride, uint32_t S, uint32_t sym,
-    C *__restrict__ numer, C *__restrict__ denom, uint32_t *__restrict__ cnum,
-    uint32_t *__restrict__ cden)
-{
-    constexpr uint32_t kLogBuckets = (CAP <= 1024) ? kRankLogB : kRankLogB + 1;
-    constexpr uint32_t kBuckets = 1u << kLogBuckets;
-    __shared__ uint32_t K[CAP + kRankProbeMax];
-    __shared__ uint16_t Bkt[kBuckets + 1];
-    __shared__ uint32_t s_maxn;
-    const uint32_t qr = xcd_row(blockIdx.x, n_qry);
-    if (qr >= n_qry) return;
-    const uint32_t q = q_lo + qr;
-    const uint64_t seg = row_seg[q];
-    const uint32_t n = (uint32_t)(seg & 0xFFFFFF);
-    if (n == 0) return;
-    const uint64_t base = seg >> 24;
-    const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t lb = qry_len[q];
-    const uint32_t *B = qry + (uint64_t)q * qry_stride;
-    if (threadIdx.x == 0) s_maxn = 0;
-    {
-        constexpr int kStage = (CAP + 64 * kRankWaves - 1) / (64 * kRankWaves);
-        uint32_t v[kStage];
-#pragma unroll
-        for (int u = 0; u < kStage; u++) {
-            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            v[u] = t < lb ? B[t] : 0u;
-        }
-#pragma unroll
-        for (int u = 0; u < kStage; u++) {
-            const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            if (t < lb) K[t] = v[u];
-        }
-    }
-    if (threadIdx.x < kRankProbeMax) K[lb + threadIdx.x] = 0xFFFFFFFFu;   // above every id
-    __syncthreads();
-    const uint32_t bmin = lb ? K[0] : 0u, bmax = lb ? K[lb - 1] : 0u;
-    const uint32_t span = bmax - bmin;
-    const uint32_t bits = span ? 32 - __clz(span) : 0;
-    const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
-    const uint32_t top = span >> shift;                       // the last B id's bucket
-    for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
-        const uint32_t bj = j < lb ? (K[j] - bmin) >> shift : top + 1;
-        const uint32_t bp = j > 0 ? ((K[j - 1] - bmin) >> shift) + 1 : 0;
-        for (uint32_t b = bp; b <= bj; b++) Bkt[b] = (uint16_t)j;
-    }
-    __syncthreads();
-    uint32_t mx = 0;
-    for (uint32_t j = threadIdx.x; j < lb; j += blockDim.x)
-        mx = max(mx, j + 1 - (uint32_t)Bkt[(K[j] - bmin) >> shift]);
-#pragma unroll
-    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
-    if (lane == 0 && mx) atomicMax(&s_maxn, mx);
-    __syncthreads();
-    const uint32_t maxn = s_maxn;
-    const uint32_t np = maxn <= 2 ? 2u : maxn <= 3 ? 3u : maxn <= 4 ? 4u
-                      : maxn <= (uint32_t)kRankProbeMax ? (uint32_t)kRankProbeMax : 0u;
-
-    const uint32_t ld = ref_stride < (uint64_t)CAP ? (uint32_t)ref_stride : (uint32_t)CAP;
-    const uint64_t pair_row = (uint64_t)q * n_ref;
-    constexpr uint32_t kChunk = 128;
-    struct Row { __amdgpu_buffer_rsrc_t rsrc; uint32_t la; uint64_t o; };
-    auto open_row = [&](uint64_t o) -> Row {
-        const uint32_t rr = __builtin_amdgcn_readfirstlane((uint32_t)(o - pair_row));
-        const uintptr_t Ar = (uintptr_t)(ref + (uint64_t)rr * ref_stride);
-        const uint32_t plo = __builtin_amdgcn_readfirstlane((uint32_t)Ar);
-        const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(Ar >> 32));
-        Row R;
-        R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)phi << 32) | plo), 0,
-                                                   (int)__builtin_amdgcn_readfirstlane(ld * 4u),
-                                                   0x00020000);
-        R.la = ref_len[rr];
-        R.o = o;
-        return R;
-    };
-    struct Pair { uint32_t e0, e1; };
-    auto load_chunk = [&](const Row &R, uint32_t t) -> Pair {
-        Pair P;
-        P.e0 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + lane) * 4u, 0, 0);
-        P.e1 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + 64 + lane) * 4u, 0, 0);
-        return P;
-    };
-    auto cand_at = [&](uint32_t cc) -> uint64_t {
-        return cand[base + __builtin_amdgcn_readfirstlane(cc)];
-    };
-    // j = #{B < a}, and the wave mask of the lanes whose a is in B
-    auto probe = [&](auto NPc, uint32_t a, uint32_t &j) -> uint64_t {
-        constexpr int NP = decltype(NPc)::value;
-        const uint32_t t = a <= bmin ? 0u : min((a - bmin) >> shift, top + 1);
-        const uint32_t lo = Bkt[t];
-        if constexpr (NP > 0) {
-            uint32_t p = lo;
-            bool eq = false;
-#pragma unroll
-            for (int u = 0; u < NP; u++) {
-                const uint32_t k = K[lo + u];
-                p += k < a ? 1u : 0u;
-                eq |= k == a;
-            }
-            j = p;
-            return __builtin_amdgcn_ballot_w64(eq);
-        } else {
-            uint32_t jj = lo;
-            bool eq = false;
-            for (uint32_t u = 0; u < maxn; u++) {
-                const uint32_t k = K[min(lo + u, lb)];
-                jj += (k < a && lo + u < lb) ? 1u : 0u;
-                eq |= k == a && lo + u < lb;
-            }
-            j = jj;
-            return __builtin_amdgcn_ballot_w64(eq);
-        }
-    };
-    auto run = [&](auto NPc) {
-        Pair cur, nxt, pf;
-        Row Rc{};
-        if (wave < n) { Rc = open_row(cand_at(wave)); pf = load_chunk(Rc, 0); }
-        for (uint32_t c = wave; c < n; c += kRankWaves) {
-            const Row R = Rc;
-            cur = pf;
-            if (c + kRankWaves < n) { Rc = open_row(cand_at(c + kRankWaves)); pf = load_chunk(Rc, 0); }
-            const uint32_t la = R.la;
-            const bool need_all = la < S && lb < S;
-            const uint32_t nch = (la + kChunk - 1) / kChunk;
-            const int rl = (int)la - (int)(nch - 1) * (int)kChunk;
-            const int r0 = min(rl, 64), r1 = rl - 64;
-            const uint64_t vl0 = r0 >= 64 ? ~0ULL : r0 > 0 ? (1ULL << r0) - 1 : 0ULL;
-            const uint64_t vl1 = r1 >= 64 ? ~0ULL : r1 > 0 ? (1ULL << r1) - 1 : 0ULL;
-            uint32_t shared_below = 0, cnt = 0;
-            const uint32_t s_exit = need_all ? 0xFFFFFFFFu : S;
-            auto chunk = [&](uint32_t t, uint64_t vm0, uint64_t vm1) -> uint32_t {
-                uint32_t j0, j1;
-                const uint64_t m0 = probe(NPc, cur.e0, j0) & vm0;
-                const uint64_t m1 = probe(NPc, cur.e1, j1) & vm1;
-                const uint32_t i0 = t * kChunk;
-                const uint32_t b0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m0 >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m0, 0u));
-                const uint32_t b1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(m1 >> 32),
-                                                              __builtin_amdgcn_mbcnt_lo((uint32_t)m1, 0u));
-                const uint32_t k0 = shared_below + b0;
-                const uint32_t k1 = shared_below + (uint32_t)__popcll(m0) + b1;
-                const uint32_t u0 = i0 + lane + j0 - k0, u1 = i0 + 64 + lane + j1 - k1;
-                cnt += __popcll(m0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
-                       __popcll(m1 & __builtin_amdgcn_ballot_w64(u1 < S));
-                shared_below += __popcll(m0) + __popcll(m1);
-                return (uint32_t)__builtin_amdgcn_readlane((int)u1, 63);
-            };
-            bool exited = false;
-            uint32_t t = 0;
-            for (; t + 1 < nch; t++) {
-                nxt = load_chunk(R, t + 1);
-                if (chunk(t, ~0ULL, ~0ULL) >= s_exit) { exited = true; break; }
-                cur = nxt;
-            }
-            if (!exited && nch) chunk(t, vl0, vl1);
-            if (lane == 0) {
-                const uint64_t un = (uint64_t)la + lb - shared_below;
-                const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
-                if (cnum) {
-                    cnum[base + c] = cnt;
-                    cden[base + c] = dn;
-                    continue;
-                }
-                const uint64_t o = R.o;
-                numer[o] = (C)cnt;
-                denom[o] = (C)dn;
-                const uint32_t r = (uint32_t)(o - pair_row);
-                if (sym && r != q) {
-                    const uint64_t o2 = (uint64_t)r * n_ref + q;
-                    numer[o2] = (C)cnt;
-                    denom[o2] = (C)dn;
-                }
-            }
-        }
-    };
-    switch (np) {
-    case 2: run(std::integral_constant<int, 2>{}); break;
-    case 3: run(std::integral_constant<int, 3>{}); break;
-    case 4: run(std::integral_constant<int, 4>{}); break;
-    case kRankProbeMax: run(std::integral_constant<int, kRankProbeMax>{}); break;
-    default: run(std::integral_constant<int, 0>{}); break;
-    }
+#undef FPM_RANK_ID
 }
 
 template <typename C>
@@ -850,13 +714,13 @@ static hipError_t rank_ids_c(const uint64_t *d_cand, const uint64_t *row_seg, ui
     const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
     const uint64_t cap = std::max(ref_stride, qry_stride);
     if (cap <= 1024)
-        hipLaunchKernelGGL((rank_ids_kernel<1024, C>), g, b, 0, st, d_cand, row_seg, n_qry, q_lo,
-                           d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
-                           (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
+        hipLaunchKernelGGL((rank_rows_kernel<1024, C, true>), g, b, 0, st, d_cand, row_seg, n_qry,
+                           q_lo, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
+                           S, (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else if (cap <= 2048)
-        hipLaunchKernelGGL((rank_ids_kernel<2048, C>), g, b, 0, st, d_cand, row_seg, n_qry, q_lo,
-                           d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride, S,
-                           (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
+        hipLaunchKernelGGL((rank_rows_kernel<2048, C, true>), g, b, 0, st, d_cand, row_seg, n_qry,
+                           q_lo, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
+                           S, (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
