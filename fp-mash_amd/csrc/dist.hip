@@ -12,8 +12,6 @@
 #include "fpm_device.hpp"
 #include "fpm_kernels.hpp"
 
-#include <type_traits>
-
 // Floating-point expressions are evaluated as written, one rounding per operation: no
 // multiply-add contraction (HIP's default contracts a*b + c into one FMA).  The reference's
 // distance and GSL p-value arithmetic is x86-64 double code without FMA, and contracting here
@@ -387,48 +385,15 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     }
 }
 
-// IDS (rows of u32 dense value ids, dist_ids.hip): the ids order and identify the values
-// exactly, so K32 holds B's ids themselves, the NP reads of a's bucket give both j and the
-// equality, and there is no 64-bit confirm read (nor B's values in LDS)
-template <int NP>
-__device__ __forceinline__ uint64_t rank_chunk_ids(const uint32_t *K32, const uint16_t *Bkt,
-                                                   uint32_t shift, uint32_t top, uint32_t lb,
-                                                   uint32_t maxn, uint32_t a, uint32_t &j)
-{
-    const uint32_t t = a >> shift;
-    const uint32_t lo = Bkt[t > top ? top + 1 : t];
-    uint32_t p = lo;
-    bool eq = false;
-    if constexpr (NP > 0) {
-#pragma unroll
-        for (int q = 0; q < NP; q++) {
-            const uint32_t k = K32[lo + q];
-            p += k < a ? 1u : 0u;
-            eq |= k == a;
-        }
-    } else {
-        for (uint32_t q = 0; q < maxn; q++) {
-            const uint32_t k = K32[min(lo + q, lb)];
-            p += (k < a && lo + q < lb) ? 1u : 0u;
-            eq |= k == a && lo + q < lb;
-        }
-    }
-    j = p;
-    return __builtin_amdgcn_ballot_w64(eq);
-}
-
-template <int CAP, typename C, bool IDS = false>
+template <int CAP, typename C>
 __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t *__restrict__ cand, const uint64_t *__restrict__ row_seg, uint32_t n_qry,
-    uint32_t q_lo, const void *__restrict__ ref_v, const uint32_t *__restrict__ ref_len,
-    uint64_t ref_stride, uint32_t n_ref, const void *__restrict__ qry_v,
+    uint32_t q_lo, const uint64_t *__restrict__ ref, const uint32_t *__restrict__ ref_len,
+    uint64_t ref_stride, uint32_t n_ref, const uint64_t *__restrict__ qry,
     const uint32_t *__restrict__ qry_len, uint64_t qry_stride, uint32_t S, uint32_t sym,
     C *__restrict__ numer, C *__restrict__ denom, uint32_t *__restrict__ cnum,
     uint32_t *__restrict__ cden)
 {
-    using V = std::conditional_t<IDS, uint32_t, uint64_t>;
-    const V *__restrict__ ref = static_cast<const V *>(ref_v);
-    const V *__restrict__ qry = static_cast<const V *>(qry_v);
     constexpr uint32_t kLogBuckets = (CAP <= 1024) ? kRankLogB : kRankLogB + 1;
     constexpr uint32_t kBuckets = 1u << kLogBuckets;
     // fixed-size LDS arrays: their compile-time offsets fold into the ds_read instructions.
@@ -440,7 +405,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // 16 KB: one address add per key read)
     __shared__ struct {
         uint32_t k[CAP + kRankProbeMax];
-        uint64_t v[IDS ? 1 : CAP + kRankProbeMax];
+        uint64_t v[CAP + kRankProbeMax];
     } sKB;
     uint32_t *const K32 = sKB.k;
     uint64_t *const Bs = sKB.v;
@@ -456,14 +421,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t base = seg >> 24;
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
-    const V *B = qry + (uint64_t)q * qry_stride;
+    const uint64_t *B = qry + (uint64_t)q * qry_stride;
     if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; }
     {
         // stage B: every load of the row issued before the first LDS store (4 in flight per
         // thread: CAP / 256 with CAP 1024; a serial load-store loop paid the global latency
         // once per value)
         constexpr int kStage = (CAP + 64 * kRankWaves - 1) / (64 * kRankWaves);
-        V v[kStage];
+        uint64_t v[kStage];
 #pragma unroll
         for (int u = 0; u < kStage; u++) {
             const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
@@ -472,19 +437,16 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #pragma unroll
         for (int u = 0; u < kStage; u++) {
             const uint32_t t = threadIdx.x + u * 64 * kRankWaves;
-            if (t < lb) {
-                if constexpr (IDS) K32[t] = v[u];
-                else Bs[t] = v[u];
-            }
+            if (t < lb) Bs[t] = v[u];
         }
     }
-    // sentinels past the end: no A value is below them (ids are < 2^31)
+    // sentinels past the end: no A value is below them
     if (threadIdx.x < kRankProbeMax) {
-        if constexpr (!IDS) Bs[lb + threadIdx.x] = ~0ULL;
+        Bs[lb + threadIdx.x] = ~0ULL;
         K32[lb + threadIdx.x] = 0xFFFFFFFFu;
     }
     __syncthreads();
-    const uint64_t bmax = lb ? (IDS ? (uint64_t)K32[lb - 1] : Bs[lb - 1]) : 0;
+    const uint64_t bmax = lb ? Bs[lb - 1] : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
     const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
     const uint32_t kshift = bits > 32 ? bits - 32 : 0;
@@ -497,9 +459,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // bucket up to its own, so each thread fills one gap.
     uint32_t dup = 0;
     for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
-        const uint64_t v = j < lb ? (IDS ? (uint64_t)K32[j] : Bs[j]) : 0;
-        const uint64_t vp = j > 0 ? (IDS ? (uint64_t)K32[j - 1] : Bs[j - 1]) : 0;
-        if (!IDS && j < lb) {
+        const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
+        if (j < lb) {
             const uint32_t k = (uint32_t)(v >> kshift);
             K32[j] = k;
             dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
@@ -513,7 +474,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // the largest bucket: element j is the (j - Bkt[bucket(j)] + 1)-th of its bucket
     uint32_t mx = 0;
     for (uint32_t j = threadIdx.x; j < lb; j += blockDim.x)
-        mx = max(mx, j + 1 - (uint32_t)Bkt[(uint32_t)((IDS ? (uint64_t)K32[j] : Bs[j]) >> shift)]);
+        mx = max(mx, j + 1 - (uint32_t)Bkt[(uint32_t)(Bs[j] >> shift)]);
 #pragma unroll
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
     if (lane == 0 && mx) atomicMax(&s_maxn, mx);
@@ -549,28 +510,22 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         const uint32_t phi = __builtin_amdgcn_readfirstlane((uint32_t)(Ar >> 32));
         Row R;
         R.rsrc = __builtin_amdgcn_make_buffer_rsrc((void *)(((uintptr_t)phi << 32) | plo), 0,
-                                                   (int)__builtin_amdgcn_readfirstlane(ld * (uint32_t)sizeof(V)),
+                                                   (int)__builtin_amdgcn_readfirstlane(ld * 8u),
                                                    0x00020000);
         R.la = ref_len[rr];
         R.o = o;
         return R;
     };
-    struct Pair { V e0, e1; };
+    struct Pair { uint64_t e0, e1; };
     auto load_group = [&](const Row &R, uint32_t gi, Pair (&dst)[kGroup]) {
 #pragma unroll
         for (int u = 0; u < kGroup; u++) {
             const uint32_t t = gi * kGroup + u;
-            if constexpr (IDS) {
-                dst[u].e0 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + lane) * 4u, 0, 0);
-                dst[u].e1 = __builtin_amdgcn_raw_buffer_load_b32(R.rsrc, (t * kChunk + 64 + lane) * 4u,
+            const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
+            const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
                                                                  0, 0);
-            } else {
-                const auto v0 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + lane) * 8u, 0, 0);
-                const auto v1 = __builtin_amdgcn_raw_buffer_load_b64(R.rsrc, (t * kChunk + 64 + lane) * 8u,
-                                                                     0, 0);
-                dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
-                dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
-            }
+            dst[u].e0 = ((uint64_t)v0[1] << 32) | v0[0];
+            dst[u].e1 = ((uint64_t)v1[1] << 32) | v1[0];
         }
     };
     auto cand_at = [&](uint32_t cc) -> uint64_t {
@@ -678,19 +633,6 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
 #define FPM_RANK_NP(NP_, HI_) \
     run([&](uint64_t a, uint32_t &j) { \
         return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
-#define FPM_RANK_ID(NP_) \
-    run([&](uint32_t a, uint32_t &j) { \
-        return rank_chunk_ids<NP_>(k_, bk_, shift, top, lb, maxn, a, j); })
-    if constexpr (IDS) {
-        (void)bs_;
-        switch (np) {
-        case 2: FPM_RANK_ID(2); break;
-        case 3: FPM_RANK_ID(3); break;
-        case 4: FPM_RANK_ID(4); break;
-        case kRankProbeMax: FPM_RANK_ID(kRankProbeMax); break;
-        default: FPM_RANK_ID(0); break;
-        }
-    } else {
     const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
     switch (np) {
     case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;
@@ -699,47 +641,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     case kRankProbeMax: FPM_RANK_NP(kRankProbeMax, false); break;
     default: FPM_RANK_NP(0, false); break;
     }
-    }
 #undef FPM_RANK_NP
-#undef FPM_RANK_ID
-}
-
-template <typename C>
-static hipError_t rank_ids_c(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                             const uint32_t *d_ref, const uint32_t *d_ref_len, uint64_t ref_stride,
-                             uint32_t n_ref, const uint32_t *d_qry, const uint32_t *d_qry_len,
-                             uint64_t qry_stride, uint32_t S, bool sym, C *d_numer, C *d_denom,
-                             uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st, uint32_t q_lo)
-{
-    const dim3 g(xcd_grid(n_qry)), b(64 * kRankWaves);
-    const uint64_t cap = std::max(ref_stride, qry_stride);
-    if (cap <= 1024)
-        hipLaunchKernelGGL((rank_rows_kernel<1024, C, true>), g, b, 0, st, d_cand, row_seg, n_qry,
-                           q_lo, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
-                           S, (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
-    else if (cap <= 2048)
-        hipLaunchKernelGGL((rank_rows_kernel<2048, C, true>), g, b, 0, st, d_cand, row_seg, n_qry,
-                           q_lo, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len, qry_stride,
-                           S, (uint32_t)sym, d_numer, d_denom, d_cnum, d_cden);
-    else
-        return hipErrorInvalidValue;
-    return hipGetLastError();
-}
-
-hipError_t launch_rank_ids(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                           const uint32_t *d_ref_ids, const uint32_t *d_ref_len, uint64_t ref_stride,
-                           uint32_t n_ref, const uint32_t *d_qry_ids, const uint32_t *d_qry_len,
-                           uint64_t qry_stride, uint32_t S, bool sym, Counts cnt, uint32_t *d_cnum,
-                           uint32_t *d_cden, hipStream_t st, uint32_t q_lo)
-{
-    if (!n_qry) return hipSuccess;
-    if (cnt.c16)
-        return rank_ids_c(d_cand, row_seg, n_qry, d_ref_ids, d_ref_len, ref_stride, n_ref,
-                          d_qry_ids, d_qry_len, qry_stride, S, sym, (uint16_t *)cnt.numer,
-                          (uint16_t *)cnt.denom, d_cnum, d_cden, st, q_lo);
-    return rank_ids_c(d_cand, row_seg, n_qry, d_ref_ids, d_ref_len, ref_stride, n_ref, d_qry_ids,
-                      d_qry_len, qry_stride, S, sym, (uint32_t *)cnt.numer, (uint32_t *)cnt.denom,
-                      d_cnum, d_cden, st, q_lo);
 }
 
 template <typename C>

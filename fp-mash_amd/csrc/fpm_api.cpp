@@ -143,7 +143,7 @@ struct fpm_ctx {
     std::vector<std::pair<hipEvent_t, hipEvent_t>> ev[FPM_K_COUNT];
     // grow-only device scratch, one buffer per named slot (no allocation in steady state)
     struct Slot { void *p = nullptr; size_t bytes = 0; };
-    Slot scratch[24];
+    Slot scratch[22];
     unsigned long long *host_counters = nullptr;   // pinned + mapped, for the events read-back
     unsigned long long *dev_counters = nullptr;    // its device-side address
     unsigned long long pub_seq = 0;                // last sequence number published into it
@@ -2050,13 +2050,6 @@ static const bool g_idx_one_pass = [] {
     return !(v && v[0] == '0');
 }();
 
-// FPM_RANK_IDS=1 (experiment, A/B): a set against itself walks dense u32 value ids
-// (dist_ids.hip) in the candidate compare instead of the u64 hashes
-static const bool g_rank_ids = [] {
-    const char *v = getenv("FPM_RANK_IDS");
-    return v && v[0] == '1';
-}();
-
 static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
 {
     IdxGeom geom{};
@@ -2543,25 +2536,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 if (int rc = launch_fill(true)) return rc;
             }
             if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
-            uint32_t *d_ids = nullptr;
-            if (g_rank_ids && rows_merge && self_set) {
-                const size_t sb = dense_ids_scratch((uint64_t)n_ref * ref_stride);
-                void *sc, *ids;
-                HIP_TRY(scratch(ctx, 21, sb, &sc));
-                HIP_TRY(scratch(ctx, 22, (size_t)n_ref * ref_stride * 4, &ids));
-                d_ids = (uint32_t *)ids;
-                TimedLaunch tl(ctx, FPM_K_INDEX, st);
-                HIP_TRY(launch_dense_ids((const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref, sc,
-                                         sb, d_ids, st));
-                tl.done();
-            }
             {
                 TimedLaunch tl(ctx, FPM_K_COMPARE, st);
-                if (d_ids)
-                    HIP_TRY(launch_rank_ids((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
-                                            d_ids, d_ref_len, ref_stride, n_ref, d_ids, d_qry_len,
-                                            qry_stride, sketch_size, sym, cnt, cnum, cden, st));
-                else if (rows_merge)
+                if (rows_merge)
                     HIP_TRY(launch_merge_rows((const uint64_t *)cand, (const uint64_t *)row_seg, n_qry,
                                               (const uint64_t *)d_ref, d_ref_len, ref_stride, n_ref,
                                               (const uint64_t *)d_qry, d_qry_len, qry_stride,

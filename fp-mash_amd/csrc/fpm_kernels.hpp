@@ -218,18 +218,6 @@ hipError_t launch_merge_rows(const uint64_t *d_cand, const uint64_t *row_seg, ui
                              uint32_t *d_cnum, uint32_t *d_cden, hipStream_t st, uint32_t q_lo = 0);
 // (d_cnum, d_cden non-null: results go to candidate slot c instead of the grid cells;
 // q_lo, n_qry: the query rows [q_lo, q_lo + n_qry), whose probe has run)
-// dense value ids of a u64 sketch set (dist_ids.hip, experiment): d_ids[cell] = the rank of the
-// cell's value among the set's distinct values
-size_t dense_ids_scratch(uint64_t E);
-hipError_t launch_dense_ids(const uint64_t *d_rows, const uint32_t *d_len, uint64_t stride,
-                            uint32_t n_rows, void *scratch, size_t scratch_bytes, uint32_t *d_ids,
-                            hipStream_t st);
-// the same on rows of u32 dense value ids (dense_ids) instead of the u64 hashes
-hipError_t launch_rank_ids(const uint64_t *d_cand, const uint64_t *row_seg, uint32_t n_qry,
-                           const uint32_t *d_ref_ids, const uint32_t *d_ref_len, uint64_t ref_stride,
-                           uint32_t n_ref, const uint32_t *d_qry_ids, const uint32_t *d_qry_len,
-                           uint64_t qry_stride, uint32_t S, bool sym, Counts cnt, uint32_t *d_cnum,
-                           uint32_t *d_cden, hipStream_t st, uint32_t q_lo = 0);
 
 // -fp CFL text: newline index, then one lane per line (fingerprint.hip)
 uint32_t text_blocks(uint64_t len);
