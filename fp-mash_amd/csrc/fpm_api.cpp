@@ -1629,9 +1629,10 @@ int fpm_fp_text_stage(fpm_ctx *ctx, const char *text, uint64_t text_len, uint64_
             HIP_TRY(launch_fp_nl_count(j->d_text, text_len, blk_cnt, blk_off, scan_s, st));
             tl.done();
         }
-        uint32_t tot = 0;
-        HIP_TRY(hipMemcpyAsync(&tot, blk_off + nb, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        // the total (blk_off[nb], 8-B aligned: blk_off starts nb words into an aligned block)
+        // through the mapped counter block: no copy + stream sync round trip
+        if (int rc = read_counters(ctx, (const unsigned long long *)(blk_off + nb), 1, st)) return rc;
+        const uint32_t tot = (uint32_t)ctx->host_counters[0];
         n_nl = tot;
     }
     HIP_TRY(j->alloc(&j->d_line_start, (n_nl + 1) * 8));
@@ -1697,14 +1698,17 @@ int fpm_fp_text_refs(fpm_fptext *j, uint64_t cap, uint64_t *n_refs, uint64_t *fi
             HIP_TRY(launch_fp_heads(j->d_new_id, n, blk_cnt, blk_off, scan_s, st));
             tl.done();
         }
-        uint32_t tot = 0;
-        HIP_TRY(hipMemcpyAsync(&tot, blk_off + nb, 4, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
+        // the total (blk_off[nb], 8-B aligned: blk_off starts nb words into an aligned block)
+        // through the mapped counter block: no copy + stream sync round trip
+        if (int rc = read_counters(ctx, (const unsigned long long *)(blk_off + nb), 1, st)) return rc;
+        const uint32_t tot = (uint32_t)ctx->host_counters[0];
         j->n_refs = tot;
-        HIP_TRY(j->alloc(&j->d_first, (size_t)tot * 8 + 8));
-        HIP_TRY(j->alloc(&j->d_length, (size_t)tot * 8 + 8));
-        HIP_TRY(j->alloc(&j->d_ref_id_off, (size_t)tot * 8 + 8));
-        HIP_TRY(j->alloc(&j->d_ref_id_len, (size_t)tot * 4 + 4));
+        uint64_t *blk4;
+        HIP_TRY(j->alloc(&blk4, (size_t)tot * 28 + 32));
+        j->d_first = blk4;
+        j->d_ref_id_off = blk4 + tot;
+        j->d_length = blk4 + 2 * (size_t)tot;
+        j->d_ref_id_len = reinterpret_cast<uint32_t *>(blk4 + 3 * (size_t)tot);
         TimedLaunch tl(ctx, FPM_K_FPTEXT, st);
         HIP_TRY(launch_fp_refs(j->d_new_id, n, blk_off, tot, j->d_n_vals, j->d_id_off,
                                j->d_id_len, j->d_first, j->d_length, j->d_ref_id_off,
@@ -1715,6 +1719,20 @@ int fpm_fp_text_refs(fpm_fptext *j, uint64_t cap, uint64_t *n_refs, uint64_t *fi
     *n_refs = j->n_refs;
     if (cap < j->n_refs || !j->n_refs) return FPM_OK;     // sized by this call
     const uint64_t m = j->n_refs;
+    // the four arrays are one device block (first, ID offset, length: u64; ID length: u32):
+    // one copy into the pinned ring and one wait, then spread into the caller's arrays
+    const size_t bytes = m * 28;
+    if (bytes <= fpm_ctx::kRingBytes) {
+        HIP_TRY(ensure_ring(ctx));
+        HIP_TRY(hipMemcpyAsync(ctx->ring[0], j->d_first, bytes, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        const char *r = static_cast<const char *>(ctx->ring[0]);
+        if (first_line) memcpy(first_line, r, m * 8);
+        if (id_off) memcpy(id_off, r + m * 8, m * 8);
+        if (length) memcpy(length, r + m * 16, m * 8);
+        if (id_len) memcpy(id_len, r + m * 24, m * 4);
+        return FPM_OK;
+    }
     HIP_TRY(hipStreamSynchronize(st));
     if (first_line) HIP_TRY(copy_out(ctx, first_line, j->d_first, m * 8));
     if (id_off) HIP_TRY(copy_out(ctx, id_off, j->d_ref_id_off, m * 8));

@@ -16,6 +16,7 @@ namespace fpm {
 
 constexpr int kBlock = 256;
 constexpr int kSkWpe = 7;   // waves per SIMD asked of the tile kernel for P <= 2048
+constexpr int kSkWpeThr = 8;   // and of the survivors-only instance (17.9 KB of LDS: 8 tiles per CU)
 constexpr int kWaves = kBlock / 64;
 
 // Phase timestamps of the tile kernel for tools/micro/sketch_phases.hip (which defines
@@ -390,6 +391,11 @@ __device__ __forceinline__ void sketch_tile(
     constexpr int KW = THR ? (PS > (I::kBytes + 7) / 8 ? PS : (I::kBytes + 7) / 8) : P;
     __shared__ __attribute__((aligned(16))) uint64_t keys[KW];
     static_assert(I::kBytes <= 8 * KW, "staging fits in keys");
+    // THR: the sort's bucket counters (bins) reuse the survivor slots, dead once their keys
+    // are copied into keys[]: 17.7 KB of LDS per tile instead of 21.9 KB (9 tiles per CU fit,
+    // 8 by waves)
+    constexpr int kBins = P >= 4096 ? P / 4 : P / 2;
+    static_assert(!THR || kBins <= 2 * (kBlock * kSurv + kSurvShared), "bins fit the slots");
     __shared__ uint64_t surv[THR ? kBlock * kSurv + kSurvShared : 1];   // shared area last
     __shared__ uint32_t s_over, s_shared;
     uint32_t *const img = reinterpret_cast<uint32_t *>(keys);
@@ -398,7 +404,8 @@ __device__ __forceinline__ void sketch_tile(
     uint8_t *const compl_tab = alpha + 256;
     __shared__ uint32_t scan_tmp[kWaves + 1];
     __shared__ uint32_t wcnt[ES * kWaves + 1];
-    __shared__ uint32_t bins[P >= 4096 ? P / 4 : P / 2];
+    __shared__ uint32_t bins_own[THR ? 1 : kBins];
+    uint32_t *const bins = THR ? reinterpret_cast<uint32_t *>(surv) : bins_own;
     __shared__ uint32_t big_bucket, s_cut;
 
     FPM_PHASE_DECL;
@@ -628,7 +635,7 @@ __device__ __forceinline__ void sketch_tile(
 }
 
 template <int P, int K, bool THR = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(P <= 2048 || THR ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(THR ? kSkWpeThr : P <= 2048 ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count,
     TileDesc *__restrict__ redo, uint32_t *__restrict__ redo_n)
