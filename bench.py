@@ -587,7 +587,7 @@ def compact_out(ctx, cells):
 
 
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
-           steps=3, warmup=1, parity=True, vblocks=1):
+           steps=3, warmup=1, parity=True, vblocks=1, cpu=False):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
     the ranks (strong scaling).  A timed step is the whole job on every rank:
       1. sketch its contiguous block of families (each family generated from its own seed,
@@ -844,6 +844,25 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
                "pairs": int(sum(r_["pairs"] for r_ in res)),
                "pairs_sharing": int(sum(r_["pairs_sharing"] for r_ in res)),
                "ok": all(r_["ok"] for r_ in res), "check_s": time.perf_counter() - t_c}
+    cpu_res = None
+    if cpu and rank == 0 and ws == 1 and parity:
+        # the reference's compare (CommandDistance.cpp:365-450: the literal walk + p-value per
+        # pair, a worker pool) as the oracle's port on the CPUs available: 100 query rows x all
+        # n references, scaled to the n x n grid (no text: the bench's C4 keeps its output in
+        # HBM)
+        from oracle import oracle as O
+        th = _threads()
+        qrows = sample_rows(n, 100, salt=9)
+        t_c = time.perf_counter()
+        O.dist_grid(refs, [seq_len] * n, [refs[int(q)] for q in qrows], [seq_len] * len(qrows),
+                    s, k, 4.0 ** k, threads=th)
+        t_s = time.perf_counter() - t_c
+        rate = len(qrows) * n / t_s
+        cpu_res = {"kind": "port", "cores": th, "pairs_per_s": rate,
+                   "grid_s_extrapolated": n * n / rate,
+                   "sample": f"oracle literal walk + p-values, {len(qrows)} query rows x {n} "
+                             f"references on {th} threads in {t_s:.1f} s, scaled to {n * n:.3g} "
+                             "pairs"}
     for rs in refsets.values():
         L.fpm_refset_free(rs)
     for o in outs:
@@ -874,7 +893,9 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "jobs_rank0": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                            for j in jobs], "cells_rank0": cells,
             "path_rank0": fpmash.DIST_PATHS[int(dst["sparse"])],
-            "candidates_all_ranks": cand, "parity": par}
+            "candidates_all_ranks": cand, "parity": par, "cpu_baseline": cpu_res,
+            "speedup_vs_cpu": (cpu_res["grid_s_extrapolated"] / (el / steps)
+                               if cpu_res else None)}
 
 
 def cli_phases(stderr: bytes, prefix="[fpmash] "):
@@ -1206,7 +1227,7 @@ def balanced_file_shards(lengths, ws):
 
 
 def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21, steps=2,
-           warmup=1, parity=True):
+           warmup=1, parity=True, cpu=False):
     """C5: RefSeq-scale sketch of n_genomes x length bp, k=21, s=10,000, default
     (per-file, concatenated) mode: one sketch per genome.  Files are sharded over the ranks
     as contiguous ranges balanced by bases; each rank stages its genomes in HBM once and the
@@ -1296,6 +1317,25 @@ def c5_leg(ctx, grp, ws, rank, n_genomes=1000, length=5_000_000, s=10_000, k=21,
         out["parity"] = {"genomes_checked": idx, "sketch_exact": ok, "ok": all(ok),
                          "shards": balanced_file_shards(lengths, ws),
                          "check_s": time.perf_counter() - t_c}
+    if cpu and rank == 0 and ws == 1:
+        # the reference's sketchFile (Sketch.cpp:1299-1488: one MinHashHeap per genome, files
+        # dealt to the -p threads) through its own compiled getHash + MinHashHeap (oracle/_ref):
+        # one genome per thread on the CPUs available, scaled to the n_genomes files
+        from oracle import oracle as O
+        th = _threads()
+        sample = [c5_genome(g, length) for g in range(min(th, n_genomes))]
+        t_c = time.perf_counter()
+        rsk = O.ref_sketch_batch(sample, k=k, s=s, threads=th)
+        t_s = time.perf_counter() - t_c
+        if rsk is not None:
+            rate = len(sample) * length / t_s
+            out["cpu_baseline"] = {
+                "kind": "reference", "cores": th, "bases_per_s": rate,
+                "step_s_extrapolated": n_genomes * length / rate,
+                "sample": f"{len(sample)} genomes x {length / 1e6:g} Mb, one per thread on {th} "
+                          f"threads, the reference's getHash + MinHashHeap (oracle/_ref) in "
+                          f"{t_s:.1f} s, scaled to {n_genomes} genomes"}
+            out["speedup_vs_cpu"] = out["cpu_baseline"]["step_s_extrapolated"] / (el_max / steps)
     return out
 
 
@@ -1467,8 +1507,12 @@ def compact_line(d, detail_path=None):
         "c3_dist_ms": _r(g(c3, "dist_ms")), "c3_dense_walk_ms": _r(g(c3, "dense_walk_ms")),
         "c3_parse_device_ms": _r(g(c3, "parse_device_ms")),
         "c4_ms_per_step": _r(g(c4, "ms_per_step")), "c4_mpairs_per_s": _r(g(c4, "mpairs_per_s")),
+        "c4_cpu_mpairs_per_s": _r((g(c4, "cpu_baseline", "pairs_per_s") or 0) / 1e6 or None),
+        "c4_speedup_vs_cpu": _r(g(c4, "speedup_vs_cpu"), 3),
         "c4_output": g(c4, "output"),
         "c5_ms_per_step": _r(g(c5, "ms_per_step")), "c5_bases_per_s": _r(g(c5, "bases_per_s")),
+        "c5_cpu_bases_per_s": _r(g(c5, "cpu_baseline", "bases_per_s")),
+        "c5_speedup_vs_cpu": _r(g(c5, "speedup_vs_cpu"), 3),
         "split_ms_per_step": _r(g(sp, "ms_per_step")),
         "cli_sketch_wall_s": _r(g(cli, "cli_sketch_wall_s")),
         "cli_dist_wall_s": _r(g(cli, "cli_dist_wall_s")),
@@ -1693,7 +1737,7 @@ def main():
             b.free()
         cells.free()
         c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
-                    parity=not args.no_parity)
+                    parity=not args.no_parity, cpu=not args.no_cpu_baseline)
     c4g = None
     if ws == 1 and grp.nccl is not None:
         # the multi-GPU data path once on this GPU, outside every timed number: rows
@@ -1704,7 +1748,8 @@ def main():
 
     c5 = None
     if not args.no_c5:
-        c5 = c5_leg(ctx, grp, ws, rank, n_genomes=args.c5_genomes, parity=not args.no_parity)
+        c5 = c5_leg(ctx, grp, ws, rank, n_genomes=args.c5_genomes, parity=not args.no_parity,
+                    cpu=not args.no_cpu_baseline)
 
     split = None
     if not args.no_split:
