@@ -20,7 +20,7 @@ print('$s', 'c5', round(d['ms_per_step'],3), {k: round(v['ms'],3) for k, v in d[
     fi
     if [ "${AB_LEG:-c2}" = c4 ]; then
       env "${envs[@]}" timeout -k 10 300 python bench.py --steps 2 --warmup 1 --no-cpu-baseline \
-        --no-c3 --no-c5 --no-cli --no-fp-text --no-split --no-parity --no-full-grid \
+        --no-c3 --no-c5 --no-cli --no-cli-fp --no-gather-check --no-fp-text --no-split --no-parity --no-full-grid \
         --detail gpurun_out/env_$tag$i.detail.json > gpurun_out/env_$tag$i.json 2>&1 || exit 1
       python3 -c "
 import json; d=json.load(open('gpurun_out/env_$tag$i.detail.json'))['c4_dist']
@@ -29,7 +29,7 @@ print('$s', 'c4', round(d['ms_per_step'],3), d['phase_ms_rank0'],
       continue
     fi
     env "${envs[@]}" timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline \
-      --no-c3 --no-c4 --no-c5 --no-cli --no-fp-text --no-split --no-parity --no-full-grid \
+      --no-c3 --no-c4 --no-c5 --no-cli --no-cli-fp --no-fp-text --no-split --no-parity --no-full-grid \
       --detail gpurun_out/env_$tag$i.detail.json > gpurun_out/env_$tag$i.json 2>&1 || exit 1
     python3 -c "
 import json; d=json.load(open('gpurun_out/env_$tag$i.detail.json'))

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
   -k "$K" > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
-BENCH_ARGS=${BENCH_ARGS:---steps 20 --warmup 3 --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-split --no-full-grid --no-parity} \
+BENCH_ARGS=${BENCH_ARGS:---steps 20 --warmup 3 --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-cli-fp --no-split --no-full-grid --no-parity} \
   timeout -k 10 900 bash tools/ab_bench.sh fp-mash_amd/lib/libfpmash.so fp-mash_amd/lib/$B.so $N \
   > $O/ab.txt 2>&1 || { tail -20 $O/ab.txt; exit 1; }
 cat $O/ab.txt

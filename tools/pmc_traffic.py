@@ -146,7 +146,8 @@ def main():
         # the C2 step only: the side legs (-fp text, C3, C4) would add dispatches to the groups
         bench_args = [os.path.join(ROOT, "bench.py"), "--steps", str(a.steps), "--warmup",
                       str(a.warmup), "--no-cpu-baseline", "--no-fp-text", "--no-c3", "--no-c4",
-                      "--no-c5", "--no-cli", "--no-split", "--no-parity", "--no-full-grid"]
+                      "--no-c5", "--no-cli", "--no-cli-fp", "--no-split", "--no-parity",
+                      "--no-full-grid", "--no-gather-check"]
     else:
         bench_args = [os.path.join(ROOT, "tools", "leg_run.py"), "--leg", a.leg]
         if a.leg == "c5":

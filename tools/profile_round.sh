@@ -28,7 +28,7 @@ for leg in ${LEGS:-c3 c4 c5}; do
   rm -rf gpurun_out/pmc_traffic_$leg
 done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$TAG -o prof --output-format csv \
-  -- python3 bench.py --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-split --no-parity --no-full-grid \
+  -- python3 bench.py --no-cpu-baseline --no-fp-text --no-c3 --no-c4 --no-c5 --no-cli --no-cli-fp --no-split --no-parity --no-full-grid --no-gather-check \
   --steps 5 --warmup 2 > gpurun_out/prof_$TAG.log 2>&1 || { tail -20 gpurun_out/prof_$TAG.log; exit 1; }
 f=$(find gpurun_out/prof_$TAG -name '*kernel_stats.csv' | head -1)
 cp "$f" $O/kernel_stats_$TAG.csv && echo "stats ok"

@@ -9,7 +9,7 @@ N=${1:-2}
 mkdir -p gpurun_out
 FPMASH_BENCH_ONE_DEVICE=1 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 \
   --nproc-per-node "$N" --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus "$N" \
-  --steps 3 --warmup 1 --no-cpu-baseline --no-cli --c4-n 6000 --c5-genomes 24 \
+  --steps 3 --warmup 1 --no-cpu-baseline --no-cli --no-cli-fp --c4-n 6000 --c5-genomes 24 \
   --split-bases 20000000 --detail gpurun_out/rehearse_detail.json \
   > gpurun_out/rehearse.json 2> gpurun_out/rehearse.err || { tail -30 gpurun_out/rehearse.err; exit 1; }
 python3 -c "
