@@ -354,31 +354,42 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
     if (__any(over) && lane == 0) atomicOr(overflow, 1u);
 }
 
-// ---- 1c. level 2: one workgroup per partition, LDS counting sort by the next l2 bits.
-// A partition of up to `cap` entries (C2: ~9.8k of 1e7 / 1024) is read once into registers
+// ---- 1c. level 2: LDS counting sort of each partition by the next l2 bits.
+// A partition of up to 16k entries (C2: ~9.8k of 1e7 / 1024) is read once into registers
 // (16 per thread), counted, scattered into an LDS copy of its entries and written out
-// coalesced; a larger one (C4: ~49k) reads its slice of tent twice and scatters straight to
-// `entries` (the previous form for every partition: tent read twice and the entries written
-// in scattered 4-B pieces, ~2x the algorithmic bytes).
+// coalesced.  A larger one is read twice (count, then scatter through the LDS copy).  At
+// l2 > 13 (C4: 16,384 sub-buckets of ~3 entries, partitions of ~49k) the sub-bucket range is
+// split over 2^lsplit workgroups on one XCD (blockIdx % 8 alike: the slice is fetched from
+// HBM about once, then from that XCD's L2): each counts its part of the sub-buckets (32 KB
+// of counters) and the entries below it, reads the slice again and scatters its range's
+// entries through the LDS, so every entry is written coalesced.  A range past `cap` scatters
+// straight to `entries` in 4-B pieces (the round-4 form for C4: tent read twice, entries
+// written ~6.5x their bytes: 0.64 ms).
 constexpr int kBucketThreads = 1024;
 static_assert(kBucketThreads == (int)kParts, "one-pass build: one partition fill per thread");
+static_assert(kParts % 8 == 0, "split partitions map to one XCD");
 constexpr int kBucketPer = 16;                   // entries per thread in registers
 __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     const uint64_t *__restrict__ tent_all, uint32_t ntiles,
     const uint32_t *__restrict__ tile_off, IdxGeom g, uint32_t cap, uint32_t *__restrict__ dir,
     uint32_t *__restrict__ entries_all, unsigned long long *__restrict__ sqsum,
-    const uint32_t *__restrict__ part_fill)
+    const uint32_t *__restrict__ part_fill, uint32_t lsplit)
 {
-    extern __shared__ uint32_t sh[];             // 2^l2 counters, then cursors; then cap entries
+    extern __shared__ uint32_t sh[];             // the range's counters, then cursors; then cap entries
     __shared__ uint32_t wsum[kBucketThreads / 64];
     __shared__ unsigned long long wsq[kBucketThreads / 64];
-    const uint32_t p = blockIdx.x;
+    __shared__ uint32_t s_below;
+    // blockIdx = ((p >> 3) << lsplit | j) << 3 | (p & 7): workgroup j of partition p
+    const uint32_t ns = 1u << lsplit;
+    const uint32_t p = ((blockIdx.x >> 3) >> lsplit) * 8 + (blockIdx.x & 7);
+    const uint32_t j = (blockIdx.x >> 3) & (ns - 1);
     // this partition's entries are tent[s0, s1) and go to entries[s0, s1) (exact build), or
     // (one-pass build) tent[p * g.cap, + fill) going to entries from the sum of the fills of
     // the partitions before it (one fill per thread, block-reduced)
     uint32_t s0, s1;
     const uint64_t *tent = tent_all;
     uint32_t *entries = entries_all;
+    if (threadIdx.x == 0) s_below = 0;
     if (part_fill) {
         const uint32_t f = min(part_fill[threadIdx.x], g.cap);
         uint32_t below = threadIdx.x < p ? f : 0u;
@@ -398,13 +409,14 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         s0 = tile_off[(uint64_t)p * ntiles];
         s1 = tile_off[(uint64_t)(p + 1) * ntiles];   // [kParts * ntiles] = total
     }
-    const uint32_t nsb = 1u << g.l2, sbmask = nsb - 1;
+    const uint32_t sbmask = (1u << g.l2) - 1;
+    const uint32_t nsb = 1u << (g.l2 - lsplit), lo = j * nsb;   // sub-buckets [lo, lo + nsb)
     uint32_t *const out = sh + nsb;
-    const bool in_lds = s1 - s0 <= cap && cap <= (uint32_t)(kBucketThreads * kBucketPer);
+    const bool in_reg = ns == 1 && s1 - s0 <= min(cap, (uint32_t)(kBucketThreads * kBucketPer));
     for (uint32_t b = threadIdx.x; b < nsb; b += kBucketThreads) sh[b] = 0;
     __syncthreads();
     uint64_t K[kBucketPer];
-    if (in_lds) {
+    if (in_reg) {
 #pragma unroll
         for (int u = 0; u < kBucketPer; u++) {
             const uint32_t e = s0 + threadIdx.x + u * kBucketThreads;
@@ -415,8 +427,10 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
             if (s0 + threadIdx.x + u * kBucketThreads < s1)
                 atomicAdd(&sh[(uint32_t)(K[u] >> 32) & sbmask], 1u);
     } else {
-        // 4 independent loads in flight per thread
+        // 4 independent loads in flight per thread; entries of the sub-buckets below the
+        // range are only counted (they sit before it in `entries`)
         constexpr uint32_t kU = 4;
+        uint32_t below = 0;
         for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
             uint64_t Kg[kU];
 #pragma unroll
@@ -426,7 +440,16 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
             }
 #pragma unroll
             for (uint32_t u = 0; u < kU; u++)
-                if (e0 + u * kBucketThreads < s1) atomicAdd(&sh[(uint32_t)(Kg[u] >> 32) & sbmask], 1u);
+                if (e0 + u * kBucketThreads < s1) {
+                    const uint32_t sub = (uint32_t)(Kg[u] >> 32) & sbmask, d = sub - lo;
+                    if (d < nsb) atomicAdd(&sh[d], 1u);
+                    else below += sub < lo ? 1u : 0u;
+                }
+        }
+        if (lsplit) {
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) below += __shfl_xor(below, d, 64);
+            if ((threadIdx.x & 63) == 0 && below) atomicAdd(&s_below, below);
         }
     }
     __syncthreads();
@@ -441,13 +464,17 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
     for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
     if (lane == 63) wsum[wave] = x;
     __syncthreads();
-    uint32_t acc = x - run;
-    for (int w = 0; w < wave; w++) acc += wsum[w];
+    uint32_t acc = x - run, tot = 0;
+    for (int w = 0; w < kBucketThreads / 64; w++) {
+        acc += w < wave ? wsum[w] : 0u;
+        tot += wsum[w];
+    }
+    const uint32_t base = s0 + s_below;          // the range's first entry
     unsigned long long sq = 0;
     for (uint32_t b = b0; b < b0 + per && b < nsb; b++) {
         const uint32_t c = sh[b];
         sh[b] = acc;
-        dir[((uint64_t)p << g.l2) + b] = s0 + acc;
+        dir[((uint64_t)p << g.l2) + lo + b] = base + acc;
         acc += c;
         sq += (unsigned long long)c * c;
     }
@@ -459,14 +486,14 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         for (int d = 32; d > 0; d >>= 1) sq += __shfl_down(sq, d, 64);
         if (lane == 0) wsq[wave] = sq;
     }
-    if (p == kParts - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
+    if (p == kParts - 1 && j == ns - 1 && threadIdx.x == 0) dir[(uint64_t)kParts << g.l2] = s1;
     __syncthreads();
     if (sqsum && threadIdx.x == 0) {
         unsigned long long t = 0;
         for (int w = 0; w < kBucketThreads / 64; w++) t += wsq[w];
-        if (t) atomicAdd(&sqsum[1 + (p & 63)], t);
+        if (t) atomicAdd(&sqsum[1 + ((p * ns + j) & 63)], t);
     }
-    if (in_lds) {
+    if (in_reg) {
 #pragma unroll
         for (int u = 0; u < kBucketPer; u++)
             if (s0 + threadIdx.x + u * kBucketThreads < s1) {
@@ -477,6 +504,8 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         for (uint32_t i = threadIdx.x; i < s1 - s0; i += kBucketThreads) entries[s0 + i] = out[i];
         return;
     }
+    // the range through LDS when it fits (tot is block-uniform), else straight to `entries`
+    const bool lds = tot <= cap;
     constexpr uint32_t kU = 4;
     for (uint32_t e0 = s0 + threadIdx.x; e0 < s1; e0 += kU * kBucketThreads) {
         uint64_t Kg[kU];
@@ -488,10 +517,17 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
 #pragma unroll
         for (uint32_t u = 0; u < kU; u++)
             if (e0 + u * kBucketThreads < s1) {
-                const uint32_t pos = atomicAdd(&sh[(uint32_t)(Kg[u] >> 32) & sbmask], 1u);
-                entries[s0 + pos] = (uint32_t)Kg[u];
+                const uint32_t d = ((uint32_t)(Kg[u] >> 32) & sbmask) - lo;
+                if (d < nsb) {
+                    const uint32_t pos = atomicAdd(&sh[d], 1u);
+                    if (lds) out[pos] = (uint32_t)Kg[u];
+                    else entries[base + pos] = (uint32_t)Kg[u];
+                }
             }
     }
+    if (!lds) return;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kBucketThreads) entries[base + i] = out[i];
 }
 
 // ---- exclusive scan of u32 counts (n <= 2^31), three launches ----
@@ -1045,10 +1081,24 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     hipLaunchKernelGGL(idx_kmax_kernel, dim3(kg), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
                        stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero, acc,
                        one_pass ? part_fill : nullptr, one_pass ? kParts : 0u);
-    const uint64_t cnt_bytes0 = (uint64_t)4 << g.l2;
-    const uint32_t lds_cap = cnt_bytes0 <= 16384 ? (uint32_t)(kBucketThreads * kBucketPer) : 0u;
-    if (hipError_t e = dyn_lds_attr(1, (const void *)idx_bucket_kernel,
-                                    16384 + kBucketThreads * kBucketPer * 4))
+    // level 2: the sub-bucket range split over 2^lsplit workgroups until its counters fit
+    // 32 KB and a range's mean entries 24k (C4, E = 5e7: 2 per partition).  The LDS copy: 16k
+    // entries (80 KB with the counters, two workgroups per CU) when the ranges' mean fits 12k
+    // (C2), else all the LDS beside the counters, one workgroup per CU (C4: 2 x 32k-entry
+    // ranges per partition, index 0.92 -> 0.80 ms against 4 x 16k, C4 6.31-6.52 -> 6.21-6.26
+    // ms, same box, r05j)
+    uint32_t lsplit = 0;
+    const double part_mean = (double)n_ref * (double)stride / (double)kParts;
+    while (lsplit < g.l2 && lsplit < 4 &&
+           (((uint64_t)4 << (g.l2 - lsplit)) > 32768 || part_mean / (double)(1u << lsplit) > 24576.0))
+        lsplit++;
+    const uint64_t cnt_bytes0 = (uint64_t)4 << (g.l2 - lsplit);
+    constexpr uint32_t kLdsBytes = 159 * 1024;
+    const uint32_t lds_cap = part_mean / (double)(1u << lsplit) <= 12288.0
+                                 ? (uint32_t)(kBucketThreads * kBucketPer)
+                                 : (uint32_t)((kLdsBytes - cnt_bytes0) / 4);
+    const dim3 bgrid(kParts << lsplit);
+    if (hipError_t e = dyn_lds_attr(1, (const void *)idx_bucket_kernel, kLdsBytes))
         return e;
     if (one_pass) {
         if (hipError_t e = dyn_lds_attr(2, (const void *)idx_part_scatter1_kernel, kIdxTile * 8))
@@ -1056,10 +1106,10 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
         hipLaunchKernelGGL(idx_part_scatter1_kernel, dim3(ntiles), dim3(kIdxThreads),
                            (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic,
                            n_ref, hash_bytes, g, part_fill, tent, unsorted, overflow);
-        hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
+        hipLaunchKernelGGL(idx_bucket_kernel, bgrid, dim3(kBucketThreads),
                            (size_t)(cnt_bytes0 + (uint64_t)lds_cap * 4), st, (const uint64_t *)tent,
                            ntiles, (const uint32_t *)nullptr, g, lds_cap, dir, entries, self_events,
-                           (const uint32_t *)part_fill);
+                           (const uint32_t *)part_fill, lsplit);
         return hipGetLastError();
     }
     hipLaunchKernelGGL(idx_part_hist_kernel, dim3(ntiles), dim3(kIdxThreads), 0, st, d_ref,
@@ -1076,10 +1126,10 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                        g, tent);
     // LDS copy of a partition's entries when they fit beside the counters (two workgroups per
     // CU: 80 KiB each at l2 = 12); cap 0 = every partition on the global two-pass path
-    hipLaunchKernelGGL(idx_bucket_kernel, dim3(kParts), dim3(kBucketThreads),
+    hipLaunchKernelGGL(idx_bucket_kernel, bgrid, dim3(kBucketThreads),
                        (size_t)(cnt_bytes0 + (uint64_t)lds_cap * 4), st, (const uint64_t *)tent,
                        ntiles, (const uint32_t *)tile_off, g, lds_cap, dir, entries, self_events,
-                       (const uint32_t *)nullptr);
+                       (const uint32_t *)nullptr, lsplit);
     return hipGetLastError();
 }
 

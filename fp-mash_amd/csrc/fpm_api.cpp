@@ -157,7 +157,6 @@ struct fpm_ctx {
     // side stream for the sparse dist's fill (a pure write stream that runs beside the
     // latency-bound candidate compare); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
-    hipStream_t aux_mask = nullptr;     // the early fill's stream (FPM_FILL_EARLY, A/B)
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
@@ -495,7 +494,6 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->host_counters) (void)hipHostFree(ctx->host_counters);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
-    if (ctx->aux_mask) (void)hipStreamDestroy(ctx->aux_mask);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
@@ -2070,26 +2068,6 @@ static const bool g_idx_one_pass = [] {
     return !(v && v[0] == '0');
 }();
 
-// FPM_FILL_EARLY=k (A/B): the counts fill of a large grid starts when the dist call does, on a
-// stream masked to every k-th CU, beside the index build, the probe and the rank kernel
-// (instead of beside the rank kernel alone on every CU)
-static const int g_fill_early = [] {
-    const char *v = getenv("FPM_FILL_EARLY");
-    return v ? atoi(v) : 0;
-}();
-
-static hipError_t ensure_aux_mask(fpm_ctx *ctx, int every)
-{
-    if (ctx->aux_mask) return hipSuccess;
-    hipDeviceProp_t prop;
-    hipError_t e = hipGetDeviceProperties(&prop, ctx->device);
-    if (e != hipSuccess) return e;
-    const int n_cu = prop.multiProcessorCount;
-    std::vector<uint32_t> mask((n_cu + 31) / 32, 0u);
-    for (int c = 0; c < n_cu; c += std::max(1, every)) mask[c / 32] |= 1u << (c % 32);
-    return hipExtStreamCreateWithCUMask(&ctx->aux_mask, (uint32_t)mask.size(), mask.data());
-}
-
 static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
 {
     IdxGeom geom{};
@@ -2292,8 +2270,6 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                                      : ctx->fill_counts != 0));
     const bool need_fill = fin && (!compact || fill_cnt);
     bool fill_pending = false;
-    // the compact counts of a large grid filled from the start of the call (FPM_FILL_EARLY)
-    const bool early_fill = g_fill_early > 0 && try_sparse && compact && fill_cnt;
     // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
     // start) and submits the fill after later work on `st`
     auto launch_fill = [&](bool record_in) -> int {
@@ -2304,14 +2280,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         fill.max_dist = fin->max_dist;
         fill.max_pvalue = fin->max_pvalue;
         HIP_TRY(ensure_aux(ctx));
-        hipStream_t fst = ctx->aux;
-        if (early_fill) {
-            HIP_TRY(ensure_aux_mask(ctx, g_fill_early));
-            fst = ctx->aux_mask;
-        }
         if (record_in) HIP_TRY(hipEventRecord(ctx->ev_in, st));
-        HIP_TRY(hipStreamWaitEvent(fst, ctx->ev_in, 0));
-        TimedLaunch tl(ctx, FPM_K_FILL, fst);
+        HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
+        TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
         // the flattened fill runs ~35 % faster alone but slows a rank kernel beside it more
         // (C2, 1e8 cells / 2.3e8 events: rank 0.66 -> 0.70 ms while the fill shrank 0.63 ->
         // 0.57; C4, 2.5e9 cells: 14.1 -> 12.8-13.3 ms).  The fill is the long pole when its
@@ -2320,7 +2291,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
         const long double cells_w = (long double)n_pairs * (want_mir ? 2 : 1);
         const bool flat = cells_w * 1.6L > (long double)ctx->last_events;
         HIP_TRY(launch_dist_fill(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size,
-                                 fill_cnt ? cnt : Counts{}, fill, fst, flat));
+                                 fill_cnt ? cnt : Counts{}, fill, ctx->aux, flat));
         if (want_mir) {
             // the transposed grid: the ref rows as queries against the query rows
             PairFill mf = fill;
@@ -2328,15 +2299,13 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             mf.pval = compact ? nullptr : fin->mir.pval;
             mf.pass = compact ? nullptr : fin->mir.pass;
             HIP_TRY(launch_dist_fill(d_qry_len, n_qry, d_ref_len, n_ref, sketch_size,
-                                     fin->mir.cnt, mf, fst, flat));
+                                     fin->mir.cnt, mf, ctx->aux, flat));
         }
         tl.done();
-        HIP_TRY(hipEventRecord(ctx->ev_fill, fst));
+        HIP_TRY(hipEventRecord(ctx->ev_fill, ctx->aux));
         fill_pending = true;
         return FPM_OK;
     };
-    if (early_fill)
-        if (int rc = launch_fill(true)) return rc;
     if (try_sparse) {
         const uint64_t NB = 1ULL << geom.nbits;
         void *ctr;
@@ -2577,11 +2546,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             // first would take every CU before the rank kernel's workgroups arrive (rank +
             // fill 0.39 + 1.51 -> 0.55 + 1.67 ms at N = 8).  The fill may start where the probe
             // ends (ev_in recorded here) but is submitted after the candidate compare.
-            const bool defer_fill = need_fill && !fill_pending && skip_count && rows_merge;
+            const bool defer_fill = need_fill && skip_count && rows_merge;
             if (defer_fill) {
                 HIP_TRY(ensure_aux(ctx));
                 HIP_TRY(hipEventRecord(ctx->ev_in, st));
-            } else if (need_fill && !fill_pending) {
+            } else if (need_fill) {
                 if (int rc = launch_fill(true)) return rc;
             }
             if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
@@ -2639,9 +2608,6 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             return FPM_OK;
         }
     }
-    // (an early fill writes the grid's count defaults: the dense compare rewrites every cell
-    // after it)
-    if (fill_pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
     if (compare_grid_img_ok(hash_bytes, sketch_size, ref_stride, qry_stride)) {
         size_t ub, bb;
         compare_grid_img_scratch(n_qry, sketch_size, ref_stride, qry_stride, &ub, &bb);

@@ -982,6 +982,45 @@ def test_index_one_pass_overflow_rebuilds(ctx, oracle):
     assert np.array_equal(got, nu) and np.array_equal(gde, de)
 
 
+@pytest.mark.parametrize("n_ref,skew", [(16700, False), (36000, False), (36000, True)])
+def test_index_split_level2(ctx, oracle, n_ref, skew):
+    """The level-2 index pass beyond one 16k-entry register copy per partition.  E = 1.67e7
+    (l2 = 12, partitions of ~16.3k): those over 16,384 entries are read twice and scattered
+    through the LDS.  E = 3.6e7 (l2 = 14: C4's geometry): the sub-bucket range split over 2
+    workgroups per partition, each scattering its half through the LDS.  skew: every list also
+    holds 30 of 4,000 values spread over ~128 buckets of one range, so that range holds
+    ~1.1e6 entries: the one-pass slot overflows, the exact build runs, and the range takes
+    the global scatter.  Sampled query rows equal the oracle."""
+    import fpmash
+    rng = np.random.default_rng(n_ref + skew)
+    members = 100
+    lists = []
+    for _ in range(n_ref // members):
+        core = rng.integers(1, 2 ** 63, size=1100, dtype=np.uint64)
+        pick = np.argpartition(rng.random((members, core.size)), 1000, axis=1)[:, :1000]
+        lists += list(np.sort(core[pick], axis=1))
+    if skew:
+        narrow = np.unique(rng.integers(1 << 40, (1 << 40) + (1 << 46), size=4000, dtype=np.uint64))
+        lists = [np.union1d(x, narrow[rng.integers(0, narrow.size, size=30)]) for x in lists]
+    L = [len(x) * 5 for x in lists]
+    qrows = list(range(0, n_ref, n_ref // 12))[:12]
+    qry = [lists[r] for r in qrows]
+    S = max(len(x) for x in lists)
+    before = ctx.index_rebuilds()
+    ctx.set_dist_mode(fpmash.DIST_SPARSE)
+    try:
+        nu, de, listed = ctx.dist_list(lists, qry, S, ref_lengths=L, qry_lengths=[L[r] for r in qrows],
+                                       cap=1 << 20, expand=False)
+        st = ctx.last_dist_stats()
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+    assert st["sparse"]
+    assert (ctx.index_rebuilds() > before) == skew
+    onu, ode, _, _ = oracle.dist_grid(lists, L, qry, [L[r] for r in qrows], S, 21, 4.0 ** 21,
+                                      threads=8, with_pvalue=False)
+    assert np.array_equal(nu, onu) and np.array_equal(de, ode)
+
+
 def test_index_exact_build_forced():
     """FPM_IDX_ONEPASS=0 (read at library load: a child process) forces the exact two-pass
     index build; the sorted and the -fp dist grids still equal the oracle."""
