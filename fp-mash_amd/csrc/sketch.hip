@@ -271,6 +271,11 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
     constexpr int KW = K ? (K + 3) / 4 : 8;                // dwords per window (max)
     constexpr int W = (E + 3) / 4 + KW + 1;                // dwords covering the E windows
     uint32_t vbits = 0;                                    // bit e: window e is a valid k-mer
+    // the seed through an opaque move: otherwise the compiler, short of SGPRs in the unrolled
+    // window loop, reloads it from the kernel arguments once per window (an s_load and an
+    // s_waitcnt lgkmcnt(0) per hash)
+    uint32_t seed;
+    asm volatile("s_mov_b32 %0, %1" : "=s"(seed) : "s"(p.seed));
     const uint32_t i0 = (uint32_t)tid * E;
     if (i0 < nk) {
         // validity of the E windows from one 64-bit read of the bit image
@@ -354,7 +359,7 @@ __device__ __forceinline__ uint32_t tile_hash(const TileDesc &td, const SketchKP
                 uint64_t wd[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) wd[j] = (uint64_t)d[2 * j] | ((uint64_t)d[2 * j + 1] << 32);
-                const uint64_t h = murmur_h1_le32(wd, (int)k, p.seed);
+                const uint64_t h = murmur_h1_le32(wd, (int)k, seed);
                 sink(e, p.use64 ? h : (h & 0xffffffffULL));   // getHash hash.cpp:30-37
             }
             vbits = okbits;
@@ -635,7 +640,7 @@ __device__ __forceinline__ void sketch_tile(
 }
 
 template <int P, int K, bool THR = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(THR ? kSkWpeThr : P <= 2048 ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(THR ? (K ? kSkWpeThr : 6) : P <= 2048 ? kSkWpe : P == 4096 ? 4 : 1))) void sketch_tiles_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ tiles, SketchKParams p,
     const uint64_t *__restrict__ thr, uint64_t *__restrict__ out, uint32_t *__restrict__ out_count,
     TileDesc *__restrict__ redo, uint32_t *__restrict__ redo_n)
@@ -647,7 +652,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(THR ? kS
 // a fixed grid takes them in turn, so the count stays on the device (no host read between
 // the two launches: fpm_sketch_run stays asynchronous on its stream).
 template <int K>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void sketch_redo_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(3))) void sketch_redo_kernel(
     const uint8_t *__restrict__ seq, const TileDesc *__restrict__ redo,
     const uint32_t *__restrict__ redo_n, SketchKParams p, const uint64_t *__restrict__ thr,
     uint64_t *__restrict__ out, uint32_t *__restrict__ out_count)

@@ -19,6 +19,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--leg", choices=["c3", "c4", "c5"], required=True)
     ap.add_argument("--c5-genomes", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=21, help="C5's k-mer size (21: the config)")
     a = ap.parse_args()
     grp = bench.Group(1)
     with fpmash.Context(0) as ctx:
@@ -27,7 +28,7 @@ def main():
         elif a.leg == "c4":
             r = bench.c4_leg(ctx, grp, 1, 0, 0, steps=2, warmup=1, parity=False)
         else:
-            r = bench.c5_leg(ctx, grp, 1, 0, n_genomes=a.c5_genomes, steps=3, warmup=1,
+            r = bench.c5_leg(ctx, grp, 1, 0, n_genomes=a.c5_genomes, k=a.k, steps=3, warmup=1,
                              parity=False)
     print(json.dumps(r, default=str))
 
