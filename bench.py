@@ -587,7 +587,7 @@ def compact_out(ctx, cells):
 
 
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
-           steps=3, warmup=1, parity=True, vblocks=1, cpu=False):
+           steps=3, warmup=1, parity=True, vblocks=1, cpu=False, prefill=True):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
     the ranks (strong scaling).  A timed step is the whole job on every rank:
       1. sketch its contiguous block of families (each family generated from its own seed,
@@ -738,6 +738,12 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
 
     def run(timed):
         t0 = time.perf_counter()
+        if prefill and not gathered:
+            # the grid's no-shared-hash counts (10 GB) written beside the sketch kernels on the
+            # library's side stream (fpm_dist_list_prefill), instead of beside the rank kernel:
+            # 6.34-6.35 -> 5.80 ms, same box, r05n (tools/leg_run.py --no-prefill: the A/B)
+            p_ = outs[0]["p"]
+            fpmash._check(L.fpm_dist_list_prefill(ctx.h, p_[0].ptr, p_[1].ptr, n, n, s, st))
         job.run(st)
         if timed:
             ctx.synchronize()
@@ -1582,6 +1588,10 @@ def main():
     st = ctx.stream
 
     def step():
+        # (no counts prefill here: the probe writes the 1e8 cells' defaults as it goes; written
+        # beside the sketch kernels instead, fpm_dist_list_prefill, they slowed the sketch and
+        # the index build more than the probe gained: 0.996-1.001 -> 1.010-1.016 ms, same box,
+        # r05n; on C4's 2.5e9 cells it wins, c4_leg)
         job.run(st)
         fpmash._check(L.fpm_dist_list_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
                                           d_cnt, d_len.ptr, stride, n, 8, args.s, args.k,

@@ -1009,6 +1009,82 @@ hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uin
     return hipGetLastError();
 }
 
+// A compact grid's counts before its sketches exist (fpm_dist_list_prefill): numer 0 and
+// denom S in every cell, i.e. min(S, la + lb) (CommandDistance.cpp:416-418 at common = 0) for
+// every pair whose lists hold at least S hashes together.  VEC: 8 cells per lane, one 16-B
+// store per array (both arrays 16-B aligned).
+template <bool VEC>
+__global__ __launch_bounds__(256) void dist_counts_const_kernel(uint16_t *__restrict__ numer,
+                                                                uint16_t *__restrict__ denom,
+                                                                uint64_t cells, uint32_t S)
+{
+    const uint64_t o = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (o >= cells) return;
+    if (VEC && o + 8 <= cells) {
+        const uint32_t d = S | (S << 16);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store((u32x4){0u, 0u, 0u, 0u}, (u32x4 *)(numer + o));
+        __builtin_nontemporal_store((u32x4){d, d, d, d}, (u32x4 *)(denom + o));
+        return;
+    }
+    for (uint64_t c = o; c < cells && c < o + 8; c++) {
+        numer[c] = 0;
+        denom[c] = (uint16_t)S;
+    }
+}
+
+hipError_t launch_dist_counts_const(uint16_t *numer, uint16_t *denom, uint64_t cells, uint32_t S,
+                                    hipStream_t st)
+{
+    if (!cells) return hipSuccess;
+    const uint64_t blocks = (cells + 8 * 256 - 1) / (8 * 256);
+    if (blocks >= (1ULL << 31)) return hipErrorInvalidValue;
+    const bool vec = (((uintptr_t)numer | (uintptr_t)denom) & 15) == 0;
+    if (vec)
+        hipLaunchKernelGGL(dist_counts_const_kernel<true>, dim3((uint32_t)blocks), dim3(256), 0, st,
+                           numer, denom, cells, S);
+    else
+        hipLaunchKernelGGL(dist_counts_const_kernel<false>, dim3((uint32_t)blocks), dim3(256), 0,
+                           st, numer, denom, cells, S);
+    return hipGetLastError();
+}
+
+// After a prefill, the pairs whose lists hold fewer than S hashes together: denom = la + lb.
+// One workgroup per 64 query rows; a row with lq >= S has none (la + lq >= S for every ref),
+// so with full sketches every workgroup stops after one length read per row.
+__global__ __launch_bounds__(256) void dist_counts_fixup_kernel(
+    const uint32_t *__restrict__ ref_len, uint32_t n_ref, const uint32_t *__restrict__ qry_len,
+    uint32_t n_qry, uint32_t S, uint16_t *__restrict__ denom)
+{
+    __shared__ uint64_t s_rows;
+    const uint32_t q0 = blockIdx.x * 64;
+    if (threadIdx.x < 64) {                      // wave 0: the rows that need a sweep
+        const uint32_t q = q0 + threadIdx.x;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(q < n_qry && qry_len[q] < S);
+        if (threadIdx.x == 0) s_rows = m;
+    }
+    __syncthreads();
+    for (uint64_t m = s_rows; m; m &= m - 1) {
+        const uint32_t q = q0 + (uint32_t)__builtin_ctzll(m);
+        const uint32_t lq = qry_len[q];
+        uint16_t *const row = denom + (uint64_t)q * n_ref;
+        for (uint32_t r = threadIdx.x; r < n_ref; r += 256) {
+            const uint32_t d = ref_len[r] + lq;
+            if (d < S) row[r] = (uint16_t)d;
+        }
+    }
+}
+
+hipError_t launch_dist_counts_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
+                                    const uint32_t *d_qry_len, uint32_t n_qry, uint32_t S,
+                                    uint16_t *denom, hipStream_t st)
+{
+    if (!n_ref || !n_qry) return hipSuccess;
+    hipLaunchKernelGGL(dist_counts_fixup_kernel, dim3((n_qry + 63) / 64), dim3(256), 0, st,
+                       d_ref_len, n_ref, d_qry_len, n_qry, S, denom);
+    return hipGetLastError();
+}
+
 // The same per-pair arithmetic as dist_finalize_kernel, for the candidate cells of the
 // sparse path only (the probe wrote every other cell's final values).  Grid-stride over the
 // device-side candidate count; with `sym` each candidate (q, r), r <= q, also finalizes its

@@ -158,6 +158,14 @@ struct fpm_ctx {
     // latency-bound candidate compare); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
+    // a compact grid's counts written ahead on `aux` (fpm_dist_list_prefill), until the dist
+    // call on that grid takes it over (or any other dist call waits for it): ev_prefill
+    struct Prefill {
+        const void *numer = nullptr, *denom = nullptr;
+        uint32_t n_ref = 0, n_qry = 0, S = 0;
+        bool pending = false;
+    } prefill;
+    hipEvent_t ev_prefill = nullptr;
     // pinned staging ring for host -> device copies of pageable caller memory
     static constexpr int kRing = 4;
     static constexpr size_t kRingBytes = 8u << 20;
@@ -349,6 +357,7 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
     hipError_t e = hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_in, hipEventDisableTiming);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_fill, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ctx->ev_prefill, hipEventDisableTiming);
     return e;
 }
 
@@ -496,6 +505,7 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
+    if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -2053,6 +2063,9 @@ struct DistFinal {
     // swapped call
     DistOut mir;
     bool *mirrored = nullptr;
+    // the grid's counts were prefilled (fpm_dist_list_prefill): no defaults of its own, the
+    // short pairs corrected after ev_prefill, before the first cell write
+    bool prefilled = false;
     bool compact() const { return prim.list.count != nullptr; }
     bool has_mirror() const { return mir.cnt.numer != nullptr; }
 };
@@ -2243,6 +2256,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     if (int rc = set_device(ctx)) return rc;
     if (hash_bytes != 4 && hash_bytes != 8) return fail(FPM_EINVAL, "hash_bytes must be 4 or 8");
     hipStream_t st = pick_stream(ctx, stream);
+    if (ctx->prefill.pending) {
+        // a prefill this call does not take over: nothing here may run beside it
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
+        ctx->prefill.pending = false;
+    }
     const uint64_t n_pairs = (uint64_t)n_ref * n_qry;
     ctx->last_sparse = 0;
     ctx->last_events = 0;
@@ -2266,10 +2284,23 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     // (same box, full output): C4's 2.5e9-pair grid 16.7 -> 15.4 ms; C2's 1e8 pairs +1 %, so
     // by grid size.  A transposed grid's defaults are written by the fill only.  The compact
     // output needs a fill only for the counts.
-    const bool fill_cnt = fin && (want_mir || (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28)
-                                                                     : ctx->fill_counts != 0));
+    const bool prefilled = fin && fin->prefilled;
+    const bool fill_cnt = fin && !prefilled &&
+                          (want_mir || (ctx->fill_counts < 0 ? n_pairs >= (1ULL << 28)
+                                                             : ctx->fill_counts != 0));
     const bool need_fill = fin && (!compact || fill_cnt);
     bool fill_pending = false;
+    // a prefilled grid: wait for the prefill, then correct the pairs whose lists hold fewer
+    // than S hashes together, before the first write of a cell (once)
+    bool prefill_done = !prefilled;
+    auto settle_prefill = [&]() -> int {
+        if (prefill_done) return FPM_OK;
+        prefill_done = true;
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
+        HIP_TRY(launch_dist_counts_fixup(d_ref_len, n_ref, d_qry_len, n_qry, sketch_size,
+                                         (uint16_t *)cnt.denom, st));
+        return FPM_OK;
+    };
     // record_in = false: the caller recorded ev_in on `st` already (at the point the fill may
     // start) and submits the fill after later work on `st`
     auto launch_fill = [&](bool record_in) -> int {
@@ -2512,7 +2543,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);
                 HIP_TRY(launch_probe_rows(p_qry, d_qry_len, p_qry_stride, n_qry, n_ref, hash_bytes,
                                           geom, dir, entries, d_ref_len, sketch_size, sym,
-                                          !fill_cnt, self_set, cnt, (uint64_t *)cand, n_cand,
+                                          !fill_cnt && !prefilled, self_set, cnt,
+                                          (uint64_t *)cand, n_cand,
                                           (uint64_t *)row_seg, p_qry_it,
                                           skip_count ? unsorted : nullptr,
                                           skip_count ? events : nullptr, st));
@@ -2554,6 +2586,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                 if (int rc = launch_fill(true)) return rc;
             }
             if (fill_pending && !cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+            if (!cnum)                              // the literal walk writes cells in place
+                if (int rc = settle_prefill()) return rc;
             {
                 TimedLaunch tl(ctx, FPM_K_COMPARE, st);
                 if (rows_merge)
@@ -2571,6 +2605,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             if (defer_fill)
                 if (int rc = launch_fill(false)) return rc;
             if (fill_pending && cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
+            if (int rc = settle_prefill()) return rc;
             if (fin) {
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
                 if (compact) {
@@ -2607,6 +2642,11 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             ctx->last_cand_stream = st;
             return FPM_OK;
         }
+    }
+    // the dense compare writes every cell: after a prefill, not beside it
+    if (prefilled && !prefill_done) {
+        HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
+        prefill_done = true;
     }
     if (compare_grid_img_ok(hash_bytes, sketch_size, ref_stride, qry_stride)) {
         size_t ub, bb;
@@ -2664,8 +2704,19 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                                     (compact ? ": list qry / ref / distance / p-value buffers required"
                                              : ": distance and p-value buffers required"));
     hipStream_t st = pick_stream(ctx, stream);
+    // the prefill of this very grid (fpm_dist_list_prefill) is taken over; any other waits in
+    // compare_impl
+    bool prefilled = false;
+    if (ctx->prefill.pending) {
+        const fpm_ctx::Prefill &pf = ctx->prefill;
+        prefilled = compact && out.cnt.c16 && !mirror && !rs && pf.numer == out.cnt.numer &&
+                    pf.denom == out.cnt.denom && pf.n_ref == n_ref && pf.n_qry == n_qry &&
+                    pf.S == sketch_size;
+        if (prefilled) ctx->prefill.pending = false;
+    }
     if (compact) HIP_TRY(hipMemsetAsync(out.list.count, 0, 8, st));
     DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue, out};
+    fin.prefilled = prefilled;
     bool finalized = false, mirrored = false;
     if (mirror) {
         fin.mir = *mirror;
@@ -2773,6 +2824,30 @@ int fpm_dist_list_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len
     return dist_dev_impl(ctx, d_ref, d_ref_len, d_ref_length, ref_stride, n_ref, d_qry, d_qry_len,
                          d_qry_length, qry_stride, n_qry, hash_bytes, sketch_size, kmer_size,
                          kmer_space, max_dist, max_pvalue, o, stream, "fpm_dist_list_dev");
+}
+
+int fpm_dist_list_prefill(fpm_ctx *ctx, uint16_t *d_numer, uint16_t *d_denom, uint32_t n_ref,
+                          uint32_t n_qry, uint32_t sketch_size, void *stream)
+{
+    if (int rc = set_device(ctx)) return rc;
+    if (!d_numer || !d_denom) return fail(FPM_EINVAL, "fpm_dist_list_prefill: numer / denom buffers required");
+    if (sketch_size > 65535)
+        return fail(FPM_EINVAL, "fpm_dist_list_prefill: sketch_size must be <= 65535 (u16 counts)");
+    hipStream_t st = pick_stream(ctx, stream);
+    HIP_TRY(ensure_aux(ctx));
+    // one prefill at a time: an earlier one nobody took over is waited for by `stream` first
+    if (ctx->prefill.pending) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
+    HIP_TRY(hipEventRecord(ctx->ev_in, st));
+    HIP_TRY(hipStreamWaitEvent(ctx->aux, ctx->ev_in, 0));
+    {
+        TimedLaunch tl(ctx, FPM_K_FILL, ctx->aux);
+        HIP_TRY(launch_dist_counts_const(d_numer, d_denom, (uint64_t)n_ref * n_qry, sketch_size,
+                                         ctx->aux));
+        tl.done();
+    }
+    HIP_TRY(hipEventRecord(ctx->ev_prefill, ctx->aux));
+    ctx->prefill = fpm_ctx::Prefill{d_numer, d_denom, n_ref, n_qry, sketch_size, true};
+    return FPM_OK;
 }
 
 int fpm_dist_finalize_dev(fpm_ctx *ctx, const uint32_t *d_numer, const uint32_t *d_denom,

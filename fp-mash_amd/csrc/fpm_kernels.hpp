@@ -195,6 +195,13 @@ struct PairFill {
 hipError_t launch_dist_fill(const uint32_t *d_ref_len, uint32_t n_ref, const uint32_t *d_qry_len,
                             uint32_t n_qry, uint32_t S, Counts cnt, const PairFill &fill,
                             hipStream_t st, bool flat = true);
+// A compact grid's counts written ahead of its dist call (fpm_dist_list_prefill): (0, S) in
+// every cell; then, once the lists are known, denom = la + lb where la + lb < S
+hipError_t launch_dist_counts_const(uint16_t *numer, uint16_t *denom, uint64_t cells, uint32_t S,
+                                    hipStream_t st);
+hipError_t launch_dist_counts_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
+                                    const uint32_t *d_qry_len, uint32_t n_qry, uint32_t S,
+                                    uint16_t *denom, hipStream_t st);
 // `defaults`: also write (0, min(S, la+lb)) to every numer / denom cell of the row (off
 // when launch_dist_fill already did)
 hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint64_t stride,

@@ -106,6 +106,7 @@ SYMBOLS = [
     ("fpm_dist_list_dev", C.c_int, [vp, vp, vp, vp, C.c_uint64, C.c_uint32, vp, vp, vp,
                                     C.c_uint64, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32,
                                     C.c_double, C.c_double, C.c_double, vp, vp, vp, vp]),
+    ("fpm_dist_list_prefill", C.c_int, [vp, vp, vp, C.c_uint32, C.c_uint32, C.c_uint32, vp]),
     ("fpm_fp_positional_grid", C.c_int, [vp, vp, u32p, C.c_uint64, C.c_uint32, vp, u32p,
                                          C.c_uint64, C.c_uint32, C.c_uint32, C.c_double,
                                          C.c_double, u32p, u32p, f64p, f64p, u8p]),
@@ -641,10 +642,11 @@ class Context:
 
     def dist_list(self, ref_lists, qry_lists, sketch_size, use64=True, k=21, kmer_space=None,
                   ref_lengths=None, qry_lengths=None, max_dist=-1.0, max_pvalue=-1.0, cap=None,
-                  expand=True):
+                  expand=True, prefill=False):
         """dist() through fpm_dist_list_dev (the compact output: u16 counts + the list of
         cells with numer > 0).  expand=True: the five per-cell arrays (expand_compact), else
-        (numer, denom, listed)."""
+        (numer, denom, listed).  prefill=True: the counts prefilled first
+        (fpm_dist_list_prefill, taken over by the dist call)."""
         dt = np.uint64 if use64 else np.uint32
         w = max([len(x) for x in list(ref_lists) + list(qry_lists)] + [1])
         R, rl = _dense(ref_lists, w, dt)
@@ -669,6 +671,9 @@ class Context:
             outs = [DeviceBuffer(self, max(n, 1) * 2) for _ in range(2)]
             bufs += outs
             lst = CellList(self, cap if cap is not None else max(n, 1))
+            if prefill:
+                _check(lib().fpm_dist_list_prefill(self.h, outs[0].ptr, outs[1].ptr, nr, nq,
+                                                   sketch_size, None))
             _check(lib().fpm_dist_list_dev(self.h, dR, drl, drL, w, nr, dQ, dql, dqL, w, nq,
                                            8 if use64 else 4, sketch_size, k, kmer_space,
                                            max_dist, max_pvalue, outs[0].ptr, outs[1].ptr,

@@ -320,6 +320,18 @@ int fpm_dist_list_dev(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_len
                       uint32_t sketch_size, uint32_t kmer_size, double kmer_space,
                       double max_dist, double max_pvalue, uint16_t *d_numer, uint16_t *d_denom,
                       const fpm_cell_list *list, void *stream);
+/* The compact grid's counts ahead of the call that computes them, e.g. before the sketches
+ * exist: numer 0 and denom sketch_size in all n_qry x n_ref u16 cells, on the context's side
+ * stream after the work already on `stream` (a pure write stream beside the sketch kernels).
+ * The next fpm_dist_list_dev on this context whose numer / denom / n_ref / n_qry /
+ * sketch_size are these takes it over: it writes no no-shared-hash counts of
+ * its own, sets denom = la + lb where la + lb < sketch_size (compareSketches' min(S, la + lb)
+ * at common = 0, CommandDistance.cpp:416-418) and writes its cells after the prefill.  Any
+ * other dist call on the context waits for it first.  Until then only that call (or
+ * fpm_ctx_synchronize) orders the grid against the prefill.  No reference counterpart: its
+ * compare writes every pair (CommandDistance.cpp:365-430). */
+int fpm_dist_list_prefill(fpm_ctx *ctx, uint16_t *d_numer, uint16_t *d_denom, uint32_t n_ref,
+                          uint32_t n_qry, uint32_t sketch_size, void *stream);
 /* host-buffer convenience: compare + finalize */
 int fpm_dist(fpm_ctx *ctx, const void *ref, const uint32_t *ref_len, const uint64_t *ref_length,
              uint64_t ref_stride, uint32_t n_ref, const void *qry, const uint32_t *qry_len,

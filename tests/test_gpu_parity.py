@@ -1150,3 +1150,76 @@ def test_refset_unsorted_query_block(ctx, oracle):
         np.testing.assert_allclose(got[3], pv.ravel(), rtol=RTOL, atol=0)
         for b in bufs + outs:
             b.free()
+
+
+@pytest.mark.parametrize("data", ["self", "other", "fp", "short"])
+def test_dist_list_prefill(ctx, oracle, data, dist_mode):
+    """fpm_dist_list_prefill before fpm_dist_list_dev (the counts written ahead as (0, S), the
+    dist call correcting the pairs with la + lb < S and writing its cells after the prefill):
+    the same counts and list as without it, equal to the oracle, in every dist mode; sorted
+    sketches against themselves (symmetric path) and another set, unsorted -fp lists (the
+    literal walk writes cells in place), short sketches (la + lb < S: the correction), and
+    empty lists."""
+    import fpmash
+    from fpmash import datagen
+    if data == "fp":
+        rng = np.random.default_rng(43)
+        sk = [rng.integers(0, 60, size=int(rng.integers(0, 400))).astype(np.uint32)
+              for _ in range(90)]
+        sk[5] = sk[5][:0]
+        qsk = sk[::-1][:50]
+        S, k, space, use64 = 300, 1, 10.0, False
+        lens = np.array([len(x) * 3 + 7 for x in sk], np.uint64)
+        qlens = lens[::-1][:50].copy()
+    else:
+        P = fpmash.make_params(k=21, s=500)
+        if data == "short":
+            rng = np.random.default_rng(5)
+            seqs = [bytes(rng.choice(list(b"ACGT"), size=int(rng.integers(15, 700))))
+                    for _ in range(70)]
+            seqs += datagen.family_dna(2, 10, 900, sub_rate=(0.0, 0.05), seed=6)
+        else:
+            seqs = datagen.family_dna(8, 12, 1500, sub_rate=(0.0, 0.08), seed=31)
+            seqs += [b"N" * 300, b"", b"ACGT" * 3]
+        sk = ctx.sketch(P, seqs)
+        qsk = sk if data in ("self", "short") else sk[::-1][:60]
+        S, k, space, use64 = 500, 21, 4.0 ** 21, True
+        lens = np.array([len(x) for x in seqs], np.uint64)
+        qlens = lens if qsk is sk else lens[::-1][:60].copy()
+    kw = dict(use64=use64, k=k, kmer_space=space, ref_lengths=lens, qry_lengths=qlens)
+    a = ctx.dist_list(sk, qsk, S, prefill=True, **kw)
+    b = ctx.dist_list(sk, qsk, S, **kw)
+    for key in ("numer", "denom", "distance", "pvalue", "pass"):
+        assert np.array_equal(a[key], b[key]), key
+    nu, de, _, _ = oracle.dist_grid(sk, list(lens), qsk, list(qlens), S, k, space, use64=use64,
+                                    with_pvalue=False)
+    assert np.array_equal(a["numer"], nu) and np.array_equal(a["denom"], de)
+    if data == "short":
+        assert (de < S).sum() > 100          # the correction rewrote these
+
+
+def test_dist_list_prefill_not_taken_over(ctx, oracle):
+    """A prefill whose grid the next dist call does not write: that call waits for it, its own
+    grid is exact, and the prefilled grid holds (0, S) after the stream work; a second prefill
+    while one is pending orders the first before the caller's stream."""
+    import fpmash
+    from fpmash import datagen
+    P = fpmash.make_params(k=21, s=400)
+    seqs = datagen.family_dna(5, 10, 1200, sub_rate=(0.0, 0.05), seed=12)
+    sk = ctx.sketch(P, seqs)
+    n = len(sk)
+    lens = [len(x) for x in seqs]
+    L = fpmash.lib()
+    spare = [fpmash.DeviceBuffer(ctx, 64 * 64 * 2) for _ in range(4)]
+    fpmash._check(L.fpm_dist_list_prefill(ctx.h, spare[0].ptr, spare[1].ptr, 64, 64, 300, None))
+    fpmash._check(L.fpm_dist_list_prefill(ctx.h, spare[2].ptr, spare[3].ptr, 64, 64, 400, None))
+    d = ctx.dist_list(sk, sk, 400, ref_lengths=lens, qry_lengths=lens)
+    ctx.synchronize()
+    nu, de, _, _ = oracle.dist_grid(sk, lens, sk, lens, 400, 21, 4.0 ** 21, with_pvalue=False)
+    assert np.array_equal(d["numer"], nu) and np.array_equal(d["denom"], de)
+    for i, S in ((0, 300), (2, 400)):
+        assert not spare[i].to_array(np.uint16, 64 * 64).any()
+        assert (spare[i + 1].to_array(np.uint16, 64 * 64) == S).all()
+    for b in spare:
+        b.free()
+    assert n > 0
