@@ -763,6 +763,18 @@ struct fpm_sketch_job {
     TileDesc *d_redo = nullptr;
     uint32_t *d_redo_n = nullptr;
     uint32_t n4 = 0;                 // class-4 tiles (the redo list's capacity)
+    // tight bounds (groups with a selection): each slot's bound is the sample's kt-th smallest
+    // hash instead of its s-th (d_kt), the s-th kept as d_thr_safe; a group left with fewer
+    // than s hashes (sketch_short_kernel: d_short = count, then the slots) is redone with the
+    // safe bound: its tiles and selections again, from the host copies below
+    bool tight = false;
+    uint32_t *d_kt = nullptr, *d_slot_group = nullptr, *d_short = nullptr;
+    uint64_t *d_thr_safe = nullptr;
+    std::vector<TileDesc> h_tiles;          // the main tiles by class (class_begin)
+    std::vector<SelDesc> h_sel;             // the selections (sample levels, then main)
+    TileDesc *d_rtiles = nullptr;           // the redo's subsets (allocated on first use)
+    SelDesc *d_rsel = nullptr;
+    int32_t last_short = -1;                // groups redone by the last run (-1: no tight bounds)
     // -M pass (allocated on first use)
     uint32_t *d_mult = nullptr;
     unsigned long long *d_first = nullptr;
@@ -778,6 +790,8 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_stiles); (void)hipFree(j->d_smerge); (void)hipFree(j->d_srow);
     (void)hipFree(j->d_thr);
     (void)hipFree(j->d_redo); (void)hipFree(j->d_redo_n);
+    (void)hipFree(j->d_kt); (void)hipFree(j->d_slot_group); (void)hipFree(j->d_short);
+    (void)hipFree(j->d_thr_safe); (void)hipFree(j->d_rtiles); (void)hipFree(j->d_rsel);
     (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
@@ -1166,7 +1180,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     alloc((void **)&job->d_sel_rows, sel_rows.size() * sizeof(uint32_t));
     alloc((void **)&job->d_sel_failed, (sel.size() + 2) * sizeof(uint32_t));
     if (e == hipSuccess && !sel.empty())
-        e = hipHostMalloc((void **)&job->h_sel_failed, 2 * sizeof(uint32_t), hipHostMallocDefault);
+        e = hipHostMalloc((void **)&job->h_sel_failed, 3 * sizeof(uint32_t), hipHostMallocDefault);
     {
         // the survivors-only tile kernel for the class-4 tiles when every one carries its
         // group's bound and that bound leaves few survivors per tile: a group's main pass keeps
@@ -1190,6 +1204,31 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             alloc((void **)&job->d_redo, (size_t)n4 * sizeof(TileDesc));
             alloc((void **)&job->d_redo_n, sizeof(uint32_t));
         }
+    }
+    // tight bounds where every sampled group has a selection: kt = f s + 8 sqrt(f s) + 32 of
+    // the sample's hashes (f = the group's sampled share of tiles), so ~kt / f >= s of the
+    // group's distinct hashes lie below it with ~8 standard deviations to spare (C5: 864 of
+    // the sample's 10,000; the group keeps ~14k hashes instead of ~160k)
+    std::vector<uint32_t> kt, slot_group;
+    if (use_sel && !srow.empty() && !sel.empty()) {
+        kt.assign(srow.size(), s);
+        slot_group.assign(srow.size(), 0);
+        for (uint32_t g = 0; g < n_groups; g++) {
+            if (!slot_of[g]) continue;
+            const uint32_t i = slot_of[g] - 1;
+            slot_group[i] = g;
+            const double f = (double)((ntile_of[g] + kSampleEvery - 1) / kSampleEvery) / ntile_of[g];
+            const double fs = f * s;
+            kt[i] = (uint32_t)std::min<double>(s, std::ceil(fs + 8.0 * std::sqrt(fs) + 32.0));
+        }
+        job->tight = true;
+        alloc((void **)&job->d_kt, kt.size() * sizeof(uint32_t));
+        alloc((void **)&job->d_slot_group, slot_group.size() * sizeof(uint32_t));
+        alloc((void **)&job->d_short, (srow.size() + 1) * sizeof(uint32_t));
+        alloc((void **)&job->d_thr_safe, srow.size() * sizeof(uint64_t));
+        job->h_tiles = by_class;
+        job->h_sel = sel;
+        job->last_short = 0;
     }
     if (e != hipSuccess) {
         job_release(job);
@@ -1224,6 +1263,10 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         e = copy_in(ctx, job->d_sel, sel.data(), sel.size() * sizeof(SelDesc));
     if (e == hipSuccess && !sel_rows.empty())
         e = copy_in(ctx, job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t));
+    if (e == hipSuccess && !kt.empty())
+        e = copy_in(ctx, job->d_kt, kt.data(), kt.size() * sizeof(uint32_t));
+    if (e == hipSuccess && !slot_group.empty())
+        e = copy_in(ctx, job->d_slot_group, slot_group.data(), slot_group.size() * sizeof(uint32_t));
     if (e != hipSuccess) {
         job_release(job);
         delete job;
@@ -1259,6 +1302,55 @@ static int fallback_descs(fpm_sketch_job *job)
     };
     if (int rc = upload(job->fplan, &job->d_fmerge)) return rc;
     return upload(job->sfplan, &job->d_sfmerge);
+}
+
+// The groups a tight bound left short (their slots in d_short[1 ..], bounds already raised
+// to the safe ones by sketch_short_kernel): their main tiles and selections once more
+template <typename TilesPass>
+static int redo_short(fpm_sketch_job *job, uint32_t n_short, hipStream_t st, TilesPass &tiles_pass)
+{
+    fpm_ctx *ctx = job->ctx;
+    std::vector<uint32_t> slots(n_short);
+    HIP_TRY(hipMemcpyAsync(slots.data(), job->d_short + 1, n_short * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint8_t> is_short(job->n_slots + 1, 0);
+    for (uint32_t i : slots)
+        if (i < job->n_slots) is_short[i] = 1;
+    std::vector<TileDesc> sub;
+    uint32_t begin[kTileClasses + 1] = {0};
+    for (int c = 0; c < kTileClasses; c++) {
+        for (uint32_t t = job->class_begin[c]; t < job->class_begin[c + 1]; t++) {
+            const TileDesc &td = job->h_tiles[t];
+            if (td.thr_slot && is_short[td.thr_slot - 1]) sub.push_back(td);
+        }
+        begin[c + 1] = (uint32_t)sub.size();
+    }
+    std::vector<SelDesc> rsel;
+    std::vector<uint32_t> rbegin{0};
+    for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
+        for (uint32_t i = job->sel_begin[l]; i < job->sel_begin[l + 1]; i++) {
+            const SelDesc &d = job->h_sel[i];
+            if (d.slot != 0xFFFFFFFFu && d.slot < job->n_slots && is_short[d.slot]) rsel.push_back(d);
+        }
+        rbegin.push_back((uint32_t)rsel.size());
+    }
+    if (!job->d_rtiles)
+        HIP_TRY(hipMalloc((void **)&job->d_rtiles, std::max<size_t>(1, job->h_tiles.size()) * sizeof(TileDesc)));
+    if (!job->d_rsel)
+        HIP_TRY(hipMalloc((void **)&job->d_rsel, std::max<size_t>(1, job->h_sel.size()) * sizeof(SelDesc)));
+    if (!sub.empty()) HIP_TRY(copy_in(ctx, job->d_rtiles, sub.data(), sub.size() * sizeof(TileDesc)));
+    if (!rsel.empty()) HIP_TRY(copy_in(ctx, job->d_rsel, rsel.data(), rsel.size() * sizeof(SelDesc)));
+    if (int rc = tiles_pass(job->d_rtiles, begin, true)) return rc;
+    for (size_t l = 0; l + 1 < rbegin.size(); l++) {
+        const uint32_t b = rbegin[l], n = rbegin[l + 1] - b;
+        if (!n) continue;
+        TimedLaunch tl(ctx, FPM_K_MERGE, st);
+        HIP_TRY(launch_group_select(job->d_rsel + b, n, job->d_sel_rows, job->d_rows, job->d_count,
+                                    job->kp.s, job->d_thr, job->d_sel_failed, st));
+        tl.done();
+    }
+    return FPM_OK;
 }
 
 extern "C" {
@@ -1331,11 +1423,13 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
             }
         }
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,
-                                        job->kp.s, job->d_thr, st));
+                                        job->kp.s, job->tight ? job->d_kt : nullptr, job->d_thr,
+                                        job->tight ? job->d_thr_safe : nullptr, st));
     }
     // (the selections of each batch of genomes on a side stream beside the next batch's
     // tiles measured a wash on C5: the 120 KB-LDS selection workgroups take the tiles' CUs)
     if (int rc = tiles_pass(job->d_tiles, job->class_begin, true)) return rc;
+    const bool tight = job->tight && job->n_slots;
     if (job->n_sel) {
         for (size_t l = 0; l + 1 < job->sel_begin.size(); l++) {
             const uint32_t b = job->sel_begin[l], n = job->sel_begin[l + 1] - b;
@@ -1351,12 +1445,43 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
     if (job->n_sel) {
         // a selection that did not fit (more repeated values below the cut than LDS holds):
         // the pairwise merges of every sampled group's lists (rare; one host round trip)
-        HIP_TRY(hipStreamSynchronize(st));
-        if (*job->h_sel_failed) {
+        auto fallback = [&]() -> int {
             if (int rc = fallback_descs(job)) return rc;
             return merge_pass(job->d_fmerge, job->fround_begin, job->fround_small);
+        };
+        HIP_TRY(hipStreamSynchronize(st));
+        if (*job->h_sel_failed)
+            if (int rc = fallback()) return rc;
+        if (tight) {
+            // the groups the tight bound left short, once every group's count is final: listed,
+            // their bound raised to the safe one, and their tiles and selections run again
+            HIP_TRY(hipMemsetAsync(job->d_short, 0, sizeof(uint32_t), st));
+            HIP_TRY(launch_sketch_short(job->d_slot_group, job->n_slots, job->d_count, job->kp.s,
+                                        job->d_thr, job->d_thr_safe, job->d_short, job->d_short + 1,
+                                        st));
+            HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 2, job->d_short, sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            const uint32_t n_short = job->h_sel_failed[2];
+            job->last_short = (int32_t)n_short;
+            if (n_short) {
+                HIP_TRY(hipMemsetAsync(fail_main, 0, sizeof(uint32_t), st));
+                if (int rc = redo_short(job, n_short, st, tiles_pass)) return rc;
+                HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                if (*job->h_sel_failed)
+                    if (int rc = fallback()) return rc;
+            }
         }
     }
+    return FPM_OK;
+}
+
+int fpm_sketch_job_short_groups(fpm_sketch_job *job, int32_t *n_short)
+{
+    if (!job || !n_short) return fail(FPM_EINVAL, "null argument");
+    *n_short = job->last_short;
     return FPM_OK;
 }
 

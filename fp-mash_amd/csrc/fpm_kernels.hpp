@@ -74,10 +74,17 @@ hipError_t launch_sketch_mult(int cls, int pass, const uint8_t *d_seq, const Til
                               unsigned long long *d_first, const uint64_t *d_ttop, hipStream_t st);
 hipError_t launch_mult_ttop(const uint32_t *d_count, uint32_t n_groups, uint32_t s,
                             const unsigned long long *d_first, uint64_t *d_ttop, hipStream_t st);
-// thr[i] = s-th smallest of sample row srow[i] when it holds s hashes, else no bound
+// thr_safe[i] = s-th smallest of sample row srow[i] when it holds s hashes, else no bound;
+// thr[i] = its kt[i]-th smallest (d_kt null: thr = thr_safe)
 hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
-                                   const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
-                                   hipStream_t st);
+                                   const uint32_t *d_count, uint32_t s, const uint32_t *d_kt,
+                                   uint64_t *d_thr, uint64_t *d_thr_safe, hipStream_t st);
+// slots whose group (slot_group[i]) ended with fewer than s hashes under thr < thr_safe:
+// listed (d_short_slots, count *d_n_short, zeroed by the caller), thr raised to thr_safe
+hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
+                               const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
+                               const uint64_t *d_thr_safe, uint32_t *d_n_short,
+                               uint32_t *d_short_slots, hipStream_t st);
 uint32_t merge_small_cap();   // list length merge_small_kernel stages in LDS
 // one long group's sketch selected from its bounded tile lists (rows row_ids[row_begin ..
 // row_begin + n_rows)) into out_row; slot: its bound thr[slot] (0xFFFFFFFF: none, the

@@ -917,24 +917,63 @@ hipError_t launch_mult_ttop(const uint32_t *d_count, uint32_t n_groups, uint32_t
     return hipGetLastError();
 }
 
+// thr_safe[i] = the s-th smallest of sample row srow[i] when it holds s hashes (a subset's
+// order statistic: >= the group's own s-th smallest), else no bound.  thr[i] = the tighter
+// kt[i]-th smallest (kt: null = the safe bound): the sample holds ~f of the group's windows,
+// so ~kt / f of the group's distinct hashes lie below it, and kt = f s + 8 sqrt(f s) + 32
+// leaves the group >= s of them unless its values repeat across its tiles; a group left with
+// fewer than s is found after its selection (sketch_short_kernel) and redone with thr_safe.
 __global__ void sketch_threshold_kernel(const uint32_t *__restrict__ srow, uint32_t n_slots,
                                         const uint64_t *__restrict__ rows,
                                         const uint32_t *__restrict__ count, uint32_t s,
-                                        uint64_t *__restrict__ thr)
+                                        const uint32_t *__restrict__ kt,
+                                        uint64_t *__restrict__ thr, uint64_t *__restrict__ thr_safe)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_slots) return;
     const uint32_t r = srow[i];
-    thr[i] = count[r] >= s ? rows[(uint64_t)r * s + s - 1] : ~0ULL;
+    const bool full = count[r] >= s;
+    const uint64_t safe = full ? rows[(uint64_t)r * s + s - 1] : ~0ULL;
+    if (thr_safe) thr_safe[i] = safe;
+    thr[i] = full && kt ? rows[(uint64_t)r * s + min(kt[i], s) - 1] : safe;
 }
 
 hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, const uint64_t *d_rows,
-                                   const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
-                                   hipStream_t st)
+                                   const uint32_t *d_count, uint32_t s, const uint32_t *d_kt,
+                                   uint64_t *d_thr, uint64_t *d_thr_safe, hipStream_t st)
 {
     if (!n_slots) return hipSuccess;
     hipLaunchKernelGGL(sketch_threshold_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
-                       d_srow, n_slots, d_rows, d_count, s, d_thr);
+                       d_srow, n_slots, d_rows, d_count, s, d_kt, d_thr, d_thr_safe);
+    return hipGetLastError();
+}
+
+// The sampled groups whose tight bound left fewer than s distinct hashes (their values repeat
+// across tiles): listed in short_slots[0 .. *n_short) (zeroed by the caller), and their bound
+// raised to the safe one for the redo of their tiles and selection.
+__global__ void sketch_short_kernel(const uint32_t *__restrict__ slot_group, uint32_t n_slots,
+                                    const uint32_t *__restrict__ count, uint32_t s,
+                                    uint64_t *__restrict__ thr,
+                                    const uint64_t *__restrict__ thr_safe,
+                                    uint32_t *__restrict__ n_short, uint32_t *__restrict__ short_slots)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    if (count[slot_group[i]] < s && thr[i] < thr_safe[i]) {
+        short_slots[atomicAdd(n_short, 1u)] = i;
+        thr[i] = thr_safe[i];
+    }
+}
+
+hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
+                               const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
+                               const uint64_t *d_thr_safe, uint32_t *d_n_short,
+                               uint32_t *d_short_slots, hipStream_t st)
+{
+    if (!n_slots) return hipSuccess;
+    hipLaunchKernelGGL(sketch_short_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
+                       d_slot_group, n_slots, d_count, s, d_thr, d_thr_safe, d_n_short,
+                       d_short_slots);
     return hipGetLastError();
 }
 
@@ -1180,8 +1219,43 @@ __global__ __launch_bounds__(kSelThreads) void group_select_kernel(
         tot = t;
         return pre + x - v;
     };
+    // The rows' mean length picks how the waves walk them: a wave per row, lanes over its keys
+    // (the sample's rows: thousands of keys each), or, for short rows (a tight bound leaves a
+    // C5 tile ~11 keys), a lane per row, 64 rows per wave in flight (a wave per row waited
+    // out three dependent loads per ~11 keys: the selection took 1.9 ms of C5's step)
+    uint32_t n_keys = 0;
+    for (uint32_t ri = tid; ri < d.n_rows; ri += kSelThreads) n_keys += count[row_ids[d.row_begin + ri]];
+    {
+        uint32_t tot;
+        (void)block_scan(n_keys, tot);
+        n_keys = tot;
+    }
+    const bool lane_rows = n_keys < 32u * d.n_rows;
     // every kept key of the group with key < lim (lim = 0: all), handed to f(key)
     auto for_keys = [&](uint64_t lim, auto f) {
+        if (lane_rows) {
+            for (uint32_t r0 = wave * 64; r0 < d.n_rows; r0 += kWaves * 64) {
+                const uint32_t ri = r0 + lane;
+                uint32_t c = 0;
+                const uint64_t *base = rows;
+                if (ri < d.n_rows) {
+                    const uint32_t row = row_ids[d.row_begin + ri];
+                    c = count[row];
+                    base = rows + (uint64_t)row * s;
+                }
+                uint32_t cmax = c;
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) cmax = max(cmax, (uint32_t)__shfl_xor(cmax, o, 64));
+                for (uint32_t i = 0; i < cmax; i++) {
+                    if (i < c) {
+                        const uint64_t key = base[i];
+                        if (lim && key >= lim) c = i;      // lists are ascending: this row is done
+                        else f(key);
+                    }
+                }
+            }
+            return;
+        }
         for (uint32_t ri = wave; ri < d.n_rows; ri += kWaves) {
             const uint32_t row = row_ids[d.row_begin + ri];
             const uint32_t c = count[row];

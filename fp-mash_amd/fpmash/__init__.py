@@ -80,6 +80,7 @@ SYMBOLS = [
     ("fpm_merge_small_spills", C.c_int, [vp, u64p]),
     ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
     ("fpm_sketch_job_redo_tiles", C.c_int, [vp, C.POINTER(C.c_int32)]),
+    ("fpm_sketch_job_short_groups", C.c_int, [vp, C.POINTER(C.c_int32)]),
     ("fpm_sketch_job_free", None, [vp]),
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
     ("fpm_fp_hash_lines_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32, vp,
@@ -364,6 +365,13 @@ class SketchJob:
         job does not use that kernel); waits for the device"""
         n = C.c_int32()
         _check(lib().fpm_sketch_job_redo_tiles(self.h, C.byref(n)))
+        return n.value
+
+    def short_groups(self):
+        """long groups of the last run() redone under the sample's s-th smallest hash after
+        the tight bound left them short (-1: no tight bounds in this job)"""
+        n = C.c_int32()
+        _check(lib().fpm_sketch_job_short_groups(self.h, C.byref(n)))
         return n.value
 
     def device_output(self):

@@ -168,6 +168,13 @@ int fpm_sketch_job_info(fpm_sketch_job *job, uint64_t *seq_bytes, uint64_t *n_ti
  * result does not depend on it): -1 when the job does not use that kernel (no long groups, or
  * s too large for their bound to leave few survivors per tile).  Waits for the device. */
 int fpm_sketch_job_redo_tiles(fpm_sketch_job *job, int32_t *n_redo);
+/* Long groups of the last run() that their tight bound (the sample's kt-th smallest hash,
+ * kt ~ f s + 8 sqrt(f s) + 32 for a sampled share f of the group's tiles) left with fewer
+ * than s hashes, so their tiles and selection ran again under the sample's s-th smallest
+ * (values repeated across the group's tiles): a test hook; the sketches are MinHashHeap's
+ * either way (MinHashHeap.cpp:68-146).  -1 when the job has no tight bounds (no long
+ * groups, or s beyond the one-workgroup selection). */
+int fpm_sketch_job_short_groups(fpm_sketch_job *job, int32_t *n_short);
 void fpm_sketch_job_free(fpm_sketch_job *job);
 
 /* Bottom-s of the union of n_lists sketches (device rows of stride s, ascending and

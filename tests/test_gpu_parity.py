@@ -635,13 +635,40 @@ def test_sketch_survivors_kernel_redo(ctx, oracle, kind):
             n_redo = job.redo_tiles()
             if kind == "random":
                 assert n_redo == 0
+                assert job.short_groups() == 0  # the tight bound held
             else:
                 assert n_redo > 400             # 488 tiles, nearly all of them
+                # the sample holds all ~3,000 distinct k-mers: its kt-th smallest leaves the
+                # group ~160 of them, so the group is redone under the s-th smallest
+                assert job.short_groups() == 1
         rows, cnt = job.fetch()
     finally:
         job.free()
     exp = oracle.sketch_batch(oracle.params(k=21, s=1000), [seq])
     check_sketches([rows[0, : cnt[0]]], exp)
+
+
+@pytest.mark.parametrize("s", [2000, 10000])
+def test_sketch_tight_bound_short_groups(ctx, oracle, s):
+    """Long groups bounded by the sample's kt-th smallest hash (kt ~ f s + 8 sqrt(f s) + 32):
+    random genomes keep >= s hashes under it (short_groups() == 0); a genome of one 300 kb unit
+    repeated 7 times has ~2.2x as many distinct k-mers as its sample, so the tight bound leaves
+    it short and it is redone under the sample's s-th smallest (short_groups() == 1).  Every
+    sketch equals the reference heap's, over two runs of the job (bounds recomputed each run)."""
+    import fpmash
+    rng = np.random.default_rng(s + 3)
+    recs = [rand_seq(rng, 2_000_000), rand_seq(rng, 300_000) * 7, rand_seq(rng, 1_500_000)]
+    P = fpmash.make_params(k=21, s=s)
+    job = ctx.sketch_job(P, recs, groups=[0, 1, 2], n_groups=3)
+    try:
+        for _ in range(2):
+            job.run(ctx.stream)
+            assert job.short_groups() == 1
+        rows, cnt = job.fetch()
+    finally:
+        job.free()
+    exp = oracle.sketch_batch(oracle.params(k=21, s=s), recs, groups=[0, 1, 2], n_groups=3)
+    check_sketches([rows[g, : cnt[g]] for g in range(3)], exp)
 
 
 def test_sketch_survivors_kernel_off_for_large_s(ctx):
