@@ -946,7 +946,15 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     // sketched in a sample pass (own temp rows and merge plan); the sample's s-th smallest
     // hash is >= the group's s-th smallest, so the full pass drops every hash above it and
     // its merges move ~kSampleEvery*s hashes per group instead of every tile's bottom-s.
+    // The sample rate per group: every E-th tile, E = the group's k-mers / 8 s within
+    // [16, 64], so a sample holds ~8 s k-mers: enough for its s-th smallest (the safe bound)
+    // and a tight kt-th one.  C5's 5 Mb genomes: E = 61, C5 23.6 -> 21.9 ms against E = 16
+    // (22.8 ms at 16 s k-mers, E = 31), same box, r05x / r05y.
     constexpr uint32_t kSampleEvery = 16;
+    std::vector<uint32_t> every(n_groups, kSampleEvery);
+    for (uint32_t g = 0; g < n_groups; g++)
+        every[g] = (uint32_t)std::min<uint64_t>(
+            64, std::max<uint64_t>(kSampleEvery, (uint64_t)ntile_of[g] * kChunkKmers / (8ULL * s)));
     std::vector<uint32_t> slot_of(n_groups, 0);          // 0: not sampled, else slot + 1
     std::vector<TileDesc> stiles;
     std::vector<std::vector<uint32_t>> slists(n_groups);
@@ -955,10 +963,10 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         std::vector<uint32_t> seen(n_groups, 0);
         for (size_t t = 0; t < tiles.size(); t++) {
             const uint32_t g = tile_group[t];
-            const uint64_t sample_kmers = (uint64_t)(ntile_of[g] / kSampleEvery) * kChunkKmers;
-            if (ntile_of[g] < 2 * kSampleEvery || sample_kmers < 4ULL * s) continue;
+            const uint64_t sample_kmers = (uint64_t)(ntile_of[g] / every[g]) * kChunkKmers;
+            if (ntile_of[g] < 2 * every[g] || sample_kmers < 4ULL * s) continue;
             if (!slot_of[g]) { srow.push_back(0); slot_of[g] = (uint32_t)srow.size(); }
-            if (seen[g]++ % kSampleEvery == 0) {
+            if (seen[g]++ % every[g] == 0) {
                 TileDesc st = tiles[t];
                 st.out_row = n_rows;
                 st.thr_slot = 0;
@@ -975,7 +983,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     for (size_t t = 0; t < tiles.size(); t++) {
         const uint32_t g = tile_group[t];
         uint64_t e = std::min<uint64_t>(s, tiles[t].n_bytes >= k ? tiles[t].n_bytes - k + 1 : 0);
-        if (slot_of[g]) e = std::min<uint64_t>(e, 2ULL * kSampleEvery * s / ntile_of[g] + 64);
+        if (slot_of[g]) e = std::min<uint64_t>(e, 2ULL * every[g] * s / ntile_of[g] + 64);
         if (tiles[t].out_row < est.size()) est[tiles[t].out_row] = e;
     }
     for (auto &st : stiles)
@@ -1181,34 +1189,10 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     alloc((void **)&job->d_sel_failed, (sel.size() + 2) * sizeof(uint32_t));
     if (e == hipSuccess && !sel.empty())
         e = hipHostMalloc((void **)&job->h_sel_failed, 3 * sizeof(uint32_t), hipHostMallocDefault);
-    {
-        // the survivors-only tile kernel for the class-4 tiles when every one carries its
-        // group's bound and that bound leaves few survivors per tile: a group's main pass keeps
-        // about kSampleEvery * s of its hashes (the sample's s-th smallest bounds them), so a
-        // tile keeps ~kSampleEvery * s / (the group's tiles); est (2x margin + 64, above) must
-        // stay within half of what one tile holds, or most tiles would be hashed twice (their
-        // survivors overflow and the plain kernel redoes them).  (C5 one GPU: 31.2 -> 25.8 ms,
-        // same box, r04; C5 tiles: est 326 of 1,024)
-        const uint32_t b4 = class_begin[4], n4 = class_begin[5] - b4;
-        std::vector<uint64_t> slot_est(srow.size() + 1, ~0ULL);
-        for (uint32_t g = 0; g < n_groups; g++)
-            if (slot_of[g]) slot_est[slot_of[g]] = 2ULL * kSampleEvery * s / ntile_of[g] + 64;
-        bool all = n4 > 0;
-        for (uint32_t i = 0; all && i < n4; i++) {
-            const uint32_t sl = by_class[b4 + i].thr_slot;
-            all = sl != 0 && slot_est[sl] <= kThrTileKeys / 2;
-        }
-        job->thr4 = all;
-        job->n4 = n4;
-        if (all) {
-            alloc((void **)&job->d_redo, (size_t)n4 * sizeof(TileDesc));
-            alloc((void **)&job->d_redo_n, sizeof(uint32_t));
-        }
-    }
     // tight bounds where every sampled group has a selection: kt = f s + 8 sqrt(f s) + 32 of
     // the sample's hashes (f = the group's sampled share of tiles), so ~kt / f >= s of the
-    // group's distinct hashes lie below it with ~8 standard deviations to spare (C5: 864 of
-    // the sample's 10,000; the group keeps ~14k hashes instead of ~160k)
+    // group's distinct hashes lie below it with ~8 standard deviations to spare (C5 at E = 61:
+    // ~300 of the sample's 10,000; the group keeps ~18k hashes instead of ~160k)
     std::vector<uint32_t> kt, slot_group;
     if (use_sel && !srow.empty() && !sel.empty()) {
         kt.assign(srow.size(), s);
@@ -1217,7 +1201,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             if (!slot_of[g]) continue;
             const uint32_t i = slot_of[g] - 1;
             slot_group[i] = g;
-            const double f = (double)((ntile_of[g] + kSampleEvery - 1) / kSampleEvery) / ntile_of[g];
+            const double f = (double)((ntile_of[g] + every[g] - 1) / every[g]) / ntile_of[g];
             const double fs = f * s;
             kt[i] = (uint32_t)std::min<double>(s, std::ceil(fs + 8.0 * std::sqrt(fs) + 32.0));
         }
@@ -1229,6 +1213,37 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         job->h_tiles = by_class;
         job->h_sel = sel;
         job->last_short = 0;
+    }
+    {
+        // the survivors-only tile kernel for the class-4 tiles when every one carries its
+        // group's bound and that bound leaves few survivors per tile: a group's main pass keeps
+        // about kSampleEvery * s of its hashes (the sample's s-th smallest bounds them), so a
+        // tile keeps ~kSampleEvery * s / (the group's tiles); est (2x margin + 64, above) must
+        // stay within half of what one tile holds, or most tiles would be hashed twice (their
+        // survivors overflow and the plain kernel redoes them).  (C5 one GPU: 31.2 -> 25.8 ms,
+        // same box, r04; C5 tiles: est 326 of 1,024)
+        const uint32_t b4 = class_begin[4], n4 = class_begin[5] - b4;
+        // (tight bounds: ~kt / f survivors per group; a short group's redo under the safe bound
+        // keeps ~E s per group, and its tiles that overflow are redone by the plain kernel)
+        std::vector<uint64_t> slot_est(srow.size() + 1, ~0ULL);
+        for (uint32_t g = 0; g < n_groups; g++) {
+            if (!slot_of[g]) continue;
+            const double f = (double)((ntile_of[g] + every[g] - 1) / every[g]) / ntile_of[g];
+            slot_est[slot_of[g]] = job->tight
+                                       ? (uint64_t)(2.0 * kt[slot_of[g] - 1] / f / ntile_of[g]) + 64
+                                       : 2ULL * every[g] * s / ntile_of[g] + 64;
+        }
+        bool all = n4 > 0;
+        for (uint32_t i = 0; all && i < n4; i++) {
+            const uint32_t sl = by_class[b4 + i].thr_slot;
+            all = sl != 0 && slot_est[sl] <= kThrTileKeys / 2;
+        }
+        job->thr4 = all;
+        job->n4 = n4;
+        if (all) {
+            alloc((void **)&job->d_redo, (size_t)n4 * sizeof(TileDesc));
+            alloc((void **)&job->d_redo_n, sizeof(uint32_t));
+        }
     }
     if (e != hipSuccess) {
         job_release(job);
