@@ -459,6 +459,37 @@ __device__ __forceinline__ void sketch_tile(
         for (uint32_t i = tid; i < nsh; i += kBlock) keys[total + i] = surv[kBlock * kSurv + i];
         total += nsh;
         __syncthreads();
+        if (total <= 64) {
+            // (block-uniform) a tight bound leaves a C5 tile ~15 survivors: one wave ranks them
+            // against each other (a loop of `total` broadcasts), drops repeats and writes the row,
+            // instead of the bucket table, its scans and barriers below
+            if (tid < 64) {
+                const uint64_t v = tid < total ? keys[tid] : 0;
+                const uint32_t vlo = (uint32_t)v, vhi = (uint32_t)(v >> 32);
+                // the first copy of each value, then the distinct values below each key
+                bool first = tid < total;
+#pragma unroll 1
+                for (uint32_t j = 0; j < total; j++) {
+                    const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vhi, (int)j) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readlane((int)vlo, (int)j);
+                    first = first && !(j < tid && y == v);
+                }
+                const uint64_t fm = __builtin_amdgcn_ballot_w64(first);
+                uint32_t rank = 0;
+#pragma unroll 1
+                for (uint32_t j = 0; j < total; j++) {
+                    const uint64_t y = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)vhi, (int)j) << 32) |
+                                       (uint32_t)__builtin_amdgcn_readlane((int)vlo, (int)j);
+                    rank += ((fm >> j) & 1) && y < v ? 1u : 0u;
+                }
+                if (first && rank < p.s) out[(uint64_t)td.out_row * p.s + rank] = v;
+                if (tid == 0) {
+                    const uint32_t nd = (uint32_t)__popcll(fm);
+                    out_count[td.out_row] = nd < p.s ? nd : p.s;
+                }
+            }
+            return;
+        }
         vbits = 0;
 #pragma unroll
         for (int e = 0; e < ES; e++) {
