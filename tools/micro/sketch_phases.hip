@@ -56,7 +56,7 @@ int main(int argc, char **argv)
     for (int it = 0; it < 6; it++) {
         hipEventRecord(e0);
         hipLaunchKernelGGL((sketch_tiles_kernel<P_ARG, K_ARG>), dim3(n), dim3(256), 0, 0, d_seq, d_t, p,
-                           (const uint64_t *)d_thr, d_out, d_cnt);
+                           (const uint64_t *)d_thr, d_out, d_cnt, (TileDesc *)nullptr, (uint32_t *)nullptr);
         hipEventRecord(e1);
         hipEventSynchronize(e1);
         float ms; hipEventElapsedTime(&ms, e0, e1);
