@@ -775,6 +775,12 @@ struct fpm_sketch_job {
     TileDesc *d_rtiles = nullptr;           // the redo's subsets (allocated on first use)
     SelDesc *d_rsel = nullptr;
     int32_t last_short = -1;                // groups redone by the last run (-1: no tight bounds)
+    // a-priori sample bounds (d_thr[n_slots ..]): a sample left short is redone unbounded
+    bool sbounded = false;
+    uint32_t *d_sshort = nullptr;           // count, then the slots
+    std::vector<TileDesc> h_stiles;         // the sample tiles by class (sclass_begin)
+    std::vector<uint32_t> h_ssel_tag;       // each sample selection's slot
+    int32_t last_sample_short = -1;
     // -M pass (allocated on first use)
     uint32_t *d_mult = nullptr;
     unsigned long long *d_first = nullptr;
@@ -792,6 +798,7 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_redo); (void)hipFree(j->d_redo_n);
     (void)hipFree(j->d_kt); (void)hipFree(j->d_slot_group); (void)hipFree(j->d_short);
     (void)hipFree(j->d_thr_safe); (void)hipFree(j->d_rtiles); (void)hipFree(j->d_rsel);
+    (void)hipFree(j->d_sshort);
     (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
@@ -958,7 +965,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     std::vector<uint32_t> slot_of(n_groups, 0);          // 0: not sampled, else slot + 1
     std::vector<TileDesc> stiles;
     std::vector<std::vector<uint32_t>> slists(n_groups);
-    std::vector<uint32_t> srow;
+    std::vector<uint32_t> srow, sgroup;                  // sgroup: each sample tile's group
     {
         std::vector<uint32_t> seen(n_groups, 0);
         for (size_t t = 0; t < tiles.size(); t++) {
@@ -972,6 +979,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
                 st.thr_slot = 0;
                 slists[g].push_back(n_rows++);
                 stiles.push_back(st);
+                sgroup.push_back(g);
             }
         }
         for (size_t t = 0; t < tiles.size(); t++) tiles[t].thr_slot = slot_of[tile_group[t]];
@@ -1035,13 +1043,45 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     std::vector<uint32_t> sel_rows;
     std::vector<std::vector<SelDesc>> ssel_lv, sel_lv;
     const bool use_sel = (uint64_t)s + s / 8 + 64 <= group_select_cap();
+    // A sample's tiles keep only the hashes below an a-priori bound: hash values are uniform,
+    // so of a sample's N windows ~frac N lie below frac of the hash range, and frac =
+    // (1.25 s + 16 sqrt(s)) / N leaves >= s of them (C5: ~14k of a sample's 82k) with ~40
+    // standard deviations to spare.  The sample's selection then reads ~6x fewer keys.  A
+    // sample left with fewer than s (values repeated across its tiles) gives its group no
+    // bound, as a sample shorter than s always did (the sketches do not depend on it).
+    std::vector<uint64_t> sbound(srow.size(), ~0ULL);
+    if (use_sel && !srow.empty()) {
+        std::vector<uint64_t> ns(srow.size(), 0);
+        for (size_t i = 0; i < stiles.size(); i++)
+            ns[slot_of[sgroup[i]] - 1] += stiles[i].n_bytes >= k ? stiles[i].n_bytes - k + 1 : 0;
+        const double range = kp.use64 ? 18446744073709551616.0 : 4294967296.0;
+        for (size_t i = 0; i < srow.size(); i++) {
+            const double frac = (1.25 * s + 16.0 * std::sqrt((double)s)) / std::max<double>(1, ns[i]);
+            if (frac < 0.5) sbound[i] = (uint64_t)(frac * range);
+        }
+        const uint32_t n_sl = (uint32_t)srow.size();
+        for (size_t i = 0; i < stiles.size(); i++) {
+            const uint32_t sl = slot_of[sgroup[i]];
+            if (sbound[sl - 1] != ~0ULL) {
+                stiles[i].thr_slot = n_sl + sl;              // d_thr[n_slots + slot]
+                if (stiles[i].out_row < est.size())
+                    est[stiles[i].out_row] = std::min<uint64_t>(
+                        est[stiles[i].out_row], (uint64_t)(2.0 * (double)sbound[sl - 1] / range *
+                                                           stiles[i].n_bytes) + 64);
+            }
+        }
+    }
+    // tags (optional): per level, the slot of each descriptor (sample selections carry slot
+    // 0xFFFFFFFF on the device; the host finds a group's descriptors by the tag)
     auto build_sel = [&](const std::vector<uint32_t> &rows0, uint32_t final_row, uint32_t slot,
-                         std::vector<std::vector<SelDesc>> &lv) {
+                         std::vector<std::vector<SelDesc>> &lv,
+                         std::vector<std::vector<uint32_t>> *tags = nullptr, uint32_t tag = 0) {
         constexpr uint64_t kKeysPerWG = 1u << 19;
         constexpr size_t kRowsPerWG = 4096;
         std::vector<uint32_t> cur = rows0;
         for (size_t level = 0;; level++) {
             if (lv.size() <= level) lv.resize(level + 1);
+            if (tags && tags->size() <= level) tags->resize(level + 1);
             std::vector<std::pair<size_t, size_t>> ch;
             size_t a = 0;
             uint64_t acc = 0;
@@ -1058,6 +1098,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             if (ch.size() == 1) {
                 lv[level].push_back(SelDesc{(uint32_t)sel_rows.size(), (uint32_t)cur.size(),
                                             final_row, slot});
+                if (tags) (*tags)[level].push_back(tag);
                 sel_rows.insert(sel_rows.end(), cur.begin(), cur.end());
                 return;
             }
@@ -1070,6 +1111,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
                 est[r] = std::min<uint64_t>(s, sum);
                 lv[level].push_back(SelDesc{(uint32_t)sel_rows.size(),
                                             (uint32_t)(c.second - c.first), r, slot});
+                if (tags) (*tags)[level].push_back(tag);
                 sel_rows.insert(sel_rows.end(), cur.begin() + c.first, cur.begin() + c.second);
                 next.push_back(r);
             }
@@ -1080,12 +1122,13 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     std::vector<uint32_t> sfrb;
     std::vector<uint8_t> sfsmall;
     std::vector<std::vector<uint32_t>> sflists(n_groups), flists(n_groups);
+    std::vector<std::vector<uint32_t>> ssel_tag_lv;
     if (use_sel)
         for (uint32_t g = 0; g < n_groups; g++) {
             if (!slot_of[g] || slists[g].size() < 2) continue;
             const uint32_t r = n_rows++;                    // the sample's sketch row
             srow[slot_of[g] - 1] = r;
-            build_sel(slists[g], r, 0xFFFFFFFFu, ssel_lv);
+            build_sel(slists[g], r, 0xFFFFFFFFu, ssel_lv, &ssel_tag_lv, slot_of[g] - 1);
             sflists[g].swap(slists[g]);
         }
     plan_rounds(slists, [&](uint32_t g) {
@@ -1102,11 +1145,12 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     plan_rounds(lists, [](uint32_t g) { return g; }, mplan, rb, msmall);
     // d_sel: the sample levels, then the main levels; level boundaries for the launches
     std::vector<SelDesc> sel;
-    std::vector<uint32_t> ssel_begin{0}, sel_begin;
+    std::vector<uint32_t> ssel_begin{0}, sel_begin, ssel_tag;
     for (auto &l : ssel_lv) {
         sel.insert(sel.end(), l.begin(), l.end());
         ssel_begin.push_back((uint32_t)sel.size());
     }
+    for (auto &l : ssel_tag_lv) ssel_tag.insert(ssel_tag.end(), l.begin(), l.end());
     sel_begin.push_back((uint32_t)sel.size());
     for (auto &l : sel_lv) {
         sel.insert(sel.end(), l.begin(), l.end());
@@ -1183,7 +1227,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
     alloc((void **)&job->d_stiles, sby_class.size() * sizeof(TileDesc));
     alloc((void **)&job->d_smerge, splan.size() * sizeof(MergeDesc));
     alloc((void **)&job->d_srow, srow.size() * sizeof(uint32_t));
-    alloc((void **)&job->d_thr, srow.size() * sizeof(uint64_t));
+    alloc((void **)&job->d_thr, 2 * srow.size() * sizeof(uint64_t));   // main, then sample bounds
     alloc((void **)&job->d_sel, sel.size() * sizeof(SelDesc));
     alloc((void **)&job->d_sel_rows, sel_rows.size() * sizeof(uint32_t));
     alloc((void **)&job->d_sel_failed, (sel.size() + 2) * sizeof(uint32_t));
@@ -1213,6 +1257,15 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         job->h_tiles = by_class;
         job->h_sel = sel;
         job->last_short = 0;
+        bool any_sb = false;
+        for (uint64_t b : sbound) any_sb = any_sb || b != ~0ULL;
+        if (any_sb) {
+            job->sbounded = true;
+            job->h_stiles = sby_class;
+            job->h_ssel_tag = ssel_tag;
+            job->last_sample_short = 0;
+            alloc((void **)&job->d_sshort, (srow.size() + 1) * sizeof(uint32_t));
+        }
     }
     {
         // the survivors-only tile kernel for the class-4 tiles when every one carries its
@@ -1278,6 +1331,8 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         e = copy_in(ctx, job->d_sel, sel.data(), sel.size() * sizeof(SelDesc));
     if (e == hipSuccess && !sel_rows.empty())
         e = copy_in(ctx, job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t));
+    if (e == hipSuccess && !sbound.empty())
+        e = copy_in(ctx, job->d_thr + srow.size(), sbound.data(), sbound.size() * sizeof(uint64_t));
     if (e == hipSuccess && !kt.empty())
         e = copy_in(ctx, job->d_kt, kt.data(), kt.size() * sizeof(uint32_t));
     if (e == hipSuccess && !slot_group.empty())
@@ -1319,6 +1374,65 @@ static int fallback_descs(fpm_sketch_job *job)
     return upload(job->sfplan, &job->d_sfmerge);
 }
 
+// device room for a redo's tile and selection subsets (allocated on first use)
+static int redo_buffers(fpm_sketch_job *job)
+{
+    if (!job->d_rtiles)
+        HIP_TRY(hipMalloc((void **)&job->d_rtiles,
+                          std::max<size_t>(1, std::max(job->h_tiles.size(), job->h_stiles.size())) *
+                              sizeof(TileDesc)));
+    if (!job->d_rsel)
+        HIP_TRY(hipMalloc((void **)&job->d_rsel, std::max<size_t>(1, job->h_sel.size()) * sizeof(SelDesc)));
+    return FPM_OK;
+}
+
+// The samples an a-priori bound left short (slots in d_sshort[1 ..], bounds lifted by
+// sketch_sample_short_kernel): their sample tiles and sample selections once more
+template <typename TilesPass>
+static int redo_sample_short(fpm_sketch_job *job, uint32_t n_short, hipStream_t st,
+                             TilesPass &tiles_pass)
+{
+    fpm_ctx *ctx = job->ctx;
+    std::vector<uint32_t> slots(n_short);
+    HIP_TRY(hipMemcpyAsync(slots.data(), job->d_sshort + 1, n_short * sizeof(uint32_t),
+                           hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::vector<uint8_t> is_short(job->n_slots + 1, 0);
+    for (uint32_t i : slots)
+        if (i < job->n_slots) is_short[i] = 1;
+    std::vector<TileDesc> sub;
+    uint32_t begin[kTileClasses + 1] = {0};
+    for (int c = 0; c < kTileClasses; c++) {
+        for (uint32_t t = job->sclass_begin[c]; t < job->sclass_begin[c + 1]; t++) {
+            const TileDesc &td = job->h_stiles[t];
+            if (td.thr_slot > job->n_slots && is_short[td.thr_slot - job->n_slots - 1]) sub.push_back(td);
+        }
+        begin[c + 1] = (uint32_t)sub.size();
+    }
+    std::vector<SelDesc> rsel;
+    std::vector<uint32_t> rbegin{0};
+    for (size_t l = 0; l + 1 < job->ssel_begin.size(); l++) {
+        for (uint32_t i = job->ssel_begin[l]; i < job->ssel_begin[l + 1]; i++)
+            if (i < job->h_ssel_tag.size() && job->h_ssel_tag[i] < job->n_slots &&
+                is_short[job->h_ssel_tag[i]])
+                rsel.push_back(job->h_sel[i]);
+        rbegin.push_back((uint32_t)rsel.size());
+    }
+    if (int rc = redo_buffers(job)) return rc;
+    if (!sub.empty()) HIP_TRY(copy_in(ctx, job->d_rtiles, sub.data(), sub.size() * sizeof(TileDesc)));
+    if (!rsel.empty()) HIP_TRY(copy_in(ctx, job->d_rsel, rsel.data(), rsel.size() * sizeof(SelDesc)));
+    if (int rc = tiles_pass(job->d_rtiles, begin, false)) return rc;
+    for (size_t l = 0; l + 1 < rbegin.size(); l++) {
+        const uint32_t b = rbegin[l], n = rbegin[l + 1] - b;
+        if (!n) continue;
+        TimedLaunch tl(ctx, FPM_K_MERGE, st);
+        HIP_TRY(launch_group_select(job->d_rsel + b, n, job->d_sel_rows, job->d_rows, job->d_count,
+                                    job->kp.s, job->d_thr, job->d_sel_failed + 1, st));
+        tl.done();
+    }
+    return FPM_OK;
+}
+
 // The groups a tight bound left short (their slots in d_short[1 ..], bounds already raised
 // to the safe ones by sketch_short_kernel): their main tiles and selections once more
 template <typename TilesPass>
@@ -1350,10 +1464,7 @@ static int redo_short(fpm_sketch_job *job, uint32_t n_short, hipStream_t st, Til
         }
         rbegin.push_back((uint32_t)rsel.size());
     }
-    if (!job->d_rtiles)
-        HIP_TRY(hipMalloc((void **)&job->d_rtiles, std::max<size_t>(1, job->h_tiles.size()) * sizeof(TileDesc)));
-    if (!job->d_rsel)
-        HIP_TRY(hipMalloc((void **)&job->d_rsel, std::max<size_t>(1, job->h_sel.size()) * sizeof(SelDesc)));
+    if (int rc = redo_buffers(job)) return rc;
     if (!sub.empty()) HIP_TRY(copy_in(ctx, job->d_rtiles, sub.data(), sub.size() * sizeof(TileDesc)));
     if (!rsel.empty()) HIP_TRY(copy_in(ctx, job->d_rsel, rsel.data(), rsel.size() * sizeof(SelDesc)));
     if (int rc = tiles_pass(job->d_rtiles, begin, true)) return rc;
@@ -1430,11 +1541,33 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         }
         if (int rc = merge_pass(job->d_smerge, job->sround_begin, job->sround_small)) return rc;
         if (job->n_ssel) {
-            HIP_TRY(hipStreamSynchronize(st));
-            if (job->h_sel_failed[1]) {
+            auto sample_fallback = [&]() -> int {
                 if (int rc = fallback_descs(job)) return rc;
-                if (int rc = merge_pass(job->d_sfmerge, job->sfround_begin, job->sfround_small))
-                    return rc;
+                return merge_pass(job->d_sfmerge, job->sfround_begin, job->sfround_small);
+            };
+            HIP_TRY(hipStreamSynchronize(st));
+            if (job->h_sel_failed[1])
+                if (int rc = sample_fallback()) return rc;
+            if (job->sbounded) {
+                // samples their a-priori bound left short: redone unbounded
+                HIP_TRY(hipMemsetAsync(job->d_sshort, 0, sizeof(uint32_t), st));
+                HIP_TRY(launch_sketch_sample_short(job->d_srow, job->n_slots, job->d_count,
+                                                   job->kp.s, job->d_thr + job->n_slots,
+                                                   job->d_sshort, job->d_sshort + 1, st));
+                HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 2, job->d_sshort, sizeof(uint32_t),
+                                       hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                const uint32_t n_ss = job->h_sel_failed[2];
+                job->last_sample_short = (int32_t)n_ss;
+                if (n_ss) {
+                    HIP_TRY(hipMemsetAsync(fail_samp, 0, sizeof(uint32_t), st));
+                    if (int rc = redo_sample_short(job, n_ss, st, tiles_pass)) return rc;
+                    HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 1, fail_samp, sizeof(uint32_t),
+                                           hipMemcpyDeviceToHost, st));
+                    HIP_TRY(hipStreamSynchronize(st));
+                    if (job->h_sel_failed[1])
+                        if (int rc = sample_fallback()) return rc;
+                }
             }
         }
         HIP_TRY(launch_sketch_threshold(job->d_srow, job->n_slots, job->d_rows, job->d_count,

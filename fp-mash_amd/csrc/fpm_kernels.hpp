@@ -81,6 +81,11 @@ hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, con
                                    uint64_t *d_thr, uint64_t *d_thr_safe, hipStream_t st);
 // slots whose group (slot_group[i]) ended with fewer than s hashes under thr < thr_safe:
 // listed (d_short_slots, count *d_n_short, zeroed by the caller), thr raised to thr_safe
+// samples (sample row srow[i]) left with fewer than s hashes under their a-priori bound
+// d_sbound[i] (< ~0): listed (count *d_n_short, zeroed by the caller), bound lifted to ~0
+hipError_t launch_sketch_sample_short(const uint32_t *d_srow, uint32_t n_slots,
+                                      const uint32_t *d_count, uint32_t s, uint64_t *d_sbound,
+                                      uint32_t *d_n_short, uint32_t *d_short_slots, hipStream_t st);
 hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
                                const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                const uint64_t *d_thr_safe, uint32_t *d_n_short,

@@ -996,6 +996,32 @@ __global__ void sketch_short_kernel(const uint32_t *__restrict__ slot_group, uin
     }
 }
 
+// The samples whose a-priori bound (sbound[i], fpm_sketch_stage) left fewer than s hashes
+// (values repeated across the sample's tiles): listed, and their bound lifted for the redo.
+__global__ void sketch_sample_short_kernel(const uint32_t *__restrict__ srow, uint32_t n_slots,
+                                           const uint32_t *__restrict__ count, uint32_t s,
+                                           uint64_t *__restrict__ sbound,
+                                           uint32_t *__restrict__ n_short,
+                                           uint32_t *__restrict__ short_slots)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n_slots) return;
+    if (count[srow[i]] < s && sbound[i] != ~0ULL) {
+        short_slots[atomicAdd(n_short, 1u)] = i;
+        sbound[i] = ~0ULL;
+    }
+}
+
+hipError_t launch_sketch_sample_short(const uint32_t *d_srow, uint32_t n_slots,
+                                      const uint32_t *d_count, uint32_t s, uint64_t *d_sbound,
+                                      uint32_t *d_n_short, uint32_t *d_short_slots, hipStream_t st)
+{
+    if (!n_slots) return hipSuccess;
+    hipLaunchKernelGGL(sketch_sample_short_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
+                       d_srow, n_slots, d_count, s, d_sbound, d_n_short, d_short_slots);
+    return hipGetLastError();
+}
+
 hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
                                const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                const uint64_t *d_thr_safe, uint32_t *d_n_short,
