@@ -74,7 +74,7 @@ __device__ __forceinline__ uint32_t key_fp(uint64_t K, const IdxGeom &g, uint64_
     return (uint32_t)((K * mult) >> (64 - g.fbits));
 }
 
-// Tiles of kIdxTile matrix cells, 1024 threads each (16 cells per thread, 4 loads in
+// Tiles of g.tile (<= kIdxTile) matrix cells, 1024 threads each (16 cells per thread, 4 loads in
 // flight): 611 tiles at the bench's E = 1e7, ~10 waves per SIMD.  Row of cell e = e / stride
 // by a 64-bit multiply-high with magic = floor((2^64 - 1) / stride) + 1, exact for e < 2^31
 // (the error term e / 2^64 stays below the 1 / stride gap to the next integer).
@@ -154,9 +154,10 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_hist_kernel(
     const uint64_t mult = idx_mult(g);
     for (uint32_t p = threadIdx.x; p < kParts; p += kIdxThreads) hist[p] = 0;
     __syncthreads();
-    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
+    const uint32_t e0 = blockIdx.x * g.tile, lane = threadIdx.x & 63;
+    const uint32_t n = min(n_ref * stride, e0 + g.tile);     // this tile's cells end here
     bool uns = false;
-    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
         uint64_t key[kIdxU];
         bool v[kIdxU], nx[kIdxU];
 #pragma unroll
@@ -228,8 +229,9 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter_kernel(
         lcur[p] = pre + x - c;
     }
     __syncthreads();
-    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile;
-    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+    const uint32_t e0 = blockIdx.x * g.tile;
+    const uint32_t n = min(n_ref * stride, e0 + g.tile);     // this tile's cells end here
+    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
         uint64_t K[kIdxU];
         uint32_t rr[kIdxU];
         bool v[kIdxU];
@@ -278,10 +280,11 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
     const uint64_t mult = idx_mult(g);
     lcur[threadIdx.x] = 0;
     __syncthreads();
-    const uint32_t n = n_ref * stride, e0 = blockIdx.x * kIdxTile, lane = threadIdx.x & 63;
+    const uint32_t e0 = blockIdx.x * g.tile, lane = threadIdx.x & 63;
+    const uint32_t n = min(n_ref * stride, e0 + g.tile);     // this tile's cells end here
     bool uns = false;
     // pass 1: the tile's partition counts (and the sortedness flags)
-    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
         uint64_t key[kIdxU];
         bool v[kIdxU], nx[kIdxU];
 #pragma unroll
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
     }
     __syncthreads();
     // pass 2: the keys again (L2-resident), grouped by partition in LDS
-    for (uint32_t c0 = 0; c0 < kIdxTile; c0 += kIdxU * kIdxThreads) {
+    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
         uint64_t K[kIdxU];
         uint32_t rr[kIdxU];
         bool v[kIdxU];
@@ -1104,7 +1107,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
         if (hipError_t e = dyn_lds_attr(2, (const void *)idx_part_scatter1_kernel, kIdxTile * 8))
             return e;
         hipLaunchKernelGGL(idx_part_scatter1_kernel, dim3(ntiles), dim3(kIdxThreads),
-                           (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic,
+                           (size_t)g.tile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic,
                            n_ref, hash_bytes, g, part_fill, tent, unsorted, overflow);
         hipLaunchKernelGGL(idx_bucket_kernel, bgrid, dim3(kBucketThreads),
                            (size_t)(cnt_bytes0 + (uint64_t)lds_cap * 4), st, (const uint64_t *)tent,
@@ -1121,7 +1124,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     if (hipError_t e = dyn_lds_attr(0, (const void *)idx_part_scatter_kernel, kIdxTile * 8))
         return e;
     hipLaunchKernelGGL(idx_part_scatter_kernel, dim3(ntiles), dim3(kIdxThreads),
-                       (size_t)kIdxTile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic, n_ref,
+                       (size_t)g.tile * 8, st, d_ref, d_ref_len, (uint32_t)stride, magic, n_ref,
                        hash_bytes, ntiles, (const uint32_t *)tile_hist, (const uint32_t *)tile_off,
                        g, tent);
     // LDS copy of a partition's entries when they fit beside the counters (two workgroups per

@@ -2364,7 +2364,16 @@ static IdxGeom make_geom(uint32_t n_ref, uint64_t E)
     geom.nbits = kIdxL1 + geom.l2;
     geom.rbits = rbits;
     geom.fbits = 32 - rbits;
-    geom.ntiles = (uint32_t)((E + kIdxTile - 1) / kIdxTile);
+    // level-1 tiles (one 1024-thread workgroup per CU: their LDS staging holds 8 B per cell)
+    // in whole rounds of 256: the cells per tile trimmed so that the last round is not a
+    // fraction of the chip (C2's 1e7 cells: 752 tiles of 13,312 instead of 611 of 16,384)
+    {
+        const uint64_t rounds = std::max<uint64_t>(1, (E + 256ULL * kIdxTile - 1) / (256ULL * kIdxTile));
+        uint64_t tile = (E + 256 * rounds - 1) / (256 * rounds);
+        tile = std::min<uint64_t>(kIdxTile, std::max<uint64_t>(1024, (tile + 1023) / 1024 * 1024));
+        geom.tile = (uint32_t)tile;
+        geom.ntiles = (uint32_t)((E + tile - 1) / tile);
+    }
     // one-pass level 1: each partition's slot holds 1.5 x the mean + 6 sigma + 64 entries.
     // Bottom-s sketch values are uniform below each row's own maximum, and the rows' maxima
     // differ, so the density over the indexed range [0, kmax] tapers towards kmax and the low

@@ -143,13 +143,14 @@ hipError_t launch_walk_candidates(const uint64_t *d_cand, const unsigned long lo
 
 // bucket index over ref hashes (dist_index.hip)
 constexpr uint32_t kIdxL1 = 10;        // level-1 partition bits
-constexpr uint32_t kIdxTile = 16384;   // matrix cells per level-1 tile (~16 entries per partition)
+constexpr uint32_t kIdxTile = 16384;   // the most matrix cells per level-1 tile (~16 entries per partition)
 struct IdxGeom {
     uint32_t l2;       // level-2 bits (1..14)
     uint32_t nbits;    // bucket bits = kIdxL1 + l2
     uint32_t rbits;    // ref-id bits in a u32 entry
     uint32_t fbits;    // key-fingerprint bits in a u32 entry (32 - rbits, >= 8)
     uint32_t ntiles;   // level-1 tiles
+    uint32_t tile;     // matrix cells per level-1 tile (<= kIdxTile, a multiple of 1024)
     // device pointer: the largest indexed key (idx_kmax_kernel), from which every kernel
     // derives the bucket scale (bucket_of / key_fp in dist_index.hip)
     const unsigned long long *kmax;
