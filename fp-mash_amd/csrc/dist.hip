@@ -355,9 +355,9 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
     bool over;
     uint32_t lo;
     if constexpr (HI) {
-        const uint32_t t = (uint32_t)(a >> 32) >> (shift - 32);
-        over = t > top;
-        lo = Bkt[over ? top + 1 : t];
+        // shift = 52: t < kBuckets, and the directory past top holds lb (the sentinels)
+        over = false;
+        lo = Bkt[(uint32_t)(a >> 32) >> (shift - 32)];
     } else {
         const uint64_t t = a >> shift;
         over = t > (uint64_t)top;
@@ -370,6 +370,7 @@ __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_
         for (int q = 0; q < NP; q++) p += K32[lo + q] < ka ? 1u : 0u;
         const uint64_t v = Bs[p];
         j = p + (v < a ? 1u : 0u);
+        if constexpr (HI) return __builtin_amdgcn_ballot_w64(v == a);
         return __builtin_amdgcn_ballot_w64(v == a) & ~__builtin_amdgcn_ballot_w64(over);
     } else {
         uint32_t jj = lo;
@@ -469,6 +470,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
         const uint32_t bp = j > 0 ? (uint32_t)(vp >> shift) + 1 : 0;
         for (uint32_t b = bp; b <= bj; b++) Bkt[b] = (uint16_t)j;
     }
+    // the directory past top + 1 (HI rows read it unclamped; top >= 2^(kLogBuckets - 1))
+    for (uint32_t b = top + 2 + threadIdx.x; b <= kBuckets; b += blockDim.x) Bkt[b] = (uint16_t)lb;
     if (dup) s_keydup = 1;
     __syncthreads();
     // the largest bucket: element j is the (j - Bkt[bucket(j)] + 1)-th of its bucket
@@ -531,43 +534,46 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     auto cand_at = [&](uint32_t cc) -> uint64_t {
         return cand[base + __builtin_amdgcn_readfirstlane(cc)];
     };
-    // one group of kGroup chunks: shared-hash count below the union rank S (cnt), shared
-    // values so far (shared_below); returns the union rank of the last valid element of the
-    // group's last chunk
+    // one chunk (kGroup = 1): shared-hash count below the union rank S (cnt), shared values
+    // so far (shared_below); returns the union rank of the chunk's largest value (full chunks)
     // vm0 / vm1: the lanes whose e0 / e1 are values of the row (all of them but in a row's
     // last chunk, whose masks the candidate loop computes once)
-    auto rank_group = [&](auto probe, uint32_t g0, uint64_t vm0, uint64_t vm1,
+    // Union ranks increase with the value, so a full chunk whose largest value (lane 63's e1)
+    // ranks below S counts every shared value it holds: that rank comes from one lane's j and
+    // scalar popcounts, and the per-lane ranks (mbcnt, the u < S ballots) are only computed for
+    // the chunk that crosses S and for the row's last chunk.
+    auto rank_group = [&](auto probe, uint32_t g0, bool last, uint64_t vm0, uint64_t vm1,
                           const Pair (&cur)[kGroup], uint32_t &shared_below,
                           uint32_t &cnt) -> uint32_t {
-        uint32_t j0[kGroup], j1[kGroup];
-        uint64_t m0[kGroup], m1[kGroup];
-#pragma unroll
-        for (int g = 0; g < kGroup; g++) {
-            m0[g] = probe(cur[g].e0, j0[g]);
-            m1[g] = probe(cur[g].e1, j1[g]);
-        }
+        uint32_t j0, j1;
+        const uint64_t m0 = probe(cur[0].e0, j0);
+        const uint64_t m1 = probe(cur[0].e1, j1);
+        const uint32_t i0 = g0 * kChunk;
+        const uint64_t a0 = m0 & vm0, a1 = m1 & vm1;
+        const uint32_t p0 = (uint32_t)__popcll(a0), p1 = (uint32_t)__popcll(a1);
         uint32_t u_last = 0;
-#pragma unroll
-        for (int g = 0; g < kGroup; g++) {
-            const uint32_t i0 = (g0 + g) * kChunk;
-            const uint64_t a0 = m0[g] & vm0, a1 = m1[g] & vm1;
+        if (!last) {
+            const uint32_t jl = (uint32_t)__builtin_amdgcn_readlane((int)j1, 63);
+            u_last = i0 + (kChunk - 1) + jl -
+                     (shared_below + p0 + (uint32_t)__popcll(a1 & 0x7FFFFFFFFFFFFFFFULL));
+        }
+        if (!last && u_last < S) {
+            cnt += p0 + p1;
+        } else {
             const uint32_t b0 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a0, 0u));
             const uint32_t b1 = __builtin_amdgcn_mbcnt_hi(
                 (uint32_t)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)a1, 0u));
             const uint32_t k0 = shared_below + b0;
-            const uint32_t k1 = shared_below + (uint32_t)__popcll(a0) + b1;
-            const uint32_t u0 = i0 + lane + j0[g] - k0, u1 = i0 + 64 + lane + j1[g] - k1;
+            const uint32_t k1 = shared_below + p0 + b1;
+            const uint32_t u0 = i0 + lane + j0 - k0, u1 = i0 + 64 + lane + j1 - k1;
             cnt += __popcll(a0 & __builtin_amdgcn_ballot_w64(u0 < S)) +
                    __popcll(a1 & __builtin_amdgcn_ballot_w64(u1 < S));
-            shared_below += __popcll(a0) + __popcll(a1);
-            // the union rank of the chunk's last value (lane 63's e1), read for the early exit
-            // after full chunks only: after the row's last chunk the walk ends anyway
-            if (g == kGroup - 1) u_last = (uint32_t)__builtin_amdgcn_readlane((int)u1, 63);
         }
+        shared_below += p0 + p1;
         return u_last;
     };
-    auto run = [&](auto probe) {
+    auto run = [&](auto probe, bool fast) {
         Pair cur[kGroup], nxt[kGroup], pf[kGroup];
         Row Rc{};
         if (wave < n) { Rc = open_row(cand_at(wave)); load_group(Rc, 0, pf); }
@@ -601,13 +607,19 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
             uint32_t gi = 0;
             for (; gi + 1 < ngr; gi++) {
                 load_group(R, gi + 1, nxt);
-                const uint32_t u_last = rank_group(probe, gi * kGroup, ~0ULL, ~0ULL, cur,
+                const uint32_t u_last = rank_group(probe, gi * kGroup, false, ~0ULL, ~0ULL, cur,
                                                    shared_below, cnt);
                 if (u_last >= s_exit) { exited = true; break; }
 #pragma unroll
                 for (int u = 0; u < kGroup; u++) cur[u] = nxt[u];
             }
-            if (!exited && ngr) rank_group(probe, gi * kGroup, vl0, vl1, cur, shared_below, cnt);
+            if (!exited && ngr) {
+                // fast-path rows: B holds no ~0 value (its key would equal the sentinel's), and
+                // an A value ~0 (only ever A's last) would match the sentinel: not shared
+                const uint64_t x0 = fast ? __builtin_amdgcn_ballot_w64(cur[0].e0 == ~0ULL) : 0;
+                const uint64_t x1 = fast ? __builtin_amdgcn_ballot_w64(cur[0].e1 == ~0ULL) : 0;
+                rank_group(probe, gi * kGroup, true, vl0 & ~x0, vl1 & ~x1, cur, shared_below, cnt);
+            }
             if (lane == 0) {
                 const uint64_t un = (uint64_t)la + lb - shared_below;
                 const uint32_t dn = need_all ? (un < S ? (uint32_t)un : S) : S;
@@ -632,7 +644,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t *k_ = K32;
 #define FPM_RANK_NP(NP_, HI_) \
     run([&](uint64_t a, uint32_t &j) { \
-        return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); })
+        return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); }, NP_ > 0)
     const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
     switch (np) {
     case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;

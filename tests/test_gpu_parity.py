@@ -410,7 +410,8 @@ def test_dist_sparse_large_grid(ctx, oracle):
 def _sorted_lists(rng):
     """Sorted distinct u64 lists that stress the rank kernel's bucket table: values near
     2**64 (shift 52), tiny values (shift 0), one crowded bucket (long in-bucket search),
-    heavy overlap with lists shorter than S (denom < S), and long lists (CAP 2048)."""
+    heavy overlap with lists shorter than S (denom < S), long lists (CAP 2048), and the value
+    2**64 - 1 (equal to the rank kernel's sentinel) in lists sharing other values."""
     pool = np.unique(rng.integers(0, 2 ** 64, size=6000, dtype=np.uint64))
     lists = []
     for i in range(24):
@@ -425,6 +426,8 @@ def _sorted_lists(rng):
     lists += [crowd, crowd[::2], np.union1d(crowd[:50], small[:300])]
     core = pool[:300]
     lists += [core, core[:250], core[50:], pool[:2000], pool[1000:3000]]   # near-identical, long
+    # the value 2**64 - 1 in A against a B without it (it meets B's sentinels) and with it
+    lists += [np.append(core[:280], np.uint64(2 ** 64 - 1)), np.append(core[20:], top[-3:])]
     return lists
 
 
