@@ -279,30 +279,53 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
     static_assert(kParts == kIdxThreads, "one partition per thread");
     const uint64_t mult = idx_mult(g);
     lcur[threadIdx.x] = 0;
-    __syncthreads();
     const uint32_t e0 = blockIdx.x * g.tile, lane = threadIdx.x & 63;
     const uint32_t n = min(n_ref * stride, e0 + g.tile);     // this tile's cells end here
+    const uint32_t nu = g.tile / kIdxThreads;                // cells per thread (<= kPer)
+    // the tile's keys stay in registers across both passes: every load of the tile issued at
+    // once (cell e0 + u * 1024 + tid: each load coalesced), the length reads beside them (a
+    // key past its row's length is loaded and dropped), and lane 63 loads the next cell for the
+    // sortedness test gets the next cell's key from the next wave's lane 0 through the LDS.
+    // (Was 4 loads in flight per thread and the keys read again for the scatter: two dependent
+    // load rounds per 4 cells.)
+    constexpr int kPer = kIdxTile / kIdxThreads;
+    constexpr int kW = kIdxThreads / 64;
+    __shared__ uint64_t first[kPer + 1][kW];                  // lane 0's key of each (u, wave)
+    uint64_t key[kPer];
+    uint32_t la[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; u++) {
+        const uint32_t e = e0 + u * kIdxThreads + threadIdx.x;
+        const bool in = (uint32_t)u < nu && e < n;
+        la[u] = in ? ref_len[min(row_of(e, stride, magic), n_ref - 1)] : 0u;
+        key[u] = in ? load_key(ref, hash_bytes, e) : 0;
+    }
+    const uint32_t wave_id = threadIdx.x >> 6;
+    if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < kPer; u++) first[u][wave_id] = key[u];
+    }
+    // the cell after the tile (the last wave's lane 63 of the last u): loaded once
+    if (threadIdx.x == 0) {
+        const uint32_t e = e0 + nu * kIdxThreads;
+        first[nu][0] = e < n_ref * stride ? load_key(ref, hash_bytes, e) : 0;
+    }
+    __syncthreads();                                          // lcur cleared, first[] written
     bool uns = false;
+    uint32_t vbits = 0;                                       // bit u: cell u is a list entry
     // pass 1: the tile's partition counts (and the sortedness flags)
-    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
-        uint64_t key[kIdxU];
-        bool v[kIdxU], nx[kIdxU];
 #pragma unroll
-        for (int u = 0; u < kIdxU; u++) {
-            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
-            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
-            const uint32_t la = e < n ? ref_len[min(r, n_ref - 1)] : 0;
-            v[u] = e < n && i < la;
-            nx[u] = v[u] && i + 1 < la;
-            key[u] = v[u] ? load_key(ref, hash_bytes, e) : 0;
-        }
-#pragma unroll
-        for (int u = 0; u < kIdxU; u++) {
-            uint64_t nk = __shfl_down((unsigned long long)key[u], 1, 64);
-            if (lane == 63 && nx[u])
-                nk = load_key(ref, hash_bytes, (uint64_t)e0 + c0 + u * kIdxThreads + threadIdx.x + 1);
-            uns |= nx[u] && !(key[u] < nk);
-            if (v[u]) atomicAdd(&lcur[bucket_of(norm_key(key[u], hash_bytes), g, mult) >> g.l2], 1u);
+    for (int u = 0; u < kPer; u++) {
+        const uint32_t e = e0 + u * kIdxThreads + threadIdx.x;
+        const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
+        const bool v = (uint32_t)u < nu && e < n && i < la[u];
+        const bool nx = v && i + 1 < la[u];
+        uint64_t nk = __shfl_down((unsigned long long)key[u], 1, 64);
+        if (lane == 63) nk = wave_id + 1 < kW ? first[u][wave_id + 1] : first[u + 1][0];
+        uns |= nx && !(key[u] < nk);
+        if (v) {
+            vbits |= 1u << u;
+            atomicAdd(&lcur[bucket_of(norm_key(key[u], hash_bytes), g, mult) >> g.l2], 1u);
         }
     }
     if (__any(uns) && lane == 0) atomicOr(unsorted, 1u);
@@ -323,27 +346,16 @@ __global__ __launch_bounds__(kIdxThreads) void idx_part_scatter1_kernel(
         gbase[p] = c ? atomicAdd(&part_fill[p], c) : 0u;
     }
     __syncthreads();
-    // pass 2: the keys again (L2-resident), grouped by partition in LDS
-    for (uint32_t c0 = 0; c0 < g.tile; c0 += kIdxU * kIdxThreads) {
-        uint64_t K[kIdxU];
-        uint32_t rr[kIdxU];
-        bool v[kIdxU];
+    // pass 2: the registers' keys grouped by partition in LDS
 #pragma unroll
-        for (int u = 0; u < kIdxU; u++) {
-            const uint32_t e = e0 + c0 + u * kIdxThreads + threadIdx.x;
-            const uint32_t r = row_of(e, stride, magic), i = e - r * stride;
-            v[u] = e < n && i < ref_len[min(r, n_ref - 1)];
-            rr[u] = r;
-            K[u] = v[u] ? norm_key(load_key(ref, hash_bytes, e), hash_bytes) : 0;
+    for (int u = 0; u < kPer; u++)
+        if (vbits >> u & 1u) {
+            const uint32_t e = e0 + u * kIdxThreads + threadIdx.x;
+            const uint64_t K = norm_key(key[u], hash_bytes);
+            const uint32_t part = bucket_of(K, g, mult) >> g.l2;
+            const uint32_t pos = atomicAdd(&lcur[part], 1u);
+            stage[pos] = ((uint64_t)part << kPartShift) | pack_l1(K, row_of(e, stride, magic), g, mult);
         }
-#pragma unroll
-        for (int u = 0; u < kIdxU; u++)
-            if (v[u]) {
-                const uint32_t part = bucket_of(K[u], g, mult) >> g.l2;
-                const uint32_t pos = atomicAdd(&lcur[part], 1u);
-                stage[pos] = ((uint64_t)part << kPartShift) | pack_l1(K[u], rr[u], g, mult);
-            }
-    }
     __syncthreads();
     const uint32_t total = lcur[kParts - 1];
     bool over = false;
