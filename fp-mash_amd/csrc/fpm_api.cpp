@@ -1545,21 +1545,36 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
                 if (int rc = fallback_descs(job)) return rc;
                 return merge_pass(job->d_sfmerge, job->sfround_begin, job->sfround_small);
             };
-            HIP_TRY(hipStreamSynchronize(st));
-            if (job->h_sel_failed[1])
-                if (int rc = sample_fallback()) return rc;
-            if (job->sbounded) {
-                // samples their a-priori bound left short: redone unbounded
+            // samples their a-priori bound left short, counted before the one host read that
+            // also fetches the selections' failure flag (a listing without `raise` changes
+            // nothing but the list, so a count stale from a failed selection is harmless: after
+            // the fallback the samples are counted again); a redo lists them again with their
+            // bounds lifted
+            auto list_sample_short = [&](bool raise) -> int {
                 HIP_TRY(hipMemsetAsync(job->d_sshort, 0, sizeof(uint32_t), st));
                 HIP_TRY(launch_sketch_sample_short(job->d_srow, job->n_slots, job->d_count,
                                                    job->kp.s, job->d_thr + job->n_slots,
-                                                   job->d_sshort, job->d_sshort + 1, st));
+                                                   job->d_sshort, job->d_sshort + 1, raise, st));
                 HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 2, job->d_sshort, sizeof(uint32_t),
                                        hipMemcpyDeviceToHost, st));
-                HIP_TRY(hipStreamSynchronize(st));
+                return FPM_OK;
+            };
+            if (job->sbounded)
+                if (int rc = list_sample_short(false)) return rc;
+            HIP_TRY(hipStreamSynchronize(st));
+            if (job->h_sel_failed[1]) {
+                if (int rc = sample_fallback()) return rc;
+                if (job->sbounded) {
+                    if (int rc = list_sample_short(false)) return rc;
+                    HIP_TRY(hipStreamSynchronize(st));
+                }
+            }
+            if (job->sbounded) {
+                // samples left short: redone unbounded
                 const uint32_t n_ss = job->h_sel_failed[2];
                 job->last_sample_short = (int32_t)n_ss;
                 if (n_ss) {
+                    if (int rc = list_sample_short(true)) return rc;   // the same list, lifted
                     HIP_TRY(hipMemsetAsync(fail_samp, 0, sizeof(uint32_t), st));
                     if (int rc = redo_sample_short(job, n_ss, st, tiles_pass)) return rc;
                     HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 1, fail_samp, sizeof(uint32_t),
@@ -1597,22 +1612,35 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
             if (int rc = fallback_descs(job)) return rc;
             return merge_pass(job->d_fmerge, job->fround_begin, job->fround_small);
         };
-        HIP_TRY(hipStreamSynchronize(st));
-        if (*job->h_sel_failed)
-            if (int rc = fallback()) return rc;
-        if (tight) {
-            // the groups the tight bound left short, once every group's count is final: listed,
-            // their bound raised to the safe one, and their tiles and selections run again
+        // the groups the tight bound left short, counted before the one host read that also
+        // fetches the selections' failure flag (a listing without `raise` changes nothing but
+        // the list, so a count stale from a failed selection is harmless: after the fallback
+        // the groups are counted again); a redo lists them again with their bounds raised
+        auto list_short = [&](bool raise) -> int {
             HIP_TRY(hipMemsetAsync(job->d_short, 0, sizeof(uint32_t), st));
             HIP_TRY(launch_sketch_short(job->d_slot_group, job->n_slots, job->d_count, job->kp.s,
                                         job->d_thr, job->d_thr_safe, job->d_short, job->d_short + 1,
-                                        st));
+                                        raise, st));
             HIP_TRY(hipMemcpyAsync(job->h_sel_failed + 2, job->d_short, sizeof(uint32_t),
                                    hipMemcpyDeviceToHost, st));
-            HIP_TRY(hipStreamSynchronize(st));
+            return FPM_OK;
+        };
+        if (tight)
+            if (int rc = list_short(false)) return rc;
+        HIP_TRY(hipStreamSynchronize(st));
+        if (*job->h_sel_failed) {
+            if (int rc = fallback()) return rc;
+            if (tight) {
+                if (int rc = list_short(false)) return rc;
+                HIP_TRY(hipStreamSynchronize(st));
+            }
+        }
+        if (tight) {
+            // their tiles and selections run again
             const uint32_t n_short = job->h_sel_failed[2];
             job->last_short = (int32_t)n_short;
             if (n_short) {
+                if (int rc = list_short(true)) return rc;   // the same list, raised
                 HIP_TRY(hipMemsetAsync(fail_main, 0, sizeof(uint32_t), st));
                 if (int rc = redo_short(job, n_short, st, tiles_pass)) return rc;
                 HIP_TRY(hipMemcpyAsync(job->h_sel_failed, fail_main, sizeof(uint32_t),

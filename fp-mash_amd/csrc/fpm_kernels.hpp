@@ -80,16 +80,19 @@ hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, con
                                    const uint32_t *d_count, uint32_t s, const uint32_t *d_kt,
                                    uint64_t *d_thr, uint64_t *d_thr_safe, hipStream_t st);
 // slots whose group (slot_group[i]) ended with fewer than s hashes under thr < thr_safe:
-// listed (d_short_slots, count *d_n_short, zeroed by the caller), thr raised to thr_safe
+// listed (d_short_slots, count *d_n_short, zeroed by the caller), with `raise` thr raised to
+// thr_safe
 // samples (sample row srow[i]) left with fewer than s hashes under their a-priori bound
-// d_sbound[i] (< ~0): listed (count *d_n_short, zeroed by the caller), bound lifted to ~0
+// d_sbound[i] (< ~0): listed (count *d_n_short, zeroed by the caller), with `raise` the bound
+// lifted to ~0
 hipError_t launch_sketch_sample_short(const uint32_t *d_srow, uint32_t n_slots,
                                       const uint32_t *d_count, uint32_t s, uint64_t *d_sbound,
-                                      uint32_t *d_n_short, uint32_t *d_short_slots, hipStream_t st);
+                                      uint32_t *d_n_short, uint32_t *d_short_slots, bool raise,
+                                      hipStream_t st);
 hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
                                const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                const uint64_t *d_thr_safe, uint32_t *d_n_short,
-                               uint32_t *d_short_slots, hipStream_t st);
+                               uint32_t *d_short_slots, bool raise, hipStream_t st);
 uint32_t merge_small_cap();   // list length merge_small_kernel stages in LDS
 // one long group's sketch selected from its bounded tile lists (rows row_ids[row_begin ..
 // row_begin + n_rows)) into out_row; slot: its bound thr[slot] (0xFFFFFFFF: none, the

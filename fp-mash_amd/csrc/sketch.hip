@@ -980,19 +980,23 @@ hipError_t launch_sketch_threshold(const uint32_t *d_srow, uint32_t n_slots, con
 }
 
 // The sampled groups whose tight bound left fewer than s distinct hashes (their values repeat
-// across tiles): listed in short_slots[0 .. *n_short) (zeroed by the caller), and their bound
-// raised to the safe one for the redo of their tiles and selection.
+// across tiles): listed in short_slots[0 .. *n_short) (zeroed by the caller), and with `raise`
+// their bound raised to the safe one for the redo of their tiles and selection (a listing
+// without it has no effect but the list, so it may run before the counts are known final).
+// Under the safe bound (the sample's s-th smallest, < ~0 when the sample holds s values) a
+// group always keeps >= s, so a count below s means the tight bound.
 __global__ void sketch_short_kernel(const uint32_t *__restrict__ slot_group, uint32_t n_slots,
                                     const uint32_t *__restrict__ count, uint32_t s,
                                     uint64_t *__restrict__ thr,
                                     const uint64_t *__restrict__ thr_safe,
-                                    uint32_t *__restrict__ n_short, uint32_t *__restrict__ short_slots)
+                                    uint32_t *__restrict__ n_short, uint32_t *__restrict__ short_slots,
+                                    uint32_t raise)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_slots) return;
     if (count[slot_group[i]] < s && thr[i] < thr_safe[i]) {
         short_slots[atomicAdd(n_short, 1u)] = i;
-        thr[i] = thr_safe[i];
+        if (raise) thr[i] = thr_safe[i];
     }
 }
 
@@ -1002,35 +1006,37 @@ __global__ void sketch_sample_short_kernel(const uint32_t *__restrict__ srow, ui
                                            const uint32_t *__restrict__ count, uint32_t s,
                                            uint64_t *__restrict__ sbound,
                                            uint32_t *__restrict__ n_short,
-                                           uint32_t *__restrict__ short_slots)
+                                           uint32_t *__restrict__ short_slots, uint32_t raise)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n_slots) return;
     if (count[srow[i]] < s && sbound[i] != ~0ULL) {
         short_slots[atomicAdd(n_short, 1u)] = i;
-        sbound[i] = ~0ULL;
+        if (raise) sbound[i] = ~0ULL;
     }
 }
 
 hipError_t launch_sketch_sample_short(const uint32_t *d_srow, uint32_t n_slots,
                                       const uint32_t *d_count, uint32_t s, uint64_t *d_sbound,
-                                      uint32_t *d_n_short, uint32_t *d_short_slots, hipStream_t st)
+                                      uint32_t *d_n_short, uint32_t *d_short_slots, bool raise,
+                                      hipStream_t st)
 {
     if (!n_slots) return hipSuccess;
     hipLaunchKernelGGL(sketch_sample_short_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
-                       d_srow, n_slots, d_count, s, d_sbound, d_n_short, d_short_slots);
+                       d_srow, n_slots, d_count, s, d_sbound, d_n_short, d_short_slots,
+                       (uint32_t)raise);
     return hipGetLastError();
 }
 
 hipError_t launch_sketch_short(const uint32_t *d_slot_group, uint32_t n_slots,
                                const uint32_t *d_count, uint32_t s, uint64_t *d_thr,
                                const uint64_t *d_thr_safe, uint32_t *d_n_short,
-                               uint32_t *d_short_slots, hipStream_t st)
+                               uint32_t *d_short_slots, bool raise, hipStream_t st)
 {
     if (!n_slots) return hipSuccess;
     hipLaunchKernelGGL(sketch_short_kernel, dim3((n_slots + 255) / 256), dim3(256), 0, st,
                        d_slot_group, n_slots, d_count, s, d_thr, d_thr_safe, d_n_short,
-                       d_short_slots);
+                       d_short_slots, (uint32_t)raise);
     return hipGetLastError();
 }
 
