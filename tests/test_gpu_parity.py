@@ -431,6 +431,59 @@ def _sorted_lists(rng):
     return lists
 
 
+def _shared_and_near_lists(rng):
+    """Sorted distinct u64 lists for the sparse path's index, probe and rank kernels:
+    * 300 values shared by 150 rows (posting buckets of 150 entries, a family of 150),
+    * rows built from the same 400 base values offset by 0, 1 or 2 (rows of different offsets
+      share no value but every value's bucket and fingerprint: candidates sharing nothing),
+    * rows holding v, v + 1 and v ^ 32 together (equal top 32 bits: equal rank keys, so the
+      rank kernel's clamped loop; a crowded index bucket), against rows holding only v."""
+    top = np.uint64(1) << np.uint64(63)
+    common = rng.integers(0, 2 ** 63, size=300, dtype=np.uint64) | top
+    lists = []
+    for i in range(150):
+        own = rng.integers(0, 2 ** 64, size=int(rng.integers(200, 800)), dtype=np.uint64)
+        lists.append(np.unique(np.concatenate([common, own])))
+    base = (rng.integers(0, 2 ** 62, size=400, dtype=np.uint64) << np.uint64(2)) | top
+    for i in range(30):
+        pick = np.sort(rng.choice(base, size=int(rng.integers(300, 400)), replace=False))
+        lists.append(np.unique(pick + np.uint64(i % 3)))
+    v = np.unique(rng.integers(0, 2 ** 62, size=200, dtype=np.uint64) << np.uint64(6)) | top
+    for i in range(12):
+        vv = rng.choice(v, size=150, replace=False)
+        parts = [vv] if i % 2 else [vv, vv + np.uint64(1), vv ^ np.uint64(32)]
+        lists.append(np.unique(np.concatenate(parts + [common[: 40 * (i % 3)]])))
+    return lists
+
+
+@pytest.mark.parametrize("compact", [False, True])
+def test_dist_shared_rows_and_near_collisions(ctx, oracle, compact):
+    """Hashes shared across many rows and same-bucket near-collisions (_shared_and_near_lists)
+    through the forced sparse path, as one set against itself (the symmetric probe and rank,
+    and the compact list) and against a copy; every cell equals the reference walk's
+    (CommandDistance.cpp:376-400) at S = 1000 and S = 300."""
+    import fpmash
+    rng = np.random.default_rng(77)
+    lists = _shared_and_near_lists(rng)
+    lengths = [int(x) for x in rng.integers(10 ** 4, 10 ** 6, size=len(lists))]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE)
+    try:
+        for S in (1000, 300):
+            nu, de, di, pv = oracle.dist_grid(lists, lengths, lists, lengths, S, 21, 4.0 ** 21)
+            for other in (lists, [x.copy() for x in lists]):
+                # the compact list is expanded (expand_compact asserts it holds exactly the
+                # cells with numer > 0)
+                run = ctx.dist_list if compact else ctx.dist
+                got = run(lists, other, S, use64=True, k=21, ref_lengths=lengths,
+                          qry_lengths=lengths)
+                assert np.array_equal(got["numer"].astype(np.uint32), nu), S
+                assert np.array_equal(got["denom"].astype(np.uint32), de), S
+                np.testing.assert_allclose(got["distance"], di, rtol=RTOL, atol=0)
+                assert ctx.last_dist_stats()["sparse"] == 2
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
 @pytest.mark.parametrize("mode", ["sparse", "dense"])
 def test_dist_rank_kernel_edges(ctx, oracle, mode):
     import fpmash
