@@ -1099,8 +1099,9 @@ hipError_t launch_dist_counts_fixup(const uint32_t *d_ref_len, uint32_t n_ref,
 
 // The same per-pair arithmetic as dist_finalize_kernel, for the candidate cells of the
 // sparse path only (the probe wrote every other cell's final values).  Grid-stride over the
-// device-side candidate count; with `sym` each candidate (q, r), r <= q, also finalizes its
-// mirror (r, q), whose numer / denom the rank kernel wrote.
+// device-side candidate count; with `sym` each candidate (q, r) (one of the pair's two cells,
+// probe_rows_kernel) also finalizes its mirror (r, q), whose numer / denom the rank kernel
+// wrote.
 __device__ __forceinline__ void finalize_cell(uint64_t o, uint32_t c, uint32_t d, uint64_t len_ref,
                                               uint64_t len_qry, uint32_t kmer_size,
                                               double kmer_space, double max_dist,

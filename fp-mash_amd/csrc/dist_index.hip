@@ -713,8 +713,20 @@ void probe_rows_kernel(
     const uint64_t mult = idx_mult(g);
     const uint32_t r0 = blockIdx.y * chunk_refs;
     const uint32_t r1 = min(n_ref, r0 + chunk_refs);
-    // symmetric self-comparison: only refs r <= q become candidates of row q
-    const uint32_t r1c = sym ? min(r1, q + 1) : r1;
+    // symmetric self-comparison: each unordered pair {q, r} is a candidate of one of its two
+    // rows: of the lower row when q + r is odd, of the higher (and the diagonal) when it is
+    // even, so every row ranks about half of its partners.  (r <= q gave a row all of its lower
+    // partners: a family's last rows ranked ~100 candidates and its first ~1, and the rank
+    // kernel ended on the heavy rows' workgroups.)  The events mark every partner; the mask is
+    // applied per bitmap word when the candidates are taken (no test per event).
+    auto word_mask = [&](uint32_t w) -> uint32_t {
+        if (!sym) return ~0u;
+        const uint32_t rb = r0 + 32 * w;                       // bit i <-> ref rb + i
+        const uint32_t odd = ((q ^ rb) & 1u) ? 0x55555555u : 0xAAAAAAAAu;   // q + r odd
+        // gt: the bits of refs above q
+        const uint32_t gt = q < rb ? ~0u : q - rb >= 31 ? 0u : ~((2u << (q - rb)) - 1u);
+        return (odd & gt) | (~odd & ~gt);
+    };
     const uint32_t nwords = (r1 - r0 + 31) / 32;
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) rowbits[w] = 0;
     __syncthreads();
@@ -725,7 +737,7 @@ void probe_rows_kernel(
     // one set against itself: row q's own entry sits in the bucket of each of its hashes,
     // so a bucket of one entry holds only that entry.  Such buckets (the unique hashes, most
     // of a sketch) are not read; the pair (q, q) they would mark is set here.
-    if (self_set && threadIdx.x == 0 && lq > 0 && q >= r0 && q < r1c)
+    if (self_set && threadIdx.x == 0 && lq > 0 && q >= r0 && q < r1)
         atomicOr(&rowbits[(q - r0) >> 5], 1u << ((q - r0) & 31));
     const uint64_t rowoff = (uint64_t)q * stride;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -806,7 +818,7 @@ void probe_rows_kernel(
                     const uint32_t e = e0 + 64 * u;
                     const uint32_t r = en[u] & rmask;
                     const bool hit = e < wn && (en[u] >> g.rbits) == (uint32_t)(tab[u] >> 32) &&
-                                     r >= r0 && r < r1c;
+                                     r >= r0 && r < r1;
                     wi[u] = hit ? r - r0 : 0u;
                     const uint32_t word = rowbits[wi[u] >> 5];
                     need |= (hit && !(word & (1u << (wi[u] & 31)))) ? (1u << u) : 0u;
@@ -828,7 +840,7 @@ void probe_rows_kernel(
     __syncthreads();
     // candidates of this row: popcount per word -> block scan -> append
     uint32_t mycnt = 0;
-    for (uint32_t w = threadIdx.x; w < nwords; w += 256) mycnt += __popc(rowbits[w]);
+    for (uint32_t w = threadIdx.x; w < nwords; w += 256) mycnt += __popc(rowbits[w] & word_mask(w));
     uint32_t x = mycnt;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) { uint32_t y = __shfl_up(x, d, 64); if (lane >= d) x += y; }
@@ -845,7 +857,7 @@ void probe_rows_kernel(
     uint64_t pos = row_base + wpre + x - mycnt;
     const uint64_t pair_row = (uint64_t)q * n_ref;
     for (uint32_t w = threadIdx.x; w < nwords; w += 256) {
-        uint32_t b = rowbits[w];
+        uint32_t b = rowbits[w] & word_mask(w);
         const uint64_t bit0 = pair_row + r0 + (uint64_t)w * 32;
         while (b) {
             int t = __builtin_ctz(b);

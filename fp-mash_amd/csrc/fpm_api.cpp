@@ -2846,8 +2846,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             bool rows_merge = all_sorted && hash_bytes == 8 && n_ref <= (1u << 19) &&
                               lcap <= 2048;
             // one sorted set against itself: (numer, denom) of sorted distinct lists is
-            // symmetric in the two sets, so only candidates r <= q are ranked and each result
-            // is written to both cells (q, r) and (r, q)
+            // symmetric in the two sets, so each unordered pair is ranked once (by the row the
+            // probe gives it: pair parity) and each result is written to both cells (q, r) and
+            // (r, q)
             const bool sym = rows_merge && self_set;
             {
                 TimedLaunch tl(ctx, FPM_K_PROBE, st);

@@ -507,8 +507,9 @@ def test_dist_rank_kernel_edges(ctx, oracle, mode):
 
 
 def test_dist_self_symmetric_path(ctx, oracle):
-    """One sorted set against itself (same buffers) ranks only r <= q and mirrors; the result
-    equals the same data passed as a separate copy and the oracle."""
+    """One sorted set against itself (same buffers) ranks each unordered pair once (in the
+    row the probe's pair-parity rule gives it) and mirrors; the result equals the same data
+    passed as a separate copy and the oracle."""
     import fpmash
     seqs, sk = _family_sketches(oracle, n_fam=8, members=12, seed=11)
     sk = sk + [sk[0][:10], np.zeros(0, np.uint64), sk[5][:700]]
