@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     uint32_t *const K32 = sKB.k;
     uint64_t *const Bs = sKB.v;
     __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
-    __shared__ uint32_t s_maxn, s_keydup, s_next;
+    __shared__ uint32_t s_maxn, s_keydup;
     // rows [q_lo, q_lo + n_qry) of the grid (a part of the rows, whose probe ran before)
     const uint32_t qr = xcd_row(blockIdx.x, n_qry);
     if (qr >= n_qry) return;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
     const uint64_t *B = qry + (uint64_t)q * qry_stride;
-    if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; s_next = kRankWaves; }
+    if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; }
     {
         // stage B: every load of the row issued before the first LDS store (4 in flight per
         // thread: CAP / 256 with CAP 1024; a serial load-store loop paid the global latency
@@ -576,22 +576,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     auto run = [&](auto probe, bool fast) {
         Pair cur[kGroup], nxt[kGroup], pf[kGroup];
         Row Rc{};
-        // candidates taken in turn from a workgroup counter (the first kRankWaves by wave id):
-        // a wave whose candidates exit early takes more of them, instead of waiting at the end
-        // of the row for the wave with the slow ones
-        auto grab = [&]() -> uint32_t {
-            uint32_t v = 0;
-            if (lane == 0) v = atomicAdd(&s_next, 1u);
-            return __builtin_amdgcn_readfirstlane(v);
-        };
         if (wave < n) { Rc = open_row(cand_at(wave)); load_group(Rc, 0, pf); }
-        uint32_t cn = 0;
-        for (uint32_t c = wave; c < n; c = cn) {
+        for (uint32_t c = wave; c < n; c += kRankWaves) {
             const Row R = Rc;
 #pragma unroll
             for (int u = 0; u < kGroup; u++) cur[u] = pf[u];
-            cn = grab();
-            if (cn < n) { Rc = open_row(cand_at(cn)); load_group(Rc, 0, pf); }
+            if (c + kRankWaves < n) { Rc = open_row(cand_at(c + kRankWaves)); load_group(Rc, 0, pf); }
             const uint32_t la = R.la;
             const uint64_t o = R.o;
             const bool need_all = la < S && lb < S;       // denom depends on #shared
