@@ -36,29 +36,44 @@ from fpmash import datagen  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 VALU_ISSUE_PER_S = 1024 * 2.4e9 / 2   # wave64 VALU instructions/s: 1024 SIMDs, 2 cycles each
-# per-launch HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (tools/pmc_traffic.py,
-# regenerated on the GPU box whenever the kernels change)
-def _latest_pmc():
-    """profiles/rNN/pmc_traffic.json of the newest round that has one."""
+# per-launch HBM bytes and SQ counters from rocprofv3 PMC passes (tools/pmc_traffic.py, run on
+# the GPU box into gpurun_out/TAG/ and copied into profiles/rNN/ here by tools/collect.py).
+# Every file carries the build id of the libfpmash.so it measured; counters of another build
+# are not attached to this run's kernel times (roofline.traffic etc. null, with a note).
+def pmc_dir(arg=None):
+    """--pmc-dir, else the newest profiles/rNN that holds a pmc_traffic.json"""
     import glob
+    if arg:
+        return arg if os.path.isabs(arg) else os.path.join(ROOT, arg)
     found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", "pmc_traffic.json")))
-    return found[-1] if found else os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    return os.path.dirname(found[-1]) if found else None
 
 
-PMC_TRAFFIC = _latest_pmc()
+def load_pmc(name, directory):
+    """(counters dict, note): the PMC file `name` of `directory` when it measured the build
+    loaded now, else (None, why not)."""
+    path = os.path.join(directory, name) if directory else None
+    if not path or not os.path.exists(path):
+        return None, f"no {name}"
+    d = json.load(open(path))
+    rel = os.path.relpath(path, ROOT)
+    have, want = d.get("build_id"), fpmash.build_id()
+    if have is None or have != want:
+        return None, (f"{rel} measured build {have}, this run loads build {want}: "
+                      "counters of another build are not attached")
+    d["source"] = rel
+    return d, None
 
 
-def leg_counters(leg):
-    """A side leg's per-kernel counters (tools/pmc_traffic.py --leg, the newest
-    profiles/rNN/pmc_<leg>.json, measured on the GPU box): average launch time, HBM traffic
+def leg_counters(leg, directory=None):
+    """A side leg's per-kernel counters (tools/pmc_traffic.py --leg, pmc_<leg>.json of the PMC
+    directory, measured on the GPU box on this same build): average launch time, HBM traffic
     rate against the 8 TB/s peak, VALU-issue fraction, wave-state split, L2 hit rate and LDS
     bank-conflict cycles, and the bound those numbers point to (the leg's bound claims are
-    read from here, not asserted).  None when no profile exists."""
-    import glob
-    found = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", f"pmc_{leg}.json")))
-    if not found:
-        return None
-    d = json.load(open(found[-1]))
+    read from here, not asserted).  {"note": ...} when there is no profile of this build."""
+    d, note = load_pmc(f"pmc_{leg}.json", directory)
+    if d is None:
+        return {"note": note}
     ks = {}
     for k, v in d.get("kernels", {}).items():
         if not v.get("avg_ns"):
@@ -77,7 +92,7 @@ def leg_counters(leg):
                  "l2_hit_frac": (v.get("l2") or {}).get("hit_frac"),
                  "lds_bank_conflict_cycles": (v.get("l2") or {}).get("lds_bank_conflict_cycles"),
                  "bound_by_counters": bound}
-    return {"source": os.path.relpath(found[-1], ROOT), "command": d.get("command"),
+    return {"source": d["source"], "build_id": d.get("build_id"), "command": d.get("command"),
             "kernels": dict(sorted(ks.items(), key=lambda kv: -kv[1]["avg_ms"] *
                                    (kv[1]["calls"] or 1)))}
 METRIC = "bases/s sketched + Mpairs/s dist, k=21 s=1000, 1/2/4/8 MI355X; %HBM roofline"
@@ -118,6 +133,10 @@ def parse():
                          "output (fpm_dist_dev16)")
     ap.add_argument("--no-parity", action="store_true",
                     help="skip the oracle checks of the C2 / C3 / C4 results")
+    ap.add_argument("--pmc-dir", default=None,
+                    help="directory of the pmc_*.json counter files to attach (default: the "
+                         "newest profiles/rNN holding one); used only when they carry the "
+                         "loaded library's build id")
     ap.add_argument("--detail", default=os.path.join(ROOT, "gpurun_out", "bench_detail.json"),
                     help="side file for the full result (per-kernel tables, leg counters, CLI "
                          "phases); '' = none.  The printed line keeps the headline numbers")
@@ -131,7 +150,7 @@ def parse_args_for_test(**kw):
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
                            no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True,
                            no_split=True, split_bases=1_000_000_000, detail="",
-                           no_full_grid=True)
+                           no_full_grid=True, pmc_dir=None)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -1494,7 +1513,8 @@ def compact_line(d, detail_path=None):
     line["config"] = d.get("config")
     line["roofline"] = {k: (_r(roof.get(k)) if isinstance(roof.get(k), float) else roof.get(k))
                         for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel",
-                                  "avg_launch_ms", "alg_bytes_per_launch", "valu_issue_frac")}
+                                  "avg_launch_ms", "alg_bytes_per_launch", "valu_issue_frac",
+                                  "traffic_source", "traffic_note", "build_id")}
     if roof.get("wave_state_frac"):
         line["roofline"]["wave_state_frac"] = {k: _r(v, 3) for k, v in
                                                roof["wave_state_frac"].items()}
@@ -1703,9 +1723,9 @@ def main():
                                     "ref + query sketches read + u16 numer/denom (4 B/pair) written")
         alg[N[fpmash.K_FINALIZE]] = (n_pairs * (2 + 2) + n_listed * 25,
                                      "numer/denom read, 25 B per listed cell written")
-    traffic = {}
-    if os.path.exists(PMC_TRAFFIC):
-        traffic = json.load(open(PMC_TRAFFIC)).get("kernels", {})
+    pmc_at = pmc_dir(args.pmc_dir)
+    pmc, pmc_note = load_pmc("pmc_traffic.json", pmc_at)
+    traffic = (pmc or {}).get("kernels", {})
     # the dominant kernel: the longest single launch
     dom = max(ktimes, key=lambda k_: ktimes[k_]["total_ms"] / ktimes[k_]["launches"])
     achieved = alg[dom][0] / (ktimes[dom]["avg_ms"] * 1e-3) / 1e9 if dom in alg else None
@@ -1723,7 +1743,10 @@ def main():
                             (ktimes[dom]["avg_ms"] * 1e-3 * VALU_ISSUE_PER_S)
                             if dom in traffic and "sq" in traffic[dom] else None),
         "wave_state_frac": traffic.get(dom, {}).get("wave_state_frac"),
-        "traffic_source": os.path.relpath(PMC_TRAFFIC, ROOT) if dom in traffic else None,
+        "traffic_source": pmc["source"] if dom in traffic else None,
+        "traffic_note": pmc_note if pmc_note else (None if dom in traffic else
+                                                   f"no counters for {dom} in {pmc['source']}"),
+        "build_id": fpmash.build_id(),
         "alg_bytes_per_launch": alg.get(dom, (None, ""))[0],
         "alg_bytes_formula": alg.get(dom, (None, ""))[1],
         "avg_launch_ms": ktimes[dom]["avg_ms"],
@@ -1777,7 +1800,7 @@ def main():
 
     for leg, r_ in (("c3", c3), ("c4", c4), ("c5", c5)):
         if r_ is not None:
-            r_["counters"] = leg_counters(leg)
+            r_["counters"] = leg_counters(leg, pmc_at)
 
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:

@@ -45,6 +45,7 @@ vp = C.c_void_p
 # every symbol include/fpmash.h declares: (name, restype, argtypes)
 SYMBOLS = [
     ("fpm_abi_version", C.c_int, []),
+    ("fpm_build_id", C.c_char_p, []),
     ("fpm_last_error", C.c_char_p, []),
     ("fpm_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("fpm_ctx_create", C.c_int, [C.c_int, C.POINTER(vp)]),
@@ -200,6 +201,22 @@ def make_params(k=21, s=1000, seed=42, alphabet=ALPHABET_NUCLEOTIDE, noncanonica
 
 
 _LIB = None
+
+
+def build_id(path=None):
+    """The build id a libfpmash.so carries (fpm_build_id: a hash of the sources it was
+    compiled from), read from the file's "fpm-build-id:<id>" text without loading it, so a
+    process that must not touch the GPU (tools/pmc_traffic.py) can stamp its profiles with it.
+    None when the file is absent or carries no id."""
+    import mmap
+    import re
+    path = path or LIB_PATH
+    try:
+        with open(path, "rb") as f, mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ) as m:
+            hit = re.search(rb"fpm-build-id:([0-9a-f]{16})", m)
+            return bytes(hit.group(1)).decode() if hit else None
+    except (OSError, ValueError):
+        return None
 
 
 def lib():

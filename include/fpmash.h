@@ -58,6 +58,11 @@ typedef struct fpm_sketch_params {
 
 /* ---- context / device --------------------------------------------------- */
 int fpm_abi_version(void);
+/* The build id of this libfpmash.so: the first 16 hex digits of a SHA-256 over the sources it
+ * was compiled from (csrc/, include/fpmash.h, the Makefile), also embedded in the file as the
+ * text "fpm-build-id:<id>" so a profile can be stamped with the build it measured without
+ * loading the library (tools/pmc_traffic.py, bench.py's roofline check). */
+const char *fpm_build_id(void);
 const char *fpm_last_error(void);
 int fpm_device_count(int *count);
 int fpm_ctx_create(int device, fpm_ctx **out);

@@ -10,7 +10,7 @@ count Infinity-Cache traffic (L2 memory-side requests), so they are an upper bou
 HBM bytes.  rocprofv3 reports both in KiB.
 
 Run it on the GPU box (this process never touches the GPU itself):
-    python3 tools/pmc_traffic.py --out profiles/r02/pmc_traffic.json
+    python3 tools/pmc_traffic.py --out gpurun_out/TAG/pmc_traffic.json
 """
 from __future__ import annotations
 
@@ -132,7 +132,9 @@ def kernel_times(outdir: str, bench_args: list[str]) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "r03", "pmc_traffic.json"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic.json"),
+                    help="written under gpurun_out/ on the GPU box; copied into profiles/rNN/ "
+                         "in the build container after the pull (tools/collect.py)")
     ap.add_argument("--work", default=os.path.join(ROOT, "gpurun_out", "pmc_traffic"))
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
@@ -200,8 +202,13 @@ def main():
             # wave64 VALU instructions per launch / (launch time x 1024 SIMDs x 2.4 GHz / 2)
             v["valu_issue_frac"] = (v["sq"].get("insts_valu", 0.0) / (secs * 1024 * 2.4e9 / 2)
                                     if secs else None)
+    sys.path.insert(0, os.path.join(ROOT, "fp-mash_amd"))
+    import fpmash                                   # (reads the .so's build id, no GPU)
     out = {
         "leg": a.leg,
+        # the build these counters measured: bench.py drops them from `roofline` when the
+        # library it loads carries another id
+        "build_id": fpmash.build_id(),
         "command": " ".join(["python3"] + [os.path.relpath(x, ROOT) if x.startswith(ROOT) else x
                                            for x in bench_args]),
         "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes over "
