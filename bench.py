@@ -119,8 +119,12 @@ def parse():
     ap.add_argument("--c4-n", type=int, default=50_000)
     ap.add_argument("--no-cli-fp", action="store_true",
                     help="skip the -fp CLI leg (sketch -fp x10, paste -fp, dist -fp)")
-    ap.add_argument("--no-gather-check", action="store_true",
-                    help="at N = 1: skip the C4 gathered-path check (one-rank RCCL group)")
+    ap.add_argument("--no-gather-check", "--no-vblocks-check", dest="no_gather_check",
+                    action="store_true",
+                    help="at N = 1: skip the checks of the N > 1 paths on this GPU (C4 with "
+                         "three virtual blocks; the RCCL min-merge on a one-rank communicator)")
+    ap.add_argument("--no-c4-shares", action="store_true",
+                    help="at N = 1: skip timing rank shares of N = 2/4/8 C4 runs on this GPU")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 RefSeq-scale sketch leg")
     ap.add_argument("--no-cli", action="store_true",
                     help="skip the end-to-end CLI leg (fpmash sketch + dist, 1e8 text lines)")
@@ -150,7 +154,7 @@ def parse_args_for_test(**kw):
                            no_fp_text=True, no_c3=True, no_c4=True, c4_n=50_000,
                            no_parity=True, no_c5=True, c5_genomes=1000, no_cli=True,
                            no_split=True, split_bases=1_000_000_000, detail="",
-                           no_full_grid=True, pmc_dir=None)
+                           no_full_grid=True, pmc_dir=None, no_c4_shares=True)
     for k_, v in kw.items():
         setattr(a, k_, v)
     return a
@@ -180,34 +184,21 @@ def dist_env():
 
 
 class Group:
-    """Barrier + max over ranks.  gloo (host-side) keeps the timing collective off
-    the device; the data path itself has no collective (independent batches)."""
+    """Barrier + max / sum over ranks on a host-side gloo group (the timing collectives stay off
+    the device; the C2 / C4 / C5 data paths have no collective).  comm(ctx) builds the one
+    device communicator the path has: RCCL inside libfpmash (fpmash.Comm) for the split
+    genome's min-merge, its unique id broadcast over gloo."""
 
-    def __init__(self, ws, local=0, nccl=False, single_rank_nccl=False):
-        """single_rank_nccl: at ws = 1, a one-rank process group with its RCCL group anyway
-        (the C4 leg's gathered data path run once on one GPU, c4_gather_check)"""
+    def __init__(self, ws):
         self.ws = ws
-        self.nccl = None
-        if ws > 1 or (nccl and single_rank_nccl):
+        self.dist = None
+        self._comm = None
+        if ws > 1:
             import datetime
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            if ws == 1 and "MASTER_PORT" not in os.environ:
-                import socket
-                so = socket.socket()
-                so.bind(("127.0.0.1", 0))
-                os.environ["MASTER_PORT"] = str(so.getsockname()[1])
-                so.close()
-            os.environ.setdefault("RANK", "0")
-            os.environ.setdefault("WORLD_SIZE", str(ws))
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
             self.dist = dist
-            if nccl:
-                # RCCL (backend "nccl") for the C4 leg's sketch-row all-gather over xGMI
-                import torch
-                torch.cuda.set_device(local)
-                self.nccl = dist.new_group(backend="nccl",
-                                           timeout=datetime.timedelta(seconds=300))
 
     def barrier(self):
         if self.ws > 1:
@@ -228,6 +219,30 @@ class Group:
         t = torch.tensor([x], dtype=torch.float64)
         self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
         return float(t.item())
+
+    def comm(self, ctx):
+        """fpmash.Comm over all ranks on ctx's device (created once; blocks until every rank
+        has joined).  None when the ranks share one GPU (FPMASH_BENCH_ONE_DEVICE: RCCL refuses
+        two ranks per device): min-merges then go over gloo."""
+        if self._comm is None and not os.environ.get("FPMASH_BENCH_ONE_DEVICE"):
+            rank = 0
+            if self.ws > 1:
+                import torch
+                rank = self.dist.get_rank()
+                uid = torch.zeros(fpmash.COMM_ID_BYTES, dtype=torch.uint8)
+                if rank == 0:
+                    uid[:] = torch.frombuffer(bytearray(fpmash.comm_unique_id()), dtype=torch.uint8)
+                self.dist.broadcast(uid, 0)
+                uid = bytes(uid.numpy().tobytes())
+            else:
+                uid = fpmash.comm_unique_id()
+            self._comm = fpmash.Comm(ctx, self.ws, rank, uid)
+        return self._comm
+
+    def close(self):
+        if self._comm is not None:
+            self._comm.close()
+            self._comm = None
 
 
 def make_batch(args, rank):
@@ -438,11 +453,13 @@ def check_grid_rows(outs, n_ref, rows, exp, max_dist=1.0, max_pvalue=1.0):
             "ok": counts_ok and dist_ok and pv_ok and pass_ok}
 
 
-def parity_summary(c2, c3, c4, c5=None, cli=None, split=None, c4_gather=None, cli_fp=None):
+def parity_summary(c2, c3, c4, c5=None, cli=None, split=None, c4_gather=None, cli_fp=None,
+                   comm=None):
     """the line's `parity` object: every oracle check of this run and whether all passed"""
     parts = {"c2": c2, "c3_fp": c3.get("parity") if c3 else None,
              "c4": c4.get("parity") if c4 else None,
-             "c4_gather": c4_gather.get("parity") if c4_gather else None,
+             "c4_vblocks": c4_gather.get("parity") if c4_gather else None,
+             "comm_min_merge": comm,
              "c5": c5.get("parity") if c5 else None,
              "split": split.get("parity") if split else None,
              "cli": cli.get("parity") if cli else None,
@@ -605,45 +622,56 @@ def compact_out(ctx, cells):
             fpmash.CellList(ctx, min(cells, max(1 << 20, min(1 << 26, cells // 16))))]
 
 
+def c4_rows(lo, hi, members=100, seq_len=2000):
+    """Rows [lo, hi) of the C4 set: family f (members consecutive rows) generated from its own
+    seed, so any rank builds any range of rows without the rest of the set."""
+    out = []
+    for f in range(lo // members, (hi + members - 1) // members):
+        fam = datagen.family_dna(1, members, seq_len, sub_rate=(0.01, 0.10), seed=4000 + f)
+        out += fam[max(lo, f * members) - f * members: min(hi, (f + 1) * members) - f * members]
+    return out
+
+
+def merge_spans(ranges):
+    """the union of [lo, hi) ranges as sorted disjoint spans"""
+    out = []
+    for lo, hi in sorted(r for r in ranges if r[1] > r[0]):
+        if out and lo <= out[-1][1]:
+            out[-1][1] = max(out[-1][1], hi)
+        else:
+            out.append([lo, hi])
+    return [tuple(x) for x in out]
+
+
 def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_len=2000,
            steps=3, warmup=1, parity=True, vblocks=1, cpu=False, prefill=True):
     """C4: one all-vs-all dist of n family-structured sketches, sharded over
-    the ranks (strong scaling).  A timed step is the whole job on every rank:
-      1. sketch its contiguous block of families (each family generated from its own seed,
-         so the data does not depend on the GPU count);
-      2. all-gather the sketch rows and counts (RCCL over xGMI, the "nccl" backend,
-         N x s x 8 B = 400 MB at n = 50k) -- the job's only exchange: the reference set fits
-         every GPU's HBM many times over, so no min-merge / ring rotation is needed;
-      3. its share of the n x n grid (fpmash.shard.pair_block_jobs): every unordered pair of
-         blocks is compared on one rank and written twice (the grid and its transpose:
-         sorted sketches give symmetric results), so each rank indexes only its own block
-         (plus, for even N, one more block), compares ~n^2 / 2N pairs and writes ~n^2 / N
-         cells, left in HBM in the compact output of SURVEY §8(b)/(d): u16 numer / denom of
-         every cell + distance / FP64 p-value / pass of the cells with numer > 0 (the indexes
-         are rebuilt inside the step).
-    With one rank there is no gather and the whole grid is the library's symmetric self
-    path (fpm_dist_list_dev with the queries = the references).
-    vblocks > 1 (one rank, the check of the gathered data path on one GPU): the rank's rows go
-    through the all-gather anyway (RCCL with a one-rank nccl group), the set is cut into
-    vblocks blocks, and the rank runs every virtual rank's block-pair jobs (pair_block_jobs) on
-    the gathered rows: refsets and the self / mirror list calls on torch-allocated pointers."""
+    the ranks (strong scaling), with NO data-path collective: north_star keeps RCCL for "the
+    final min-merge only where the reference set exceeds one GPU's HBM", and C4's 400 MB set
+    fits every GPU many times over.  The reference runs the grid on one pthreads pool
+    (CommandDistance.cpp:224-261); here the grid is dealt as unordered block pairs
+    (fpmash.shard.pair_block_jobs): every unordered pair of blocks is compared on one rank and
+    written twice (grid + transpose: sorted sketches give symmetric results), so a rank
+    compares ~n^2 / 2N pairs and writes ~n^2 / N cells.  A timed step on every rank:
+      1. sketch the rows its jobs read -- its own block and the (N - 1) / 2 blocks (+ half a
+         block for even N) it is paired with, ~(N + 1) / 2N of the set -- from the inputs
+         every rank holds (each family generated from its own seed: the same data at any N);
+      2. its block pairs on those local rows: the own block on the library's symmetric self
+         path, the others through fpm_refset_dist_mirror_list_dev; the indexes are rebuilt
+         inside the step; output left in HBM in the compact form of SURVEY §8(b)/(d) (u16
+         numer / denom of every cell + distance / FP64 p-value / pass of the cells with
+         numer > 0).
+    With one rank the whole grid is one fpm_dist_list_dev call on the symmetric self path,
+    with the no-shared-hash counts prefilled beside the sketch (fpm_dist_list_prefill).
+    One rank's share of an N-rank run is measured alone on one GPU by passing ws = N, rank =
+    r with a one-process group (bench `c4_shares`): the rank needs nothing from the others.
+    vblocks > 1 (one rank): every virtual rank's jobs of a vblocks-way split run in this
+    process (the N > 1 job structure checked on one GPU: every cell written once)."""
     import ctypes as C
-    from fpmash.shard import all_gather_rows, pair_block_jobs, shard_range
+    from fpmash.shard import pair_block_jobs, shard_range
     fams = n // members
     n = fams * members
     bounds = [tuple(x * members for x in shard_range(fams, ws, r)) for r in range(ws)]
-    lo, hi = bounds[rank]
-    n_loc = hi - lo
-    seqs = []
-    for f in range(lo // members, hi // members):
-        seqs += datagen.family_dna(1, members, seq_len, sub_rate=(0.01, 0.10), seed=4000 + f)
-    P = fpmash.make_params(k=k, s=s)
-    job = ctx.sketch_job(P, seqs)
-    d_rows, d_cnt, _ng, stride = job.device_output()
-    L = fpmash.lib()
-    st = ctx.stream
-    g = {}
-    gathered = ws > 1 or vblocks > 1
     if vblocks > 1:
         if ws != 1:
             raise ValueError("vblocks > 1 stands in for more ranks on one rank only")
@@ -651,113 +679,70 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         jobs = [j for vr in range(vblocks) for j in pair_block_jobs(vb, vr)]
     else:
         jobs = pair_block_jobs(bounds, rank)
-    if gathered:
-        import torch
-        # RCCL gathers device tensors over xGMI; without an nccl group (the 2-rank GPU test
-        # on one card) the same rows go through gloo on host tensors and back to the device.
-        # The gathered rows land in persistent buffers (the refsets borrow pointers into them)
-        on_dev = grp.nccl is not None
-        dev = torch.device(f"cuda:{local}") if on_dev else torch.device("cpu")
-        loc_rows = torch.empty((n_loc, stride), dtype=torch.int64, device=dev)
-        loc_cnt = torch.empty((n_loc, 1), dtype=torch.int32, device=dev)
-        loc_len = torch.full((n_loc, 1), seq_len, dtype=torch.int64, device=dev)
-        g["rows"] = torch.empty((n, stride), dtype=torch.int64, device=dev)
-        g["cnt"] = torch.empty((n, 1), dtype=torch.int32, device=dev)
-        g["len"] = all_gather_rows(loc_len, n, ws, group=grp.nccl, bounds=bounds)
-        if on_dev:
-            torch.cuda.synchronize(dev)
-            R, C_, Ln = g["rows"].data_ptr(), g["cnt"].data_ptr(), g["len"].data_ptr()
-        else:
-            g["d_rows"] = fpmash.DeviceBuffer(ctx, n * stride * 8)
-            g["d_cnt"] = fpmash.DeviceBuffer(ctx, n * 4)
-            g["d_len"] = fpmash.DeviceBuffer.from_array(ctx, g["len"].numpy())
-            R, C_, Ln = g["d_rows"].ptr, g["d_cnt"].ptr, g["d_len"].ptr
-        outs = []
-        for j in jobs:
-            (rl, rh), (ql, qh) = j["ref"], j["qry"]
-            cells = (rh - rl) * (qh - ql)
-            o = {"p": compact_out(ctx, cells)}
-            if j["kind"] == "mirror":
-                o["m"] = compact_out(ctx, cells)
-            outs.append(o)
-    else:
-        d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n, seq_len, np.uint64))
-        outs = [{"p": compact_out(ctx, n_loc * n)}]
+    single = ws == 1 and vblocks == 1          # one self job over the whole set
+    # the rows this rank's jobs read, sketched locally in one job (span order)
+    spans = merge_spans([j["ref"] for j in jobs] + [j["qry"] for j in jobs])
+    base, seqs = [], []
+    for lo_, hi_ in spans:
+        base.append(len(seqs))
+        seqs += c4_rows(lo_, hi_, members, seq_len)
+    n_loc = len(seqs)
+
+    def loc(g):
+        """local row of global row g"""
+        for (lo_, hi_), b_ in zip(spans, base):
+            if lo_ <= g < hi_:
+                return b_ + g - lo_
+        raise KeyError(g)
+    P = fpmash.make_params(k=k, s=s)
+    job = ctx.sketch_job(P, seqs)
+    del seqs
+    d_rows, d_cnt, _ng, stride = job.device_output()
+    d_len = fpmash.DeviceBuffer.from_array(ctx, np.full(n_loc, seq_len, np.uint64))
+    L = fpmash.lib()
+    st = ctx.stream
+
+    def rows_at(g):
+        """(rows, counts, lengths) device pointers at global row g"""
+        r_ = loc(g)
+        return d_rows + r_ * stride * 8, d_cnt + r_ * 4, d_len.ptr + r_ * 8
+    outs = []
+    for j in jobs:
+        (rl, rh), (ql, qh) = j["ref"], j["qry"]
+        o = {"p": compact_out(ctx, (rh - rl) * (qh - ql))}
+        if j["kind"] == "mirror":
+            o["m"] = compact_out(ctx, (rh - rl) * (qh - ql))
+        outs.append(o)
     refsets = {}
-    # multi-rank phases: the sketch, the all-gather window (this rank's own block against
-    # itself runs beside it: that job reads only local rows), the jobs after the gather
-    phase = ({"sketch": 0.0, "gather_beside_self_job": 0.0, "dist_after_gather": 0.0}
-             if gathered else {"sketch": 0.0, "gather": 0.0, "dist": 0.0})
+    phase = {"sketch": 0.0, "dist": 0.0}
 
-    def gather_start():
-        """The rank's rows and counts into the collective's buffers, then the all-gathers
-        launched asynchronously (RCCL on its own stream, or gloo threads); returns the
-        function that waits for them."""
-        if on_dev:
-            fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
-            fpmash._check(L.fpm_memcpy_d2d(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
-        else:
-            fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_rows.data_ptr(), d_rows, n_loc * stride * 8))
-            fpmash._check(L.fpm_memcpy_d2h(ctx.h, loc_cnt.data_ptr(), d_cnt, n_loc * 4))
-        ctx.synchronize()
-        fin_rows = all_gather_rows(loc_rows, n, ws, group=grp.nccl, bounds=bounds,
-                                   out=g["rows"], async_op=True)
-        fin_cnt = all_gather_rows(loc_cnt, n, ws, group=grp.nccl, bounds=bounds, out=g["cnt"],
-                                  async_op=True)
-
-        def finish():
-            fin_rows()
-            fin_cnt()
-            if on_dev:
-                torch.cuda.synchronize(dev)
-            else:
-                fpmash._check(L.fpm_memcpy_h2d(ctx.h, R, g["rows"].data_ptr(), n * stride * 8))
-                fpmash._check(L.fpm_memcpy_h2d(ctx.h, C_, g["cnt"].data_ptr(), n * 4))
-        return finish
-
-    def gather():
-        gather_start()()
-
-    own = (lo, hi)
-
-    def local_job(j):
-        """the own block against itself: its rows as the sketch left them (no gathered copy
-        needed, so it runs beside the gather)"""
-        return j["kind"] == "self" and j["ref"] == own
-
-    def job_query(j):
-        (ql, qh) = j["qry"]
-        if local_job(j):
-            # the own block's rows as the sketch left them (the refset's own pointers: the
-            # library's symmetric self path)
-            return (d_rows, d_cnt, Ln + ql * 8, stride, qh - ql)
-        return (R + ql * stride * 8, C_ + ql * 4, Ln + ql * 8, stride, qh - ql)
-
-    def dist_share(which="all"):
-        """which: "self" = the own block's index + its self job (local rows only), "rest" =
-        the other indexes + the mirror jobs (gathered rows), "all" = both."""
-        for key, rs in refsets.items():
-            if which == "all" or (which == "self") == (key == own):
-                fpmash._check(L.fpm_refset_reindex(rs, st))
+    def dist_share():
+        if single:
+            p_ = outs[0]["p"]
+            fpmash._check(L.fpm_dist_list_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
+                                              d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
+                                              1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref, st))
+            return
+        for rs in refsets.values():
+            fpmash._check(L.fpm_refset_reindex(rs, st))
         for j, o in zip(jobs, outs):
-            if which != "all" and (which == "self") != local_job(j):
-                continue
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
-            rs = refsets[(rl, rh)]
-            q = job_query(j)
+            q = rows_at(ql) + (stride, qh - ql)
             p_ = o["p"]
             if j["kind"] == "self":
-                fpmash._check(L.fpm_refset_dist_list_dev(rs, *q, s, k, 4.0 ** k, 1.0, 1.0,
-                                                         p_[0].ptr, p_[1].ptr, p_[2].ref, st))
+                # the query pointers are the refset's own: the library's symmetric self path
+                fpmash._check(L.fpm_refset_dist_list_dev(refsets[(rl, rh)], *q, s, k, 4.0 ** k,
+                                                         1.0, 1.0, p_[0].ptr, p_[1].ptr,
+                                                         p_[2].ref, st))
             else:
                 m_ = o["m"]
                 fpmash._check(L.fpm_refset_dist_mirror_list_dev(
-                    rs, *q, s, k, 4.0 ** k, 1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref,
-                    m_[0].ptr, m_[1].ptr, m_[2].ref, st))
+                    refsets[(rl, rh)], *q, s, k, 4.0 ** k, 1.0, 1.0, p_[0].ptr, p_[1].ptr,
+                    p_[2].ref, m_[0].ptr, m_[1].ptr, m_[2].ref, st))
 
     def run(timed):
         t0 = time.perf_counter()
-        if prefill and not gathered:
+        if prefill and single:
             # the grid's no-shared-hash counts (10 GB) written beside the sketch kernels on the
             # library's side stream (fpm_dist_list_prefill), instead of beside the rank kernel:
             # 6.34-6.35 -> 5.80 ms, same box, r05n (tools/leg_run.py --no-prefill: the A/B)
@@ -767,43 +752,22 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         if timed:
             ctx.synchronize()
         t1 = time.perf_counter()
-        if gathered:
-            finish = gather_start()
-            dist_share("self")          # beside the gather: local rows only
-            finish()
-            if timed:
-                ctx.synchronize()
-        t2 = time.perf_counter()
-        if gathered:
-            dist_share("rest")
-        else:
-            p_ = outs[0]["p"]
-            fpmash._check(L.fpm_dist_list_dev(ctx.h, d_rows, d_cnt, d_len.ptr, stride, n, d_rows,
-                                              d_cnt, d_len.ptr, stride, n, 8, s, k, 4.0 ** k,
-                                              1.0, 1.0, p_[0].ptr, p_[1].ptr, p_[2].ref, st))
+        dist_share()
         if timed:
             ctx.synchronize()
-            t3 = time.perf_counter()
-            ks = list(phase)
-            phase[ks[0]] += t1 - t0
-            phase[ks[1]] += t2 - t1
-            phase[ks[2]] += t3 - t2
-    if gathered:
-        # the indexes live as long as the leg (rebuilt in every step by fpm_refset_reindex)
+            phase["sketch"] += t1 - t0
+            phase["dist"] += time.perf_counter() - t1
+    if not single:
+        # the indexes live as long as the leg over the job's output rows (rebuilt in every
+        # step by fpm_refset_reindex after the sketch rewrote them)
         job.run(st)
         ctx.synchronize()
-        gather()
         for j in jobs:
             rl, rh = j["ref"]
             if (rl, rh) not in refsets:
                 h = C.c_void_p()
-                # the own block's index over the sketch output itself (no gathered copy
-                # needed: its self job runs while the gather is in flight); others over the
-                # gathered rows
-                rp, cp = (d_rows, d_cnt) if (rl, rh) == own else (R + rl * stride * 8,
-                                                                  C_ + rl * 4)
-                fpmash._check(L.fpm_refset_create_dev(ctx.h, rp, cp, Ln + rl * 8, stride,
-                                                      rh - rl, 8, s, C.byref(h)))
+                fpmash._check(L.fpm_refset_create_dev(ctx.h, *rows_at(rl), stride, rh - rl, 8,
+                                                      s, C.byref(h)))
                 refsets[(rl, rh)] = h
     for _ in range(warmup):
         run(False)
@@ -813,9 +777,9 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
     for _ in range(steps):
         run(False)
     ctx.synchronize()
-    el = time.perf_counter() - t0
+    el_own = time.perf_counter() - t0
     grp.barrier()
-    el = grp.max(el)
+    el = grp.max(el_own)
     listed = 0
     for o in outs:
         for key in ("p", "m"):
@@ -841,17 +805,18 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             kt[name] = {"ms": tot, "launches": cnt_}
     ctx.reset_timing()
     par = None
+    rows_h = cnt_h = None
+    if (parity and (rank == 0 or parity == "all")) or (cpu and rank == 0 and single):
+        rows_h, cnt_h = job.fetch()
+
+    def ref(g):
+        r_ = loc(g)
+        return rows_h[r_, :cnt_h[r_]]
     if parity and (rank == 0 or parity == "all"):
         # the CPU leg's checker: sampled rows of each of this rank's grids (and their
         # transposes) x all their references
         from oracle import oracle as O
         t_c = time.perf_counter()
-        if gathered:
-            rows_h = g["rows"].cpu().numpy().view(np.uint64)
-            cnt_h = g["cnt"].cpu().numpy()[:, 0]
-        else:
-            rows_h, cnt_h = job.fetch()
-        refs = [rows_h[i, :cnt_h[i]] for i in range(n)]
         grids = []
         for j, o in zip(jobs, outs):
             (rl, rh), (ql, qh) = j["ref"], j["qry"]
@@ -862,15 +827,16 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         res = []
         for gi, (bufs, (rl, rh), (ql, qh)) in enumerate(grids):
             q = sample_rows(qh - ql, per, salt=4 + gi)
-            gr = O.dist_grid(refs[rl:rh], [seq_len] * (rh - rl), [refs[ql + int(x)] for x in q],
-                             [seq_len] * len(q), s, k, 4.0 ** k, threads=_threads())
+            gr = O.dist_grid([ref(g) for g in range(rl, rh)], [seq_len] * (rh - rl),
+                             [ref(ql + int(x)) for x in q], [seq_len] * len(q), s, k, 4.0 ** k,
+                             threads=_threads())
             res.append(check_grid_rows(bufs, rh - rl, q, gr))
         par = {"grids": len(grids), "rows": int(sum(r_["rows"] for r_ in res)),
                "pairs": int(sum(r_["pairs"] for r_ in res)),
                "pairs_sharing": int(sum(r_["pairs_sharing"] for r_ in res)),
                "ok": all(r_["ok"] for r_ in res), "check_s": time.perf_counter() - t_c}
     cpu_res = None
-    if cpu and rank == 0 and ws == 1 and parity:
+    if cpu and rank == 0 and single:
         # the reference's compare (CommandDistance.cpp:365-450: the literal walk + p-value per
         # pair, a worker pool) as the oracle's port on the CPUs available: 100 query rows x all
         # n references, scaled to the n x n grid (no text: the bench's C4 keeps its output in
@@ -878,6 +844,7 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         from oracle import oracle as O
         th = _threads()
         qrows = sample_rows(n, 100, salt=9)
+        refs = [ref(g) for g in range(n)]
         t_c = time.perf_counter()
         O.dist_grid(refs, [seq_len] * n, [refs[int(q)] for q in qrows], [seq_len] * len(qrows),
                     s, k, 4.0 ** k, threads=th)
@@ -894,26 +861,23 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
         for bl in o.values():
             for b in bl:
                 b.free()
-    if not gathered:
-        d_len.free()
-    for key in ("d_rows", "d_cnt", "d_len"):
-        if key in g:
-            g[key].free()
+    d_len.free()
     job.free()
     cells = sum((j["ref"][1] - j["ref"][0]) * (j["qry"][1] - j["qry"][0]) *
                 (2 if j["kind"] == "mirror" else 1) for j in jobs)
     return {"config": f"C4: all-vs-all dist of {n} family-structured {seq_len} bp sketches "
-                      f"(k={k}, s={s}); a step = sketch own block + all-gather of the sketch "
-                      f"rows (RCCL) + this rank's block pairs (each unordered pair compared once, "
-                      f"grid + transpose written), {ws} GPU(s)",
-            "n_gpus": ws, "pairs": n * n, "steps": steps, "ms_per_step": el / steps * 1e3,
+                      f"(k={k}, s={s}); a step = sketch the rows this rank's block pairs read "
+                      f"+ its block pairs (each unordered pair compared once, grid + transpose "
+                      f"written), no collective, {ws} GPU(s)",
+            "n_gpus": ws, "rank": rank, "pairs": n * n, "steps": steps,
+            "ms_per_step": el / steps * 1e3, "ms_per_step_this_rank": el_own / steps * 1e3,
             "output": "u16 numer/denom per pair + listed pairs with numer > 0 (SURVEY 8(d))",
             "listed_pairs_all_ranks": listed,
             "mpairs_per_s": n * n / (el / steps) / 1e6, "scaling": "strong",
             "phase_ms_rank0": {k_: v * 1e3 for k_, v in phase.items()},
             "kernels_rank0": kt,
-            "collective": (None if not gathered else "all_gather (nccl = RCCL)" if on_dev
-                           else "all_gather (gloo, host tensors)"),
+            "collective": None, "exchange_ms": 0.0,
+            "rows_sketched_rank0": n_loc, "rows_owned_rank0": bounds[rank][1] - bounds[rank][0],
             "virtual_blocks": vblocks,
             "jobs_rank0": [{"kind": j["kind"], "ref": list(j["ref"]), "qry": list(j["qry"])}
                            for j in jobs], "cells_rank0": cells,
@@ -921,6 +885,27 @@ def c4_leg(ctx, grp, ws, rank, local, n=50_000, members=100, s=1000, k=21, seq_l
             "candidates_all_ranks": cand, "parity": par, "cpu_baseline": cpu_res,
             "speedup_vs_cpu": (cpu_res["grid_s_extrapolated"] / (el / steps)
                                if cpu_res else None)}
+
+
+def c4_shares(ctx, n=50_000, s=1000, k=21, world_sizes=(2, 4, 8), steps=3, warmup=1):
+    """One rank's share of an N-rank C4 run, measured alone on this GPU: C4 has no exchange,
+    so rank r of N needs nothing from the other ranks (c4_leg with ws = N, rank = r and a
+    one-process group).  Rank 0 and rank N - 1 (for even N the ranks >= N/2 index a second
+    block): the slower of the two is the N-GPU step this GPU's numbers predict, with no
+    collective time to add."""
+    one = Group(1)
+    out = {}
+    for ws in world_sizes:
+        per = {}
+        for r in sorted({0, ws - 1}):
+            x = c4_leg(ctx, one, ws, r, 0, n=n, s=s, k=k, steps=steps, warmup=warmup,
+                       parity=False)
+            per[r] = {"ms_per_step": x["ms_per_step"], "phase_ms": x["phase_ms_rank0"],
+                      "rows_sketched": x["rows_sketched_rank0"], "cells": x["cells_rank0"]}
+        worst = max(v["ms_per_step"] for v in per.values())
+        out[ws] = {"ranks": per, "share_ms_max": worst,
+                   "projected_mpairs_per_s": n * n / (worst * 1e-3) / 1e6}
+    return out
 
 
 def cli_phases(stderr: bytes, prefix="[fpmash] "):
@@ -1391,13 +1376,51 @@ def split_genome_range(lo, hi):
     return np.concatenate(out).tobytes() if out else b""
 
 
+def comm_check(ctx, grp, s=2000, k=21):
+    """The min-merge's RCCL path (fpm_sketch_min_merge_comm) on a one-rank communicator: one
+    300 kb genome sketched in four k-mer ranges, each range's bottom-s row min-merged through
+    the communicator (a one-rank gather is a copy, then the device merge) in turn, and the four
+    merged rows merged again, against the oracle's sketch of the whole genome."""
+    from fpmash.shard import kmer_shard, min_merge
+    from oracle import oracle as O
+    t0 = time.perf_counter()
+    seq = datagen.family_dna(1, 1, 300_000, seed=77)[0]
+    P = fpmash.make_params(k=k, s=s)
+    comm = grp.comm(ctx)
+    parts = [seq[a:b] for a, b in (kmer_shard(len(seq), k, 4, r) for r in range(4))]
+    job = ctx.sketch_job(P, parts)
+    job.run(ctx.stream)
+    d_rows, d_cnt, _ng, stride = job.device_output()
+    got = [min_merge(ctx, d_rows + i * stride * 8, d_cnt + i * 4, s, 1, comm=comm)
+           for i in range(4)]
+    m = np.zeros((4, s), np.uint64)
+    for i, (h, n_) in enumerate(got):
+        m[i, :n_] = h
+    rows_d = fpmash.DeviceBuffer.from_array(ctx, m)
+    cnt_d = fpmash.DeviceBuffer.from_array(ctx, np.array([n_ for _, n_ in got], np.uint32))
+    o, oc = fpmash.DeviceBuffer(ctx, s * 8), fpmash.DeviceBuffer(ctx, 4)
+    fpmash._check(fpmash.lib().fpm_sketch_merge_dev(ctx.h, rows_d.ptr, cnt_d.ptr, 4, s, o.ptr,
+                                                    oc.ptr, None))
+    n_ = int(oc.to_array(np.uint32, 1)[0])
+    merged = o.to_array(np.uint64, s)[:n_]
+    job.free()
+    exp = O.sketch_batch(O.params(k=k, s=s), [seq])[0]
+    exp_parts = O.sketch_batch(O.params(k=k, s=s), parts)
+    ok_parts = all(n_i == len(e) and np.array_equal(h, e) for (h, n_i), e in zip(got, exp_parts))
+    ok = bool(ok_parts and n_ == len(exp) and np.array_equal(merged, exp))
+    return {"ok": ok, "one_rank_merges_equal_parts": bool(ok_parts),
+            "merged_equals_whole": bool(n_ == len(exp) and np.array_equal(merged, exp)),
+            "collective": "RCCL in libfpmash (fpm_sketch_min_merge_comm), 1 rank",
+            "check_s": time.perf_counter() - t0}
+
+
 def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, steps=3,
               warmup=1, parity=True):
     """One sketch split over the GPUs (north_star: "RCCL ... for the final min-merge where a
     single sketch exceeds one GPU"): one genome of `length` bases, its k-mer starts sharded
     into contiguous ranges (fpmash.shard.kmer_shard: k - 1 bases of overlap), each rank
-    sketches its range, and the ranks' bottom-s rows are all-gathered (RCCL over xGMI on an
-    nccl group) and min-merged on the device (fpm_sketch_merge_dev).  Timed step: sketch +
+    sketches its range, and the ranks' bottom-s rows are all-gathered (RCCL over xGMI inside
+    libfpmash, fpm_sketch_min_merge_comm) and min-merged on the device.  Timed step: sketch +
     gather + merge.  Check (outside the timed steps): the merged sketch equals the sketch of
     the whole genome in one piece, computed on rank 0 (at N = 1: four parts merged in one
     process against the whole); the merge itself is pinned to the oracle in
@@ -1408,15 +1431,12 @@ def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, s
     job = ctx.sketch_job(P, [split_genome_range(lo, hi)], groups=[0], n_groups=1)
     d_rows, d_cnt, _ng, _stride = job.device_output()
     st = ctx.stream
-    dev = None
-    if ws > 1 and grp.nccl is not None:
-        import torch
-        dev = torch.device(f"cuda:{local}")
+    comm = grp.comm(ctx) if ws > 1 else None
 
     def step():
         job.run(st)
         if ws > 1:
-            return min_merge(ctx, d_rows, d_cnt, s, ws, group=grp.nccl, device=dev)
+            return min_merge(ctx, d_rows, d_cnt, s, ws, comm=comm, group=None)
         ctx.synchronize()
         return None
     for _ in range(warmup):
@@ -1434,8 +1454,8 @@ def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, s
         merged = (rows[0, : cnt[0]], int(cnt[0]))
     out = {"config": f"one {length / 1e9:g} Gb genome, k={k}, s={s}, k-mer starts sharded over "
                      f"{ws} GPU(s), bottom-s rows all-gathered "
-                     f"({'RCCL' if dev is not None else 'none' if ws == 1 else 'gloo'}) and "
-                     "min-merged on the device",
+                     f"({'RCCL in libfpmash' if comm is not None else 'none' if ws == 1 else 'gloo'})"
+                     " and min-merged on the device",
            "n_gpus": ws, "bases": length, "steps": steps, "ms_per_step": el / steps * 1e3,
            "bases_per_s": length / (el / steps), "scaling": "strong"}
     if parity and rank == 0:
@@ -1523,7 +1543,8 @@ def compact_line(d, detail_path=None):
         "cores_note": cpu.get("cores_note"),
         "kind": cpu.get("kind"), "sample": cpu.get("sample"), "cpu_model": cpu.get("cpu_model")}
     line["parity"] = {"c2": _ok(par.get("c2")), "c3_fp": _ok(par.get("c3_fp")),
-                      "c4": _ok(par.get("c4")), "c4_gather": _ok(par.get("c4_gather")),
+                      "c4": _ok(par.get("c4")), "c4_vblocks": _ok(par.get("c4_vblocks")),
+                      "comm_min_merge": _ok(par.get("comm_min_merge")),
                       "c5": _ok(par.get("c5")),
                       "split": _ok(par.get("split")), "cli": _ok(par.get("cli")),
                       "cli_fp": _ok(par.get("cli_fp")),
@@ -1544,6 +1565,10 @@ def compact_line(d, detail_path=None):
         "c4_cpu_mpairs_per_s": _r((g(c4, "cpu_baseline", "pairs_per_s") or 0) / 1e6 or None),
         "c4_speedup_vs_cpu": _r(g(c4, "speedup_vs_cpu"), 3),
         "c4_output": g(c4, "output"),
+        "c4_exchange_ms": g(c4, "exchange_ms"),
+        "c4_share_ms_n2": _r(g(d, "c4_shares", 2, "share_ms_max")),
+        "c4_share_ms_n4": _r(g(d, "c4_shares", 4, "share_ms_max")),
+        "c4_share_ms_n8": _r(g(d, "c4_shares", 8, "share_ms_max")),
         "c5_ms_per_step": _r(g(c5, "ms_per_step")), "c5_bases_per_s": _r(g(c5, "bases_per_s")),
         "c5_cpu_bases_per_s": _r(g(c5, "cpu_baseline", "bases_per_s")),
         "c5_speedup_vs_cpu": _r(g(c5, "speedup_vs_cpu"), 3),
@@ -1577,13 +1602,7 @@ def compact_line(d, detail_path=None):
 def main():
     args = parse()
     ws, rank, local = dist_env()
-    # torch (RCCL groups) before the library's context: torch bundles its own HIP runtime,
-    # which finds no GPU when it starts after libfpmash's (system ROCm) runtime has; started
-    # first, both see the device and device pointers pass between them (fpm_memcpy_d2d of a
-    # torch tensor checked on the MI355X box, r04)
-    grp = Group(ws, local, nccl=not (args.no_c4 and args.no_split) and
-                not os.environ.get("FPMASH_BENCH_ONE_DEVICE"),
-                single_rank_nccl=not (args.no_c4 or args.no_gather_check))
+    grp = Group(ws)
     ctx = fpmash.Context(local)
     seqs = make_batch(args, rank)
     n = len(seqs)
@@ -1780,13 +1799,18 @@ def main():
         cells.free()
         c4 = c4_leg(ctx, grp, ws, rank, local, n=args.c4_n, s=args.s, k=args.k,
                     parity=not args.no_parity, cpu=not args.no_cpu_baseline)
-    c4g = None
-    if ws == 1 and grp.nccl is not None:
-        # the multi-GPU data path once on this GPU, outside every timed number: rows
-        # all-gathered by a one-rank RCCL group into torch tensors, three virtual blocks'
-        # self / mirror jobs on those pointers, every grid sampled against the oracle
-        c4g = c4_leg(ctx, grp, ws, rank, local, n=6000, s=args.s, k=args.k, steps=1, warmup=1,
-                     parity="all" if not args.no_parity else False, vblocks=3)
+    c4g = comm_chk = shares = None
+    if ws == 1 and not args.no_gather_check:
+        # the N > 1 paths on this GPU, outside every timed number: the C4 job structure of a
+        # three-way split (every virtual rank's self / mirror jobs, every grid sampled against
+        # the oracle), and the RCCL min-merge inside libfpmash on a one-rank communicator
+        if not args.no_c4:
+            c4g = c4_leg(ctx, grp, ws, rank, local, n=6000, s=args.s, k=args.k, steps=1,
+                         warmup=1, parity="all" if not args.no_parity else False, vblocks=3)
+        if not args.no_parity:
+            comm_chk = comm_check(ctx, grp)
+    if ws == 1 and not args.no_c4 and not args.no_c4_shares:
+        shares = c4_shares(ctx, n=args.c4_n, s=args.s, k=args.k)
 
     c5 = None
     if not args.no_c5:
@@ -1852,7 +1876,9 @@ def main():
             "fp_text": fp_leg,
             "c3_fp": c3,
             "c4_dist": c4,
-            "c4_gather_check": c4g,
+            "c4_vblocks_check": c4g,
+            "c4_shares": shares,
+            "comm_check": comm_chk,
             "c5_sketch": c5,
             "split_sketch": split,
             "cli": cli,
@@ -1861,11 +1887,12 @@ def main():
             "kernel_roofline": per_kernel_roof,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "parity": parity_summary(c2par, c3, c4, c5, cli, split, c4g, cli_fp),
+            "parity": parity_summary(c2par, c3, c4, c5, cli, split, c4g, cli_fp, comm_chk),
         }
         path = write_detail(detail, args.detail)
         print(json.dumps(compact_line(detail, path)))
     job.free()
+    grp.close()
     ctx.close()
 
 

@@ -439,6 +439,12 @@ struct TimedLaunch {
     }
 };
 
+// errors of fpm_comm.cpp, reported through the same fpm_last_error() text
+__attribute__((visibility("hidden"))) int fpm_detail_fail(int code, const std::string &msg)
+{
+    return fail(code, msg);
+}
+
 static int set_device(fpm_ctx *ctx)
 {
     if (!ctx) return fail(FPM_EINVAL, "null context");

@@ -150,7 +150,13 @@ SYMBOLS = [
     ("fpm_seq_free", None, [vp]),
     ("fpm_host_alloc", C.c_int, [vp, C.POINTER(vp), C.c_size_t]),
     ("fpm_host_free", C.c_int, [vp, vp]),
+    ("fpm_comm_unique_id", C.c_int, [C.c_char_p]),
+    ("fpm_comm_create", C.c_int, [vp, C.c_int, C.c_int, C.c_char_p, C.POINTER(vp)]),
+    ("fpm_comm_destroy", None, [vp]),
+    ("fpm_comm_all_gather", C.c_int, [vp, vp, vp, C.c_size_t, vp]),
+    ("fpm_sketch_min_merge_comm", C.c_int, [vp, vp, vp, C.c_uint32, vp, vp, vp]),
 ]
+COMM_ID_BYTES = 128
 
 
 class CellListStruct(C.Structure):
@@ -422,6 +428,41 @@ class SketchJob:
             self.free()
         except Exception:
             pass
+
+
+def comm_unique_id() -> bytes:
+    """fpm_comm_unique_id: the 128-byte RCCL unique id one rank makes and the others receive
+    over a host channel (bench.Group broadcasts it over gloo)."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(lib().fpm_comm_unique_id(buf))
+    return buf.raw
+
+
+class Comm:
+    """fpm_comm: an RCCL communicator on the context's device and HIP runtime (the library's
+    own), for the cross-GPU min-merge.  Blocks in the constructor until all nranks ranks
+    have joined with the same id."""
+
+    def __init__(self, ctx, nranks, rank, uid: bytes):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("RCCL unique id must be 128 bytes")
+        h = vp()
+        _check(lib().fpm_comm_create(ctx.h, int(nranks), int(rank), uid, C.byref(h)))
+        self.h, self.ctx, self.nranks, self.rank = h.value, ctx, int(nranks), int(rank)
+
+    def all_gather(self, d_send, d_recv, nbytes, stream=None):
+        _check(lib().fpm_comm_all_gather(self.h, d_send, d_recv, int(nbytes), stream))
+
+    def min_merge(self, d_row, d_count, s, d_out, d_out_count, stream=None):
+        """fpm_sketch_min_merge_comm: every rank's bottom-s row gathered and merged on the
+        device (enqueued on the stream)"""
+        _check(lib().fpm_sketch_min_merge_comm(self.h, d_row, d_count, int(s), d_out,
+                                               d_out_count, stream))
+
+    def close(self):
+        if self.h:
+            lib().fpm_comm_destroy(self.h)
+            self.h = None
 
 
 class Context:

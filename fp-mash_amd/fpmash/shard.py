@@ -1,10 +1,14 @@
-"""Multi-GPU sharding of one sketch + dist job.
+"""Multi-GPU sharding of one sketch + dist job (configs C4 / C5 and a split
+genome).  One process per GPU, no exchange in the C4 / C5 data paths:
 
-One process per GPU.  Sequences (and so sketches) are split into contiguous shards;
-every rank sketches its shard, the sketch rows are all-gathered (RCCL over xGMI with
-the "nccl" backend, gloo on CPU in the tests) so each GPU holds the whole reference set,
-and each rank computes its own query rows against all references.  The gather is the
-only exchange; the dist rows of different ranks are independent.
+* C4 (all-vs-all dist): the set is cut into contiguous row blocks and the grid is dealt as
+  unordered block pairs (pair_block_jobs); every rank sketches the rows its pairs read from
+  the inputs it holds, so no sketch row crosses GPUs.
+* C5 (one sketch per genome file): contiguous file ranges per rank; the finished sketches are
+  reassembled in file order on rank 0 on the host (all_gather_rows over gloo).
+* One sketch split over GPUs (a genome's k-mer ranges, kmer_shard): the bottom-s rows are
+  min-merged through RCCL inside libfpmash (min_merge with an fpmash.Comm) -- the one
+  collective north_star names ("the final min-merge").
 """
 from __future__ import annotations
 
@@ -16,8 +20,8 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
 
 def all_gather_rows(local, n_total: int, world: int, group=None, bounds=None, out=None,
                     async_op: bool = False):
-    """Concatenate every rank's `local` rows (a [n_local, w] tensor, any dtype) in rank
-    order.  Shards may differ in size (`bounds`: each rank's [lo, hi), default
+    """Concatenate every rank's `local` rows (a [n_local, w] host tensor over gloo, any dtype)
+    in rank order (the C5 leg's ordered reassembly of per-file sketches on rank 0).  Shards may differ in size (`bounds`: each rank's [lo, hi), default
     shard_range): each is padded to the largest before the collective and the padding is
     dropped afterwards.  `out`: a preallocated [n_total, w] tensor to write into (its storage
     stays put across calls, so device pointers into it stay valid).  async_op: the
@@ -108,51 +112,41 @@ def kmer_shard(length: int, k: int, world: int, rank: int) -> tuple[int, int]:
     return a, (b + k - 1 if b > a else a)
 
 
-def min_merge(ctx, d_row: int, d_count: int, s: int, world: int, group=None, device=None):
-    """The cross-GPU min-merge of one sketch computed in parts: every rank's bottom-s row
-    (device pointers: s u64 hashes + a u32 count) is all-gathered (RCCL over xGMI with an
-    "nccl" group, or host tensors over gloo when `device` is None) and merged on the device
-    with fpm_sketch_merge_dev (MinHashHeap.cpp:68-146: the s smallest distinct of a union are
-    the s smallest of the union of the parts' s smallest).  Returns (hashes, count) as host
-    arrays."""
+def min_merge(ctx, d_row: int, d_count: int, s: int, world: int, comm=None, group=None):
+    """The cross-GPU min-merge of one sketch computed in parts (north_star: RCCL "for the final
+    min-merge"): every rank's bottom-s row (device pointers: s u64 hashes + a u32 count) is
+    merged with every other rank's (MinHashHeap.cpp:68-146: the s smallest distinct of a union
+    are the s smallest of the union of the parts' s smallest).  With `comm` (fpmash.Comm) the
+    rows are all-gathered by RCCL over xGMI inside libfpmash and merged on the device on the
+    context stream (fpm_sketch_min_merge_comm: no host step between them); without it (ranks
+    sharing one GPU in the tests and rehearsals, where RCCL refuses two ranks per device) the
+    rows go through the gloo `group` as host tensors and are merged by fpm_sketch_merge_dev.
+    Returns (hashes, count) as host arrays."""
     import numpy as np
-    import torch
-    import torch.distributed as dist
 
     import fpmash
     L = fpmash.lib()
-    dev = device if device is not None else torch.device("cpu")
-    row = torch.zeros((1, s + 1), dtype=torch.int64, device=dev)   # hashes, then the count
-    if device is not None:
-        # the zero fill ran on torch's stream; ctx's stream is non-blocking and unordered
-        # with it, so the fill must finish before the copies below land in `row`
-        torch.cuda.synchronize(dev)
-        fpmash._check(L.fpm_memcpy_d2d(ctx.h, row.data_ptr(), d_row, s * 8))
-        fpmash._check(L.fpm_memcpy_d2d(ctx.h, row.data_ptr() + s * 8, d_count, 4))
-        ctx.synchronize()
+    out = fpmash.DeviceBuffer(ctx, s * 8)
+    oc = fpmash.DeviceBuffer(ctx, 4)
+    if comm is not None:
+        comm.min_merge(d_row, d_count, s, out.ptr, oc.ptr)
     else:
-        fpmash._check(L.fpm_memcpy_d2h(ctx.h, row.data_ptr(), d_row, s * 8))
+        import torch
+        import torch.distributed as dist
+        row = np.zeros((1, s + 1), np.int64)                       # hashes, then the count
+        fpmash._check(L.fpm_memcpy_d2h(ctx.h, row.ctypes.data, d_row, s * 8))
         c = np.zeros(1, np.uint32)
         fpmash._check(L.fpm_memcpy_d2h(ctx.h, c.ctypes.data, d_count, 4))
         row[0, s] = int(c[0])
-    parts = [torch.empty_like(row) for _ in range(world)]
-    dist.all_gather(parts, row, group=group)
-    allr = torch.cat(parts, dim=0)                                   # [world, s + 1]
-    if device is None:
-        allr_np = allr.numpy()
-        rows = fpmash.DeviceBuffer.from_array(ctx, np.ascontiguousarray(allr_np[:, :s]))
-        cnts = fpmash.DeviceBuffer.from_array(ctx, allr_np[:, s].astype(np.uint32))
-        rp, cp = rows.ptr, cnts.ptr
-    else:
-        rows_t = allr[:, :s].contiguous()
-        cnts_t = allr[:, s].to(torch.int32).contiguous()
-        torch.cuda.synchronize(dev)
-        rp, cp = rows_t.data_ptr(), cnts_t.data_ptr()
-    out = fpmash.DeviceBuffer(ctx, s * 8)
-    oc = fpmash.DeviceBuffer(ctx, 4)
-    fpmash._check(L.fpm_sketch_merge_dev(ctx.h, rp, cp, world, s, out.ptr, oc.ptr, None))
-    ctx.synchronize()
-    n = int(oc.to_array(np.uint32, 1)[0])
+        t = torch.from_numpy(row)
+        parts = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+        allr = torch.cat(parts, dim=0).numpy()                       # [world, s + 1]
+        rows = fpmash.DeviceBuffer.from_array(ctx, np.ascontiguousarray(allr[:, :s]))
+        cnts = fpmash.DeviceBuffer.from_array(ctx, allr[:, s].astype(np.uint32))
+        fpmash._check(L.fpm_sketch_merge_dev(ctx.h, rows.ptr, cnts.ptr, world, s, out.ptr,
+                                             oc.ptr, None))
+    n = int(oc.to_array(np.uint32, 1)[0])        # (ordered after the merge on the stream)
     h = out.to_array(np.uint64, s)[:n]
     out.free()
     oc.free()

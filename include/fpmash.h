@@ -446,6 +446,32 @@ int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_le
                            uint32_t *out_numer, uint32_t *out_denom, double *out_dist,
                            double *out_pvalue, uint8_t *out_pass);
 
+/* ---- communicator: RCCL over xGMI for the cross-GPU min-merge ------------------------
+ * north_star reserves the collective for "the final min-merge only where the reference set
+ * exceeds one GPU's HBM" (or one sketch is split over GPUs).  The reference has no collective:
+ * one process, one pthreads pool (ThreadPool.h:13-61) feeding one MinHashHeap per genome
+ * (Sketch.cpp:1354-1422).  The communicator lives on the context's device and HIP runtime
+ * (librccl is dlopen'ed on first use); the caller carries the 128-byte unique id from one rank
+ * to the others over any host channel (ncclGetUniqueId / ncclCommInitRank's contract). */
+#define FPM_COMM_ID_BYTES 128
+typedef struct fpm_comm fpm_comm;
+int fpm_comm_unique_id(uint8_t id[FPM_COMM_ID_BYTES]);
+/* blocks until all nranks ranks have called it with the same id */
+int fpm_comm_create(fpm_ctx *ctx, int nranks, int rank, const uint8_t id[FPM_COMM_ID_BYTES],
+                    fpm_comm **out);
+void fpm_comm_destroy(fpm_comm *comm);
+/* every rank's `bytes` of d_send, in rank order, into d_recv (nranks x bytes), enqueued on
+ * `stream` (NULL: the context stream) */
+int fpm_comm_all_gather(fpm_comm *comm, const void *d_send, void *d_recv, size_t bytes,
+                        void *stream);
+/* The min-merge of one sketch computed in parts (MinHashHeap.cpp:68-146: the s smallest
+ * distinct of a union = the s smallest of the union of the parts' s smallest): every rank's
+ * ascending bottom-s row (s hashes, d_count valid) all-gathered into library buffers and merged
+ * on the device (fpm_sketch_merge_dev) into d_out / d_out_count on every rank; enqueued on
+ * `stream` (NULL: the context stream). */
+int fpm_sketch_min_merge_comm(fpm_comm *comm, const uint64_t *d_row, const uint32_t *d_count,
+                              uint32_t s, uint64_t *d_out, uint32_t *d_out_count, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

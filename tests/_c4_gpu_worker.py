@@ -1,8 +1,8 @@
 """Worker for test_multirank.test_c4_leg_ranks_one_gpu (-m gpu): bench.c4_leg, the C4 job
-(sketch own block -> all-gather of the sketch rows -> this rank's block pairs of the all-vs-all
+(sketch the rows its block pairs read -> this rank's block pairs of the all-vs-all
 grid, fpmash.shard.pair_block_jobs: own block on the symmetric self path, the other block
 pairs as a grid + its transpose through fpm_refset_dist_mirror_dev), on WORLD_SIZE ranks that
-share the one visible GPU through libfpmash, with the rows gathered over gloo.  Every rank
+share the one visible GPU through libfpmash.  Every rank
 checks sampled rows of each of its grids and transposes against the oracle."""
 import json
 import os
@@ -11,6 +11,10 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "fp-mash_amd")):
     sys.path.insert(0, p)
+
+# every rank on device 0: no RCCL communicator (it refuses two ranks per device), min-merges
+# over gloo (bench.Group.comm)
+os.environ["FPMASH_BENCH_ONE_DEVICE"] = "1"
 
 import bench  # noqa: E402
 import fpmash  # noqa: E402

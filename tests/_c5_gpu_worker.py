@@ -13,6 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "fp-mash_amd")):
     sys.path.insert(0, p)
 
+# every rank on device 0: no RCCL communicator (it refuses two ranks per device), min-merges
+# over gloo (bench.Group.comm)
+os.environ["FPMASH_BENCH_ONE_DEVICE"] = "1"
+
 import bench  # noqa: E402
 import fpmash  # noqa: E402
 

@@ -48,9 +48,9 @@ def test_shard_gather_two_ranks():
 @pytest.mark.parametrize("ws", [2, 3])
 def test_c4_leg_ranks_one_gpu(ws):
     """bench.c4_leg at world size 2 and 3 through libfpmash (all ranks on the one visible GPU,
-    rows gathered over gloo): every rank's grids and transposes (block pairs, including the
-    half-block split of even world sizes) match the oracle, and the ranks' cells add up to the
-    whole n x n grid."""
+    each sketching the rows its block pairs read, no collective): every rank's grids and
+    transposes (block pairs, including the half-block split of even world sizes) match the
+    oracle, and the ranks' cells add up to the whole n x n grid."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={ws}",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
            os.path.join(ROOT, "tests", "_c4_gpu_worker.py")]
@@ -66,27 +66,30 @@ def test_c4_leg_ranks_one_gpu(ws):
 
 
 @pytest.mark.gpu
-def test_c4_gathered_path_nccl_one_gpu():
-    """The on-device multi-GPU data path, run on the one GPU with a one-rank RCCL group
-    (tests/_c4_nccl_worker.py): the C4 leg's all-gather into torch tensors over RCCL, block
-    indexes and self / mirror compares on those torch-allocated pointers (2 and 3 virtual
-    blocks: the even split's half blocks too), every grid and transpose row sampled against
-    the oracle and the cells adding up to the whole grid; and shard.min_merge with device=."""
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1",
-           "--master-addr", "127.0.0.1", "--master-port", str(free_port()),
-           os.path.join(ROOT, "tests", "_c4_nccl_worker.py")]
+def test_vblocks_and_comm_one_gpu():
+    """The N > 1 paths on the one GPU (tests/_vblocks_comm_worker.py): C4 with 2 and 3 virtual
+    blocks (self / mirror jobs on locally sketched rows, no collective; every grid and transpose
+    row sampled against the oracle; the cells add up to the whole grid), rank 3 of an N = 4
+    run alone (it sketches its own block and the blocks it is paired with), and the RCCL
+    min-merge inside libfpmash on a one-rank communicator against the oracle."""
+    cmd = [sys.executable, os.path.join(ROOT, "tests", "_vblocks_comm_worker.py")]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=240)
     assert p.returncode == 0, p.stderr[-3000:]
     res = [json.loads(l.split(" ", 1)[1]) for l in p.stdout.splitlines()
-           if l.startswith("C4NCCL ")]
+           if l.startswith("VBCOMM ")]
     assert len(res) == 1
     r = res[0]
     for vb, c in r["c4"].items():
-        assert c["collective"] == "all_gather (nccl = RCCL)", c
+        assert c["collective"] is None, c
         assert c["cells"] == c["pairs"], (vb, c)
         assert c["parity"]["ok"] and c["parity"]["pairs_sharing"] > 0, (vb, c)
         assert any(j["kind"] == "mirror" for j in c["jobs"])
-    assert r["min_merge_ok"]
+    sh = r["share"]
+    assert sh["parity"]["ok"] and sh["parity"]["pairs_sharing"] > 0, sh
+    # rank 3 of 4: its block, block 0 (the cyclic next, (ws - 1) // 2 = 1 block) and the
+    # even split's second index of block 1 against its own second half
+    assert sh["rows_owned"] == 1000 and sh["rows_sketched"] == 3000, sh
+    assert r["comm"]["ok"], r["comm"]
 
 
 @pytest.mark.gpu
