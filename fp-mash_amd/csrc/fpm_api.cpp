@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <string>
+#include <system_error>
 #include <vector>
 
 using namespace fpm;
@@ -89,8 +90,14 @@ class CopyPool {
         const unsigned want = (unsigned)std::min<size_t>(kMaxThreads + 1, n / kPart);
         if (want <= 1) { memcpy(dst, src, n); return; }
         std::unique_lock<std::mutex> lk(mu_);
-        while (th_.size() + 1 < want && th_.size() < threads())
-            th_.emplace_back([this] { work(); });
+        while (th_.size() + 1 < want && th_.size() < threads()) {
+            // (at the process's thread limit: fewer parts, never an exception through the C ABI)
+            try {
+                th_.emplace_back([this] { work(); });
+            } catch (const std::system_error &) {
+                break;
+            }
+        }
         const unsigned parts = (unsigned)std::min<size_t>(want, th_.size() + 1);
         const size_t per = (n + parts - 1) / parts;
         char *d = static_cast<char *>(dst);
@@ -784,6 +791,9 @@ struct fpm_sketch_job {
     // a-priori sample bounds (d_thr[n_slots ..]): a sample left short is redone unbounded
     bool sbounded = false;
     uint32_t *d_sshort = nullptr;           // count, then the slots
+    uint64_t *d_sbound0 = nullptr;          // the a-priori sample bounds as staged: restored
+                                            // into d_thr at every run (a short sample's redo
+                                            // lifts its bound in d_thr)
     std::vector<TileDesc> h_stiles;         // the sample tiles by class (sclass_begin)
     std::vector<uint32_t> h_ssel_tag;       // each sample selection's slot
     int32_t last_sample_short = -1;
@@ -804,7 +814,7 @@ static void job_release(fpm_sketch_job *j)
     (void)hipFree(j->d_redo); (void)hipFree(j->d_redo_n);
     (void)hipFree(j->d_kt); (void)hipFree(j->d_slot_group); (void)hipFree(j->d_short);
     (void)hipFree(j->d_thr_safe); (void)hipFree(j->d_rtiles); (void)hipFree(j->d_rsel);
-    (void)hipFree(j->d_sshort);
+    (void)hipFree(j->d_sshort); (void)hipFree(j->d_sbound0);
     (void)hipFree(j->d_sel); (void)hipFree(j->d_sel_rows); (void)hipFree(j->d_sel_failed);
     (void)hipFree(j->d_fmerge);
     (void)hipFree(j->d_sfmerge);
@@ -1271,6 +1281,7 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
             job->h_ssel_tag = ssel_tag;
             job->last_sample_short = 0;
             alloc((void **)&job->d_sshort, (srow.size() + 1) * sizeof(uint32_t));
+            alloc((void **)&job->d_sbound0, srow.size() * sizeof(uint64_t));
         }
     }
     {
@@ -1339,6 +1350,8 @@ static int stage_core(fpm_ctx *ctx, const fpm_sketch_params *p, StageRecords &R,
         e = copy_in(ctx, job->d_sel_rows, sel_rows.data(), sel_rows.size() * sizeof(uint32_t));
     if (e == hipSuccess && !sbound.empty())
         e = copy_in(ctx, job->d_thr + srow.size(), sbound.data(), sbound.size() * sizeof(uint64_t));
+    if (e == hipSuccess && job->d_sbound0)
+        e = copy_in(ctx, job->d_sbound0, sbound.data(), sbound.size() * sizeof(uint64_t));
     if (e == hipSuccess && !kt.empty())
         e = copy_in(ctx, job->d_kt, kt.data(), kt.size() * sizeof(uint32_t));
     if (e == hipSuccess && !slot_group.empty())
@@ -1533,6 +1546,9 @@ int fpm_sketch_run(fpm_sketch_job *job, void *stream)
         HIP_TRY(hipMemsetAsync(job->d_sel_failed, 0, (job->n_ssel + job->n_sel + 2) * sizeof(uint32_t),
                                st));
     if (job->n_slots) {   // sample pass of long groups -> per-group hash bounds
+        if (job->sbounded)   // the bounds as staged (a previous run's redo lifted some)
+            HIP_TRY(hipMemcpyAsync(job->d_thr + job->n_slots, job->d_sbound0,
+                                   job->n_slots * sizeof(uint64_t), hipMemcpyDeviceToDevice, st));
         if (int rc = tiles_pass(job->d_stiles, job->sclass_begin, false)) return rc;
         if (job->n_ssel) {
             for (size_t l = 0; l + 1 < job->ssel_begin.size(); l++) {
@@ -1664,6 +1680,13 @@ int fpm_sketch_job_short_groups(fpm_sketch_job *job, int32_t *n_short)
 {
     if (!job || !n_short) return fail(FPM_EINVAL, "null argument");
     *n_short = job->last_short;
+    return FPM_OK;
+}
+
+int fpm_sketch_job_sample_short(fpm_sketch_job *job, int32_t *n_short)
+{
+    if (!job || !n_short) return fail(FPM_EINVAL, "null argument");
+    *n_short = job->sbounded ? job->last_sample_short : -1;
     return FPM_OK;
 }
 
@@ -3042,8 +3065,12 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
     }
     if (int rc = compare_impl(ctx, d_ref, d_ref_len, ref_stride, n_ref, d_qry, d_qry_len,
                               qry_stride, n_qry, hash_bytes, sketch_size, out.cnt, stream, &fin,
-                              &finalized, rs))
+                              &finalized, rs)) {
+        // an error before the compare ordered itself after a taken-over prefill: the side
+        // stream may still be writing the caller's counts, so wait for it before returning
+        if (prefilled) (void)hipEventSynchronize(ctx->ev_prefill);
         return rc;
+    }
     // the transposed grid, when the compare could not scatter it (dense path, unsorted lists:
     // their literal walk is not symmetric): the swapped call, ref and query sets exchanged
     auto mirror_swapped = [&]() -> int {

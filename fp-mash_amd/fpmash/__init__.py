@@ -82,6 +82,7 @@ SYMBOLS = [
     ("fpm_sketch_job_info", C.c_int, [vp, u64p, u64p, u64p]),
     ("fpm_sketch_job_redo_tiles", C.c_int, [vp, C.POINTER(C.c_int32)]),
     ("fpm_sketch_job_short_groups", C.c_int, [vp, C.POINTER(C.c_int32)]),
+    ("fpm_sketch_job_sample_short", C.c_int, [vp, C.POINTER(C.c_int32)]),
     ("fpm_sketch_job_free", None, [vp]),
     ("fpm_fp_hash_lines", C.c_int, [vp, u64p, u64p, C.c_uint64, C.c_uint32, C.c_uint32, vp]),
     ("fpm_fp_hash_lines_dev", C.c_int, [vp, vp, vp, C.c_uint64, C.c_uint32, C.c_uint32, vp,
@@ -395,6 +396,13 @@ class SketchJob:
         the tight bound left them short (-1: no tight bounds in this job)"""
         n = C.c_int32()
         _check(lib().fpm_sketch_job_short_groups(self.h, C.byref(n)))
+        return n.value
+
+    def sample_short(self):
+        """samples of the last run() the a-priori sample bound left short, redone unbounded
+        (-1: the job's samples carry no such bound)"""
+        n = C.c_int32()
+        _check(lib().fpm_sketch_job_sample_short(self.h, C.byref(n)))
         return n.value
 
     def device_output(self):

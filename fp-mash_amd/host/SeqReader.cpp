@@ -146,6 +146,11 @@ bool gunzipImage(const unsigned char *p, size_t n, std::string &image)
     }
     void *dec = D.alloc();
     if (!dec) return false;
+    // released on every path out, the bad_alloc below included
+    struct DecGuard {
+        const Deflate &lib; void *d;
+        ~DecGuard() { lib.free_(d); }
+    } guard{D, dec};
     image.clear();
     size_t at = 0;
     bool ok = true;
@@ -160,7 +165,6 @@ bool gunzipImage(const unsigned char *p, size_t n, std::string &image)
         if (!gunzipMember(dec, p + at, n - at, image, hint + 1, &used)) { ok = false; break; }
         at += used;
     }
-    D.free_(dec);
     return ok;
     } catch (const std::bad_alloc &) {
         // (the caller falls back to zlib's gzread, which grows the image as it inflates)

@@ -180,6 +180,11 @@ int fpm_sketch_job_redo_tiles(fpm_sketch_job *job, int32_t *n_redo);
  * either way (MinHashHeap.cpp:68-146).  -1 when the job has no tight bounds (no long
  * groups, or s beyond the one-workgroup selection). */
 int fpm_sketch_job_short_groups(fpm_sketch_job *job, int32_t *n_short);
+/* Samples of the last fpm_sketch_run that the a-priori sample bound (~1.25 s + 16 sqrt s of
+ * the sample's windows below it) left with fewer than s distinct hashes and that were redone
+ * unbounded (a test hook, like the two above; every run starts from the staged bounds).  -1
+ * when the job's samples carry no a-priori bound. */
+int fpm_sketch_job_sample_short(fpm_sketch_job *job, int32_t *n_short);
 void fpm_sketch_job_free(fpm_sketch_job *job);
 
 /* Bottom-s of the union of n_lists sketches (device rows of stride s, ascending and

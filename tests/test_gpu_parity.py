@@ -687,9 +687,11 @@ def test_sketch_survivors_kernel_redo(ctx, oracle, kind):
     P = fpmash.make_params(k=21, s=1000)
     job = ctx.sketch_job(P, [seq], groups=[0], n_groups=1)
     try:
+        n_ss = []
         for _ in range(2):                      # the count is reset by every run
             job.run(ctx.stream)
             n_redo = job.redo_tiles()
+            n_ss.append(job.sample_short())
             if kind == "random":
                 assert n_redo == 0
                 assert job.short_groups() == 0  # the tight bound held
@@ -698,6 +700,9 @@ def test_sketch_survivors_kernel_redo(ctx, oracle, kind):
                 # the sample holds all ~3,000 distinct k-mers: its kt-th smallest leaves the
                 # group ~160 of them, so the group is redone under the s-th smallest
                 assert job.short_groups() == 1
+        # every run starts from the staged a-priori sample bounds (a redo lifts them in the
+        # run's bound array only): the same samples are found short on the second run
+        assert n_ss[0] == n_ss[1] and n_ss[0] == (0 if kind == "random" else 1), n_ss
         rows, cnt = job.fetch()
     finally:
         job.free()
