@@ -411,7 +411,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     uint32_t *const K32 = sKB.k;
     uint64_t *const Bs = sKB.v;
     __shared__ uint16_t Bkt[kBuckets + 1];             // Bkt[b] = #{B < b << shift}
-    __shared__ uint32_t s_maxn, s_keydup;
+    __shared__ uint32_t s_maxn, s_keydup, s_unsorted;
     // rows [q_lo, q_lo + n_qry) of the grid (a part of the rows, whose probe ran before)
     const uint32_t qr = xcd_row(blockIdx.x, n_qry);
     if (qr >= n_qry) return;
@@ -423,7 +423,7 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lb = qry_len[q];
     const uint64_t *B = qry + (uint64_t)q * qry_stride;
-    if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; }
+    if (threadIdx.x == 0) { s_maxn = 0; s_keydup = 0; s_unsorted = 0; }
     {
         // stage B: every load of the row issued before the first LDS store (4 in flight per
         // thread: CAP / 256 with CAP 1024; a serial load-store loop paid the global latency
@@ -458,13 +458,14 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // and the bucket directory: bucket b = values [b << shift, (b + 1) << shift) = B
     // positions [Bkt[b], Bkt[b + 1]).  Element j owns the buckets after its predecessor's
     // bucket up to its own, so each thread fills one gap.
-    uint32_t dup = 0;
+    uint32_t dup = 0, uns = 0;
     for (uint32_t j = threadIdx.x; j <= lb; j += blockDim.x) {
         const uint64_t v = j < lb ? Bs[j] : 0, vp = j > 0 ? Bs[j - 1] : 0;
         if (j < lb) {
             const uint32_t k = (uint32_t)(v >> kshift);
             K32[j] = k;
             dup |= (j > 0 && (uint32_t)(vp >> kshift) == k) | (k == 0xFFFFFFFFu);
+            uns |= j > 0 && !(vp < v);
         }
         const uint32_t bj = j < lb ? (uint32_t)(v >> shift) : top + 1;
         const uint32_t bp = j > 0 ? (uint32_t)(vp >> shift) + 1 : 0;
@@ -473,7 +474,12 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     // the directory past top + 1 (HI rows read it unclamped; top >= 2^(kLogBuckets - 1))
     for (uint32_t b = top + 2 + threadIdx.x; b <= kBuckets; b += blockDim.x) Bkt[b] = (uint16_t)lb;
     if (dup) s_keydup = 1;
+    if (uns) s_unsorted = 1;
     __syncthreads();
+    // a row that is not strictly ascending (a rank kernel enqueued before the probe's
+    // sortedness flag was read, fpm_api.cpp; its results are then dropped): nothing to rank,
+    // and its directory would not bound the bucket loop below
+    if (s_unsorted) return;
     // the largest bucket: element j is the (j - Bkt[bucket(j)] + 1)-th of its bucket
     uint32_t mx = 0;
     for (uint32_t j = threadIdx.x; j < lb; j += blockDim.x)

@@ -32,9 +32,18 @@
 namespace fpm {
 
 constexpr uint32_t kParts = 1u << kIdxL1;    // level-1 partitions (top 10 key bits)
+// Bucket ref-id ranges (the directory's second half, idx_minspan): (min id << 8) | (max - min)
+// of the bucket's entries when max - min < kSpanUnknown, else kSpanUnknown (unknown / empty).
+// The probe skips reading a bucket whose whole range is already marked in its row bitmap:
+// every entry's ref is then marked whatever the entry holds, so the candidates are the same.
+// Sketches of related sequences (a family's members, adjacent ids) share most of their
+// hashes, so after the first of a row's hashes mark the family, most buckets are covered.
+constexpr uint32_t kSpanUnknown = 0xFF;
 // posting events in flight per lane in the probe (4: 0.307 ms, 12 without the 8-wave cap
-// 0.339 ms, against 0.298-0.301 ms at 8)
-#define PROBE_KU 8
+// 0.339 ms, against 0.298-0.301 ms at 8, before the covered-bucket skip)
+#ifndef PROBE_KU
+#define PROBE_KU 4
+#endif
 
 __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_bytes, uint64_t idx)
 {
@@ -508,6 +517,22 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         for (int w = 0; w < kBucketThreads / 64; w++) t += wsq[w];
         if (t) atomicAdd(&sqsum[1 + ((p * ns + j) & 63)], t);
     }
+    // each bucket's ref-id range (idx_minspan): from the placed entries in LDS, sub-bucket d
+    // holding out[sh[d - 1], sh[d]) once every entry is placed (sh[d] = its end)
+    uint32_t *const minspan = dir + ((uint64_t)1 << g.nbits) + 1 + ((uint64_t)p << g.l2) + lo;
+    const uint32_t rmask = (1u << g.rbits) - 1;
+    auto write_minspan = [&]() {
+        for (uint32_t d = threadIdx.x; d < nsb; d += kBucketThreads) {
+            const uint32_t a = d ? sh[d - 1] : 0u, e = sh[d];
+            uint32_t mn = 0xFFFFFFFFu, mx = 0;
+            for (uint32_t i = a; i < e; i++) {
+                const uint32_t r = out[i] & rmask;
+                mn = min(mn, r);
+                mx = max(mx, r);
+            }
+            minspan[d] = e > a && mx - mn < kSpanUnknown ? (mn << 8) | (mx - mn) : kSpanUnknown;
+        }
+    };
     if (in_reg) {
 #pragma unroll
         for (int u = 0; u < kBucketPer; u++)
@@ -517,6 +542,7 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
             }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < s1 - s0; i += kBucketThreads) entries[s0 + i] = out[i];
+        write_minspan();
         return;
     }
     // the range through LDS when it fits (tot is block-uniform), else straight to `entries`
@@ -540,9 +566,14 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
                 }
             }
     }
-    if (!lds) return;
+    if (!lds) {
+        // (the entries went straight to global memory: no ranges, the probe reads these buckets)
+        for (uint32_t d = threadIdx.x; d < nsb; d += kBucketThreads) minspan[d] = kSpanUnknown;
+        return;
+    }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kBucketThreads) entries[base + i] = out[i];
+    write_minspan();
 }
 
 // ---- exclusive scan of u32 counts (n <= 2^31), three launches ----
@@ -696,7 +727,7 @@ void probe_rows_kernel(
     C *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg,
     const uint32_t *__restrict__ qry_it_len, uint32_t *__restrict__ q_unsorted,
-    unsigned long long *__restrict__ events)
+    unsigned long long *__restrict__ events, uint64_t cap, uint32_t *__restrict__ cand_over)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
     __shared__ uint32_t wsum[4];
@@ -742,13 +773,14 @@ void probe_rows_kernel(
     const uint64_t rowoff = (uint64_t)q * stride;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t rmask = (uint32_t)((1ULL << g.rbits) - 1);
+    const uint32_t *__restrict__ minspan = dir + ((uint64_t)1 << g.nbits) + 1;
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
     // loaded together (their global loads overlap) before the batches are expanded
     constexpr int kB = 4;
     uint64_t ev_w = 0;      // this wave's posting events (with `events`)
     uint32_t uns = 0;       // an out-of-order or repeated value in the row (with `q_unsorted`)
     for (uint32_t jb = wave * 64; jb < lit; jb += 256 * kB) {
-        uint32_t st_b[kB], cnt_b[kB], tgt_b[kB];
+        uint32_t st_b[kB], cnt_b[kB], tgt_b[kB], ms_b[kB];
 #pragma unroll
         for (int bi = 0; bi < kB; bi++) {
             const uint32_t j = jb + 256 * bi + lane;
@@ -765,11 +797,36 @@ void probe_rows_kernel(
             st_b[bi] = d0;
             cnt_b[bi] = self_set && d1 - d0 == 1 ? 0u : d1 - d0;
             tgt_b[bi] = key_fp(K, g, mult);
+            ms_b[bi] = j < lit && d1 - d0 > 1 ? minspan[b] : kSpanUnknown;
         }
 #pragma unroll
       for (int bi = 0; bi < kB; bi++) {
         if (jb + 256 * bi >= lit) break;                  // wave-uniform
-        const uint32_t st = st_b[bi], cnt = cnt_b[bi], tgt = tgt_b[bi];
+        const uint32_t st = st_b[bi], tgt = tgt_b[bi];
+        uint32_t cnt = cnt_b[bi];
+        if (events) {
+            // the posting events of the row's hashes, read or not (the caller's measure of the
+            // rank work, fpm_ctx_last_dist_stats)
+            uint32_t t = cnt;
+#pragma unroll
+            for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d, 64);
+            ev_w += t;
+        }
+        {
+            // a bucket whose entries' refs are all marked already adds nothing: not read
+            const uint32_t span = ms_b[bi] & 0xFFu, mn = ms_b[bi] >> 8;
+            if (cnt && span != kSpanUnknown && mn >= r0 && mn + span < r1) {
+                const uint32_t a = mn - r0, e = a + span;
+                bool cov = true;
+                for (uint32_t w = a >> 5; cov && w <= (e >> 5); w++) {
+                    const uint32_t lo_b = w == (a >> 5) ? (a & 31u) : 0u;
+                    const uint32_t hi_b = w == (e >> 5) ? (e & 31u) : 31u;
+                    const uint32_t m = (hi_b == 31u ? ~0u : ((2u << hi_b) - 1u)) & ~((1u << lo_b) - 1u);
+                    cov = (rowbits[w] & m) == m;
+                }
+                if (cov) cnt = 0;
+            }
+        }
         uint32_t inc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -777,7 +834,6 @@ void probe_rows_kernel(
             if ((int)lane >= d) inc += y;
         }
         const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
-        ev_w += total;
         // same wave writes and reads these slots: LDS ops of one wave complete in order.
         // Event ev of hash m reads entries[st_m + ev - pre_m] = entries[base_m + ev] (u32
         // arithmetic wraps consistently).
@@ -850,13 +906,19 @@ void probe_rows_kernel(
     for (uint32_t w = 0; w < 4; w++) { if (w < wave) wpre += wsum[w]; tot += wsum[w]; }
     if (threadIdx.x == 0) {
         row_base = tot ? atomicAdd(n_cand, (unsigned long long)tot) : 0ULL;
+        // past the candidate buffer (a call enqueued before its posting events were known,
+        // fpm_api.cpp's speculated probe): nothing written, the row flagged and left empty
+        const bool over = row_base + tot > cap;
+        if (over) atomicOr(cand_over, 1u);
         // (offset << 24 | count) of this row's candidates; one ref chunk per row here
-        if (gridDim.y == 1) row_seg[q] = (row_base << 24) | (tot & 0xFFFFFF);
+        if (gridDim.y == 1) row_seg[q] = (row_base << 24) | (over ? 0u : (tot & 0xFFFFFF));
+        if (over) row_base = ~0ULL;
     }
     __syncthreads();
+    const bool dropped = row_base == ~0ULL;
     uint64_t pos = row_base + wpre + x - mycnt;
     const uint64_t pair_row = (uint64_t)q * n_ref;
-    for (uint32_t w = threadIdx.x; w < nwords; w += 256) {
+    for (uint32_t w = threadIdx.x; !dropped && w < nwords; w += 256) {
         uint32_t b = rowbits[w] & word_mask(w);
         const uint64_t bit0 = pair_row + r0 + (uint64_t)w * 32;
         while (b) {
@@ -1179,7 +1241,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
-                             unsigned long long *events, hipStream_t st, uint32_t q_lo)
+                             unsigned long long *events, uint64_t cap, uint32_t *cand_over,
+                             hipStream_t st, uint32_t q_lo)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -1197,7 +1260,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                        cref,                                                                     \
                        d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
                        (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg, \
-                       d_qry_it_len, q_unsorted, events)
+                       d_qry_it_len, q_unsorted, events, cap, cand_over)
     if (cnt.c16) FPM_PROBE(uint16_t);
     else FPM_PROBE(uint32_t);
 #undef FPM_PROBE

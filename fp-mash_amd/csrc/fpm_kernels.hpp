@@ -227,7 +227,8 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              bool self_set, Counts cnt, uint64_t *cand,
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
-                             unsigned long long *events, hipStream_t st, uint32_t q_lo = 0);
+                             unsigned long long *events, uint64_t cap, uint32_t *cand_over,
+                             hipStream_t st, uint32_t q_lo = 0);
 // (q_lo, n_qry: the query rows [q_lo, q_lo + n_qry) of the grid)
 // (d_qry_it_len non-null: the probed query rows are launch_record_rows copies of length
 // d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)

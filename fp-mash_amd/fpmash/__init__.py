@@ -135,6 +135,7 @@ SYMBOLS = [
                                                   C.c_double, vp, vp, vp, vp, vp, vp, vp]),
     ("fpm_refset_reindex", C.c_int, [vp, vp]),
     ("fpm_ctx_index_rebuilds", C.c_int, [vp, u64p]),
+    ("fpm_ctx_spec_stats", C.c_int, [vp, u64p, u64p]),
     ("fpm_refset_dist", C.c_int, [vp, vp, u32p, u64p, C.c_uint64, C.c_uint32, C.c_uint32,
                                   C.c_uint32, C.c_double, C.c_double, C.c_double, u32p, u32p,
                                   f64p, f64p, u8p]),
@@ -235,7 +236,11 @@ def lib():
                               "fpmash has no CPU fallback")
         L = C.CDLL(LIB_PATH)
         for name, res, args in SYMBOLS:
-            f = getattr(L, name)
+            # (an older build under FPMASH_LIB, a same-box A/B, may lack the newest entry
+            # points; tests/test_abi.py checks the product exports every one)
+            f = getattr(L, name, None)
+            if f is None:
+                continue
             f.restype = res
             f.argtypes = args
         _LIB = L
@@ -549,6 +554,12 @@ class Context:
         v = C.c_uint64()
         _check(lib().fpm_ctx_index_rebuilds(self.h, C.byref(v)))
         return v.value
+
+    def spec_stats(self):
+        """(kept, dropped) speculated probes since the context was created (fpm_ctx_spec_stats)"""
+        h, m = C.c_uint64(), C.c_uint64()
+        _check(lib().fpm_ctx_spec_stats(self.h, C.byref(h), C.byref(m)))
+        return h.value, m.value
 
     def last_dist_stats(self):
         sp, ev, ca = C.c_int(), C.c_uint64(), C.c_uint64()

@@ -111,6 +111,10 @@ int fpm_memset(fpm_ctx *ctx, void *dptr, int value, size_t bytes);
 /* one-pass bucket-index builds (dist_index.hip) that overflowed a level-1 slot and were
  * redone by the exact two-pass build, since the context was created */
 int fpm_ctx_index_rebuilds(fpm_ctx *ctx, uint64_t *count);
+/* dist calls whose probe was enqueued behind the index build before the host read the
+ * build's counters (a call of the previous sparse call's shape): kept (hits) or dropped and
+ * redone on the path the counters chose (misses), since the context was created */
+int fpm_ctx_spec_stats(fpm_ctx *ctx, uint64_t *hits, uint64_t *misses);
 int fpm_ctx_set_timing(fpm_ctx *ctx, int enable);
 int fpm_ctx_reset_timing(fpm_ctx *ctx);
 /* total milliseconds and launch count since the last reset (synchronises) */

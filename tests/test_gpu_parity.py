@@ -536,6 +536,97 @@ def test_dist_self_symmetric_path(ctx, oracle):
         ctx.set_dist_mode(fpmash.DIST_AUTO)
 
 
+def test_dist_speculated_probe(ctx, oracle):
+    """A dist call of the previous sparse rank-kernel call's shape enqueues its probe before the
+    host reads the index build's counters (fpm_ctx_spec_stats).  Kept when the counters confirm
+    the path and the capacity; dropped and redone when they do not: more candidates than the
+    profile's capacity (sparse random rows, then heavily shared family rows of the same shape),
+    an unsorted row (the literal walk), a near-identical set (the dense walk).  Every grid
+    equals the oracle's."""
+    import fpmash
+    import fpmash.datagen as D
+    S = 37
+    P = oracle.params(k=21, s=S)
+
+    def check(rows, lens):
+        got = ctx.dist(rows, rows, S, ref_lengths=lens, qry_lengths=lens)
+        nu, de, di, pv = oracle.dist_grid(rows, lens, rows, lens, S, 21, 4.0 ** 21)
+        assert np.array_equal(got["numer"], nu) and np.array_equal(got["denom"], de)
+        np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+        return got
+
+    # 400 rows of 37 hashes: the random rows' posting events (~5 per hash) stay below the
+    # 160,000 pairs, the families' (~12 per hash) do not
+    rand = oracle.sketch_batch(P, D.family_dna(400, 1, 1500, seed=3))
+    fam = oracle.sketch_batch(P, D.family_dna(40, 10, 1500, sub_rate=(0.0, 0.03), seed=4))
+    L = [1500] * 400
+    assert {len(x) for x in rand} == {len(x) for x in fam} == {S}
+    h0, m0 = ctx.spec_stats()
+    check(rand, L)                       # sets the profile: capacity min(events, pairs)
+    check(rand, L)                       # same shape: the speculated probe is kept
+    h1, m1 = ctx.spec_stats()
+    assert h1 == h0 + 1 and m1 == m0, (h0, m0, h1, m1)
+    g = check(fam, L)                    # more candidates than the capacity: redone
+    assert (g["numer"] > 0).sum() >= 4000          # every family pair (40 x 10 x 10)
+    h2, m2 = ctx.spec_stats()
+    assert m2 == m1 + 1, (m1, m2)
+    check(fam, L)                        # the profile grew: kept
+    h3, m3 = ctx.spec_stats()
+    assert h3 == h2 + 1 and m3 == m2
+    uns = [x.copy() for x in fam]
+    uns[5] = uns[5][::-1].copy()         # an unsorted row: the literal walk
+    check(uns, L)
+    assert ctx.last_dist_stats()["sparse"] != 2
+    near = [fam[0].copy() for _ in range(400)]
+    near[7] = rand[7]                    # near-identical rows: the dense walk
+    check(near, L)
+    assert ctx.last_dist_stats()["sparse"] == 0
+    check(fam, L)
+    h4, m4 = ctx.spec_stats()
+    assert m4 >= m3 + 1 and h4 >= h3
+
+
+@pytest.mark.parametrize("layout", ["contiguous", "interleaved"])
+def test_dist_covered_bucket_skip(ctx, oracle, layout):
+    """The probe skips a bucket whose entries' ref-id range (min id, span; idx_minspan) is
+    already marked in the row bitmap.  Families with adjacent ids (the skip's case) and with
+    interleaved ids (spans past the limit: buckets read), plus bridge rows that share a few
+    hashes with members of several families (pairs sharing 1-3 hashes, whose buckets are
+    partly covered), and a row repeated: every cell equals the oracle, on the symmetric self
+    path and against a copy."""
+    import fpmash
+    seqs, sk = _family_sketches(oracle, n_fam=10, members=12, seed=17)
+    lengths = [len(x) for x in seqs]
+    if layout == "interleaved":
+        order = [f + 10 * m for m in range(12) for f in range(10)]
+        sk = [sk[i] for i in order]
+        lengths = [lengths[i] for i in order]
+    rng = np.random.default_rng(5)
+    bridges = []
+    for b in range(6):
+        picks = [sk[int(i)][rng.integers(0, len(sk[int(i)]), size=1 + b % 3)]
+                 for i in rng.choice(len(sk), size=4, replace=False)]
+        filler = rng.integers(1, 2 ** 63, size=900, dtype=np.uint64)
+        bridges.append(np.unique(np.concatenate(picks + [filler])))
+    sk = sk + bridges + [sk[7].copy()]
+    lengths = lengths + [2000] * len(bridges) + [lengths[7]]
+    ctx.set_dist_mode(fpmash.DIST_SPARSE)
+    try:
+        a = ctx.dist(sk, sk, 1000, ref_lengths=lengths, qry_lengths=lengths)
+        assert ctx.last_dist_stats()["sparse"] == 2
+        b = ctx.dist(sk, [x.copy() for x in sk], 1000, ref_lengths=lengths, qry_lengths=lengths)
+        nu, de, di, pv = oracle.dist_grid(sk, lengths, sk, lengths, 1000, 21, 4.0 ** 21)
+        for got in (a, b):
+            assert np.array_equal(got["numer"], nu) and np.array_equal(got["denom"], de)
+            np.testing.assert_allclose(got["pvalue"], pv, rtol=RTOL, atol=0)
+        n = len(sk)
+        nb = len(bridges)
+        # the bridges share hashes with family rows: those pairs are counted
+        assert (nu.reshape(n, n)[n - 1 - nb:n - 1, :n - 1 - nb] > 0).sum() >= nb
+    finally:
+        ctx.set_dist_mode(fpmash.DIST_AUTO)
+
+
 @pytest.mark.parametrize("mode", ["auto", "dense", "sparse"])
 def test_dist_dev16_matches_u32(ctx, oracle, mode):
     """fpm_dist_dev16 (u16 numer / denom cells) gives the u32 path's results on the symmetric

@@ -21,7 +21,12 @@ for k in sketch fingerprint dist dist_index seqparse; do
   ov="KSRC_$k"; [ -n "${!ov:-}" ] && src="${!ov}"
   $HIPCC $HF -I"$PWD/csrc" -c "$src" -o "$OUT/$k.o" & pids+=($!)
 done
-$HIPCC $HF -c "$SRC/fpm_api.cpp" -o "$OUT/fpm_api.o" & pids+=($!)
+for c in "$SRC"/*.cpp; do
+  $HIPCC $HF -c "$c" -o "$OUT/$(basename "$c" .cpp).o" & pids+=($!)
+done
+id=$(cat "$SRC"/*.hip "$SRC"/*.cpp "$SRC"/*.hpp | sha256sum | cut -c1-16)
+printf 'extern "C" const char *fpm_build_id(void) { return "%s"; }\nextern "C" const char fpm_build_id_tag[] = "fpm-build-id:%s";\n' $id $id > "$OUT/build_id.cpp"
+$HIPCC $HF -c "$OUT/build_id.cpp" -o "$OUT/build_id.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-$HIPCC --offload-arch=gfx950 -shared -fPIC -o "lib/libfpmash_$NAME.so" "$OUT"/*.o
+$HIPCC --offload-arch=gfx950 -shared -fPIC -o "lib/libfpmash_$NAME.so" "$OUT"/*.o -ldl
 echo "lib/libfpmash_$NAME.so"
