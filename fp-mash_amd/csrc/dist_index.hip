@@ -32,17 +32,10 @@
 namespace fpm {
 
 constexpr uint32_t kParts = 1u << kIdxL1;    // level-1 partitions (top 10 key bits)
-// Bucket ref-id ranges (the directory's second half, idx_minspan): (min id << 8) | (max - min)
-// of the bucket's entries when max - min < kSpanUnknown, else kSpanUnknown (unknown / empty).
-// The probe skips reading a bucket whose whole range is already marked in its row bitmap:
-// every entry's ref is then marked whatever the entry holds, so the candidates are the same.
-// Sketches of related sequences (a family's members, adjacent ids) share most of their
-// hashes, so after the first of a row's hashes mark the family, most buckets are covered.
-constexpr uint32_t kSpanUnknown = 0xFF;
 // posting events in flight per lane in the probe (4: 0.307 ms, 12 without the 8-wave cap
-// 0.339 ms, against 0.298-0.301 ms at 8, before the covered-bucket skip)
+// 0.339 ms, against 0.298-0.301 ms at 8)
 #ifndef PROBE_KU
-#define PROBE_KU 4
+#define PROBE_KU 8
 #endif
 
 __device__ __forceinline__ uint64_t load_key(const void *lists, uint32_t hash_bytes, uint64_t idx)
@@ -517,22 +510,6 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
         for (int w = 0; w < kBucketThreads / 64; w++) t += wsq[w];
         if (t) atomicAdd(&sqsum[1 + ((p * ns + j) & 63)], t);
     }
-    // each bucket's ref-id range (idx_minspan): from the placed entries in LDS, sub-bucket d
-    // holding out[sh[d - 1], sh[d]) once every entry is placed (sh[d] = its end)
-    uint32_t *const minspan = dir + ((uint64_t)1 << g.nbits) + 1 + ((uint64_t)p << g.l2) + lo;
-    const uint32_t rmask = (1u << g.rbits) - 1;
-    auto write_minspan = [&]() {
-        for (uint32_t d = threadIdx.x; d < nsb; d += kBucketThreads) {
-            const uint32_t a = d ? sh[d - 1] : 0u, e = sh[d];
-            uint32_t mn = 0xFFFFFFFFu, mx = 0;
-            for (uint32_t i = a; i < e; i++) {
-                const uint32_t r = out[i] & rmask;
-                mn = min(mn, r);
-                mx = max(mx, r);
-            }
-            minspan[d] = e > a && mx - mn < kSpanUnknown ? (mn << 8) | (mx - mn) : kSpanUnknown;
-        }
-    };
     if (in_reg) {
 #pragma unroll
         for (int u = 0; u < kBucketPer; u++)
@@ -542,7 +519,6 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
             }
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < s1 - s0; i += kBucketThreads) entries[s0 + i] = out[i];
-        write_minspan();
         return;
     }
     // the range through LDS when it fits (tot is block-uniform), else straight to `entries`
@@ -566,14 +542,9 @@ __global__ __launch_bounds__(kBucketThreads) void idx_bucket_kernel(
                 }
             }
     }
-    if (!lds) {
-        // (the entries went straight to global memory: no ranges, the probe reads these buckets)
-        for (uint32_t d = threadIdx.x; d < nsb; d += kBucketThreads) minspan[d] = kSpanUnknown;
-        return;
-    }
+    if (!lds) return;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kBucketThreads) entries[base + i] = out[i];
-    write_minspan();
 }
 
 // ---- exclusive scan of u32 counts (n <= 2^31), three launches ----
@@ -773,14 +744,13 @@ void probe_rows_kernel(
     const uint64_t rowoff = (uint64_t)q * stride;
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t rmask = (uint32_t)((1ULL << g.rbits) - 1);
-    const uint32_t *__restrict__ minspan = dir + ((uint64_t)1 << g.nbits) + 1;
     // batches of 64 hashes per wave; the keys and bucket ranges of up to kB batches are
     // loaded together (their global loads overlap) before the batches are expanded
     constexpr int kB = 4;
     uint64_t ev_w = 0;      // this wave's posting events (with `events`)
     uint32_t uns = 0;       // an out-of-order or repeated value in the row (with `q_unsorted`)
     for (uint32_t jb = wave * 64; jb < lit; jb += 256 * kB) {
-        uint32_t st_b[kB], cnt_b[kB], tgt_b[kB], ms_b[kB];
+        uint32_t st_b[kB], cnt_b[kB], tgt_b[kB];
 #pragma unroll
         for (int bi = 0; bi < kB; bi++) {
             const uint32_t j = jb + 256 * bi + lane;
@@ -797,36 +767,11 @@ void probe_rows_kernel(
             st_b[bi] = d0;
             cnt_b[bi] = self_set && d1 - d0 == 1 ? 0u : d1 - d0;
             tgt_b[bi] = key_fp(K, g, mult);
-            ms_b[bi] = j < lit && d1 - d0 > 1 ? minspan[b] : kSpanUnknown;
         }
 #pragma unroll
       for (int bi = 0; bi < kB; bi++) {
         if (jb + 256 * bi >= lit) break;                  // wave-uniform
-        const uint32_t st = st_b[bi], tgt = tgt_b[bi];
-        uint32_t cnt = cnt_b[bi];
-        if (events) {
-            // the posting events of the row's hashes, read or not (the caller's measure of the
-            // rank work, fpm_ctx_last_dist_stats)
-            uint32_t t = cnt;
-#pragma unroll
-            for (int d = 32; d > 0; d >>= 1) t += __shfl_xor(t, d, 64);
-            ev_w += t;
-        }
-        {
-            // a bucket whose entries' refs are all marked already adds nothing: not read
-            const uint32_t span = ms_b[bi] & 0xFFu, mn = ms_b[bi] >> 8;
-            if (cnt && span != kSpanUnknown && mn >= r0 && mn + span < r1) {
-                const uint32_t a = mn - r0, e = a + span;
-                bool cov = true;
-                for (uint32_t w = a >> 5; cov && w <= (e >> 5); w++) {
-                    const uint32_t lo_b = w == (a >> 5) ? (a & 31u) : 0u;
-                    const uint32_t hi_b = w == (e >> 5) ? (e & 31u) : 31u;
-                    const uint32_t m = (hi_b == 31u ? ~0u : ((2u << hi_b) - 1u)) & ~((1u << lo_b) - 1u);
-                    cov = (rowbits[w] & m) == m;
-                }
-                if (cov) cnt = 0;
-            }
-        }
+        const uint32_t st = st_b[bi], cnt = cnt_b[bi], tgt = tgt_b[bi];
         uint32_t inc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -834,6 +779,7 @@ void probe_rows_kernel(
             if ((int)lane >= d) inc += y;
         }
         const uint32_t total = __builtin_amdgcn_readlane(inc, 63);
+        ev_w += total;
         // same wave writes and reads these slots: LDS ops of one wave complete in order.
         // Event ev of hash m reads entries[st_m + ev - pre_m] = entries[base_m + ev] (u32
         // arithmetic wraps consistently).

@@ -2514,11 +2514,14 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
             if (int rc = then()) return rc;
             tl.done();
         }
-        // work enqueued behind the index before its counters are read (the speculated probe:
-        // the GPU runs it while the host waits for the counters)
+        // the counters' copy first, then the work enqueued behind it before the host waits for
+        // them (the speculated probe: the GPU runs it while the host reads and enqueues the
+        // rest; enqueued before the copy, it would hold the copy, and the host, until it ends)
+        unsigned long long seq;
+        if (int rc = publish_counters(ctx, ctr, 68, st, &seq)) return rc;
         if (before_read)
             if (int rc = before_read()) return rc;
-        if (int rc = read_counters(ctx, ctr, 68, st)) return rc;
+        if (int rc = wait_counters(ctx, seq, st)) return rc;
         if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
             if (raw_of_unsorted && ((const uint32_t *)(ctx->host_counters + 66))[0] != 0)
                 return FPM_OK;
@@ -2589,8 +2592,7 @@ static int refset_build_index(fpm_refset *rs, hipStream_t st)
                      bool raw) -> int {
         const uint64_t En = (uint64_t)rs->n_ref * stride;
         void *dir, *entries;
-        // the directory, then the buckets' ref-id ranges (dist_index.hip, idx_minspan)
-        HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 8, &dir));
+        HIP_TRY(slot_buf(rs->slot[4], ((1ULL << g.nbits) + 1) * 4, &dir));
         HIP_TRY(slot_buf(rs->slot[5], En * 4, &entries));
         // the bucket pass also sums the self events (a query block that is the set itself
         // then needs no probe count)
@@ -2803,8 +2805,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             all_sorted = !rs->ref_unsorted && (rs->recorded ? false : !q_unsorted);
         } else {
             void *dir_, *entries_;
-            // the directory, then the buckets' ref-id ranges (dist_index.hip, idx_minspan)
-            HIP_TRY(scratch(ctx, 4, (NB + 1) * 8, &dir_));
+            HIP_TRY(scratch(ctx, 4, (NB + 1) * 4, &dir_));
             HIP_TRY(scratch(ctx, 5, E * 4, &entries_));
             dir = (const uint32_t *)dir_;
             entries = (const uint32_t *)entries_;
