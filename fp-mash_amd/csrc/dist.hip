@@ -343,21 +343,24 @@ constexpr uint32_t kRankLogB = 12;   // log2 buckets for CAP 1024 (CAP 2048: one
 // sentinels): j = lb.
 // NP = 0 (any row): 64-bit reads over the row's largest bucket (maxn), every position
 // clamped to the sentinel and tested against lb.
-// HI (rows whose largest value has bit 63 set, i.e. kshift = 32: full-range 64-bit hashes):
-// the key is a's high dword and the bucket a 32-bit shift of it, instead of two 64-bit shifts
-// and a 64-bit compare per value.
+// HI (rows whose bucket shift is >= 32: values of >= 32 + log2(buckets) bits, every 64-bit
+// hash sketch; a k = 21 bottom-s row holds values up to ~2^63): the key is a's high dword and
+// the bucket a 32-bit shift of it clamped to the directory's end (filled with lb up to
+// kBuckets), instead of two 64-bit shifts, a 64-bit compare and a select per value.  The high
+// dwords of a row with fewer than 64 bits are still distinct in practice (a row where two
+// are not takes the NP = 0 loop).
 template <int NP, bool HI = false>
 __device__ __forceinline__ uint64_t rank_chunk(const uint64_t *Bs, const uint32_t *K32,
                                                const uint16_t *Bkt, uint32_t shift,
                                                uint32_t kshift, uint32_t top, uint32_t lb,
-                                               uint32_t maxn, uint64_t a, uint32_t &j)
+                                               uint32_t maxn, uint32_t kb, uint64_t a, uint32_t &j)
 {
     bool over;
     uint32_t lo;
     if constexpr (HI) {
-        // shift = 52: t < kBuckets, and the directory past top holds lb (the sentinels)
+        // the directory past top holds lb (the sentinels) up to Bkt[kBuckets]
         over = false;
-        lo = Bkt[(uint32_t)(a >> 32) >> (shift - 32)];
+        lo = Bkt[min((uint32_t)(a >> 32) >> (shift - 32), kb)];
     } else {
         const uint64_t t = a >> shift;
         over = t > (uint64_t)top;
@@ -450,7 +453,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint64_t bmax = lb ? Bs[lb - 1] : 0;
     const uint32_t bits = bmax ? 64 - __clzll(bmax) : 0;
     const uint32_t shift = bits > kLogBuckets ? bits - kLogBuckets : 0;
-    const uint32_t kshift = bits > 32 ? bits - 32 : 0;
+    // HI rows (shift >= 32): the keys are the values' high dwords
+    const uint32_t kshift = shift >= 32 ? 32 : bits > 32 ? bits - 32 : 0;
     // top = the last B value's bucket; the directory stops at Bkt[top + 1] = lb (filling
     // every bucket up to kBuckets cost one thread up to kBuckets / 2 serial stores)
     const uint32_t top = (uint32_t)(bmax >> shift);
@@ -650,8 +654,8 @@ __global__ __launch_bounds__(64 * kRankWaves) void rank_rows_kernel(
     const uint32_t *k_ = K32;
 #define FPM_RANK_NP(NP_, HI_) \
     run([&](uint64_t a, uint32_t &j) { \
-        return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, a, j); }, NP_ > 0)
-    const bool hi = kshift == 32;   // bits = 64 (then shift = 52 >= 32 as well)
+        return rank_chunk<NP_, HI_>(bs_, k_, bk_, shift, kshift, top, lb, maxn, kBuckets, a, j); }, NP_ > 0)
+    const bool hi = shift >= 32;    // bits >= 32 + kLogBuckets (then kshift = 32)
     switch (np) {
     case 2: if (hi) FPM_RANK_NP(2, true); else FPM_RANK_NP(2, false); break;
     case 3: if (hi) FPM_RANK_NP(3, true); else FPM_RANK_NP(3, false); break;

@@ -587,13 +587,12 @@ def test_dist_speculated_probe(ctx, oracle):
 
 
 @pytest.mark.parametrize("layout", ["contiguous", "interleaved"])
-def test_dist_covered_bucket_skip(ctx, oracle, layout):
-    """The probe skips a bucket whose entries' ref-id range (min id, span; idx_minspan) is
-    already marked in the row bitmap.  Families with adjacent ids (the skip's case) and with
-    interleaved ids (spans past the limit: buckets read), plus bridge rows that share a few
-    hashes with members of several families (pairs sharing 1-3 hashes, whose buckets are
-    partly covered), and a row repeated: every cell equals the oracle, on the symmetric self
-    path and against a copy."""
+def test_dist_family_layouts_and_bridges(ctx, oracle, layout):
+    """Families with adjacent ids and with interleaved ids (a family's entries spread over the
+    whole id range of every bucket), plus bridge rows that share 1-3 hashes with members of
+    several families (pairs whose only shared hashes sit in other families' buckets), and a
+    row repeated: every cell equals the oracle, on the symmetric self path and against a copy.
+    (Written for the covered-bucket probe skip, measured slower and removed in round 6.)"""
     import fpmash
     seqs, sk = _family_sketches(oracle, n_fam=10, members=12, seed=17)
     lengths = [len(x) for x in seqs]
