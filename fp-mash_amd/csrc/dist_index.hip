@@ -100,7 +100,7 @@ __global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     const void *__restrict__ ref, const uint32_t *__restrict__ ref_len, uint64_t stride,
     uint32_t n_ref, uint32_t hash_bytes, unsigned long long *__restrict__ kmax,
     unsigned long long *__restrict__ zero, uint32_t nzero, unsigned long long *acc,
-    uint32_t *__restrict__ zero32, uint32_t nzero32)
+    uint32_t *__restrict__ zero32, uint32_t nzero32, unsigned long long *__restrict__ zero_x)
 {
     __shared__ unsigned long long wmax[kKmaxThreads / 64];
     __shared__ uint32_t s_last;
@@ -137,6 +137,8 @@ __global__ __launch_bounds__(kKmaxThreads) void idx_kmax_kernel(
     __threadfence();
     for (uint32_t i = threadIdx.x; i < nzero; i += kKmaxThreads) zero[i] = 0;
     for (uint32_t i = threadIdx.x; i < nzero32; i += kKmaxThreads) zero32[i] = 0;
+    // one more word of the caller's (the compact output's list count: no memset launch)
+    if (zero_x && threadIdx.x == 0) *zero_x = 0;
     __syncthreads();
     if (threadIdx.x == 0) {
         *kmax = atomicMax(&acc[0], 0ULL);
@@ -1106,7 +1108,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
                             uint32_t nzero, unsigned long long *acc, uint32_t *part_fill,
-                            uint32_t *overflow, hipStream_t st)
+                            uint32_t *overflow, hipStream_t st, unsigned long long *zero_x)
 {
     const uint32_t ntiles = g.ntiles;
     const uint64_t magic = stride > 1 ? ~0ULL / stride + 1 : 0;   // row_of's multiplier
@@ -1115,7 +1117,7 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
     const bool one_pass = g.cap != 0 && part_fill && overflow;
     hipLaunchKernelGGL(idx_kmax_kernel, dim3(kg), dim3(kKmaxThreads), 0, st, d_ref, d_ref_len,
                        stride, n_ref, hash_bytes, (unsigned long long *)g.kmax, zero, nzero, acc,
-                       one_pass ? part_fill : nullptr, one_pass ? kParts : 0u);
+                       one_pass ? part_fill : nullptr, one_pass ? kParts : 0u, zero_x);
     // level 2: the sub-bucket range split over 2^lsplit workgroups until its counters fit
     // 32 KB and a range's mean entries 24k (C4, E = 5e7: 2 per partition).  The LDS copy: 16k
     // entries (80 KB with the counters, two workgroups per CU) when the ranges' mean fits 12k

@@ -2492,7 +2492,8 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
                        uint32_t n_ref, uint32_t hash_bytes, IdxGeom &g, uint32_t *dir,
                        uint32_t *entries, unsigned long long *ctr, bool self_events,
                        hipStream_t st, Then then, bool raw_of_unsorted = false,
-                       const std::function<int()> &before_read = nullptr)
+                       const std::function<int()> &before_read = nullptr,
+                       unsigned long long *zero_x = nullptr)
 {
     for (;;) {
         const uint64_t E = (uint64_t)n_ref * stride;
@@ -2510,7 +2511,7 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
                                      (uint32_t *)tile_hist, (uint32_t *)tile_off,
                                      (uint32_t *)scan_s, (uint64_t *)tent, dir, entries, unsorted,
                                      self_events ? ctr : nullptr, ctr, 72, ctr + 72,
-                                     (uint32_t *)part_fill, overflow, st));
+                                     (uint32_t *)part_fill, overflow, st, zero_x));
             if (int rc = then()) return rc;
             tl.done();
         }
@@ -2649,7 +2650,10 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
     ctx->last_sparse = 0;
     ctx->last_events = 0;
     ctx->last_cand = 0;
-    if (n_pairs == 0) return FPM_OK;
+    if (n_pairs == 0) {
+        if (fin && fin->compact()) HIP_TRY(hipMemsetAsync(fin->prim.list.count, 0, 8, st));
+        return FPM_OK;
+    }
     const uint64_t E = (uint64_t)n_ref * ref_stride;   // index entries (upper bound)
     bool try_sparse = ctx->dist_mode == FPM_DIST_SPARSE ||
                       (ctx->dist_mode == FPM_DIST_AUTO && n_pairs >= 4096 && E > 0);
@@ -2661,6 +2665,17 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                           n_ref == n_qry;
     const bool compact = fin && fin->compact();
     const bool want_mir = fin && fin->has_mirror() && !self_set;
+    // the compact output's list count starts at zero: cleared by the index build's first
+    // kernel when this call builds an index (no memset launch), else here before the first
+    // kernel that appends to the list
+    unsigned long long *const list_cnt =
+        compact ? reinterpret_cast<unsigned long long *>(fin->prim.list.count) : nullptr;
+    bool list_zeroed = !compact;
+    auto zero_list = [&]() -> int {
+        if (!list_zeroed) HIP_TRY(hipMemsetAsync(list_cnt, 0, 8, st));
+        list_zeroed = true;
+        return FPM_OK;
+    };
     // The side-stream fill writes every cell's no-shared-hash values (full output: distance /
     // p-value / pass, 17 B per cell), and with fill_cnt the numer / denom defaults too, which
     // the probe then leaves out: the probe (event reads, latency-bound, slowed ~3x by any write
@@ -2858,8 +2873,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                      hash_bytes, geom, (const uint32_t *)dir_,
                                                      events, unsorted, st));
                                              return FPM_OK;
-                                         }))
+                                         }, false, nullptr, list_zeroed ? nullptr : list_cnt))
                     return rc;
+                list_zeroed = true;
                 all_sorted = false;
                 ev = ctx->host_counters[0];
                 return FPM_OK;
@@ -2927,8 +2943,9 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                      hash_bytes, geom, (const uint32_t *)dir_,
                                                      events, unsorted, st));
                                              return FPM_OK;
-                                         }, true, speculate))
+                                         }, true, speculate, list_zeroed ? nullptr : list_cnt))
                     return rc;
+                list_zeroed = true;
                 ev = ctx->host_counters[0];
                 all_sorted = ((const uint32_t *)(ctx->host_counters + 66))[0] == 0;
                 if (!all_sorted) {
@@ -3085,6 +3102,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             if (fill_pending && cnum) HIP_TRY(hipStreamWaitEvent(st, ctx->ev_fill, 0));
             if (int rc = settle_prefill()) return rc;
             if (fin) {
+                if (int rc = zero_list()) return rc;
                 TimedLaunch tl(ctx, FPM_K_FINALIZE, st);
                 if (compact) {
                     const CellList none{};
@@ -3121,6 +3139,8 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
             return FPM_OK;
         }
     }
+    // (dist_dev_impl lists the cells of the dense grid afterwards)
+    if (int rc = zero_list()) return rc;
     // the dense compare writes every cell: after a prefill, not beside it
     if (prefilled && !prefill_done) {
         HIP_TRY(hipStreamWaitEvent(st, ctx->ev_prefill, 0));
@@ -3192,7 +3212,7 @@ static int dist_dev_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_
                     pf.S == sketch_size;
         if (prefilled) ctx->prefill.pending = false;
     }
-    if (compact) HIP_TRY(hipMemsetAsync(out.list.count, 0, 8, st));
+    // (the list count is cleared inside compare_impl: by the index build, else a memset)
     DistFinal fin{d_ref_length, d_qry_length, kmer_size, kmer_space, max_dist, max_pvalue, out};
     fin.prefilled = prefilled;
     bool finalized = false, mirrored = false;

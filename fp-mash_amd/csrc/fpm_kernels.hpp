@@ -170,8 +170,10 @@ hipError_t launch_idx_build(const void *d_ref, const uint32_t *d_ref_len, uint64
                             uint32_t *dir, uint32_t *entries, uint32_t *unsorted,
                             unsigned long long *self_events, unsigned long long *zero,
                             uint32_t nzero, unsigned long long *acc, uint32_t *part_fill,
-                            uint32_t *overflow, hipStream_t st);
-// zero[0..nzero) is cleared first; acc[0..1]: two words that start at zero and are left at zero.
+                            uint32_t *overflow, hipStream_t st,
+                            unsigned long long *zero_x = nullptr);
+// zero[0..nzero) (and *zero_x when given) is cleared first; acc[0..1]: two words that start at
+// zero and are left at zero.
 // One-pass build (g.cap != 0): part_fill holds 2^kIdxL1 u32 (cleared by the build), *overflow
 // (inside zero[]) is set when a partition exceeded cap: the index is then unusable and the
 // caller rebuilds with g.cap = 0
