@@ -166,10 +166,6 @@ struct fpm_ctx {
     // latency-bound candidate compare); ev_in / ev_fill order it against `stream`
     hipStream_t aux = nullptr;
     hipEvent_t ev_in = nullptr, ev_fill = nullptr;
-    // a stream of its own for the counter copies of a speculated call (publish_counters): the
-    // probe enqueued behind the index build does not wait for the copy (created on first use)
-    hipStream_t pub = nullptr;
-    hipEvent_t ev_pub = nullptr;
     // a compact grid's counts written ahead on `aux` (fpm_dist_list_prefill), until the dist
     // call on that grid takes it over (or any other dist call waits for it): ev_prefill
     struct Prefill {
@@ -392,21 +388,8 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
 // wait_counters spins until it has landed, so work enqueued between them runs while the host
 // waits (the speculated rank kernel of a resident set's block, compare_impl).
 static int publish_counters(fpm_ctx *ctx, const unsigned long long *d_src, uint32_t n,
-                            hipStream_t st, unsigned long long *seq_out, hipStream_t *on = nullptr)
+                            hipStream_t st, unsigned long long *seq_out)
 {
-    // on != nullptr: the copy runs on the context's publish stream after the work queued on st
-    // so far, and *on returns that stream (for wait_counters); later work on st does not wait
-    // for it
-    if (on) {
-        if (!ctx->pub) {
-            HIP_TRY(hipStreamCreateWithFlags(&ctx->pub, hipStreamNonBlocking));
-            HIP_TRY(hipEventCreateWithFlags(&ctx->ev_pub, hipEventDisableTiming));
-        }
-        HIP_TRY(hipEventRecord(ctx->ev_pub, st));
-        HIP_TRY(hipStreamWaitEvent(ctx->pub, ctx->ev_pub, 0));
-        st = ctx->pub;
-        *on = st;
-    }
     if (!ctx->host_counters) {
         HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, kPubWords * 8,
                               hipHostMallocMapped | hipHostMallocCoherent));
@@ -565,8 +548,6 @@ void fpm_ctx_destroy(fpm_ctx *ctx)
     if (ctx->ev_in) (void)hipEventDestroy(ctx->ev_in);
     if (ctx->ev_fill) (void)hipEventDestroy(ctx->ev_fill);
     if (ctx->ev_prefill) (void)hipEventDestroy(ctx->ev_prefill);
-    if (ctx->pub) (void)hipStreamDestroy(ctx->pub);
-    if (ctx->ev_pub) (void)hipEventDestroy(ctx->ev_pub);
     for (int i = 0; i < fpm_ctx::kRing; i++) {
         if (ctx->ring[i]) (void)hipHostFree(ctx->ring[i]);
         if (ctx->ring_ev[i]) (void)hipEventDestroy(ctx->ring_ev[i]);
@@ -2538,12 +2519,10 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
         // them (the speculated probe: the GPU runs it while the host reads and enqueues the
         // rest; enqueued before the copy, it would hold the copy, and the host, until it ends)
         unsigned long long seq;
-        hipStream_t pst = st;
-        if (int rc = publish_counters(ctx, ctr, 68, st, &seq, before_read ? &pst : nullptr))
-            return rc;
+        if (int rc = publish_counters(ctx, ctr, 68, st, &seq)) return rc;
         if (before_read)
             if (int rc = before_read()) return rc;
-        if (int rc = wait_counters(ctx, seq, pst)) return rc;
+        if (int rc = wait_counters(ctx, seq, st)) return rc;
         if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
             if (raw_of_unsorted && ((const uint32_t *)(ctx->host_counters + 66))[0] != 0)
                 return FPM_OK;
@@ -2964,10 +2943,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                                      hash_bytes, geom, (const uint32_t *)dir_,
                                                      events, unsorted, st));
                                              return FPM_OK;
-                                         }, true,
-                                         can_spec ? std::function<int()>(speculate)
-                                                  : std::function<int()>(),
-                                         list_zeroed ? nullptr : list_cnt))
+                                         }, true, speculate, list_zeroed ? nullptr : list_cnt))
                     return rc;
                 list_zeroed = true;
                 ev = ctx->host_counters[0];
