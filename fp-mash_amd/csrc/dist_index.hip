@@ -682,32 +682,6 @@ __global__ void sum64_kernel(unsigned long long *events)
     if (threadIdx.x == 0) events[0] = v;
 }
 
-// The copy itself, by threads [0, kPubWords) of a workgroup (every thread of the workgroup
-// calls it: it holds barriers).  src[0] = the posting events: the sum of the 64 spread partials
-// src[1..64] (the index build's bucket pass or probe_count_kernel add into those), folded in
-// here.
-__device__ __forceinline__ void publish_block(const unsigned long long *__restrict__ src, uint32_t n,
-                                              unsigned long long *dst, unsigned long long seq)
-{
-    __shared__ unsigned long long wsum[kPubWords / 64];
-    const uint32_t t = threadIdx.x;
-    unsigned long long ev = (t >= 1 && t <= 64 && n > 64) ? src[t] : 0;
-    for (int d = 32; d > 0; d >>= 1) ev += __shfl_xor(ev, d, 64);
-    if (t < kPubWords && (t & 63) == 0) wsum[t >> 6] = ev;
-    __syncthreads();
-    if (t == 0 && n > 64) {
-        unsigned long long s = 0;
-        for (uint32_t w = 0; w < kPubWords / 64; w++) s += wsum[w];
-        dst[0] = s;
-    } else if (t < n) {
-        dst[t] = src[t];
-    }
-    __threadfence_system();
-    __syncthreads();
-    if (t == 0) __hip_atomic_store(dst + kPubWords - 1, seq, __ATOMIC_RELEASE,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // One workgroup per (query row, ref chunk): LDS bitmap of the chunk's refs.  Each wave
 // takes 64 query hashes at a time: lane l looks up the bucket [st, st + cnt) of hash l,
 // a wave scan flattens the 64 buckets into one event range, and the lanes then read
@@ -726,13 +700,9 @@ void probe_rows_kernel(
     C *__restrict__ denom, uint64_t *__restrict__ cand,
     unsigned long long *__restrict__ n_cand, uint64_t *__restrict__ row_seg,
     const uint32_t *__restrict__ qry_it_len, uint32_t *__restrict__ q_unsorted,
-    unsigned long long *__restrict__ events, uint64_t cap, uint32_t *__restrict__ cand_over,
-    PubArgs pub)
+    unsigned long long *__restrict__ events, uint64_t cap, uint32_t *__restrict__ cand_over)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t rowbits[];
-    // the index build's counters for the host (a probe enqueued before the host reads them:
-    // workgroup 0 copies them first, instead of a publish_kernel launch ahead of the probe)
-    if (pub.dst && blockIdx.x == 0 && blockIdx.y == 0) publish_block(pub.src, pub.n, pub.dst, pub.seq);
     __shared__ uint32_t wsum[4];
     __shared__ unsigned long long row_base;
     // per wave: (entry base, fingerprint) of its 64 hashes, and the owner map of an event
@@ -1037,7 +1007,24 @@ __global__ __launch_bounds__(kPubWords) void publish_kernel(const unsigned long 
                                                           uint32_t n, unsigned long long *dst,
                                                           unsigned long long seq)
 {
-    publish_block(src, n, dst, seq);
+    // src[0] = the posting events: the sum of the 64 spread partials src[1..64] (the index
+    // build's bucket pass or probe_count_kernel add into those), folded in here
+    unsigned long long ev = (threadIdx.x >= 1 && threadIdx.x <= 64 && n > 64) ? src[threadIdx.x] : 0;
+    for (int d = 32; d > 0; d >>= 1) ev += __shfl_xor(ev, d, 64);
+    __shared__ unsigned long long wsum[kPubWords / 64];
+    if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = ev;
+    __syncthreads();
+    if (threadIdx.x == 0 && n > 64) {
+        unsigned long long t = 0;
+        for (uint32_t w = 0; w < kPubWords / 64; w++) t += wsum[w];
+        dst[0] = t;
+    } else if (threadIdx.x < n) {
+        dst[threadIdx.x] = src[threadIdx.x];
+    }
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(dst + kPubWords - 1, seq, __ATOMIC_RELEASE,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned long long *h_dst,
@@ -1203,7 +1190,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
                              unsigned long long *events, uint64_t cap, uint32_t *cand_over,
-                             hipStream_t st, uint32_t q_lo, PubArgs pub)
+                             hipStream_t st, uint32_t q_lo)
 {
     if (!n_qry || !n_ref) return hipSuccess;
     const uint32_t chunk = 1u << 19;   // refs per workgroup: 64 KiB of LDS bitmap
@@ -1221,7 +1208,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                        cref,                                                                     \
                        d_ref_len, S, (uint32_t)sym, (uint32_t)defaults, vec_defaults,           \
                        (uint32_t)self_set, (C *)cnt.numer, (C *)cnt.denom, cand, n_cand, row_seg, \
-                       d_qry_it_len, q_unsorted, events, cap, cand_over, pub)
+                       d_qry_it_len, q_unsorted, events, cap, cand_over)
     if (cnt.c16) FPM_PROBE(uint16_t);
     else FPM_PROBE(uint32_t);
 #undef FPM_PROBE

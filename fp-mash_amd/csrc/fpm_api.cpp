@@ -197,7 +197,6 @@ struct fpm_ctx {
         bool self_set = false, defaults = false;
     } spec;
     uint64_t spec_hits = 0, spec_misses = 0;
-    PubArgs pub_next;                      // a counter copy the next probe launch carries
     std::vector<std::pair<void *, size_t>> pool;
     size_t pool_bytes = 0;
     std::mutex pool_mu;
@@ -388,10 +387,8 @@ static hipError_t ensure_aux(fpm_ctx *ctx)
 // The two halves: publish_counters enqueues the copy (returns its sequence number), and
 // wait_counters spins until it has landed, so work enqueued between them runs while the host
 // waits (the speculated rank kernel of a resident set's block, compare_impl).
-// defer != nullptr: no launch; *defer describes the copy for the next kernel to fold into its
-// first workgroup (launch_probe_rows' PubArgs), which the caller must launch before waiting
 static int publish_counters(fpm_ctx *ctx, const unsigned long long *d_src, uint32_t n,
-                            hipStream_t st, unsigned long long *seq_out, PubArgs *defer = nullptr)
+                            hipStream_t st, unsigned long long *seq_out)
 {
     if (!ctx->host_counters) {
         HIP_TRY(hipHostMalloc((void **)&ctx->host_counters, kPubWords * 8,
@@ -400,8 +397,7 @@ static int publish_counters(fpm_ctx *ctx, const unsigned long long *d_src, uint3
         memset(ctx->host_counters, 0, kPubWords * 8);
     }
     const unsigned long long seq = ++ctx->pub_seq;
-    if (defer) *defer = PubArgs{d_src, n, ctx->dev_counters, seq};
-    else HIP_TRY(launch_publish(d_src, n, ctx->dev_counters, seq, st));
+    HIP_TRY(launch_publish(d_src, n, ctx->dev_counters, seq, st));
     *seq_out = seq;
     return FPM_OK;
 }
@@ -2523,18 +2519,9 @@ static int build_index(fpm_ctx *ctx, const void *rows, const uint32_t *len, uint
         // them (the speculated probe: the GPU runs it while the host reads and enqueues the
         // rest; enqueued before the copy, it would hold the copy, and the host, until it ends)
         unsigned long long seq;
-        if (before_read) {
-            // the speculated probe's first workgroup copies the counters (ctx->pub_next): no
-            // publish_kernel launch and dispatch gap ahead of it
-            if (int rc = publish_counters(ctx, ctr, 68, st, &seq, &ctx->pub_next)) return rc;
+        if (int rc = publish_counters(ctx, ctr, 68, st, &seq)) return rc;
+        if (before_read)
             if (int rc = before_read()) return rc;
-            if (ctx->pub_next.dst) {            // not taken: the plain copy
-                ctx->pub_next = PubArgs{};
-                HIP_TRY(launch_publish(ctr, 68, ctx->dev_counters, seq, st));
-            }
-        } else if (int rc = publish_counters(ctx, ctr, 68, st, &seq)) {
-            return rc;
-        }
         if (int rc = wait_counters(ctx, seq, st)) return rc;
         if (g.cap && ((const uint32_t *)(ctx->host_counters + 67))[0] != 0) {
             if (raw_of_unsorted && ((const uint32_t *)(ctx->host_counters + 66))[0] != 0)
@@ -2938,9 +2925,7 @@ static int compare_impl(fpm_ctx *ctx, const void *d_ref, const uint32_t *d_ref_l
                                               (const uint32_t *)entries_, d_ref_len, sketch_size,
                                               self_set, pf.defaults, self_set, cnt,
                                               (uint64_t *)cand, n_cand, (uint64_t *)row_seg,
-                                              nullptr, nullptr, nullptr, pf.cap, cand_over, st, 0,
-                                              ctx->pub_next));
-                    ctx->pub_next = PubArgs{};      // carried by the probe's first workgroup
+                                              nullptr, nullptr, nullptr, pf.cap, cand_over, st));
                     tl.done();
                     spec_probe = true;
                     return FPM_OK;

@@ -181,14 +181,6 @@ uint64_t scan_scratch_words(uint64_t n);
 // copy n (<= kPubWords - 1) u64 counters into host-mapped memory, then write `seq` into its
 // last word (system-scope fence between): the host spins on that word
 constexpr uint32_t kPubWords = 128;
-// a publish folded into another kernel's first workgroup (launch_probe_rows): dst == nullptr
-// for none
-struct PubArgs {
-    const unsigned long long *src = nullptr;
-    uint32_t n = 0;
-    unsigned long long *dst = nullptr;
-    unsigned long long seq = 0;
-};
 hipError_t launch_publish(const unsigned long long *d_src, uint32_t n, unsigned long long *h_dst,
                           unsigned long long seq, hipStream_t st);
 // each row's records among its first min(len, S, out_stride) entries (the strict increases of
@@ -238,7 +230,7 @@ hipError_t launch_probe_rows(const void *d_qry, const uint32_t *d_qry_len, uint6
                              unsigned long long *n_cand, uint64_t *row_seg,
                              const uint32_t *d_qry_it_len, uint32_t *q_unsorted,
                              unsigned long long *events, uint64_t cap, uint32_t *cand_over,
-                             hipStream_t st, uint32_t q_lo = 0, PubArgs pub = PubArgs{});
+                             hipStream_t st, uint32_t q_lo = 0);
 // (q_lo, n_qry: the query rows [q_lo, q_lo + n_qry) of the grid)
 // (d_qry_it_len non-null: the probed query rows are launch_record_rows copies of length
 // d_qry_it_len[q]; d_qry_len stays the original list lengths for the default cells)
