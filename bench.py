@@ -193,6 +193,7 @@ class Group:
         self.ws = ws
         self.dist = None
         self._comm = None
+        self.comm_error = None     # why the ranks have no communicator (then: gloo)
         if ws > 1:
             import datetime
             import torch.distributed as dist
@@ -221,10 +222,13 @@ class Group:
         return float(t.item())
 
     def comm(self, ctx):
-        """fpmash.Comm over all ranks on ctx's device (created once; blocks until every rank
-        has joined).  None when the ranks share one GPU (FPMASH_BENCH_ONE_DEVICE: RCCL refuses
-        two ranks per device): min-merges then go over gloo."""
-        if self._comm is None and not os.environ.get("FPMASH_BENCH_ONE_DEVICE"):
+        """fpmash.Comm over all ranks on ctx's device (created once; every rank waits for the
+        others, up to FPM_COMM_INIT_TIMEOUT_S).  None when the ranks share one GPU
+        (FPMASH_BENCH_ONE_DEVICE: RCCL refuses two ranks per device), or when a rank's set-up
+        failed (every rank learns it over gloo; `comm_error` says why): min-merges then go
+        over gloo, and the leg says so."""
+        if (self._comm is None and self.comm_error is None
+                and not os.environ.get("FPMASH_BENCH_ONE_DEVICE")):
             rank = 0
             if self.ws > 1:
                 import torch
@@ -236,7 +240,18 @@ class Group:
                 uid = bytes(uid.numpy().tobytes())
             else:
                 uid = fpmash.comm_unique_id()
-            self._comm = fpmash.Comm(ctx, self.ws, rank, uid)
+            try:
+                c, err = fpmash.Comm(ctx, self.ws, rank, uid), None
+            except Exception as e:                       # noqa: BLE001 (reported in the leg)
+                c, err = None, f"rank {rank}: {e}"
+            if self.max(0.0 if c is not None else 1.0) > 0.0:
+                # some rank has none: no rank uses its (a set-up whose peers are gone is left
+                # to the process exit)
+                self.comm_error = err or "a peer rank's RCCL set-up failed"
+                print(f"[bench] RCCL communicator unavailable ({self.comm_error}); "
+                      "min-merges over gloo", file=sys.stderr, flush=True)
+                return None
+            self._comm = c
         return self._comm
 
     def close(self):
@@ -1408,10 +1423,13 @@ def comm_check(ctx, grp, s=2000, k=21):
     exp_parts = O.sketch_batch(O.params(k=k, s=s), parts)
     ok_parts = all(n_i == len(e) and np.array_equal(h, e) for (h, n_i), e in zip(got, exp_parts))
     ok = bool(ok_parts and n_ == len(exp) and np.array_equal(merged, exp))
-    return {"ok": ok, "one_rank_merges_equal_parts": bool(ok_parts),
-            "merged_equals_whole": bool(n_ == len(exp) and np.array_equal(merged, exp)),
-            "collective": "RCCL in libfpmash (fpm_sketch_min_merge_comm), 1 rank",
-            "check_s": time.perf_counter() - t0}
+    res = {"ok": ok and comm is not None, "one_rank_merges_equal_parts": bool(ok_parts),
+           "merged_equals_whole": bool(n_ == len(exp) and np.array_equal(merged, exp)),
+           "collective": "RCCL in libfpmash (fpm_sketch_min_merge_comm), 1 rank",
+           "check_s": time.perf_counter() - t0}
+    if comm is None:                 # the RCCL path did not run: not a pass
+        res["comm_error"] = grp.comm_error
+    return res
 
 
 def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, steps=3,
@@ -1458,6 +1476,8 @@ def split_leg(ctx, grp, ws, rank, local, length=1_000_000_000, s=10_000, k=21, s
                      " and min-merged on the device",
            "n_gpus": ws, "bases": length, "steps": steps, "ms_per_step": el / steps * 1e3,
            "bases_per_s": length / (el / steps), "scaling": "strong"}
+    if grp.comm_error:
+        out["comm_error"] = grp.comm_error
     if parity and rank == 0:
         t_c = time.perf_counter()
         whole = ctx.sketch(P, [split_genome_range(0, length)])[0]

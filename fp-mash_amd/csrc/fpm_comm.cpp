@@ -22,9 +22,14 @@
 
 #include <dlfcn.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 
 namespace {
 
@@ -98,6 +103,21 @@ struct fpm_comm {
     size_t rows_bytes = 0, counts_bytes = 0;
 };
 
+namespace {
+
+// The set-up's time limit: FPM_COMM_INIT_TIMEOUT_S (default 120 s).  A rank whose peers never
+// join (a peer failed before its own set-up) gets an error instead of blocking for ever, so a
+// caller can report it and go on; the abandoned set-up thread stays blocked until the process
+// ends (an abort would wait for it).
+double init_limit_s()
+{
+    const char *v = getenv("FPM_COMM_INIT_TIMEOUT_S");
+    const double t = v ? atof(v) : 0.0;
+    return t > 0.0 ? t : 120.0;
+}
+
+}  // namespace
+
 extern "C" {
 
 int fpm_comm_unique_id(uint8_t id[FPM_COMM_ID_BYTES])
@@ -135,9 +155,42 @@ int fpm_comm_create(fpm_ctx *ctx, int nranks, int rank, const uint8_t id[FPM_COM
     c->device = sdev;
     c->nranks = nranks;
     c->rank = rank;
-    if (ncclResult_t rc = r.comm_init_rank(&c->comm, nranks, u, rank)) {
-        delete c;
-        return rccl_fail("ncclCommInitRank", rc);
+    {
+        // bounded: the blocking set-up on a thread of its own, waited for up to the limit (a
+        // non-blocking RCCL set-up still waited inside the call for the missing peers)
+        struct Setup {
+            std::mutex mu;
+            std::condition_variable cv;
+            bool done = false, abandoned = false;
+            ncclResult_t rc = ncclSuccess;
+            ncclComm_t comm = nullptr;
+        };
+        auto su = std::make_shared<Setup>();
+        const int dev_ = sdev;
+        std::thread([su, &r, nranks, u, rank, dev_] {
+            (void)hipSetDevice(dev_);
+            ncclComm_t cm = nullptr;
+            const ncclResult_t rc = r.comm_init_rank(&cm, nranks, u, rank);
+            std::lock_guard<std::mutex> lk(su->mu);
+            su->rc = rc;
+            su->comm = cm;
+            su->done = true;
+            // a caller that gave up left this communicator to the process
+            su->cv.notify_all();
+        }).detach();
+        const double limit = init_limit_s();
+        std::unique_lock<std::mutex> lk(su->mu);
+        if (!su->cv.wait_for(lk, std::chrono::duration<double>(limit), [&] { return su->done; })) {
+            su->abandoned = true;
+            delete c;
+            return cfail(FPM_EHIP, "ncclCommInitRank: not every rank joined within " +
+                                       std::to_string((int)limit) + " s (FPM_COMM_INIT_TIMEOUT_S)");
+        }
+        if (su->rc != ncclSuccess) {
+            delete c;
+            return rccl_fail("ncclCommInitRank", su->rc);
+        }
+        c->comm = su->comm;
     }
     *out = c;
     return FPM_OK;

@@ -465,7 +465,9 @@ int fpm_fp_positional_grid(fpm_ctx *ctx, const void *ref, const uint32_t *ref_le
 #define FPM_COMM_ID_BYTES 128
 typedef struct fpm_comm fpm_comm;
 int fpm_comm_unique_id(uint8_t id[FPM_COMM_ID_BYTES]);
-/* blocks until all nranks ranks have called it with the same id */
+/* waits until all nranks ranks have called it with the same id, up to FPM_COMM_INIT_TIMEOUT_S
+ * seconds (default 120; a non-blocking RCCL set-up, aborted past the limit): then FPM_EHIP and a
+ * message naming the limit, instead of blocking for ever on a peer that never joins */
 int fpm_comm_create(fpm_ctx *ctx, int nranks, int rank, const uint8_t id[FPM_COMM_ID_BYTES],
                     fpm_comm **out);
 void fpm_comm_destroy(fpm_comm *comm);

@@ -20,6 +20,8 @@ def free_port():
 
 
 def test_two_rank_group(tmp_path):
+    """bench.Group over two gloo ranks: barrier / max / sum, one batch per rank, and the
+    communicator agreement (one rank's RCCL set-up fails: neither rank uses one)."""
     out = str(tmp_path / "res")
     env = dict(os.environ, FPM_TEST_OUT=out)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
@@ -30,6 +32,9 @@ def test_two_rank_group(tmp_path):
     r = [json.load(open(out + f".{i}")) for i in range(2)]
     for x in r:
         assert x["ws"] == 2 and x["max"] == 2.0 and x["sum"] == 30.0 and x["n"] == 40
+        # a failed communicator set-up on one rank: no rank uses one, and each says why
+        assert x["comm_none"] and x["comm_error"], x
+    assert "set-up failed" in r[0]["comm_error"] and "peer" in r[1]["comm_error"]
     assert r[0]["batch0"] != r[1]["batch0"]   # each rank owns its own batch
 
 
@@ -90,6 +95,33 @@ def test_vblocks_and_comm_one_gpu():
     # even split's second index of block 1 against its own second half
     assert sh["rows_owned"] == 1000 and sh["rows_sketched"] == 3000, sh
     assert r["comm"]["ok"], r["comm"]
+
+
+@pytest.mark.gpu
+def test_comm_setup_bounded_without_peers():
+    """fpm_comm_create for 2 ranks with only rank 0 present: the set-up gives up after
+    FPM_COMM_INIT_TIMEOUT_S with an error naming the limit, instead of blocking for ever (the
+    bench then reports the communicator missing and min-merges over gloo).  In a child
+    process: an aborted communicator stays out of the test process."""
+    code = (
+        "import os, sys, time\n"
+        f"sys.path[:0] = [{ROOT!r}, {os.path.join(ROOT, 'fp-mash_amd')!r}]\n"
+        "os.environ['FPM_COMM_INIT_TIMEOUT_S'] = '4'\n"
+        "import fpmash\n"
+        "ctx = fpmash.Context(0)\n"
+        "t0 = time.time()\n"
+        "try:\n"
+        "    fpmash.Comm(ctx, 2, 0, fpmash.comm_unique_id())\n"
+        "    print('JOINED', flush=True)\n"
+        "except Exception as e:\n"
+        "    print('ERR', round(time.time() - t0, 1), e, flush=True)\n"
+        "ctx.close()\n"
+        "print('CLOSED', flush=True)\n")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=100)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [l for l in p.stdout.splitlines() if l.startswith(("ERR", "JOINED"))][-1]
+    assert line.startswith("ERR") and "FPM_COMM_INIT_TIMEOUT_S" in line, line
+    assert 3.0 <= float(line.split()[1]) < 60.0, line
 
 
 @pytest.mark.gpu
