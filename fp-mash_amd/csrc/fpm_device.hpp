@@ -26,14 +26,24 @@ __device__ __forceinline__ uint64_t fmix64(uint64_t k)
     return k;
 }
 
-// (h * 5 as a shift-add on 32-bit halves instead of the two v_mad_u64_u32 it lowers to: 4 fewer
-// quarter-rate multiplies per window, yet C5 31.3 -> 31.6 ms and the C2 sketch unchanged, same
-// box, r04: the tile kernel is not bound by its multiplies.)
+// (h * 5 as a shift-add instead of the two v_mad_u64_u32 it lowers to: 4 fewer quarter-rate
+// multiplies per window, yet C5 31.3 -> 31.6 ms in r04 and 19.75 -> 19.75 ms in r06, same box;
+// the rotated products below did count: profiles/r06/murmur_rot_ab.txt)
+// x * c, opaque to the optimiser: a rotate of the product then shifts the product (two
+// v_alignbit) instead of multiplying x again by the constant shifted (LLVM folds (x * c) << r
+// into x * (c << r): two more quarter-rate multiplies per rotated product)
+__device__ __forceinline__ uint64_t mul_opaque(uint64_t x, uint64_t c)
+{
+    uint64_t p = x * c;
+    asm volatile("" : "+v"(p));
+    return p;
+}
+
 __device__ __forceinline__ void mur_block(uint64_t &h1, uint64_t &h2, uint64_t k1, uint64_t k2)
 {
-    k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+    k1 = mul_opaque(k1, kC1); k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
     h1 = rotl64(h1, 27); h1 += h2; h1 = h1 * 5 + 0x52dce729;
-    k2 *= kC2; k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2;
+    k2 = mul_opaque(k2, kC2); k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2;
     h2 = rotl64(h2, 31); h2 += h1; h2 = h2 * 5 + 0x38495ab5;
 }
 
@@ -57,8 +67,8 @@ __device__ __forceinline__ uint64_t murmur_h1_le32(const uint64_t w[4], int len,
     if (rem) {
         uint64_t k1 = (nb == 0) ? w[0] : w[2];
         uint64_t k2 = (nb == 0) ? w[1] : w[3];
-        if (rem > 8) { k2 *= kC2; k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2; }
-        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+        if (rem > 8) { k2 = mul_opaque(k2, kC2); k2 = rotl64(k2, 33); k2 *= kC1; h2 ^= k2; }
+        k1 = mul_opaque(k1, kC1); k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
     }
     return mur_final(h1, h2, (uint64_t)len);
 }
@@ -73,7 +83,7 @@ __device__ __forceinline__ uint64_t murmur_h1_u64s(LoadFn load, uint64_t n, uint
     for (; i + 2 <= n; i += 2) mur_block(h1, h2, load(i), load(i + 1));
     if (i < n) {
         uint64_t k1 = load(i);
-        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+        k1 = mul_opaque(k1, kC1); k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
     }
     return mur_final(h1, h2, (uint64_t)(int64_t)(int)(n * 8));
 }
