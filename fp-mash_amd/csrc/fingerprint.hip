@@ -178,7 +178,7 @@ __device__ __forceinline__ void fp_parse_line(Get get, uint64_t li, uint64_t b, 
     }
     if (nv & 1) {                                            // odd last value: the k1 tail
         uint64_t k1 = pend;
-        k1 *= kC1; k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
+        k1 = mul_opaque(k1, kC1); k1 = rotl64(k1, 31); k1 *= kC2; h1 ^= k1;
     }
     const uint64_t h = mur_final(h1, h2, (uint64_t)(int64_t)(int)(nv * 8));
     id_off[li] = ib;
