@@ -14,7 +14,21 @@ namespace fpm {
 constexpr uint64_t kC1 = 0x87c37b91114253d5ULL;
 constexpr uint64_t kC2 = 0x4cf5ad432745937fULL;
 
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+// rotate by a constant as two v_alignbit_b32 (LLVM otherwise emits a 64-bit shift, a 32-bit
+// shift and an or for some of them)
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r)
+{
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (r == 32) return ((uint64_t)lo << 32) | hi;
+    if (r < 32) {
+        const uint32_t s = 32 - r;                       // lo' = lo << r | hi >> s
+        return ((uint64_t)__builtin_amdgcn_alignbit(hi, lo, s) << 32) |
+               __builtin_amdgcn_alignbit(lo, hi, s);
+    }
+    const uint32_t s = 64 - r;                           // rotr by s < 32
+    return ((uint64_t)__builtin_amdgcn_alignbit(lo, hi, s) << 32) |
+           __builtin_amdgcn_alignbit(hi, lo, s);
+}
 
 __device__ __forceinline__ uint64_t fmix64(uint64_t k)
 {
